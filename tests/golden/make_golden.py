@@ -1,0 +1,255 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE code.
+
+Run in the build container only (the reference is not present on GPU boxes):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py /root/reference
+
+The reference is imported read-only from the given path.  Modules it imports
+but never uses on the hot path are stubbed (torchsummary at
+models/fusion_nets.py:8; torchvision at models/models.py:5,13), as SURVEY.md
+section 8(c) prescribes.  ``words_loss`` does not return its similarity
+matrix, so CrossEntropyLoss inside models.losses is wrapped by a recorder to
+capture the logits it is called with (models/losses.py:131-132).
+
+Each fixture is an .npz with inputs, parameters, outputs and input gradients;
+every case is seeded (manual_seed 100 per cfg/train_bert.yml:15, plus a case
+offset) so the script is reproducible.
+"""
+from __future__ import annotations
+
+import importlib.machinery
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _import_reference(root):
+    sys.path.insert(0, root)
+    sys.modules.setdefault("torchsummary", types.SimpleNamespace(summary=None))
+    import transformers  # noqa: F401  (models.models imports these names first)
+    from transformers import (AlignTextModel, BertModel, BlipTextModel,  # noqa
+                              CLIPTextModel, FlavaTextModel, GroupViTTextModel)
+    for name in ("torchvision", "torchvision.models"):
+        mod = types.ModuleType(name)
+        mod.__spec__ = importlib.machinery.ModuleSpec(name, None)
+        sys.modules[name] = mod
+    sys.modules["torchvision"].models = sys.modules["torchvision.models"]
+    import models.attention as ref_att
+    import models.fusion_nets as ref_fus
+    import models.losses as ref_loss
+    import models.models as ref_models
+    return ref_att, ref_loss, ref_fus, ref_models
+
+
+class _Args:
+    """The attribute bag the reference losses read (cfg/train_bert.yml)."""
+
+    def __init__(self, en_type="BERT", bert_words_num=32):
+        self.en_type = en_type
+        self.bert_words_num = bert_words_num
+        self.CUDA = False
+        self.device = torch.device("cpu")
+        self.aux_feat_dim_per_granularity = 256
+        smooth = types.SimpleNamespace(GAMMA1=4.0, GAMMA2=5.0, GAMMA3=10.0)
+        self.TRAIN = types.SimpleNamespace(SMOOTH=smooth)
+
+
+def _record_ce(ref_loss):
+    """Wrap nn.CrossEntropyLoss inside models.losses to capture its inputs."""
+    seen = []
+    real = torch.nn.CrossEntropyLoss
+
+    class Recorder(real):
+        def forward(self, input, target):
+            seen.append(input.detach().clone())
+            return super().forward(input, target)
+
+    proxy = types.ModuleType("nn_proxy")
+    proxy.__dict__.update(torch.nn.__dict__)
+    proxy.CrossEntropyLoss = Recorder
+    ref_loss.nn = proxy
+    return seen
+
+
+def _unit_rows(x, dim):
+    return x / x.norm(dim=dim, keepdim=True)
+
+
+def _save(name, **arrays):
+    clean = {}
+    for k, v in arrays.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().cpu().numpy()
+        clean[k] = np.asarray(v)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **clean)
+    size = sum(a.nbytes for a in clean.values())
+    print(f"{name}: {len(clean)} arrays, {size / 1024:.0f} KiB")
+
+
+def _params(module, prefix=""):
+    return {prefix + k.replace(".", "_"): v.detach().clone()
+            for k, v in module.state_dict().items()}
+
+
+def gen_func_attention(ref_att):
+    cases = {"small": (3, 16, 4, 5, 101), "t22": (2, 256, 14, 22, 102)}
+    for tag, (b, d, hw, t, seed) in cases.items():
+        torch.manual_seed(seed)
+        q = torch.randn(b, d, t)
+        ctx = torch.randn(b, d, hw, hw, requires_grad=True)
+        wc, attn = ref_att.func_attention(q, ctx, 4.0)
+        probe = torch.randn_like(wc)
+        (wc * probe).sum().backward()
+        _save(f"func_attention_{tag}", query=q, context=ctx, gamma1=4.0,
+              weighted=wc, attn=attn, probe=probe, d_context=ctx.grad)
+
+
+def gen_words_loss(ref_loss):
+    seen = _record_ce(ref_loss)
+    cases = {
+        "bert_b4_t30": dict(b=4, words=32, lens=None),
+        "bert_b6_t22": dict(b=6, words=24, lens=None),
+        "lstm_b5": dict(b=5, words=None, lens=[18, 12, 7, 15, 3]),
+    }
+    for k, (tag, cfg) in enumerate(cases.items()):
+        torch.manual_seed(200 + k)
+        b = cfg["b"]
+        # R: channels-last storage as IMIM produces it (models/models.py:401-404)
+        r = _unit_rows(torch.randn(b, 14, 14, 256), -1).permute(0, 3, 1, 2)
+        r = r.detach().requires_grad_()
+        if cfg["lens"] is None:
+            t = cfg["words"] - 2
+            w = _unit_rows(torch.randn(b, t, 256), -1).transpose(1, 2)
+            args = _Args("BERT", cfg["words"])
+            cap_lens = None
+        else:
+            tmax = max(cfg["lens"])
+            w = (torch.rand(b, tmax, 256) * 2 - 1).mul(0.6).transpose(1, 2)
+            args = _Args("LSTM")
+            cap_lens = torch.tensor(cfg["lens"])
+        labels = torch.arange(b)
+        seen.clear()
+        l0, l1, att = ref_loss.words_loss(r, w, labels, cap_lens, None, b, args)
+        (l0 + l1).backward()
+        att_diag = np.zeros((b, w.shape[2], 14, 14), np.float32)
+        for i, a in enumerate(att):
+            att_diag[i, :a.shape[1]] = a[0].detach().numpy()
+        _save(f"words_loss_{tag}", img_features=r, words_emb=w.contiguous(),
+              cap_lens=(np.asarray(cfg["lens"]) if cap_lens is not None
+                        else np.zeros(0, np.int64)),
+              bert_words_num=(cfg["words"] or 0), logits=seen[0],
+              loss0=l0, loss1=l1, att_diag=att_diag, d_img=r.grad)
+
+
+def gen_sent_global_clip(ref_loss):
+    torch.manual_seed(300)
+    b = 8
+    img = torch.randn(b, 256, requires_grad=True)
+    sent = _unit_rows(torch.randn(b, 256), -1)
+    class_ids = np.array([3, 7, 3, 1, 7, 7, 0, 5])
+    labels = torch.arange(b)
+    args = _Args()
+    seen = _record_ce(ref_loss)
+    seen.clear()
+    s0, s1 = ref_loss.sent_loss(img, sent, labels, class_ids, b, args)
+    (s0 + s1).backward()
+    _save("sent_loss_b8", cnn_code=img, rnn_code=sent, class_ids=class_ids,
+          loss0=s0, loss1=s1, logits=seen[0], d_cnn=img.grad)
+
+    img2 = img.detach().clone().requires_grad_()
+    gl = ref_loss.global_loss(img2, sent)
+    gl.backward()
+    _save("global_loss_b8", cnn_code=img2, rnn_code=sent, loss=gl,
+          d_cnn=img2.grad)
+
+    img3 = _unit_rows(img.detach(), -1).requires_grad_()
+    text = _unit_rows(torch.randn(b, 256), -1)
+    cl = ref_loss.ClipLoss()(text, img3, args)
+    cl.backward()
+    _save("clip_loss_b8", text=text, image=img3, loss=cl, d_image=img3.grad)
+
+    logits = torch.randn(b, 50, requires_grad=True)
+    tgt = torch.tensor([1, 4, 9, 0, 49, 3, 3, 7])
+    fl = ref_loss.FocalLoss(gamma=2)(logits, tgt)
+    fl.backward()
+    _save("focal_loss_b8", logits=logits, target=tgt, loss=fl,
+          d_logits=logits.grad)
+
+
+def gen_self_attention(ref_fus):
+    for tag, (b, c, hw, cross) in {"c256_hw196": (2, 256, 14, False),
+                                   "c36_hw36": (3, 36, 6, True)}.items():
+        torch.manual_seed(400 + c)
+        m = ref_fus.SelfAttention(c, scale=1)
+        x = torch.randn(b, c, hw, hw, requires_grad=True)
+        y = torch.randn(b, c, hw, hw, requires_grad=True) if cross else x
+        out = m(x, y)
+        probe = torch.randn_like(out)
+        (out * probe).sum().backward()
+        p = {"q_w": m.query_proj.weight, "q_b": m.query_proj.bias,
+             "k_w": m.key_proj.weight, "k_b": m.key_proj.bias,
+             "v_w": m.value_proj.weight, "v_b": m.value_proj.bias}
+        extra = {"d_" + k: v.grad for k, v in p.items()
+                 if c < 64 or k in ("q_w", "v_w", "v_b")}
+        _save(f"self_attention_{tag}", x=x, y=y, out=out, probe=probe,
+              d_x=x.grad, d_y=(y.grad if cross else x.grad),
+              **{k: v.detach() for k, v in p.items()}, **extra)
+
+
+def gen_working(ref_fus):
+    torch.manual_seed(500)
+    b, t = 3, 22
+    net = ref_fus.Working(256).train()
+    img = _unit_rows(torch.randn(b, 14, 14, 256), -1).permute(0, 3, 1, 2)
+    img = img.detach().requires_grad_()
+    word = _unit_rows(torch.randn(b, t, 256), -1).transpose(1, 2).contiguous()
+    gl = torch.randn(b, 256)
+    sent = torch.randn(b, 256)
+    out = net(img, word, gl, sent)
+    probe = torch.randn_like(out)
+    (out * probe).sum().backward()
+    grads = {"d_" + k.replace(".", "_"): v.grad
+             for k, v in net.named_parameters()}
+    _save("working_b3", img=img, word=word, gl_img=gl, sent=sent, out=out,
+          probe=probe, d_img=img.grad, **_params(net), **grads)
+
+
+def gen_image_heading(ref_models):
+    torch.manual_seed(600)
+    b = 2
+    args = _Args()
+    net = ref_models.ImageHeading(args).train()
+    g = torch.randn(b, 512, requires_grad=True)
+    loc = torch.randn(b, 256, 14, 14, requires_grad=True)
+    gp, r = net(g, loc)
+    pg, pr = torch.randn_like(gp), torch.randn_like(r)
+    ((gp * pg).sum() + (r * pr).sum()).backward()
+    keep = ("imim.sa.value_proj.weight", "imim.sa.query_proj.bias",
+            "imim.project_local.projection.weight", "imim.ln.weight",
+            "project_global.projection.weight")
+    grads = {"d_" + k.replace(".", "_"): v.grad
+             for k, v in net.named_parameters() if k in keep}
+    _save("image_heading_b2", global_image=g, local_image=loc, g_out=gp,
+          r_out=r, probe_g=pg, probe_r=pr, d_global=g.grad, d_local=loc.grad,
+          **_params(net), **grads)
+
+
+def main():
+    root = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    torch.set_num_threads(8)
+    ref_att, ref_loss, ref_fus, ref_models = _import_reference(root)
+    gen_func_attention(ref_att)
+    gen_words_loss(ref_loss)
+    gen_sent_global_clip(ref_loss)
+    gen_self_attention(ref_fus)
+    gen_working(ref_fus)
+    gen_image_heading(ref_models)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,81 @@
+"""ctypes binding of libtgfr_hip.so (include/tgfr.h).
+
+The library is loaded after torch so that its NEEDED libamdhip64.so.7 resolves
+to the HIP runtime torch already mapped (same SONAME): one runtime per
+process, so torch's streams and device pointers are valid in the kernels.
+There is no fallback: if the library is missing or a call fails, this module
+raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must be imported before the library is mapped)
+
+from .build import LIB
+
+_lib = None
+
+P = C.c_void_p
+I = C.c_int
+L = C.c_longlong
+F = C.c_float
+
+# name -> argtypes (restype int unless noted)
+SIGNATURES = {
+    "tgfr_version": [],
+    "tgfr_prep_rows": [P, L, L, L, I, I, I, I, P, P, P, P, P],
+    "tgfr_wr_fwd": [P, P, P, P, P, P, I, I, I, F, F, F, F, P, I, P, P, P, I, I, P],
+    "tgfr_wr_bwd": [P, P, P, P, P, P, I, I, I, F, F, F, F, P, I, P, P, P, I, P],
+    "tgfr_wr_reduce": [P, I, I, P, L, L, L, I, P],
+    "tgfr_wr_lds_bytes": [I],
+    "tgfr_cos_logits": [P, L, P, L, I, I, I, I, F, F, I, P, I, P, L, P],
+    "tgfr_cos_logits_bwd": [P, L, P, L, I, I, I, I, F, F, P, L, P, L, P, L, P],
+    "tgfr_ce_stats": [P, L, I, I, P, P, P, P],
+    "tgfr_ce_loss_grad": [P, L, I, I, I, P, P, P, P, P, F, F, P, L, P],
+    "tgfr_attn_fwd": [P, P, P, I, I, I, I, F, P, P, I, P],
+    "tgfr_attn_bwd": [P, P, P, P, P, P, I, I, I, I, F, P, P, P, P, I, P],
+}
+
+
+def lib():
+    """The loaded kernel library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise RuntimeError(
+                f"{LIB} is missing: build it with "
+                "`python -m text_guided_face_recognition_amd.build` (no CPU fallback)")
+        handle = C.CDLL(LIB, mode=C.RTLD_GLOBAL)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(handle, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = argtypes
+            fn.restype = I
+        _lib = handle
+    return _lib
+
+
+def exported_symbols():
+    return [n for n in SIGNATURES if getattr(lib(), n, None) is not None]
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with code {rc}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("tgfr kernels take device tensors only (no CPU path)")
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream

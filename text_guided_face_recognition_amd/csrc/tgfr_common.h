@@ -1,0 +1,172 @@
+// Shared device helpers for the TGFR gfx950 kernels.
+//
+// Numerics: every contraction runs on v_mfma_f32_32x32x16_bf16 with fp32
+// accumulation.  MODE_SPLIT carries each fp32 operand as a bf16 pair
+// (hi = bf16(x), lo = bf16(x - hi)) and issues hi*hi + hi*lo + lo*hi, which
+// keeps ~16 mantissa bits per operand (the fp32-parity mode); MODE_BF16 issues
+// hi*hi only (the bf16 perf mode).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LDS_AS __attribute__((address_space(3)))
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+enum { MODE_BF16 = 0, MODE_SPLIT = 1 };
+
+namespace tgfr {
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ uint16_t bf_bits(float x) {
+  return __builtin_bit_cast(uint16_t, (__bf16)x);
+}
+__device__ __forceinline__ float bf_val(uint16_t u) {
+  return __uint_as_float(((uint32_t)u) << 16);
+}
+// fp32 -> (hi, lo) bf16 pair with x ~= hi + lo to ~2^-17 relative.
+__device__ __forceinline__ void split2(float x, uint16_t& hi, uint16_t& lo) {
+  hi = bf_bits(x);
+  lo = bf_bits(x - bf_val(hi));
+}
+__device__ __forceinline__ uint32_t pack2(uint16_t a, uint16_t b) {
+  return (uint32_t)a | ((uint32_t)b << 16);
+}
+
+template <int MODE>
+__device__ __forceinline__ void mma(f32x16& acc, const bf16x8& ahi, const bf16x8& alo,
+                                    const bf16x8& bhi, const bf16x8& blo) {
+  if constexpr (MODE == MODE_SPLIT) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc, 0, 0, 0);
+  }
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 as_bf8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+// 8 fp32 values -> bf16x8 hi (and lo when split).
+template <int MODE>
+__device__ __forceinline__ void frag8(const float* v, bf16x8& hi, bf16x8& lo) {
+  uint32_t hp[4], lp[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint16_t a0, a1, b0 = 0, b1 = 0;
+    if constexpr (MODE == MODE_SPLIT) {
+      split2(v[2 * k], a0, b0);
+      split2(v[2 * k + 1], a1, b1);
+    } else {
+      a0 = bf_bits(v[2 * k]);
+      a1 = bf_bits(v[2 * k + 1]);
+    }
+    hp[k] = pack2(a0, a1);
+    lp[k] = pack2(b0, b1);
+  }
+  hi = as_bf8(make_uint4(hp[0], hp[1], hp[2], hp[3]));
+  lo = as_bf8(make_uint4(lp[0], lp[1], lp[2], lp[3]));
+}
+
+// LDS access through explicit address-space-3 pointers (byte offsets).
+extern __shared__ __attribute__((aligned(16))) char g_smem[];
+
+__device__ __forceinline__ LDS_AS char* lds_base() { return (LDS_AS char*)g_smem; }
+
+__device__ __forceinline__ uint4 lds_ld16(uint32_t off) {
+  return __builtin_bit_cast(uint4, *(LDS_AS u32x4*)(lds_base() + off));
+}
+__device__ __forceinline__ void lds_st16(uint32_t off, uint4 v) {
+  *(LDS_AS u32x4*)(lds_base() + off) = __builtin_bit_cast(u32x4, v);
+}
+__device__ __forceinline__ void lds_st8(uint32_t off, uint2 v) {
+  *(LDS_AS u32x2*)(lds_base() + off) = __builtin_bit_cast(u32x2, v);
+}
+__device__ __forceinline__ float lds_ldf(uint32_t off) {
+  return *(LDS_AS float*)(lds_base() + off);
+}
+__device__ __forceinline__ void lds_stf(uint32_t off, float v) {
+  *(LDS_AS float*)(lds_base() + off) = v;
+}
+// ds_read_b64_tr_b16: within each 16-lane group, lane 4q+p supplies the
+// address of row q (columns 4p..4p+3) of a 4-row block; lane i receives
+// column i of the 4 rows, row q in element q.
+__device__ __forceinline__ s16x4 lds_tr4(uint32_t off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(lds_base() + off));
+}
+__device__ __forceinline__ bf16x8 join_tr(s16x4 a, s16x4 b) {
+  s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Bijective XCD-aware remap of a 1-D grid: blocks L and L+8 run on one XCD,
+// so consecutive work indices returned here share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int L, int total) {
+  const int q = total / 8, r = total % 8, x = L % 8, s = L / 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + s;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
+  return v;
+}
+// Reduce over the 32 lanes of each wave half (lanes differing in bits 0..4).
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+// Reduce-scatter of 16 per-lane values over the 32 lanes of a wave half.
+// On return lane lr holds the half-total of index
+//   q(lr) = 8*b4 + 4*b3 + 2*b2 + b1  (bk = bit k of lr)
+// in BOTH lanes lr and lr^1.  16 shuffles instead of 80.
+__device__ __forceinline__ float rs16(const float (&v)[16], int lr) {
+  float w8[8], w4[4], w2[2];
+  bool up = lr & 16;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float send = up ? v[k] : v[k + 8];
+    float keep = up ? v[k + 8] : v[k];
+    w8[k] = keep + __shfl_xor(send, 16);
+  }
+  up = lr & 8;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float send = up ? w8[k] : w8[k + 4];
+    float keep = up ? w8[k + 4] : w8[k];
+    w4[k] = keep + __shfl_xor(send, 8);
+  }
+  up = lr & 4;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    float send = up ? w4[k] : w4[k + 2];
+    float keep = up ? w4[k + 2] : w4[k];
+    w2[k] = keep + __shfl_xor(send, 4);
+  }
+  up = lr & 2;
+  float send = up ? w2[0] : w2[1];
+  float w1 = (up ? w2[1] : w2[0]) + __shfl_xor(send, 2);
+  return w1 + __shfl_xor(w1, 1);
+}
+__device__ __forceinline__ int rs16_index(int lr) {
+  return (((lr >> 4) & 1) << 3) | (((lr >> 3) & 1) << 2) | (((lr >> 2) & 1) << 1) |
+         ((lr >> 1) & 1);
+}
+
+// Row index inside a 32x32 MFMA accumulator tile for register q of wave half h.
+__device__ __forceinline__ constexpr int acc_row(int q, int h) {
+  return (q & 3) + 8 * (q >> 2) + 4 * h;
+}
+
+}  // namespace tgfr

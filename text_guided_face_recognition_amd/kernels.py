@@ -122,3 +122,160 @@ def word_region_logits(img_features, words, lens, gamma1, gamma2, gamma3,
                        mode="fp32", img_offset=0, att_T=0):
     return WordRegionLogits.apply(img_features, words, lens, float(gamma1),
                                   float(gamma2), float(gamma3), mode, img_offset, att_T)
+
+
+# ------------------------------------------------------------ cos logits ---
+class CosLogits(torch.autograd.Function):
+    """scale * cos(x_b, y_i) (or scale * x_b.y_i) for all pairs, optional
+    same-class mask; gradient to x (and to y when it requires grad)."""
+
+    @staticmethod
+    def forward(ctx, x, y, scale, normalize, cls, row_offset, eps=1e-8):
+        x = x.float().contiguous()
+        y = y.float().contiguous()
+        n_x, n_y = x.shape[0], y.shape[0]
+        out = torch.empty(n_x, n_y, dtype=torch.float32, device=x.device)
+        masked = cls is not None
+        if masked:
+            cls = cls.to(device=x.device, dtype=torch.int64).contiguous()
+        call("tgfr_cos_logits", ptr(x), D, ptr(y), D, n_x, n_y, D, int(normalize),
+             float(scale), float(eps), int(masked), ptr(cls), int(row_offset), ptr(out),
+             n_y, _hip.stream())
+        ctx.save_for_backward(x, y)
+        ctx.cfg = (float(scale), int(normalize), float(eps))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        scale, normalize, eps = ctx.cfg
+        g = g.float().contiguous()
+        n_x, n_y = g.shape
+        dx = dy = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            call("tgfr_cos_logits_bwd", ptr(g), n_y, 1, ptr(x), D, ptr(y), D, n_x, n_y,
+                 D, normalize, scale, eps, ptr(dx), D, _hip.stream())
+        if ctx.needs_input_grad[1]:
+            dy = torch.empty_like(y)
+            call("tgfr_cos_logits_bwd", ptr(g), 1, n_y, ptr(y), D, ptr(x), D, n_y, n_x,
+                 D, normalize, scale, eps, ptr(dy), D, _hip.stream())
+        return dx, dy, None, None, None, None, None
+
+
+def cos_logits(x, y, scale, normalize=True, cls=None, row_offset=0):
+    return CosLogits.apply(x, y, scale, normalize, cls, row_offset)
+
+
+# ---------------------------------------------------------- contrastive CE ---
+class ContrastiveCE(torch.autograd.Function):
+    """(CE(rows), CE(columns)) of a [local rows x global columns] logit block.
+
+    Row b of this rank is global row `row_offset + b`, labelled with the
+    caption of the same index.  With a process group, the column partials are
+    exchanged with one all_gather so loss1 sees every rank's rows, exactly as
+    the reference's single-process DataParallel losses do on the gathered
+    batch.  Returned losses are this rank's contributions; summing them over
+    ranks gives the global-batch losses.
+    """
+
+    @staticmethod
+    def forward(ctx, logits, row_offset, n_global, group):
+        logits = logits.float().contiguous()
+        n_r, n_c = logits.shape
+        dev = logits.device
+        row_lse = torch.empty(n_r, dtype=torch.float32, device=dev)
+        part = torch.empty(2, n_c, dtype=torch.float32, device=dev)
+        call("tgfr_ce_stats", ptr(logits), n_c, n_r, n_c, ptr(row_lse), ptr(part[0]),
+             ptr(part[1]), _hip.stream())
+        if group is not None:
+            import torch.distributed as dist
+            allp = [torch.empty_like(part) for _ in range(dist.get_world_size(group))]
+            dist.all_gather(allp, part, group=group)
+            allp = torch.stack(allp)                     # [world, 2, n_c]
+            gmax = allp[:, 0].max(0).values
+            col_lse = gmax + torch.log((allp[:, 1] * torch.exp(allp[:, 0] - gmax)).sum(0))
+        else:
+            col_lse = part[0] + torch.log(part[1])
+        col_lse = col_lse.contiguous()
+        loss = torch.empty(2, dtype=torch.float32, device=dev)
+        inv_n = 1.0 / float(n_global)
+        call("tgfr_ce_loss", ptr(logits), n_c, n_r, int(row_offset), inv_n, ptr(row_lse),
+             ptr(col_lse), ptr(loss), _hip.stream())
+        ctx.save_for_backward(logits, row_lse, col_lse)
+        ctx.cfg = (int(row_offset), inv_n)
+        return loss[0], loss[1]
+
+    @staticmethod
+    def backward(ctx, g0, g1):
+        logits, row_lse, col_lse = ctx.saved_tensors
+        row_offset, inv_n = ctx.cfg
+        n_r, n_c = logits.shape
+        g0 = torch.zeros((), device=logits.device) if g0 is None else g0
+        g1 = torch.zeros((), device=logits.device) if g1 is None else g1
+        gs = torch.stack([g0.float().reshape(()), g1.float().reshape(())]).contiguous()
+        dl = torch.empty_like(logits)
+        call("tgfr_ce_grad", ptr(logits), n_c, n_r, n_c, row_offset, inv_n, ptr(row_lse),
+             ptr(col_lse), ptr(gs), 1.0, 1.0, ptr(dl), n_c, _hip.stream())
+        return dl, None, None, None
+
+
+def contrastive_ce(logits, row_offset=0, n_global=None, group=None):
+    n_global = logits.shape[0] if n_global is None else n_global
+    return ContrastiveCE.apply(logits, row_offset, n_global, group)
+
+
+# ------------------------------------------------------------------ bgemm ---
+def bgemm(a, b, out=None, alpha=1.0, accumulate=False, mode="fp32"):
+    """out[n] = alpha * a[n] @ b[n] (+ out[n]) for 3-D fp32 tensors of any
+    strides (transposed views cost nothing: strides are passed through)."""
+    assert a.dim() == 3 and b.dim() == 3 and a.shape[0] == b.shape[0]
+    assert a.shape[2] == b.shape[1] and a.dtype == b.dtype == torch.float32
+    nb, m, k = a.shape
+    n = b.shape[2]
+    if out is None:
+        out = torch.empty(nb, m, n, dtype=torch.float32, device=a.device)
+    call("tgfr_bgemm", ptr(a), a.stride(0), a.stride(1), a.stride(2), ptr(b), b.stride(0),
+         b.stride(1), b.stride(2), ptr(out), out.stride(0), out.stride(1), out.stride(2),
+         nb, m, n, k, float(alpha), int(accumulate), _mode(mode), _hip.stream())
+    return out
+
+
+class AttentionCore(torch.autograd.Function):
+    """O = softmax(scale * Qr Kr^T) V per sample (fusion_nets.py:103-115).
+
+    qr, kr: [N, HW, C'] (query role = key_proj(x), key role = query_proj(y));
+    v: [N, HW, C].  Returns O [N, HW, C].
+    """
+
+    @staticmethod
+    def forward(ctx, qr, kr, v, scale, mode):
+        qr, kr, v = qr.float(), kr.float(), v.float()
+        nb, hw, _ = qr.shape
+        s = bgemm(qr, kr.transpose(1, 2), mode=mode)
+        p = torch.empty_like(s)
+        call("tgfr_attn_softmax", ptr(s), ptr(p), None, nb * hw, hw, hw, float(scale),
+             _hip.stream())
+        o = bgemm(p, v, mode=mode)
+        ctx.save_for_backward(qr, kr, v, p)
+        ctx.cfg = (float(scale), mode)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qr, kr, v, p = ctx.saved_tensors
+        scale, mode = ctx.cfg
+        do = do.float()
+        nb, hw, _ = qr.shape
+        dp = bgemm(do, v.transpose(1, 2), mode=mode)
+        ds = torch.empty_like(dp)
+        call("tgfr_attn_softmax_bwd", ptr(p), ptr(dp), ptr(ds), nb * hw, hw, hw, scale,
+             _hip.stream())
+        dqr = bgemm(ds, kr, mode=mode)
+        dkr = bgemm(ds.transpose(1, 2), qr, mode=mode)
+        dv = bgemm(p.transpose(1, 2), do, mode=mode)
+        return dqr, dkr, dv, None, None
+
+
+def attention_core(qr, kr, v, scale, mode="fp32"):
+    return AttentionCore.apply(qr, kr, v, scale, mode)

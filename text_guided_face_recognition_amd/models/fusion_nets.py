@@ -1,0 +1,108 @@
+"""Drop-in for the reference's models/fusion_nets.py SelfAttention and
+Working (FCFM).  Parameter names match the reference (query_proj, key_proj,
+value_proj, conv, bn_img, ...), so reference state dicts load unchanged.
+
+The attention core (QK^T, softmax, PV and their backward) runs in the gfx950
+kernels (kernels.AttentionCore); the 1x1 projections are plain GEMMs on a
+channels-last view of the maps, so no NCHW<->NHWC copies are made.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import kernels as K
+
+__all__ = ["SelfAttention", "Working", "conv1x1"]
+
+
+def conv1x1(in_planes, out_planes):
+    return nn.Conv2d(in_planes, out_planes, kernel_size=1, stride=1, padding=0, bias=False)
+
+
+def _cl(x):
+    """[N, C, H, W] (any strides) -> [N, H*W, C] view/copy, channels last."""
+    n, c, h, w = x.shape
+    return x.permute(0, 2, 3, 1).reshape(n, h * w, c)
+
+
+class SelfAttention(nn.Module):
+    """fusion_nets.py:82-118.
+
+    forward(x, y): query role = key_proj(x), key role = query_proj(y),
+    value = value_proj(x); softmax over y's positions; output [N, C, H, W]
+    (returned as a channels-last strided view).
+    """
+
+    def __init__(self, channel_dim, scale=2):
+        super().__init__()
+        self.inplanes = channel_dim
+        self.query_proj = nn.Conv2d(self.inplanes, self.inplanes // scale, 1)
+        self.key_proj = nn.Conv2d(self.inplanes, self.inplanes // scale, 1)
+        self.value_proj = nn.Conv2d(self.inplanes, self.inplanes, 1)
+        self.sqrt_dim = np.sqrt(channel_dim / scale)
+        self.precision = "fp32"
+
+    def _w(self, conv):
+        return conv.weight.reshape(conv.weight.shape[0], -1)
+
+    def forward_cl(self, x_cl, y_cl):
+        """Channels-last core: x_cl, y_cl [N, HW, C] -> [N, HW, C]."""
+        if y_cl is x_cl:
+            w = torch.cat([self._w(self.key_proj), self._w(self.query_proj),
+                           self._w(self.value_proj)], 0)
+            b = torch.cat([self.key_proj.bias, self.query_proj.bias, self.value_proj.bias])
+            proj = F.linear(x_cl, w, b)
+            cq = self.key_proj.weight.shape[0]
+            qr, kr, v = proj[..., :cq], proj[..., cq:2 * cq], proj[..., 2 * cq:]
+        else:
+            qr = F.linear(x_cl, self._w(self.key_proj), self.key_proj.bias)
+            kr = F.linear(y_cl, self._w(self.query_proj), self.query_proj.bias)
+            v = F.linear(x_cl, self._w(self.value_proj), self.value_proj.bias)
+        return K.attention_core(qr, kr, v, 1.0 / float(self.sqrt_dim), self.precision)
+
+    def forward(self, x, y):
+        n, c, h, w = y.shape
+        assert x.shape[2] * x.shape[3] == h * w, "x and y need the same H*W (:105)"
+        x_cl = _cl(x)
+        y_cl = x_cl if y is x else _cl(y)
+        o = self.forward_cl(x_cl, y_cl)
+        return o.reshape(n, h, w, c).permute(0, 3, 1, 2)
+
+
+class Working(nn.Module):
+    """fusion_nets.py:217-258 (FCFM).  The channel_dim argument is ignored
+    exactly as in the reference (:220)."""
+
+    def __init__(self, channel_dim):
+        super().__init__()
+        channel_dim = 36
+        self.bn_img = nn.BatchNorm2d(channel_dim)
+        self.bn_word = nn.BatchNorm2d(channel_dim)
+        self.projection = nn.Linear(256, channel_dim)
+        self.sa = SelfAttention(channel_dim, scale=1)
+        self.maxpool = nn.MaxPool2d(kernel_size=2)
+        self.conv = nn.Conv2d(256, channel_dim, kernel_size=(3, 3), padding=0)
+        self.relu = nn.ReLU()
+        self.ln = nn.LayerNorm([channel_dim, 6, 6])
+        self.ln_gl_image = nn.LayerNorm([256])
+        self.ln_sent = nn.LayerNorm([256])
+        self.linear = nn.Linear(324, 128)
+
+    def forward(self, img, word, gl_img, sent):
+        img = self.maxpool(self.relu(self.conv(img)))
+        img = self.bn_img(img)
+        word = self.projection(word.transpose(1, 2))
+        word = torch.bmm(word.transpose(1, 2), word) / np.sqrt(36)
+        word = word.unsqueeze(-1).view(word.size(0), word.size(1), 6, 6)
+        word = self.bn_word(word)
+        iw = self.sa(img, word)
+        iw = self.ln(iw)
+        iw = self.maxpool(iw)
+        iw = iw.reshape(iw.size(0), -1)
+        iw = self.linear(iw)
+        gl_img = self.ln_gl_image(gl_img)
+        sent = self.ln_sent(sent)
+        return torch.concat((iw, gl_img, sent), dim=1)

@@ -1,0 +1,142 @@
+"""Drop-in for the reference's models/losses.py hot-path functions.
+
+Same names, signatures and return values as the reference; the arithmetic
+runs in the gfx950 kernels of libtgfr_hip.so (see kernels.py):
+
+  words_loss   models/losses.py:61-135   fused word<->region kernel + CE kernel
+  sent_loss    models/losses.py:19-57    cosine-logit kernel (class mask) + CE
+  global_loss  models/losses.py:329-351  cosine-logit kernel + CE
+  ClipLoss     models/losses.py:268-309  dot-product logits + CE
+  FocalLoss    models/losses.py:313-325  identity head, plain PyTorch (out of scope)
+
+Extra knobs ride on ``args`` so the call sites stay identical:
+  args.precision   "fp32" (split-bf16 MFMA, parity mode; default) or "bf16"
+  args.dist        a DistContext (see dist.py) when running one process per
+                   GPU: inputs are this rank's images, text features are the
+                   all-gathered global batch, and the returned losses are this
+                   rank's contributions (sum over ranks = the global loss).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import kernels as K
+
+__all__ = ["cosine_similarity", "sent_loss", "words_loss", "global_loss", "ClipLoss",
+           "FocalLoss"]
+
+
+def _precision(args):
+    return getattr(args, "precision", "fp32")
+
+
+def _dist(args):
+    ctx = getattr(args, "dist", None)
+    if ctx is None or not ctx.active:
+        return 0, None, None
+    return ctx.row_offset, ctx.n_global, ctx.group
+
+
+def cosine_similarity(x1, x2, dim=1, eps=1e-8):
+    """losses.py:12-16 (the clamp is on the product of the norms)."""
+    w12 = torch.sum(x1 * x2, dim)
+    w1 = torch.norm(x1, 2, dim)
+    w2 = torch.norm(x2, 2, dim)
+    return (w12 / (w1 * w2).clamp(min=eps)).squeeze()
+
+
+def _class_tensor(class_ids, device):
+    if class_ids is None:
+        return None
+    if isinstance(class_ids, np.ndarray):
+        class_ids = torch.from_numpy(class_ids)
+    return torch.as_tensor(class_ids).to(device=device, dtype=torch.int64)
+
+
+def sent_loss(cnn_code, rnn_code, labels, class_ids, batch_size, args, eps=1e-8):
+    """losses.py:19-57: gamma3-scaled cosine logits, same-class off-diagonal
+    entries masked to -inf, CE over rows and over columns."""
+    row_offset, n_global, group = _dist(args)
+    cls = _class_tensor(class_ids, cnn_code.device)
+    logits = K.cos_logits(cnn_code, rnn_code, args.TRAIN.SMOOTH.GAMMA3, True, cls,
+                          row_offset)
+    if labels is None:
+        return None, None
+    return K.contrastive_ce(logits, row_offset, n_global or logits.shape[0], group)
+
+
+def words_loss(img_features, words_emb, labels, cap_lens, class_ids, batch_size, args):
+    """losses.py:61-135 -> (loss0, loss1, att_maps).
+
+    img_features [B, 256, 14, 14] (any strides); words_emb [B_cap, 256, T'].
+    BERT: every caption uses bert_words_num - 2 words (:83); LSTM: cap_lens[i]
+    (:82).  att_maps are the matching-pair maps [1, T, 14, 14] (:97), produced
+    by the forward kernel.
+    """
+    b_img = img_features.shape[0]
+    b_cap = words_emb.shape[0]
+    if args.en_type == "BERT":
+        n_words = args.bert_words_num - 2
+        lens = torch.full((b_cap,), n_words, dtype=torch.int32)
+    else:
+        lens = torch.as_tensor(cap_lens).to(torch.int32)
+        n_words = int(lens.max())
+    words = K.words_view(words_emb, n_words)
+    row_offset, n_global, group = _dist(args)
+    smooth = args.TRAIN.SMOOTH
+    want_maps = getattr(args, "return_att_maps", True)
+    out = K.word_region_logits(img_features, words, lens, smooth.GAMMA1, smooth.GAMMA2,
+                               smooth.GAMMA3, mode=_precision(args), img_offset=row_offset,
+                               att_T=n_words if want_maps else 0)
+    logits, att = (out if want_maps else (out, None))
+    att_maps = []
+    if att is not None:
+        lens_l = lens.tolist()
+        for b in range(b_img):
+            t = lens_l[row_offset + b] if row_offset + b < b_cap else n_words
+            att_maps.append(att[b, :t].reshape(1, t, 14, 14))
+    if labels is None:
+        return None, None, att_maps
+    loss0, loss1 = K.contrastive_ce(logits, row_offset, n_global or b_img, group)
+    return loss0, loss1, att_maps
+
+
+def global_loss(cnn_code, rnn_code, eps=1e-8, temp3=10.0, args=None):
+    """losses.py:329-351 -> loss0 + loss1 (labels are arange(batch))."""
+    row_offset, n_global, group = _dist(args)
+    logits = K.cos_logits(cnn_code, rnn_code, temp3, True, None, row_offset)
+    l0, l1 = K.contrastive_ce(logits, row_offset, n_global or logits.shape[0], group)
+    return l0 + l1
+
+
+class ClipLoss(nn.Module):
+    """losses.py:268-309: un-normalised logits, mean of the two CEs."""
+
+    def __init__(self, cache_labels=False):
+        super().__init__()
+        self.cache_labels = cache_labels
+
+    def forward(self, text_features, image_features, args, logit_scale=1):
+        row_offset, n_global, group = _dist(args)
+        logits = K.cos_logits(image_features, text_features, float(logit_scale), False,
+                              None, row_offset)
+        l0, l1 = K.contrastive_ce(logits, row_offset, n_global or logits.shape[0], group)
+        return (l0 + l1) / 2
+
+
+class FocalLoss(nn.Module):
+    """losses.py:313-325 (identity head; stays PyTorch)."""
+
+    def __init__(self, gamma=0, eps=1e-7):
+        super().__init__()
+        self.gamma = gamma
+        self.eps = eps
+        self.ce = nn.CrossEntropyLoss()
+
+    def forward(self, input, target):
+        logp = self.ce(input, target)
+        p = torch.exp(-logp)
+        return ((1 - p) ** self.gamma * logp).mean()

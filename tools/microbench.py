@@ -1,0 +1,43 @@
+"""Time the word-region kernels at BASELINE config 2 (B=64, T=30) with HIP events."""
+import sys
+import torch
+import torch.nn.functional as F
+sys.path.insert(0, ".")
+from text_guided_face_recognition_amd import kernels as K
+
+
+def unit(x):
+    return x / x.norm(dim=-1, keepdim=True)
+
+
+def main(b=64, nw=30, mode="fp32", iters=20):
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    r = unit(torch.randn(b, 14, 14, 256, device=dev)).permute(0, 3, 1, 2).requires_grad_()
+    w = unit(torch.randn(b, nw, 256, device=dev))
+    lens = torch.full((b,), nw, dtype=torch.int32, device=dev)
+    labels = torch.arange(b, device=dev)
+
+    def step():
+        logits = K.word_region_logits(r, w, lens, 4.0, 5.0, 10.0, mode=mode)
+        loss = F.cross_entropy(logits, labels) + F.cross_entropy(logits.t(), labels)
+        loss.backward()
+        return loss
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        step()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    flop = 10 * 196 * 256 * nw * b * b
+    print(f"mode={mode} B={b} T={nw}: {ms:.3f} ms/step  {flop / ms / 1e9:.1f} TFLOP/s algorithmic")
+
+
+if __name__ == "__main__":
+    for mode in ("fp32", "bf16"):
+        main(mode=mode)
+        main(b=256, mode=mode)

@@ -1,0 +1,256 @@
+"""Benchmark: face-caption pairs/s of the TGFR stage-1 train step (hot path).
+
+    python bench.py [--gpus N --steps K --warmup W --precision bf16|fp32]
+
+For N > 1 the driver launches one process per GPU with torch.distributed.run
+(RCCL over xGMI); rank r owns images [r*B, (r+1)*B) and all-gathers the text
+side, so each rank's contrastive losses see the whole global batch
+(weak scaling: B = 64 images per GPU).
+
+A step is one pass of the hot path over one batch of synthetic frozen-encoder
+outputs already resident in HBM (BASELINE.json configs[1]: iResNet-100 +
+BERT-base features, bs = 64/GPU, 32-token captions -> 30 words): the image
+head (IMIM self-attention), words_loss, sent_loss, global_loss, the two
+ArcMargin/focal identity losses, backward, and both optimiser steps
+(src/train_encoders_bert.py:254-331).  The frozen encoders run under
+torch.no_grad in the reference and are not part of the measured step.
+
+Output: ONE JSON line on rank 0 with the driver's fields plus
+  roofline      dominant HIP kernel: algorithmic FLOPs per launch / its average
+                duration (HIP events on the launch stream, second timed pass)
+  cpu_baseline  the CPU oracle (oracle/tgfr_oracle.py) timed on the host cores
+                for a bounded number of steps of the same workload (rank 0, N=1)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+R, D = 196, 256
+PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=64, help="images per GPU")
+    p.add_argument("--words", type=int, default=32, help="bert_words_num (T = words-2)")
+    p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--alt-precision", default="fp32",
+                   help="also time this precision mode ('' to skip)")
+    p.add_argument("--cpu-steps", type=int, default=6)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--eager", action="store_true",
+                   help="launch kernels one by one instead of replaying a HIP graph")
+    return p.parse_args()
+
+
+def sync_barrier(ctx):
+    torch.cuda.synchronize()
+    if ctx.active:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def run_steps(trainer, batch, n):
+    out = None
+    for _ in range(n):
+        out = trainer.step(batch)
+    return out
+
+
+def time_steps(trainer, batch, ctx, steps, warmup):
+    run_steps(trainer, batch, warmup)
+    sync_barrier(ctx)
+    t0 = time.perf_counter()
+    out = run_steps(trainer, batch, steps)
+    sync_barrier(ctx)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+    if ctx.active:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item(), out
+
+
+def kernel_profile(trainer, batch, steps):
+    from text_guided_face_recognition_amd._hip import KernelTimer
+    with KernelTimer() as kt:
+        run_steps(trainer, batch, steps)
+    return kt.summary()
+
+
+def cpu_baseline(args, n_words):
+    """The CPU oracle restatement of the same step on the host cores."""
+    from oracle import tgfr_oracle as O
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
+    torch.set_num_threads(threads)
+    b = args.batch
+    gen = torch.Generator().manual_seed(100)
+    unit = lambda x: x / x.norm(dim=-1, keepdim=True)  # noqa: E731
+    g = torch.randn(b, 512, generator=gen)
+    local = torch.randn(b, 256, 14, 14, generator=gen)
+    words = unit(torch.randn(b, n_words, 256, generator=gen)).transpose(1, 2)
+    sent = unit(torch.randn(b, 256, generator=gen))
+    cls = torch.randint(0, 10000, (b,), generator=gen)
+    p = {}
+
+    def lin(o, i):
+        w = torch.empty(o, i)
+        torch.nn.init.kaiming_uniform_(w, a=5 ** 0.5)
+        return w.requires_grad_(), torch.zeros(o).requires_grad_()
+    p["q_w"], p["q_b"] = lin(256, 256)
+    p["k_w"], p["k_b"] = lin(256, 256)
+    p["v_w"], p["v_b"] = lin(256, 256)
+    for k in ("q_w", "k_w", "v_w"):
+        p[k] = p[k].detach().reshape(256, 256, 1, 1).requires_grad_()
+    hp = {"sa_" + k: v for k, v in p.items()}
+    hp["bn_w"], hp["bn_b"] = torch.ones(256).requires_grad_(), torch.zeros(256).requires_grad_()
+    hp["ln_w"] = torch.ones(256, 14, 14).requires_grad_()
+    hp["ln_b"] = torch.zeros(256, 14, 14).requires_grad_()
+    w1, hp["c1_b"] = lin(128, 256)
+    w2, hp["c2_b"] = lin(256, 128)
+    hp["c1_w"] = w1.detach().reshape(128, 256, 1, 1).requires_grad_()
+    hp["c2_w"] = w2.detach().reshape(256, 128, 1, 1).requires_grad_()
+    hp["pl_w"], hp["pl_b"] = lin(256, 256)
+    hp["pg_w"], hp["pg_b"] = lin(256, 512)
+    arc_i = torch.empty(4500, 256)
+    torch.nn.init.xavier_uniform_(arc_i)
+    arc_t = arc_i.clone()
+    arc_i.requires_grad_()
+    arc_t.requires_grad_()
+    opt_h = torch.optim.Adam(list(hp.values()), lr=1e-3, betas=(0.5, 0.999))
+    opt_c = torch.optim.SGD([arc_i, arc_t], lr=0.1, momentum=0.9, weight_decay=5e-5)
+    labels = torch.arange(b)
+    cls_np = cls.numpy()
+    cls_ids = cls % 4500
+
+    def step():
+        gp, r = O.image_heading(g, local, hp)
+        opt_h.zero_grad()
+        opt_c.zero_grad()
+        w0, w1_, _, _ = O.words_loss(r, words, labels, None, n_words, 4.0, 5.0, 10.0)
+        s0, s1, _ = O.sent_loss(gp, sent, labels, cls_np, 10.0)
+        tid = O.focal_loss(O.arc_margin(sent, arc_t, cls_ids, s=35), cls_ids)
+        iid = O.focal_loss(O.arc_margin(gp, arc_i, cls_ids, s=30), cls_ids)
+        cl, _ = O.global_loss(gp, sent)
+        total = w0 + w1_ + s0 + s1 + 100 * (tid + iid) + 2.0 * cl
+        total.backward()
+        opt_h.step()
+        opt_c.step()
+
+    step()                                   # warm-up
+    times = []
+    for _ in range(args.cpu_steps):
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    med = times[len(times) // 2]
+    return {"value": round(b / med, 3), "unit": "pairs/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{args.cpu_steps} steps (+1 warm-up) of the same bs={b}, T={n_words} "
+                      f"stage-1 step through the fp32 oracle; median step "
+                      f"{med * 1000:.0f} ms"}
+
+
+def main():
+    args = parse()
+    from text_guided_face_recognition_amd.config import make_args
+    from text_guided_face_recognition_amd.dist import init_from_env
+    from text_guided_face_recognition_amd.train import GraphedStep, Train, synthetic_batch
+
+    ctx = init_from_env()
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    n_words = args.words - 2
+
+    def build(precision):
+        torch.manual_seed(100)
+        targs = make_args(batch_size=args.batch, bert_words_num=args.words,
+                          num_classes=4500, precision=precision)
+        return Train(targs, dev, ctx)
+
+    batch = synthetic_batch(args.batch, n_words, dev, seed=100 + 1000 * ctx.rank)
+    batch = batch[:4] + (batch[4] % 4500,)
+
+    use_graph = not args.eager and not ctx.active
+
+    def runner(tr):
+        return GraphedStep(tr, batch) if use_graph else tr
+
+    trainer = build(args.precision)
+    prof = kernel_profile(trainer, batch, max(3, min(args.steps, 10)))
+    elapsed, out = time_steps(runner(trainer), batch, ctx, args.steps, args.warmup)
+    n = ctx.world
+    pairs = n * args.batch * args.steps
+    value = pairs / elapsed
+
+    alt = None
+    if args.alt_precision and args.alt_precision != args.precision:
+        tr2 = build(args.alt_precision)
+        prof2 = kernel_profile(tr2, batch, max(3, min(args.steps, 10)))
+        e2, _ = time_steps(runner(tr2), batch, ctx, args.steps, args.warmup)
+        alt = {"precision": args.alt_precision, "value": round(pairs / e2, 2),
+               "ms_per_step": round(e2 / args.steps * 1000, 4),
+               "kernels_ms": {k: round(v[1], 4) for k, v in prof2.items()}}
+
+    if ctx.rank != 0:
+        if ctx.active:
+            dist.barrier()
+        return
+
+    # roofline of the dominant word<->region kernel (SURVEY.md 8(d):
+    # fwd 4*R*D*T and bwd 6*R*D*T FLOPs per (image, caption) pair)
+    pair_count = args.batch * args.batch * n
+    flops = {"tgfr_wr_fwd": 4 * R * D * n_words * pair_count,
+             "tgfr_wr_bwd": 6 * R * D * n_words * pair_count}
+    dominant = max((k for k in prof if k in flops), key=lambda k: prof[k][1])
+    dom_ms = prof[dominant][1]
+    achieved = flops[dominant] / (dom_ms * 1e-3) / 1e12
+    roofline = {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 2),
+                "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "avg_launch_ms": round(dom_ms, 4),
+                "flop_per_launch": flops[dominant]}
+
+    cpu = None
+    if not args.no_cpu and n == 1:
+        cpu = cpu_baseline(args, n_words)
+
+    line = {
+        "metric": "face-caption pairs/sec train step (iResNet100+BERT, bs=64/GPU) "
+                  "at 1/2/4/8 MI355X",
+        "value": round(value, 2), "unit": "pairs/s", "n_gpus": n, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": args.precision, "data": "synthetic",
+        "config": {"workload": "FCAM stage-1 train step (BASELINE configs[1]): IMIM head + "
+                               "words/sent/global losses + identity heads + backward + "
+                               "optimiser, on iResNet-100/BERT-base-shaped frozen features",
+                   "global_batch": args.batch * n, "seq_len": args.words,
+                   "words_per_caption": n_words, "parallelism": f"dp{n}",
+                   "launch": "hip-graph" if use_graph else "eager"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "kernels_ms": {k: round(v[1], 4) for k, v in sorted(prof.items())},
+        "alt_precision": alt,
+    }
+    print(json.dumps(line), flush=True)
+    if ctx.active:
+        dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

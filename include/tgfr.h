@@ -1,0 +1,130 @@
+/* tgfr.h -- C ABI of libtgfr_hip.so, the MI355X (gfx950) kernels of the TGFR
+ * FCAM/FCFM training hot path.
+ *
+ * The reference (Mahedi-61/Text_Guided_Face_Recognition) is pure Python with
+ * no FFI layer; its boundary for this path is the Python call surface of
+ * models/losses.py, models/attention.py and models/fusion_nets.py.  Each entry
+ * point below replaces the arithmetic behind one of those calls (cited per
+ * function).  The Python mirror in text_guided_face_recognition_amd/models
+ * keeps the reference signatures and binds these with ctypes
+ * (text_guided_face_recognition_amd/_hip.py).
+ *
+ * Conventions
+ *   - All pointers are device pointers owned by the caller; all buffers and
+ *     workspaces are allocated by the caller.  Strides are in elements.
+ *   - `stream` is a hipStream_t passed as void*; every call only enqueues
+ *     work on it (no host synchronisation, no allocation) so calls can be
+ *     captured into a HIP graph.
+ *   - Return 0 on success, a hipError_t from the launch, or
+ *     1001 (bad shape/argument) / 1002 (bad precision mode).
+ *   - mode: 0 = bf16 MFMA operands, 1 = fp32 operands carried as bf16 hi/lo
+ *     pairs (three MFMAs per product; the fp32-parity mode).
+ *   - bf16 buffers are uint16_t bit patterns.
+ *   - Feature dim D is 256 (aux_feat_dim_per_granularity, cfg/train_bert.yml:28);
+ *     regions R = 196 (14x14, padded to 224 in the split images); words per
+ *     caption T <= 32.
+ */
+#ifndef TGFR_H
+#define TGFR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ABI version (major*100 + minor). */
+int tgfr_version(void);
+
+/* fp32 rows (element (item,row,col) at x[item*s_item + row*s_row + col*s_col])
+ * -> bf16 hi/lo [n_items][rows_pad][256] with rows >= min(n_rows, lens[item])
+ * zeroed, plus optional fp32 row L2 norms [n_items][rows_pad].  Feeds the
+ * word<->region kernels with R (image regions, models/models.py:401-404) and
+ * W (words, models/models.py:231). */
+int tgfr_prep_rows(const float* x, long long s_item, long long s_row, long long s_col,
+                   int n_items, int n_rows, int n_cols, int rows_pad, const int* lens,
+                   uint16_t* hi, uint16_t* lo, float* norms, void* stream);
+
+/* Forward of words_loss's similarity matrix for all (image b, caption i) pairs:
+ * replaces the per-caption loop of models/losses.py:73-122 together with
+ * func_attention (models/attention.py:10-43):
+ *   logits[b*ld + i] = gamma3 * log sum_{t<lens[i]} exp(gamma2 * cos_t)
+ * Also writes per-token stats [B_img][B_cap][32] float4 {Z_t, n_t, |C_t|, cos_t}
+ * and C [B_img][B_cap][32][256] fp32 (the weighted context, attention.py:41)
+ * for the backward; att (nullable) receives A2 [b][t][196] for the matching
+ * pair i == b + img_offset (the att_maps of losses.py:97). */
+int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
+                const uint16_t* Wlo, const float* Wnorm, const int* lens, int B_img, int B_cap,
+                int img_offset, float gamma1, float gamma2, float gamma3, float eps,
+                float* logits, int ld_logits, float* stats, float* Cout, float* att,
+                int att_T, int mode, void* stream);
+
+/* Backward of tgfr_wr_fwd w.r.t. the image regions given dL/dlogits: writes
+ * n_chunks partial slabs [n_chunks][B_img][224][256] (one per caption chunk);
+ * the text side is detached in the reference (utils/dataset_utils.py:42). */
+int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
+                const uint16_t* Wlo, const float* Wnorm, const int* lens, int B_img, int B_cap,
+                int n_chunks, float gamma1, float gamma2, float gamma3, float eps,
+                const float* dlogits, int ld, const float* stats, const float* Cbuf,
+                float* slab, int mode, void* stream);
+
+/* dR[b][r][d] (caller strides; r < 196) = (+)= sum over chunks of the slabs. */
+int tgfr_wr_reduce(const float* slab, int n_chunks, int B_img, float* out, long long s_b,
+                   long long s_r, long long s_d, int accumulate, void* stream);
+
+/* Dynamic LDS bytes of the forward (which = 0) / backward (1) kernels. */
+int tgfr_wr_lds_bytes(int which);
+
+/* logits[b*ldo + i] = scale * x_b.y_i / max(|x_b||y_i|, eps) (normalize = 1;
+ * sent_loss models/losses.py:38-43, global_loss :338-343) or scale * x_b.y_i
+ * (normalize = 0; ClipLoss :292-296).  masked = 1 applies the same-class
+ * off-diagonal -inf mask of sent_loss (:21-30, :48) with global class ids
+ * cls[] and this rank's first global row row_offset. */
+int tgfr_cos_logits(const float* x, long long ldx, const float* y, long long ldy, int n_x,
+                    int n_y, int d, int normalize, float scale, float eps, int masked,
+                    const long long* cls, int row_offset, float* out, long long ldo,
+                    void* stream);
+
+/* dx_b = sum_i g[b*gs0 + i*gs1] d logits[b][i] / d x_b for tgfr_cos_logits
+ * (swap x/y and the g strides for dy). */
+int tgfr_cos_logits_bwd(const float* g, long long gs0, long long gs1, const float* x,
+                        long long ldx, const float* y, long long ldy, int n_x, int n_y, int d,
+                        int normalize, float scale, float eps, float* dx, long long lddx,
+                        void* stream);
+
+/* Row log-sum-exp and column (max, sum exp) partials of a [n_r x n_c] block. */
+int tgfr_ce_stats(const float* L, long long ld, int n_r, int n_c, float* row_lse,
+                  float* col_max, float* col_sum, void* stream);
+
+/* loss[0] = inv_n * sum_b (row_lse[b] - L[b][b+off]), loss[1] = inv_n * sum_b
+ * (col_lse[b+off] - L[b][b+off]): this rank's share of nn.CrossEntropyLoss on
+ * the rows and on the transposed matrix (models/losses.py:52-53, 131-132). */
+int tgfr_ce_loss(const float* L, long long ld, int n_r, int row_offset, float inv_n,
+                 const float* row_lse, const float* col_lse, float* loss, void* stream);
+
+/* dL = w0*g0*inv_n (softmax_row - onehot) + w1*g1*inv_n (softmax_col - onehot),
+ * with g0 = gscale[0], g1 = gscale[1] read on the device (nullable: 1). */
+int tgfr_ce_grad(const float* L, long long ld, int n_r, int n_c, int row_offset, float inv_n,
+                 const float* row_lse, const float* col_lse, const float* gscale, float w0,
+                 float w1, float* dL, long long ldd, void* stream);
+
+/* Batched C[b] = alpha * A[b] B[b] (+ C[b] when accumulate) with arbitrary
+ * element strides: the QK^T and PV products of SelfAttention
+ * (models/fusion_nets.py:103, :115) and their backward. */
+int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, const float* B,
+               long long sBb, long long sBk, long long sBn, float* C, long long sCb,
+               long long sCm, long long sCn, int batch, int M, int N, int K, float alpha,
+               int accumulate, int mode, void* stream);
+
+/* P = softmax(scale * S) per row (models/fusion_nets.py:103-106), optional LSE. */
+int tgfr_attn_softmax(const float* S, float* P, float* lse, long long rows, int n, long long ld,
+                      float scale, void* stream);
+
+/* dS = scale * P * (dP - rowsum(P * dP)). */
+int tgfr_attn_softmax_bwd(const float* P, const float* dP, float* dS, long long rows, int n,
+                          long long ld, float scale, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TGFR_H */

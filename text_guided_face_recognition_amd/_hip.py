@@ -64,8 +64,45 @@ def exported_symbols():
     return [n for n in SIGNATURES if getattr(lib(), n, None) is not None]
 
 
+class KernelTimer:
+    """Brackets every library call with HIP events on torch's current stream
+    (the stream the kernels are launched on) while active."""
+
+    active = None
+
+    def __init__(self):
+        self.events = {}
+
+    def __enter__(self):
+        KernelTimer.active = self
+        return self
+
+    def __exit__(self, *exc):
+        KernelTimer.active = None
+
+    def record(self, name, fn):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        rc = fn()
+        e.record()
+        self.events.setdefault(name, []).append((s, e))
+        return rc
+
+    def summary(self):
+        """name -> (calls, average ms); synchronises."""
+        torch.cuda.synchronize()
+        out = {}
+        for name, evs in self.events.items():
+            ms = [s.elapsed_time(e) for s, e in evs]
+            out[name] = (len(ms), sum(ms) / len(ms))
+        return out
+
+
 def call(name, *args):
-    rc = getattr(lib(), name)(*args)
+    fn = getattr(lib(), name)
+    timer = KernelTimer.active
+    rc = timer.record(name, lambda: fn(*args)) if timer else fn(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed with code {rc}")
 

@@ -660,4 +660,6 @@ int tgfr_wr_reduce(const float* slab, int n_chunks, int B_img, float* out, long 
 
 int tgfr_wr_lds_bytes(int which) { return which == 0 ? F_LDS : B_LDS; }
 
+int tgfr_version(void) { return 100; }
+
 }  // extern "C"

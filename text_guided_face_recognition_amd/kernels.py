@@ -168,6 +168,24 @@ def cos_logits(x, y, scale, normalize=True, cls=None, row_offset=0):
 
 
 # ---------------------------------------------------------- contrastive CE ---
+def combine_col_partials(parts):
+    """[world, 2, n_c] per-rank (column max, sum exp(x - max)) -> global column
+    log-sum-exp [n_c]."""
+    gmax = parts[:, 0].max(0).values
+    return (gmax + torch.log((parts[:, 1] * torch.exp(parts[:, 0] - gmax)).sum(0))).contiguous()
+
+
+def exchange_col_partials(part, group):
+    """The one collective of the contrastive CE: all_gather of [2, n_c] partials."""
+    if group is None:
+        return combine_col_partials(part.unsqueeze(0))
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    allp = torch.empty((world,) + tuple(part.shape), dtype=part.dtype, device=part.device)
+    dist.all_gather_into_tensor(allp, part.contiguous(), group=group)
+    return combine_col_partials(allp)
+
+
 class ContrastiveCE(torch.autograd.Function):
     """(CE(rows), CE(columns)) of a [local rows x global columns] logit block.
 
@@ -188,16 +206,7 @@ class ContrastiveCE(torch.autograd.Function):
         part = torch.empty(2, n_c, dtype=torch.float32, device=dev)
         call("tgfr_ce_stats", ptr(logits), n_c, n_r, n_c, ptr(row_lse), ptr(part[0]),
              ptr(part[1]), _hip.stream())
-        if group is not None:
-            import torch.distributed as dist
-            allp = [torch.empty_like(part) for _ in range(dist.get_world_size(group))]
-            dist.all_gather(allp, part, group=group)
-            allp = torch.stack(allp)                     # [world, 2, n_c]
-            gmax = allp[:, 0].max(0).values
-            col_lse = gmax + torch.log((allp[:, 1] * torch.exp(allp[:, 0] - gmax)).sum(0))
-        else:
-            col_lse = part[0] + torch.log(part[1])
-        col_lse = col_lse.contiguous()
+        col_lse = exchange_col_partials(part, group)
         loss = torch.empty(2, dtype=torch.float32, device=dev)
         inv_n = 1.0 / float(n_global)
         call("tgfr_ce_loss", ptr(logits), n_c, n_r, int(row_offset), inv_n, ptr(row_lse),

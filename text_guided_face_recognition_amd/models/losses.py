@@ -68,6 +68,18 @@ def sent_loss(cnn_code, rnn_code, labels, class_ids, batch_size, args, eps=1e-8)
     return K.contrastive_ce(logits, row_offset, n_global or logits.shape[0], group)
 
 
+_LENS = {}
+
+
+def _const_lens(n, n_words, device):
+    """Device-resident per-caption word counts for the BERT path (cached, so a
+    step issues no host->device copy and can be graph-captured)."""
+    key = (n, n_words, str(device))
+    if key not in _LENS:
+        _LENS[key] = torch.full((n,), n_words, dtype=torch.int32, device=device)
+    return _LENS[key]
+
+
 def words_loss(img_features, words_emb, labels, cap_lens, class_ids, batch_size, args):
     """losses.py:61-135 -> (loss0, loss1, att_maps).
 
@@ -80,10 +92,11 @@ def words_loss(img_features, words_emb, labels, cap_lens, class_ids, batch_size,
     b_cap = words_emb.shape[0]
     if args.en_type == "BERT":
         n_words = args.bert_words_num - 2
-        lens = torch.full((b_cap,), n_words, dtype=torch.int32)
+        lens = _const_lens(b_cap, n_words, img_features.device)
     else:
         lens = torch.as_tensor(cap_lens).to(torch.int32)
         n_words = int(lens.max())
+        lens = lens.to(img_features.device)
     words = K.words_view(words_emb, n_words)
     row_offset, n_global, group = _dist(args)
     smooth = args.TRAIN.SMOOTH

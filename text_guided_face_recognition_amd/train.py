@@ -1,0 +1,177 @@
+"""Train-step mirrors of the reference trainers, on frozen-encoder features.
+
+  Train   src/train_encoders_bert.py:233-331 (stage 1, FCAM): image head (IMIM)
+          -> words_loss + sent_loss (DAMSM) + 2 ArcMargin/focal identity
+          losses + global_loss (CLIP term) -> backward -> optimiser steps.
+  Fusion  src/fusion_bert.py:195-243 (stage 2, FCFM): image head -> Working
+          -> ArcMargin(640) -> focal loss -> backward -> optimiser steps.
+
+The frozen encoders of the reference (iResNet, BERT + TextHeading under
+no_grad, utils/dataset_utils.py:38-46) are outside the hot path: a step takes
+their outputs (global [B,512], layer3 map [B,256,14,14], words [B,256,T],
+sentence [B,256], class ids) as device tensors.  ``synthetic_batch`` makes
+them with the shapes and statistics SURVEY.md 8(d) prescribes.
+
+One process per GPU: pass a DistContext; text features and class ids are
+all-gathered so every contrastive denominator sees the global batch, the
+contrastive losses are this rank's contributions (scaled by the world size
+before backward so DDP's gradient mean equals the global-batch gradient), and
+the identity losses are per-rank means (DDP's mean is the global mean).
+"""
+from __future__ import annotations
+
+import torch
+from torch.nn.parallel import DistributedDataParallel as DDP
+
+from .dist import DistContext
+from .models.fusion_nets import Working
+from .models.losses import FocalLoss, global_loss, sent_loss, words_loss
+from .models.metrics import ArcMarginProduct
+from .models.models import ImageHeading
+
+
+def _unit(x, dim=-1):
+    return x / x.norm(dim=dim, keepdim=True)
+
+
+def synthetic_batch(b, n_words, device, seed, n_ids=10000):
+    """Frozen-encoder outputs for one batch."""
+    gen = torch.Generator(device="cpu").manual_seed(seed)
+    g = torch.randn(b, 512, generator=gen)
+    local = torch.randn(b, 256, 14, 14, generator=gen)
+    words = _unit(torch.randn(b, n_words, 256, generator=gen))     # [B, T, 256] storage
+    sent = _unit(torch.randn(b, 256, generator=gen))
+    cls = torch.randint(0, n_ids, (b,), generator=gen)
+    to = dict(device=device)
+    return (g.to(**to), local.to(**to), words.to(**to).transpose(1, 2), sent.to(**to),
+            cls.to(**to))
+
+
+def _ddp(m, ctx):
+    if not ctx.active:
+        return m
+    dev = next(m.parameters()).device
+    ids = [dev.index] if dev.type == "cuda" else None
+    return DDP(m, device_ids=ids)
+
+
+class Train:
+    """Stage-1 BERT trainer step (src/train_encoders_bert.py)."""
+
+    def __init__(self, args, device, ctx=None):
+        self.args = args
+        self.ctx = ctx or DistContext()
+        args.return_att_maps = False
+        self.image_head = _ddp(ImageHeading(args).to(device), self.ctx)
+        self.image_cls = _ddp(ArcMarginProduct(args.aux_feat_dim_per_granularity,
+                                               args.num_classes, s=30, m=0.5).to(device),
+                              self.ctx)
+        self.text_cls = _ddp(ArcMarginProduct(args.aux_feat_dim_per_granularity,
+                                              args.num_classes, s=35, m=0.5).to(device),
+                             self.ctx)
+        self.ident_loss = FocalLoss(gamma=2)
+        # :212 (text_head params would join here; the text side is frozen input)
+        self.optimizer_head = torch.optim.Adam(self.image_head.parameters(),
+                                               lr=args.lr_head, betas=(0.5, 0.999),
+                                               capturable=device.type == "cuda")
+        # :219-222
+        self.optimizer_cls = torch.optim.SGD(
+            list(self.image_cls.parameters()) + list(self.text_cls.parameters()),
+            lr=0.1, momentum=0.9, weight_decay=5e-5)
+
+    def step(self, batch):
+        args, ctx = self.args, self.ctx
+        g, local, words, sent, class_ids = batch
+        b = g.shape[0]
+        ctx.set_batch(b)
+        args.dist = ctx
+        # text side: all-gathered global batch (detached, as in the reference)
+        words_g = ctx.gather_rows(words.transpose(1, 2)).transpose(1, 2)
+        sent_g = ctx.gather_rows(sent)
+        cls_g = ctx.gather_rows(class_ids)
+        labels = torch.arange(ctx.n_global, device=g.device)
+
+        img_features, words_features = self.image_head(g, local)   # :265
+        self.optimizer_head.zero_grad(set_to_none=True)
+        self.optimizer_cls.zero_grad(set_to_none=True)
+
+        w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
+        s0, s1 = sent_loss(img_features, sent_g, labels, cls_g, b, args)
+        damsm = w0 + w1 + s0 + s1                                  # :279
+        tid = self.ident_loss(self.text_cls(sent, class_ids), class_ids)      # :293-294
+        iid = self.ident_loss(self.image_cls(img_features, class_ids), class_ids)
+        cl = global_loss(img_features, sent_g, args=args)          # :310
+        contrastive = damsm + args.lambda_clip * cl
+        total = ctx.world * contrastive + args.lambda_id * (tid + iid)
+        total.backward()                                           # :323
+        self.optimizer_head.step()
+        self.optimizer_cls.step()
+        return {"damsm": damsm.detach(), "clip": cl.detach(),
+                "ident": (args.lambda_id * (tid + iid)).detach()}
+
+
+class Fusion:
+    """Stage-2 FCFM trainer step (src/fusion_bert.py)."""
+
+    def __init__(self, args, device, ctx=None):
+        self.args = args
+        self.ctx = ctx or DistContext()
+        self.image_head = _ddp(ImageHeading(args).to(device), self.ctx)
+        self.fusion_net = _ddp(Working(args.aux_feat_dim_per_granularity).to(device),
+                               self.ctx)
+        self.metric_fc = _ddp(ArcMarginProduct(640, args.num_classes, s=30, m=0.5).to(device),
+                              self.ctx)
+        self.criterion = FocalLoss(gamma=2)                        # :92-96
+        self.optimizer_cls = torch.optim.SGD(self.metric_fc.parameters(), lr=0.1,
+                                             weight_decay=5e-4)    # :119-130
+        self.optimizer_head = torch.optim.Adam(
+            list(self.image_head.parameters()) + list(self.fusion_net.parameters()),
+            weight_decay=5e-5, lr=args.lr_head,
+            capturable=device.type == "cuda")                      # :137-139
+
+    def step(self, batch):
+        g, local, words, sent, class_ids = batch
+        words = words.requires_grad_()                             # :211-212
+        sent = sent.requires_grad_()
+        img_feats, local_feats = self.image_head(g, local)         # :220
+        output = self.fusion_net(local_feats, words, img_feats, sent)   # :153
+        output = self.metric_fc(output, class_ids)                 # :224
+        self.optimizer_cls.zero_grad(set_to_none=True)
+        self.optimizer_head.zero_grad(set_to_none=True)
+        loss = self.criterion(output, class_ids)                   # :232
+        loss.backward()
+        self.optimizer_cls.step()
+        self.optimizer_head.step()
+        return {"loss": loss.detach()}
+
+
+class GraphedStep:
+    """A whole train step (forward, backward, optimiser) captured into one HIP
+    graph: the host launches one graph per step instead of ~370 kernels.
+
+    The batch tensors are static: copy the next batch into them (``load``)
+    before each replay.  Single-process only (DDP's hooks are not captured).
+    """
+
+    def __init__(self, trainer, batch, warmup=3):
+        self.batch = batch
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                trainer.step(batch)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = trainer.step(batch)
+
+    def load(self, batch):
+        for dst, src in zip(self.batch, batch):
+            if dst is not src:
+                dst.copy_(src, non_blocking=True)
+
+    def step(self, batch=None):
+        if batch is not None:
+            self.load(batch)
+        self.graph.replay()
+        return self.out

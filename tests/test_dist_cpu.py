@@ -1,0 +1,71 @@
+"""CPU, world_size 2 over gloo: the rank-major row ownership, the text-side
+all-gather and the column log-sum-exp exchange of the contrastive CE
+reproduce the single-process global-batch quantities."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from text_guided_face_recognition_amd.dist import DistContext
+        from text_guided_face_recognition_amd.kernels import (combine_col_partials,
+                                                              exchange_col_partials)
+        torch.manual_seed(0)
+        b_l = 3
+        full = torch.randn(world * b_l, world * b_l) * 4            # global logits
+        text = torch.randn(world * b_l, 5)
+        ctx = DistContext().set_batch(b_l)
+        mine = full[ctx.row_offset:ctx.row_offset + b_l]
+        # text side: each rank holds its own rows and gathers the global batch
+        gathered = ctx.gather_rows(text[ctx.row_offset:ctx.row_offset + b_l])
+        ok_gather = torch.equal(gathered, text)
+        # column partials of this rank's row block, as tgfr_ce_stats computes them
+        cmax = mine.max(0).values
+        part = torch.stack([cmax, torch.exp(mine - cmax).sum(0)])
+        col_lse = exchange_col_partials(part, ctx.group)
+        ok_lse = torch.allclose(col_lse, torch.logsumexp(full, 0), atol=1e-5)
+        # per-rank CE contributions sum to the global losses
+        n = world * b_l
+        idx = torch.arange(ctx.row_offset, ctx.row_offset + b_l)
+        diag = mine[torch.arange(b_l), idx]
+        l0 = (torch.logsumexp(mine, 1) - diag).sum() / n
+        l1 = (col_lse[idx] - diag).sum() / n
+        tot = ctx.sum(torch.stack([l0, l1]))
+        lab = torch.arange(n)
+        ref = torch.stack([torch.nn.functional.cross_entropy(full, lab),
+                           torch.nn.functional.cross_entropy(full.t(), lab)])
+        ok_loss = torch.allclose(tot, ref, atol=1e-5)
+        one = combine_col_partials(part.unsqueeze(0))
+        ok_single = torch.allclose(one, torch.logsumexp(mine, 0), atol=1e-5)
+        q.put((rank, ok_gather, ok_lse, ok_loss, ok_single, ctx.n_global))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_exchange_world2():
+    world = 2
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _free_port()
+    procs = [ctxm.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok_gather, ok_lse, ok_loss, ok_single, n_global in res:
+        assert ok_gather and ok_lse and ok_loss and ok_single, (rank, res)
+        assert n_global == 6

@@ -25,11 +25,13 @@ import torch.distributed as dist
 
 class DistContext:
     def __init__(self, group=None):
-        self.group = group
         if dist.is_available() and dist.is_initialized():
-            self.rank = dist.get_rank(group)
-            self.world = dist.get_world_size(group)
+            # an explicit handle: None means "not distributed" to the kernels
+            self.group = group if group is not None else dist.group.WORLD
+            self.rank = dist.get_rank(self.group)
+            self.world = dist.get_world_size(self.group)
         else:
+            self.group = None
             self.rank, self.world = 0, 1
         self.active = self.world > 1
         self.b_local = None
@@ -50,17 +52,37 @@ class DistContext:
         """Concatenate equally-shaped per-rank tensors along dim 0 (rank-major)."""
         if not self.active:
             return t
-        t = t.contiguous()
-        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
-                          device=t.device)
-        dist.all_gather_into_tensor(out, t, group=self.group)
-        return out
+        return all_gather_cat(t, self.group)
 
     def sum(self, t):
         if self.active:
+            if dist.get_backend(self.group) == "gloo" and t.is_cuda:
+                c = t.detach().cpu()
+                dist.all_reduce(c, group=self.group)
+                return c.to(t.device)
             t = t.clone()
             dist.all_reduce(t, group=self.group)
         return t
+
+
+def all_gather_cat(t, group=None):
+    """all_gather + concatenate along dim 0.  RCCL gathers device tensors in
+    place; gloo (CPU tests) only gathers host tensors, so it stages through host
+    memory."""
+    t = t.contiguous()
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "gloo" and t.is_cuda:
+        parts = [torch.empty_like(t, device="cpu") for _ in range(world)]
+        dist.all_gather(parts, t.cpu(), group=group)
+        return torch.cat(parts, 0).to(t.device)
+    if dist.get_backend(group) == "gloo":
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t, group=group)
+        return torch.cat(parts, 0)
+    out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
+                      device=t.device)
+    dist.all_gather_into_tensor(out, t, group=group)
+    return out
 
 
 def init_from_env(backend=None):
@@ -69,7 +91,8 @@ def init_from_env(backend=None):
         return DistContext()
     if not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("TGFR_DIST_BACKEND") or (
+                "nccl" if torch.cuda.device_count() > 0 else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
         dist.init_process_group(backend=backend)

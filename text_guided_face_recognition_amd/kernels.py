@@ -179,10 +179,8 @@ def exchange_col_partials(part, group):
     """The one collective of the contrastive CE: all_gather of [2, n_c] partials."""
     if group is None:
         return combine_col_partials(part.unsqueeze(0))
-    import torch.distributed as dist
-    world = dist.get_world_size(group)
-    allp = torch.empty((world,) + tuple(part.shape), dtype=part.dtype, device=part.device)
-    dist.all_gather_into_tensor(allp, part.contiguous(), group=group)
+    from .dist import all_gather_cat
+    allp = all_gather_cat(part.unsqueeze(0), group)
     return combine_col_partials(allp)
 
 

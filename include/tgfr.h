@@ -92,9 +92,11 @@ int tgfr_cos_logits_bwd(const float* g, long long gs0, long long gs1, const floa
                         int normalize, float scale, float eps, float* dx, long long lddx,
                         void* stream);
 
-/* Row log-sum-exp and column (max, sum exp) partials of a [n_r x n_c] block. */
+/* Row log-sum-exp and column (max, sum exp) partials of a [n_r x n_c] block;
+ * col_lse (nullable) also receives the column LSE of this block alone (the
+ * single-process case, where no exchange is needed). */
 int tgfr_ce_stats(const float* L, long long ld, int n_r, int n_c, float* row_lse,
-                  float* col_max, float* col_sum, void* stream);
+                  float* col_max, float* col_sum, float* col_lse, void* stream);
 
 /* loss[0] = inv_n * sum_b (row_lse[b] - L[b][b+off]), loss[1] = inv_n * sum_b
  * (col_lse[b+off] - L[b][b+off]): this rank's share of nn.CrossEntropyLoss on
@@ -103,18 +105,24 @@ int tgfr_ce_loss(const float* L, long long ld, int n_r, int row_offset, float in
                  const float* row_lse, const float* col_lse, float* loss, void* stream);
 
 /* dL = w0*g0*inv_n (softmax_row - onehot) + w1*g1*inv_n (softmax_col - onehot),
- * with g0 = gscale[0], g1 = gscale[1] read on the device (nullable: 1). */
+ * with the upstream gradients g0, g1 read on the device (nullable: 1). */
 int tgfr_ce_grad(const float* L, long long ld, int n_r, int n_c, int row_offset, float inv_n,
-                 const float* row_lse, const float* col_lse, const float* gscale, float w0,
-                 float w1, float* dL, long long ldd, void* stream);
+                 const float* row_lse, const float* col_lse, const float* g0, const float* g1,
+                 float w0, float w1, float* dL, long long ldd, void* stream);
 
-/* Batched C[b] = alpha * A[b] B[b] (+ C[b] when accumulate) with arbitrary
- * element strides: the QK^T and PV products of SelfAttention
- * (models/fusion_nets.py:103, :115) and their backward. */
+/* Batched C[b] = epi(alpha * A[b] B[b] (+ C[b] when accumulate) + bias) with
+ * arbitrary element strides (transposes are stride swaps): the QK^T and PV
+ * products of SelfAttention (models/fusion_nets.py:103, :115), the 1x1-conv /
+ * Linear projections of IMIM and FCFM (models/models.py:386-404), and their
+ * backward.  bias (nullable, per column) and relu form the epilogue.  With
+ * ksplit > 1 the K range is split over ksplit blocks, each writing its own
+ * slab at C + k*sCsplit (deterministic split-K; the caller sums the slabs);
+ * bias/relu/accumulate require ksplit == 1. */
 int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, const float* B,
                long long sBb, long long sBk, long long sBn, float* C, long long sCb,
                long long sCm, long long sCn, int batch, int M, int N, int K, float alpha,
-               int accumulate, int mode, void* stream);
+               int accumulate, const float* bias, int relu, int ksplit, long long sCsplit,
+               int mode, void* stream);
 
 /* P = softmax(scale * S) per row (models/fusion_nets.py:103-106), optional LSE. */
 int tgfr_attn_softmax(const float* S, float* P, float* lse, long long rows, int n, long long ld,

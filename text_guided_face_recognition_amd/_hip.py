@@ -32,10 +32,10 @@ SIGNATURES = {
     "tgfr_wr_lds_bytes": [I],
     "tgfr_cos_logits": [P, L, P, L, I, I, I, I, F, F, I, P, I, P, L, P],
     "tgfr_cos_logits_bwd": [P, L, L, P, L, P, L, I, I, I, I, F, F, P, L, P],
-    "tgfr_ce_stats": [P, L, I, I, P, P, P, P],
+    "tgfr_ce_stats": [P, L, I, I, P, P, P, P, P],
     "tgfr_ce_loss": [P, L, I, I, F, P, P, P, P],
-    "tgfr_ce_grad": [P, L, I, I, I, F, P, P, P, F, F, P, L, P],
-    "tgfr_bgemm": [P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, F, I, I, P],
+    "tgfr_ce_grad": [P, L, I, I, I, F, P, P, P, P, F, F, P, L, P],
+    "tgfr_bgemm": [P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, F, I, P, I, I, L, I, P],
     "tgfr_attn_softmax": [P, P, P, L, I, L, F, P],
     "tgfr_attn_softmax_bwd": [P, P, P, L, I, L, F, P],
 }

@@ -61,9 +61,27 @@ template <int MODE>
 __global__ __launch_bounds__(256) void bgemm_kernel(
     const float* __restrict__ A, long long sAb, long long sAm, long long sAk,
     const float* __restrict__ B, long long sBb, long long sBk, long long sBn,
-    float* __restrict__ Cm, long long sCb, long long sCm, long long sCn, int M, int N, int K,
-    float alpha, int accumulate) {
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, bt = blockIdx.z;
+    float* __restrict__ Cm, long long sCb, long long sCm, long long sCn, int M, int N, int Kfull,
+    float alpha, int accumulate, const float* __restrict__ bias, int relu, int ksplit,
+    long long sCsplit) {
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int bt = blockIdx.z / ksplit, kz = blockIdx.z % ksplit;
+  // split-K: this block reduces k in [kb, kb + K) into its own output slab
+  const int kc = ((Kfull + ksplit - 1) / ksplit + BK - 1) / BK * BK;
+  const int kb = kz * kc;
+  const int K = min(Kfull - kb, kc);
+  if (K <= 0) {
+    // empty tail slice: its slab must still hold zeros
+    const int n = n0 + 32 * (threadIdx.x / WAVE & 1) + (threadIdx.x & 31);
+    float* Cb = Cm + bt * sCb + kz * sCsplit;
+    for (int q = 0; q < 16; ++q) {
+      const int m = m0 + 32 * ((threadIdx.x / WAVE) >> 1) + acc_row(q, (threadIdx.x & 63) >> 5);
+      if (m < M && n < N) Cb[m * sCm + n * sCn] = 0.f;
+    }
+    return;
+  }
+  A += (long long)kb * sAk;
+  B += (long long)kb * sBk;
   const int tid = threadIdx.x, wid = tid / WAVE, lane = tid % WAVE;
   const int lr = lane & 31, h = lane >> 5;
   const int wm = wid >> 1, wn = wid & 1;
@@ -109,14 +127,16 @@ __global__ __launch_bounds__(256) void bgemm_kernel(
   }
   const int n = n0 + 32 * wn + lr;
   if (n >= N) return;
-  float* Cb = Cm + bt * sCb;
+  float* Cb = Cm + bt * sCb + kz * sCsplit;
+  const float bn = bias ? bias[n] : 0.f;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int m = m0 + 32 * wm + acc_row(q, h);
     if (m < M) {
       float* o = Cb + m * sCm + n * sCn;
-      const float v = alpha * acc[q];
-      *o = accumulate ? *o + v : v;
+      float v = alpha * acc[q] + bn;
+      if (accumulate) v += *o;
+      *o = relu ? fmaxf(v, 0.f) : v;
     }
   }
 }
@@ -166,16 +186,20 @@ extern "C" {
 int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, const float* B,
                long long sBb, long long sBk, long long sBn, float* C, long long sCb,
                long long sCm, long long sCn, int batch, int M, int N, int K, float alpha,
-               int accumulate, int mode, void* stream) {
-  if (batch <= 0 || M <= 0 || N <= 0 || K <= 0) return 1001;
-  const dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch);
+               int accumulate, const float* bias, int relu, int ksplit, long long sCsplit,
+               int mode, void* stream) {
+  if (batch <= 0 || M <= 0 || N <= 0 || K <= 0 || ksplit <= 0) return 1001;
+  if (ksplit > 1 && (bias || relu || accumulate)) return 1001;
+  const dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch * ksplit);
   auto* s = (hipStream_t)stream;
   if (mode == MODE_SPLIT)
     hipLaunchKernelGGL(bgemm_kernel<MODE_SPLIT>, grid, dim3(256), 2 * STAGE, s, A, sAb, sAm,
-                       sAk, B, sBb, sBk, sBn, C, sCb, sCm, sCn, M, N, K, alpha, accumulate);
+                       sAk, B, sBb, sBk, sBn, C, sCb, sCm, sCn, M, N, K, alpha, accumulate,
+                       bias, relu, ksplit, sCsplit);
   else if (mode == MODE_BF16)
     hipLaunchKernelGGL(bgemm_kernel<MODE_BF16>, grid, dim3(256), 2 * STAGE, s, A, sAb, sAm,
-                       sAk, B, sBb, sBk, sBn, C, sCb, sCm, sCn, M, N, K, alpha, accumulate);
+                       sAk, B, sBb, sBk, sBn, C, sCb, sCm, sCn, M, N, K, alpha, accumulate,
+                       bias, relu, ksplit, sCsplit);
   else
     return 1002;
   return (int)hipGetLastError();

@@ -102,7 +102,8 @@ __global__ __launch_bounds__(256) void ce_stats_kernel(const float* __restrict__
                                                        int n_r, int n_c,
                                                        float* __restrict__ row_lse,
                                                        float* __restrict__ col_max,
-                                                       float* __restrict__ col_sum) {
+                                                       float* __restrict__ col_sum,
+                                                       float* __restrict__ col_lse) {
   // blockIdx.y == 0: rows (one wave per row); == 1: columns (one thread per column)
   if (blockIdx.y == 0) {
     const int row = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
@@ -123,6 +124,7 @@ __global__ __launch_bounds__(256) void ce_stats_kernel(const float* __restrict__
     for (int r = 0; r < n_r; ++r) s += __expf(L[r * ld + c] - m);
     col_max[c] = m;
     col_sum[c] = s;
+    if (col_lse) col_lse[c] = m + __logf(s);
   }
 }
 
@@ -156,7 +158,8 @@ __global__ __launch_bounds__(256) void ce_grad_kernel(const float* __restrict__ 
                                                       int n_r, int n_c, int row_offset,
                                                       float inv_n, const float* __restrict__ row_lse,
                                                       const float* __restrict__ col_lse,
-                                                      const float* __restrict__ gscale, float w0,
+                                                      const float* __restrict__ g0p,
+                                                      const float* __restrict__ g1p, float w0,
                                                       float w1, float* __restrict__ dL,
                                                       long long ldd) {
   const long long e = blockIdx.x * 256LL + threadIdx.x;
@@ -164,8 +167,8 @@ __global__ __launch_bounds__(256) void ce_grad_kernel(const float* __restrict__ 
   const int b = e / n_c, c = e % n_c;
   const float v = L[b * ld + c];
   const float onehot = (c == row_offset + b) ? 1.f : 0.f;
-  const float g0 = (gscale ? gscale[0] : 1.f) * w0 * inv_n;
-  const float g1 = (gscale ? gscale[1] : 1.f) * w1 * inv_n;
+  const float g0 = (g0p ? *g0p : 1.f) * w0 * inv_n;
+  const float g1 = (g1p ? *g1p : 1.f) * w1 * inv_n;
   dL[b * ldd + c] = g0 * (__expf(v - row_lse[b]) - onehot) + g1 * (__expf(v - col_lse[c]) - onehot);
 }
 
@@ -196,11 +199,11 @@ int tgfr_cos_logits_bwd(const float* g, long long gs0, long long gs1, const floa
 }
 
 int tgfr_ce_stats(const float* L, long long ld, int n_r, int n_c, float* row_lse,
-                  float* col_max, float* col_sum, void* stream) {
+                  float* col_max, float* col_sum, float* col_lse, void* stream) {
   if (n_r <= 0 || n_c <= 0) return 1001;
   const int gx = max((n_r + 3) / 4, (n_c + 255) / 256);
   hipLaunchKernelGGL(ce_stats_kernel, dim3(gx, 2), dim3(256), 0, (hipStream_t)stream, L, ld,
-                     n_r, n_c, row_lse, col_max, col_sum);
+                     n_r, n_c, row_lse, col_max, col_sum, col_lse);
   return (int)hipGetLastError();
 }
 
@@ -213,13 +216,13 @@ int tgfr_ce_loss(const float* L, long long ld, int n_r, int row_offset, float in
 }
 
 int tgfr_ce_grad(const float* L, long long ld, int n_r, int n_c, int row_offset, float inv_n,
-                 const float* row_lse, const float* col_lse, const float* gscale, float w0,
-                 float w1, float* dL, long long ldd, void* stream) {
+                 const float* row_lse, const float* col_lse, const float* g0, const float* g1,
+                 float w0, float w1, float* dL, long long ldd, void* stream) {
   if (n_r <= 0 || n_c <= 0) return 1001;
   const long long n = (long long)n_r * n_c;
   hipLaunchKernelGGL(ce_grad_kernel, dim3((int)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, L, ld, n_r, n_c, row_offset, inv_n, row_lse, col_lse,
-                     gscale, w0, w1, dL, ldd);
+                     g0, g1, w0, w1, dL, ldd);
   return (int)hipGetLastError();
 }
 

@@ -202,9 +202,10 @@ class ContrastiveCE(torch.autograd.Function):
         dev = logits.device
         row_lse = torch.empty(n_r, dtype=torch.float32, device=dev)
         part = torch.empty(2, n_c, dtype=torch.float32, device=dev)
+        local_lse = torch.empty(n_c, dtype=torch.float32, device=dev) if group is None else None
         call("tgfr_ce_stats", ptr(logits), n_c, n_r, n_c, ptr(row_lse), ptr(part[0]),
-             ptr(part[1]), _hip.stream())
-        col_lse = exchange_col_partials(part, group)
+             ptr(part[1]), ptr(local_lse), _hip.stream())
+        col_lse = local_lse if group is None else exchange_col_partials(part, group)
         loss = torch.empty(2, dtype=torch.float32, device=dev)
         inv_n = 1.0 / float(n_global)
         call("tgfr_ce_loss", ptr(logits), n_c, n_r, int(row_offset), inv_n, ptr(row_lse),
@@ -218,12 +219,13 @@ class ContrastiveCE(torch.autograd.Function):
         logits, row_lse, col_lse = ctx.saved_tensors
         row_offset, inv_n = ctx.cfg
         n_r, n_c = logits.shape
-        g0 = torch.zeros((), device=logits.device) if g0 is None else g0
-        g1 = torch.zeros((), device=logits.device) if g1 is None else g1
-        gs = torch.stack([g0.float().reshape(()), g1.float().reshape(())]).contiguous()
+        w0 = 0.0 if g0 is None else 1.0
+        w1 = 0.0 if g1 is None else 1.0
+        g0 = None if g0 is None else g0.float().contiguous()
+        g1 = None if g1 is None else g1.float().contiguous()
         dl = torch.empty_like(logits)
         call("tgfr_ce_grad", ptr(logits), n_c, n_r, n_c, row_offset, inv_n, ptr(row_lse),
-             ptr(col_lse), ptr(gs), 1.0, 1.0, ptr(dl), n_c, _hip.stream())
+             ptr(col_lse), ptr(g0), ptr(g1), w0, w1, ptr(dl), n_c, _hip.stream())
         return dl, None, None, None
 
 
@@ -233,19 +235,80 @@ def contrastive_ce(logits, row_offset=0, n_global=None, group=None):
 
 
 # ------------------------------------------------------------------ bgemm ---
-def bgemm(a, b, out=None, alpha=1.0, accumulate=False, mode="fp32"):
-    """out[n] = alpha * a[n] @ b[n] (+ out[n]) for 3-D fp32 tensors of any
-    strides (transposed views cost nothing: strides are passed through)."""
+def bgemm(a, b, out=None, alpha=1.0, accumulate=False, mode="fp32", bias=None,
+          relu=False, ksplit=1):
+    """out[n] = epi(alpha * a[n] @ b[n] (+ out[n]) + bias) for 3-D fp32 tensors of
+    any strides (transposed views cost nothing: strides are passed through).
+    ksplit > 1 splits K over blocks into slabs that are summed afterwards."""
     assert a.dim() == 3 and b.dim() == 3 and a.shape[0] == b.shape[0]
     assert a.shape[2] == b.shape[1] and a.dtype == b.dtype == torch.float32
     nb, m, k = a.shape
     n = b.shape[2]
+    if ksplit > 1:
+        slab = torch.empty(ksplit, nb, m, n, dtype=torch.float32, device=a.device)
+        call("tgfr_bgemm", ptr(a), a.stride(0), a.stride(1), a.stride(2), ptr(b),
+             b.stride(0), b.stride(1), b.stride(2), ptr(slab), m * n, n, 1, nb, m, n, k,
+             float(alpha), 0, None, 0, int(ksplit), nb * m * n, _mode(mode), _hip.stream())
+        red = slab.sum(0)
+        if out is None:
+            return red
+        if accumulate:
+            out.add_(red)
+        else:
+            out.copy_(red)
+        return out
     if out is None:
         out = torch.empty(nb, m, n, dtype=torch.float32, device=a.device)
     call("tgfr_bgemm", ptr(a), a.stride(0), a.stride(1), a.stride(2), ptr(b), b.stride(0),
          b.stride(1), b.stride(2), ptr(out), out.stride(0), out.stride(1), out.stride(2),
-         nb, m, n, k, float(alpha), int(accumulate), _mode(mode), _hip.stream())
+         nb, m, n, k, float(alpha), int(accumulate), ptr(bias), int(relu), 1, 0,
+         _mode(mode), _hip.stream())
     return out
+
+
+def _ksplit(k, mn_blocks):
+    """Split-K factor that gives >= ~512 blocks for a long-K, small-output GEMM."""
+    if k < 1024 or mn_blocks >= 256:
+        return 1
+    return int(max(1, min(k // 256, -(-512 // mn_blocks))))
+
+
+class LinearRows(torch.autograd.Function):
+    """y = x W^T + b (optionally ReLU) over the rows of x [..., K]: every
+    nn.Linear / 1x1 conv of the head, on the split-bf16 MFMA GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu, mode):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).float()
+        w = weight.reshape(weight.shape[0], -1).float()
+        y = bgemm(x2.unsqueeze(0), w.t().unsqueeze(0), mode=mode,
+                  bias=None if bias is None else bias.float().contiguous(), relu=relu)[0]
+        ctx.save_for_backward(x2, w, y if relu else None)
+        ctx.cfg = (relu, mode, bias is not None, shape, weight.shape)
+        return y.reshape(*shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, y = ctx.saved_tensors
+        relu, mode, has_bias, shape, wshape = ctx.cfg
+        dy = dy.reshape(-1, w.shape[0]).float()
+        if relu:
+            dy = dy * (y > 0)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = bgemm(dy.unsqueeze(0), w.unsqueeze(0), mode=mode)[0].reshape(shape)
+        if ctx.needs_input_grad[1]:
+            mb = -(-w.shape[0] // 64) * -(-w.shape[1] // 64)
+            dw = bgemm(dy.t().unsqueeze(0), x2.unsqueeze(0), mode=mode,
+                       ksplit=_ksplit(x2.shape[0], mb))[0].reshape(wshape)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.sum(0)
+        return dx, dw, db, None, None
+
+
+def linear_rows(x, weight, bias=None, relu=False, mode="fp32"):
+    return LinearRows.apply(x, weight, bias, relu, mode)
 
 
 class AttentionCore(torch.autograd.Function):

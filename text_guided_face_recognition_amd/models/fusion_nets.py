@@ -50,17 +50,21 @@ class SelfAttention(nn.Module):
 
     def forward_cl(self, x_cl, y_cl):
         """Channels-last core: x_cl, y_cl [N, HW, C] -> [N, HW, C]."""
+        mode = self.precision
         if y_cl is x_cl:
             w = torch.cat([self._w(self.key_proj), self._w(self.query_proj),
                            self._w(self.value_proj)], 0)
             b = torch.cat([self.key_proj.bias, self.query_proj.bias, self.value_proj.bias])
-            proj = F.linear(x_cl, w, b)
+            proj = K.linear_rows(x_cl, w, b, mode=mode)
             cq = self.key_proj.weight.shape[0]
             qr, kr, v = proj[..., :cq], proj[..., cq:2 * cq], proj[..., 2 * cq:]
         else:
-            qr = F.linear(x_cl, self._w(self.key_proj), self.key_proj.bias)
-            kr = F.linear(y_cl, self._w(self.query_proj), self.query_proj.bias)
-            v = F.linear(x_cl, self._w(self.value_proj), self.value_proj.bias)
+            w = torch.cat([self._w(self.key_proj), self._w(self.value_proj)], 0)
+            b = torch.cat([self.key_proj.bias, self.value_proj.bias])
+            proj = K.linear_rows(x_cl, w, b, mode=mode)
+            cq = self.key_proj.weight.shape[0]
+            qr, v = proj[..., :cq], proj[..., cq:]
+            kr = K.linear_rows(y_cl, self._w(self.query_proj), self.query_proj.bias, mode=mode)
         return K.attention_core(qr, kr, v, 1.0 / float(self.sqrt_dim), self.precision)
 
     def forward(self, x, y):
@@ -94,7 +98,8 @@ class Working(nn.Module):
     def forward(self, img, word, gl_img, sent):
         img = self.maxpool(self.relu(self.conv(img)))
         img = self.bn_img(img)
-        word = self.projection(word.transpose(1, 2))
+        word = K.linear_rows(word.transpose(1, 2), self.projection.weight,
+                             self.projection.bias, mode=self.sa.precision)
         word = torch.bmm(word.transpose(1, 2), word) / np.sqrt(36)
         word = word.unsqueeze(-1).view(word.size(0), word.size(1), 6, 6)
         word = self.bn_word(word)
@@ -102,7 +107,16 @@ class Working(nn.Module):
         iw = self.ln(iw)
         iw = self.maxpool(iw)
         iw = iw.reshape(iw.size(0), -1)
-        iw = self.linear(iw)
+        iw = K.linear_rows(iw, self.linear.weight, self.linear.bias, mode=self.sa.precision)
         gl_img = self.ln_gl_image(gl_img)
         sent = self.ln_sent(sent)
         return torch.concat((iw, gl_img, sent), dim=1)
+
+
+def set_precision(module, mode):
+    """Set the MFMA precision mode ("fp32" split or "bf16") of every drop-in
+    module under ``module``."""
+    for m in module.modules():
+        if hasattr(m, "precision"):
+            m.precision = mode
+    return module

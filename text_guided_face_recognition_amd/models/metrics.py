@@ -1,7 +1,7 @@
 """ArcMarginProduct (models/metrics.py:17-60): the identity head that runs
-after the hot path every step.  Out of the HIP scope this round (SURVEY.md
-8(f) rank 2); plain PyTorch, with the CUDA-only one-hot (:53) replaced by a
-device-agnostic scatter."""
+after the hot path every step.  Its cosine GEMM runs
+on the split-bf16 MFMA GEMM kernel (kernels.linear_rows); the margin and the
+one-hot (CUDA-only in the reference, :53) are device-side PyTorch ops."""
 from __future__ import annotations
 
 import math
@@ -10,6 +10,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 from torch.nn.parameter import Parameter
+
+from .. import kernels as K
 
 __all__ = ["ArcMarginProduct"]
 
@@ -28,9 +30,11 @@ class ArcMarginProduct(nn.Module):
         self.sin_m = math.sin(m)
         self.th = math.cos(math.pi - m)
         self.mm = math.sin(math.pi - m) * m
+        self.precision = "fp32"
 
     def forward(self, input, label):
-        cosine = F.linear(F.normalize(input), F.normalize(self.weight))
+        cosine = K.linear_rows(F.normalize(input), F.normalize(self.weight),
+                               mode=self.precision)
         sine = torch.sqrt((1.0 - torch.pow(cosine, 2)).clamp(0, 1))
         phi = cosine * self.cos_m - sine * self.sin_m
         if self.easy_margin:

@@ -15,7 +15,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .fusion_nets import SelfAttention, _cl
+from .. import kernels as K
+from .fusion_nets import SelfAttention, _cl, set_precision
 
 __all__ = ["ProjectionHead", "IMIM", "ImageHeading"]
 
@@ -30,9 +31,11 @@ class ProjectionHead(nn.Module):
         self.gelu = nn.GELU()
         self.fc = nn.Linear(projection_dim, projection_dim)
         self.dropout = nn.Dropout(dropout)
+        self.precision = "fp32"
 
     def forward(self, x):
-        return F.normalize(self.projection(x), p=2, dim=-1)
+        y = K.linear_rows(x, self.projection.weight, self.projection.bias, mode=self.precision)
+        return F.normalize(y, p=2, dim=-1)
 
 
 class IMIM(nn.Module):
@@ -49,20 +52,22 @@ class IMIM(nn.Module):
         self.relu = nn.ReLU()
         self.conv1x1_2 = nn.Conv2d(self.channel_dim // 2, self.channel_dim, kernel_size=(1, 1))
         self.ln = nn.LayerNorm([self.channel_dim, 14, 14])
-        self.sa.precision = getattr(args, "precision", "fp32")
+        self.precision = getattr(args, "precision", "fp32")
+        set_precision(self, self.precision)
 
     def forward(self, img):
         n, c, h, w = img.shape
         z = _cl(self.bn_img(img))                       # [B, HW, C]
         z = self.sa.forward_cl(z, z)
-        # LayerNorm over (C, H, W) of each sample, affine maps in [HW, C] order
-        mu = z.mean(dim=(1, 2), keepdim=True)
-        var = z.var(dim=(1, 2), unbiased=False, keepdim=True)
+        # LayerNorm over (C, H, W) of each sample == over the last two dims of
+        # the channels-last [B, HW, C] rows, with the affine maps permuted
         wt = self.ln.weight.permute(1, 2, 0).reshape(h * w, c)
         bs = self.ln.bias.permute(1, 2, 0).reshape(h * w, c)
-        z = (z - mu) * torch.rsqrt(var + self.ln.eps) * wt + bs
-        z = F.relu(F.linear(z, self.conv1x1_1.weight.flatten(1), self.conv1x1_1.bias))
-        z = F.relu(F.linear(z, self.conv1x1_2.weight.flatten(1), self.conv1x1_2.bias))
+        z = F.layer_norm(z, (h * w, c), wt, bs, self.ln.eps)
+        z = K.linear_rows(z, self.conv1x1_1.weight, self.conv1x1_1.bias, relu=True,
+                          mode=self.precision)
+        z = K.linear_rows(z, self.conv1x1_2.weight, self.conv1x1_2.bias, relu=True,
+                          mode=self.precision)
         z = self.project_local(z)                       # [B, HW, 256], unit rows
         return z.reshape(n, h, w, -1).permute(0, 3, 1, 2)
 
@@ -75,6 +80,7 @@ class ImageHeading(nn.Module):
         self.project_global = ProjectionHead(input_dim=512,
                                              projection_dim=args.aux_feat_dim_per_granularity)
         self.imim = IMIM(args, channel_dim=256)
+        set_precision(self, getattr(args, "precision", "fp32"))
 
     def forward(self, global_image, local_image):
         local_image = self.imim(local_image)

@@ -24,7 +24,7 @@ import torch
 from torch.nn.parallel import DistributedDataParallel as DDP
 
 from .dist import DistContext
-from .models.fusion_nets import Working
+from .models.fusion_nets import Working, set_precision
 from .models.losses import FocalLoss, global_loss, sent_loss, words_loss
 from .models.metrics import ArcMarginProduct
 from .models.models import ImageHeading
@@ -69,11 +69,14 @@ class Train:
         self.text_cls = _ddp(ArcMarginProduct(args.aux_feat_dim_per_granularity,
                                               args.num_classes, s=35, m=0.5).to(device),
                              self.ctx)
+        for m in (self.image_head, self.image_cls, self.text_cls):
+            set_precision(m, args.precision)
         self.ident_loss = FocalLoss(gamma=2)
         # :212 (text_head params would join here; the text side is frozen input)
         self.optimizer_head = torch.optim.Adam(self.image_head.parameters(),
                                                lr=args.lr_head, betas=(0.5, 0.999),
-                                               capturable=device.type == "cuda")
+                                               capturable=device.type == "cuda",
+                                               fused=device.type == "cuda")
         # :219-222
         self.optimizer_cls = torch.optim.SGD(
             list(self.image_cls.parameters()) + list(self.text_cls.parameters()),
@@ -121,13 +124,16 @@ class Fusion:
                                self.ctx)
         self.metric_fc = _ddp(ArcMarginProduct(640, args.num_classes, s=30, m=0.5).to(device),
                               self.ctx)
+        for m in (self.image_head, self.fusion_net, self.metric_fc):
+            set_precision(m, args.precision)
         self.criterion = FocalLoss(gamma=2)                        # :92-96
         self.optimizer_cls = torch.optim.SGD(self.metric_fc.parameters(), lr=0.1,
                                              weight_decay=5e-4)    # :119-130
         self.optimizer_head = torch.optim.Adam(
             list(self.image_head.parameters()) + list(self.fusion_net.parameters()),
             weight_decay=5e-5, lr=args.lr_head,
-            capturable=device.type == "cuda")                      # :137-139
+            capturable=device.type == "cuda",
+                                               fused=device.type == "cuda")                      # :137-139
 
     def step(self, batch):
         g, local, words, sent, class_ids = batch

@@ -50,29 +50,34 @@ int tgfr_prep_rows(const float* x, long long s_item, long long s_row, long long 
  * func_attention (models/attention.py:10-43):
  *   logits[b*ld + i] = gamma3 * log sum_{t<lens[i]} exp(gamma2 * cos_t)
  * Also writes per-token stats [B_img][B_cap][32] float4 {Z_t, n_t, |C_t|, cos_t}
- * and C [B_img][B_cap][32][256] fp32 (the weighted context, attention.py:41)
+ * and the weighted context C (attention.py:41) as bf16 hi (Chi) and, in
+ * mode 1, lo (Clo) in chunk-major order [pair][32 chunks of 8 d][32 t][8],
  * for the backward; att (nullable) receives A2 [b][t][196] for the matching
- * pair i == b + img_offset (the att_maps of losses.py:97). */
+ * pair i == b + img_offset (the att_maps of losses.py:97).  Mode 0 keeps the
+ * image's R resident in LDS (Rlo/Wlo unused, may be NULL). */
 int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, const float* Wnorm, const int* lens, int B_img, int B_cap,
                 int img_offset, float gamma1, float gamma2, float gamma3, float eps,
-                float* logits, int ld_logits, float* stats, float* Cout, float* att,
-                int att_T, int mode, void* stream);
+                float* logits, int ld_logits, float* stats, uint16_t* Chi, uint16_t* Clo,
+                float* att, int att_T, int mode, void* stream);
 
 /* Backward of tgfr_wr_fwd w.r.t. the image regions given dL/dlogits: writes
  * n_chunks partial slabs [n_chunks][B_img][224][256] (one per caption chunk);
- * the text side is detached in the reference (utils/dataset_utils.py:42). */
+ * tok_ws is a caller workspace of B_img*B_cap*32*8 floats (per-token backward
+ * scalars).  The text side is detached in the reference
+ * (utils/dataset_utils.py:42). */
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, const float* Wnorm, const int* lens, int B_img, int B_cap,
                 int n_chunks, float gamma1, float gamma2, float gamma3, float eps,
-                const float* dlogits, int ld, const float* stats, const float* Cbuf,
-                float* slab, int mode, void* stream);
+                const float* dlogits, int ld, const float* stats, const uint16_t* Chi,
+                const uint16_t* Clo, float* tok_ws, float* slab, int mode, void* stream);
 
 /* dR[b][r][d] (caller strides; r < 196) = (+)= sum over chunks of the slabs. */
 int tgfr_wr_reduce(const float* slab, int n_chunks, int B_img, float* out, long long s_b,
                    long long s_r, long long s_d, int accumulate, void* stream);
 
-/* Dynamic LDS bytes of the forward (which = 0) / backward (1) kernels. */
+/* Dynamic LDS bytes of the streaming forward (which = 0), the fp32-mode
+ * backward (1) and the resident-R bf16 forward (2). */
 int tgfr_wr_lds_bytes(int which);
 
 /* logits[b*ldo + i] = scale * x_b.y_i / max(|x_b||y_i|, eps) (normalize = 1;

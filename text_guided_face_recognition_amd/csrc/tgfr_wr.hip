@@ -130,14 +130,39 @@ __device__ __forceinline__ void fwd_store_chunk(const StageRegs& s, int c, int b
   }
 }
 
+// C (the normalised weighted context, attention.py:41) for the backward, as
+// bf16 hi (+lo) in chunk-major order Cq[pair][c][t][8] (c = d / 8): lane
+// (t, h) holds d = 32 dt + 8 g + 4 h + 0..3, so each store instruction
+// writes 512 contiguous bytes and every 16-B chunk (8 consecutive d of one
+// token) is contiguous for the backward's global_load_lds gather.
+template <int MODE>
+__device__ __forceinline__ void store_cq(uint16_t* Chi, uint16_t* Clo, long long pair, int t,
+                                         int h, bool tvalid, float zinv, const f32x16 (&C)[8]) {
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint16_t hh[4], ll[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float v = tvalid ? C[dt][4 * g + k] * zinv : 0.f;
+        split2(v, hh[k], ll[k]);
+      }
+      const long long o = ((pair * 32 + (4 * dt + g)) * 32 + t) * 8 + 4 * h;
+      *(uint2*)(Chi + o) = make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3]));
+      if (MODE == MODE_SPLIT)
+        *(uint2*)(Clo + o) = make_uint2(pack2(ll[0], ll[1]), pack2(ll[2], ll[3]));
+    }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256, 1) void wr_fwd_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Rlo,
     const uint16_t* __restrict__ Whi, const uint16_t* __restrict__ Wlo,
     const float* __restrict__ Wnorm, const int* __restrict__ lens, int B_img, int B_cap,
     int img_offset, float g1, float g2, float g3, float eps, float* __restrict__ logits,
-    int ld_logits, float4* __restrict__ stats, float* __restrict__ Cout,
-    float* __restrict__ att, int att_T) {
+    int ld_logits, float4* __restrict__ stats, uint16_t* __restrict__ Chi,
+    uint16_t* __restrict__ Clo, float* __restrict__ att, int att_T) {
   const int groups = (B_cap + 3) / 4;
   const int work = xcd_remap(blockIdx.x, groups * B_img);
   const int b = work / groups;
@@ -310,19 +335,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_kernel(
   if (lane == 0) logits[(long long)b * ld_logits + i] = g3 * __logf(ex);
   if (stats && h == 0)
     stats[pair * TPAD + t] = tvalid ? make_float4(Z, n, cn, cosv) : make_float4(0.f, 0.f, 0.f, 0.f);
-  if (Cout) {
-    float* dst = Cout + (pair * TPAD + t) * D;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * h;
-        float4 v = make_float4(C[dt][4 * g] * zinv, C[dt][4 * g + 1] * zinv,
-                               C[dt][4 * g + 2] * zinv, C[dt][4 * g + 3] * zinv);
-        if (!tvalid) v = make_float4(0.f, 0.f, 0.f, 0.f);
-        *(float4*)(dst + d) = v;
-      }
-  }
+  if (Chi) store_cq<MODE>(Chi, Clo, pair, t, h, tvalid, zinv, C);
   if (att && b + img_offset == i) {
     // attention map of the matching pair: A2[t][r] = E[t][r] / Z_t
     float* dst = att + (long long)b * att_T * NREG;
@@ -337,106 +350,287 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_kernel(
   }
 }
 
+// ------------------------------------------------ fwd, bf16, R resident ---
+// bf16 mode only: the image's R (224 x 256 bf16 = 112 KB) stays in LDS for the
+// whole workgroup, so R is read from L2 once per (image, caption chunk)
+// instead of once per 4 captions.  Image layout: 2 halves x [224 rows][128
+// cols], 256-B rows, 16-B chunks XOR-swizzled by row -> both the row reads of
+// GEMM1 (ds_read_b128) and the transposed reads of GEMM2 (ds_read_b64_tr_b16)
+// are conflict-free.  Filled by global_load_lds with swizzled source addresses.
+__device__ __forceinline__ uint32_t roff(int row, int col) {
+  const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
+  return (col >> 7) * (RPAD * 256) + row * 256 + ((((col & 127) >> 3) ^ sw) << 4) + (col & 7) * 2;
+}
+constexpr int FR_IMG = RPAD * D * 2;                 // 114688
+constexpr int FR_OFF_ET = FR_IMG;                    // per-wave E^T tile, bf16 [32][32]
+constexpr int FR_OFF_TOK = FR_OFF_ET + 4 * 2048;
+constexpr int FR_LDS = FR_OFF_TOK + 4 * 256;
+
+__global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
+    const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi,
+    const float* __restrict__ Wnorm, const int* __restrict__ lens, int B_img, int B_cap,
+    int n_chunks, int img_offset, float g1, float g2, float g3, float eps,
+    float* __restrict__ logits, int ld_logits, float4* __restrict__ stats,
+    uint16_t* __restrict__ Chi, float* __restrict__ att, int att_T) {
+  const int work = xcd_remap(blockIdx.x, n_chunks * B_img);
+  const int b = work / n_chunks, chunk = work % n_chunks;
+  const int per = (B_cap + n_chunks - 1) / n_chunks;
+  const int c0 = chunk * per, c1 = min(B_cap, c0 + per);
+  const int tid = threadIdx.x, wid = tid / WAVE, lane = tid % WAVE;
+  const int lr = lane & 31, h = lane >> 5;
+  const int g16 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+
+  // ---- R image -> LDS: 112 one-KiB pieces, 28 per wave, swizzled sources
+  {
+    const uint16_t* src = Rhi + (long long)b * RPAD * D;
+    for (int piece = wid; piece < FR_IMG / 1024; piece += 4) {
+      const int o = piece * 1024 + lane * 16;
+      const int half = o / (RPAD * 256), rem = o % (RPAD * 256);
+      const int row = rem / 256, pc = (rem % 256) / 16;
+      const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
+      const int col = half * 128 + ((pc ^ sw) << 3);
+      __builtin_amdgcn_global_load_lds((const void*)(src + row * D + col),
+                                       (LDS_AS void*)(lds_base() + piece * 1024), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const uint32_t et = FR_OFF_ET + wid * 2048;
+  const uint32_t tok = FR_OFF_TOK + wid * 256;
+
+  for (int i = c0 + wid; i < c1; i += 4) {
+    bf16x8 Wc[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      Wc[s] = as_bf8(*(const uint4*)(Whi + ((long long)i * TPAD + lr) * D + s * 16 + h * 8));
+    const int len = lens[i];
+    // ---- GEMM1: S^T[t][r] = W[t][d] R[r][d]
+    f32x16 S[NRT];
+#pragma unroll
+    for (int j = 0; j < NRT; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) S[j][q] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+#pragma unroll
+      for (int j = 0; j < NRT; ++j) {
+        const bf16x8 bb = as_bf8(lds_ld16(roff(j * 32 + lr, s * 16 + h * 8)));
+        S[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Wc[s], bb, S[j], 0, 0, 0);
+      }
+    }
+    // ---- softmax over words per region; E overwrites S; per-token Z and N
+    float zp[16], np[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) zp[q] = np[q] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NRT; ++j) {
+      const bool rvalid = j * 32 + lr < NREG;
+      float m = -INFINITY;
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (acc_row(q, h) < len) m = fmaxf(m, S[j][q]);
+      m = fmaxf(m, __shfl_xor(m, 32));
+      float p[16], sum = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        p[q] = acc_row(q, h) < len ? __expf(S[j][q] - m) : 0.f;
+        sum += p[q];
+      }
+      sum += __shfl_xor(sum, 32);
+      const float inv = 1.f / sum;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const bool ok = rvalid && acc_row(q, h) < len;
+        const float e = ok ? __expf(g1 * (p[q] * inv)) : 0.f;
+        zp[q] += e;
+        np[q] += e * S[j][q];
+        S[j][q] = e;
+      }
+    }
+    const float zr = rs16(zp, lr), nr = rs16(np, lr);
+    if ((lr & 1) == 0) {
+      const int t = acc_row(rs16_index(lr), h);
+      lds_stf(tok + t * 4, zr);
+      lds_stf(tok + 128 + t * 4, nr);
+    }
+    if (att && b + img_offset == i) {
+      // attention map of the matching pair: A2[t][r] = E[t][r] / Z_t
+      float* dst = att + (long long)b * att_T * NREG;
+#pragma unroll
+      for (int j = 0; j < NRT; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int tt = acc_row(q, h), r = j * 32 + lr;
+          if (tt < len && tt < att_T && r < NREG)
+            dst[tt * NREG + r] = S[j][q] / lds_ldf(tok + tt * 4);
+        }
+    }
+    // ---- GEMM2: C^T[d][t] = R[r][d] E[t][r], region tile by tile
+    f32x16 C[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) C[j][q] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NRT; ++j) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint16_t hh[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hh[k] = bf_bits(S[j][4 * g + k]);
+        lds_st8(et + lr * 64 + (8 * g + 4 * h) * 2,
+                make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3])));
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int rb = 16 * s + 8 * h;
+        const uint32_t eo = et + (rb + q4) * 64 + (16 * (g16 & 1) + 4 * p4) * 2;
+        const bf16x8 bb = join_tr(lds_tr4(eo), lds_tr4(eo + 4 * 64));
+        const int r0 = j * 32 + rb + q4;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          const int col = dt * 32 + 16 * (g16 & 1) + 4 * p4;
+          const bf16x8 aa = join_tr(lds_tr4(roff(r0, col)), lds_tr4(roff(r0 + 4, col)));
+          C[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aa, bb, C[dt], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // ---- per-token epilogue (lane t = lr)
+    const int t = lr;
+    float csq = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) csq += C[dt][q] * C[dt][q];
+    csq += __shfl_xor(csq, 32);
+    const float Z = lds_ldf(tok + t * 4);
+    const float nhat = lds_ldf(tok + 128 + t * 4);
+    const bool tvalid = t < len;
+    const float zinv = 1.f / Z;
+    const float cn = sqrtf(csq) * zinv;
+    const float n = nhat * zinv;
+    const float u = Wnorm[(long long)i * TPAD + t];
+    const float cosv = n / fmaxf(u * cn, eps);
+    float ex = tvalid ? __expf(g2 * cosv) : 0.f;
+    ex = half_sum(ex);
+    const long long pair = (long long)b * B_cap + i;
+    if (lane == 0) logits[(long long)b * ld_logits + i] = g3 * __logf(ex);
+    if (stats && h == 0)
+      stats[pair * TPAD + t] =
+          tvalid ? make_float4(Z, n, cn, cosv) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (Chi) store_cq<MODE_BF16>(Chi, nullptr, pair, t, h, tvalid, zinv, C);
+  }
+}
+
 // ------------------------------------------------------------------ bwd ---
-// X image: 2 halves x [64 rows][128 cols] bf16, 256-B rows, XOR-swizzled
-// 16-B chunks so both the row reads (ds_read_b128) and the transposed reads
-// (ds_read_b64_tr_b16) are conflict-free.
+// Per (pair, token) backward scalars, from the forward stats and dL/dlogits:
+//   dcos_t = g3 * dlogit * g2 * softmax_t(g2 cos)            (losses.py:107-122)
+//   dC_t   = alpha_t W_t + beta_t C_t                          (d cos / d C_t)
+//   sigma_t = sum_r A2[t,r] dA2[t,r] = dC_t . C_t               (softmax-2 bwd)
+// stored as 8 floats {1/Z, alpha, beta, sigma, valid, 0, 0, 0} so one 1-KiB
+// global_load_lds stages a caption's table.
+__global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ stats,
+                                                     const float* __restrict__ Wnorm,
+                                                     const int* __restrict__ lens,
+                                                     const float* __restrict__ dlogits, int ld,
+                                                     int B_img, int B_cap, float g2, float g3,
+                                                     float eps, float* __restrict__ tok) {
+  const long long pair = (blockIdx.x * 256LL + threadIdx.x) / WAVE;
+  if (pair >= (long long)B_img * B_cap) return;
+  const int b = pair / B_cap, i = pair % B_cap;
+  const int t = threadIdx.x % 32;
+  const int len = lens[i];
+  const bool valid = t < len;
+  const float4 st = valid ? stats[pair * TPAD + t] : make_float4(1.f, 0.f, 0.f, 0.f);
+  const float ex = valid ? __expf(g2 * st.w) : 0.f;
+  const float tot = half_sum(ex);
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (valid) {
+    const float G = dlogits[(long long)b * ld + i] * g3;
+    const float dcos = G * g2 * ex / tot;
+    const float u = Wnorm[(long long)i * TPAD + t];
+    const float cn = st.z, n = st.y, cosv = st.w;
+    float alpha, beta;
+    if (u * cn >= eps) {
+      alpha = dcos / (u * cn);
+      beta = -dcos * cosv / (cn * cn);
+    } else {
+      alpha = dcos / eps;
+      beta = 0.f;
+    }
+    o[0] = 1.f / st.x;
+    o[1] = alpha;
+    o[2] = beta;
+    o[3] = alpha * n + beta * cn * cn;
+    o[4] = 1.f;
+  }
+  if ((threadIdx.x % WAVE) < 32) {
+    float4* dst = (float4*)(tok + (pair * TPAD + t) * 8);
+    dst[0] = make_float4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+  }
+}
+
+// X image: [64 rows][256 cols] bf16 as 2 halves x [64][128], 256-B rows,
+// 16-B chunks XOR-swizzled so the row reads (ds_read_b128) and transposed
+// reads (ds_read_b64_tr_b16) are conflict-free.  Rows 0-31 = W_i, 32-63 = C_bi.
 __device__ __forceinline__ uint32_t xoff(int row, int col) {
   const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
   return (col >> 7) * (64 * 256) + row * 256 + ((((col & 127) >> 3) ^ sw) << 4) + (col & 7) * 2;
 }
-constexpr int B_XIMG = 64 * 256 * 2;               // one bf16 image [64][256]
-constexpr int B_BUF = 2 * B_XIMG + 3 * 32 * 4;     // hi + lo + Zinv, sigma, spare
-constexpr int B_LDS = 2 * B_BUF;
+constexpr int B_XIMG = 64 * 256 * 2;      // one bf16 image
+constexpr int B_TOK = 32 * 32;            // token table, 8 floats per token
 
-// Per-token backward scalars for pair (b, i), one per lane t < 32 of the wave.
-struct TokScal {
-  float alpha, beta, sigma, zinv;
+template <int MODE>
+struct BwdCfg {
+  static constexpr int NIMG = MODE == MODE_SPLIT ? 2 : 1;
+  static constexpr int BUF = NIMG * B_XIMG + B_TOK;
+  static constexpr int LDS = 2 * BUF;
 };
-__device__ __forceinline__ TokScal bwd_tok(const float4* stats, const float* Wnorm,
-                                           const float* dlogits, int ld, int b, int i,
-                                           int B_cap, int len, float g2, float g3, float eps,
-                                           int t) {
-  TokScal r{0.f, 0.f, 0.f, 0.f};
-  const long long pair = (long long)b * B_cap + i;
-  const bool valid = t < len;
-  float4 st = valid ? stats[pair * TPAD + t] : make_float4(1.f, 0.f, 0.f, 0.f);
-  float ex = valid ? __expf(g2 * st.w) : 0.f;
-  const float tot = half_sum(ex);
-  if (!valid) return r;
-  const float G = dlogits[(long long)b * ld + i] * g3;   // d loss / d log-sum
-  const float dcos = G * g2 * ex / tot;
-  const float u = Wnorm[(long long)i * TPAD + t];
-  const float cn = st.z, n = st.y, cosv = st.w;
-  if (u * cn >= eps) {
-    r.alpha = dcos / (u * cn);
-    r.beta = -dcos * cosv / (cn * cn);
-  } else {
-    r.alpha = dcos / eps;
-    r.beta = 0.f;
-  }
-  r.sigma = r.alpha * n + r.beta * cn * cn;
-  r.zinv = 1.f / st.x;
-  return r;
-}
 
-// Stage caption i of image b into LDS buffer `buf`: rows 0-31 = W_i, rows
-// 32-63 = dC = alpha W + beta C; plus Zinv/sigma per token.
-__device__ __forceinline__ void bwd_stage(int buf, const uint16_t* Whi, const uint16_t* Wlo,
-                                          const float* Cbuf, const float4* stats,
-                                          const float* Wnorm, const int* lens,
-                                          const float* dlogits, int ld, int b, int i, int B_cap,
-                                          float g2, float g3, float eps, int tid) {
-  const uint32_t base = buf * B_BUF;
-  const int lane = tid % WAVE;
-  const int len = lens[i];
-  const TokScal ts = bwd_tok(stats, Wnorm, dlogits, ld, b, i, B_cap, len, g2, g3, eps, lane & 31);
-  if (tid < 32) {
-    lds_stf(base + 2 * B_XIMG + tid * 4, ts.zinv);
-    lds_stf(base + 2 * B_XIMG + 128 + tid * 4, ts.sigma);
+// Stage caption i of image b into LDS buffer `base` with global_load_lds:
+// pure copies (no registers), swizzled source addresses so the lane-linear
+// LDS writes land in the swizzled image.
+template <int MODE>
+__device__ __forceinline__ void bwd_stage(uint32_t base, const uint16_t* Whi, const uint16_t* Wlo,
+                                          const uint16_t* Chi, const uint16_t* Clo,
+                                          const float* tok, long long pair, int i, int wid,
+                                          int lane) {
+  constexpr int NIMG = BwdCfg<MODE>::NIMG;
+  // 32 one-KiB pieces per image: piece p covers rows 4*(p%16)..+3 of half p/16
+  for (int k = wid; k < 32 * NIMG; k += 4) {
+    const int img = k / 32, p = k % 32;
+    const int half = p / 16;
+    const int row = 4 * (p % 16) + lane / 16, pc = lane % 16;
+    const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
+    const int c = half * 16 + (pc ^ sw);           // 16-B chunk index along d
+    const uint16_t* src;
+    if (row < 32)
+      src = (img ? Wlo : Whi) + ((long long)i * TPAD + row) * D + c * 8;
+    else
+      src = (img ? Clo : Chi) + ((pair * 32 + c) * 32 + (row - 32)) * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (LDS_AS void*)(lds_base() + base + img * B_XIMG +
+                                                    half * (64 * 256) + 4 * (p % 16) * 256),
+                                     16, 0, 0);
   }
-  const long long cap_off = (long long)i * TPAD * D;
-  const long long pair = (long long)b * B_cap + i;
-  // 32 tokens x 32 pieces of 8 d; 4 pieces per thread
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int p = tid + 256 * k;
-    const int t = p / 32, seg = p % 32;
-    const int col = seg * 8;
-    const uint4 wh = *(const uint4*)(Whi + cap_off + t * D + col);
-    const uint4 wl = *(const uint4*)(Wlo + cap_off + t * D + col);
-    lds_st16(base + xoff(t, col), wh);
-    lds_st16(base + B_XIMG + xoff(t, col), wl);
-    const float a = __shfl(ts.alpha, t), bb = __shfl(ts.beta, t);
-    const float* cp = Cbuf + (pair * TPAD + t) * D + col;
-    const float4 c0 = *(const float4*)cp, c1 = *(const float4*)(cp + 4);
-    const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-    const uint32_t* whp = &wh.x;
-    const uint32_t* wlp = &wl.x;
-    uint32_t oh[4], ol[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      uint16_t h0, l0, h1, l1;
-      const float w0 = bf_val(whp[e] & 0xffff) + bf_val(wlp[e] & 0xffff);
-      const float w1 = bf_val(whp[e] >> 16) + bf_val(wlp[e] >> 16);
-      split2(a * w0 + bb * cv[2 * e], h0, l0);
-      split2(a * w1 + bb * cv[2 * e + 1], h1, l1);
-      oh[e] = pack2(h0, h1);
-      ol[e] = pack2(l0, l1);
-    }
-    lds_st16(base + xoff(32 + t, col), make_uint4(oh[0], oh[1], oh[2], oh[3]));
-    lds_st16(base + B_XIMG + xoff(32 + t, col), make_uint4(ol[0], ol[1], ol[2], ol[3]));
-  }
+  if (wid == 3)
+    __builtin_amdgcn_global_load_lds((const void*)(tok + pair * TPAD * 8 + lane * 4),
+                                     (LDS_AS void*)(lds_base() + base + NIMG * B_XIMG), 16, 0,
+                                     0);
 }
 
 template <int MODE>
 __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Rlo,
-    const uint16_t* __restrict__ Whi, const uint16_t* __restrict__ Wlo,
-    const float* __restrict__ Wnorm, const int* __restrict__ lens, int B_img, int B_cap,
-    int n_chunks, float g1, float g2, float g3, float eps, const float* __restrict__ dlogits,
-    int ld, const float4* __restrict__ stats, const float* __restrict__ Cbuf,
-    float* __restrict__ slab) {
+    const uint16_t* __restrict__ Whi, const uint16_t* __restrict__ Wlo, int B_img, int B_cap,
+    int n_chunks, float g1, const float* __restrict__ tok, const uint16_t* __restrict__ Chi,
+    const uint16_t* __restrict__ Clo, float* __restrict__ slab) {
+  constexpr int NIMG = BwdCfg<MODE>::NIMG;
+  constexpr int BUF = BwdCfg<MODE>::BUF;
   const int total = n_chunks * 2 * B_img;
   const int work = xcd_remap(blockIdx.x, total);
   const int b = work / (2 * n_chunks);
@@ -449,14 +643,15 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
   const int rt = tg * 4 + wid;
   const bool active = rt < NRT;
   const int r = rt * 32 + lr;
+  const bool rvalid = active && r < NREG;
 
   // R tile as B-operand fragments: lane (r, h), k-step s -> d = 16 s + 8 h
   bf16x8 Rh[16], Rl[16];
-  const long long roff = ((long long)b * RPAD + (active ? r : 0)) * D;
+  const long long roff_ = ((long long)b * RPAD + (active ? r : 0)) * D;
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
-    Rh[s] = as_bf8(*(const uint4*)(Rhi + roff + s * 16 + h * 8));
-    Rl[s] = MODE == MODE_SPLIT ? as_bf8(*(const uint4*)(Rlo + roff + s * 16 + h * 8)) : Rh[s];
+    Rh[s] = as_bf8(*(const uint4*)(Rhi + roff_ + s * 16 + h * 8));
+    Rl[s] = MODE == MODE_SPLIT ? as_bf8(*(const uint4*)(Rlo + roff_ + s * 16 + h * 8)) : Rh[s];
   }
   f32x16 dR[8];
 #pragma unroll
@@ -464,17 +659,23 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
 #pragma unroll
     for (int q = 0; q < 16; ++q) dR[j][q] = 0.f;
 
-  if (c0 < c1)
-    bwd_stage(0, Whi, Wlo, Cbuf, stats, Wnorm, lens, dlogits, ld, b, c0, B_cap, g2, g3, eps, tid);
+  if (c0 < c1) {
+    bwd_stage<MODE>(0, Whi, Wlo, Chi, Clo, tok, (long long)b * B_cap + c0, c0, wid, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
 
   const int g16 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
   for (int i = c0; i < c1; ++i) {
-    const int buf = (i - c0) & 1;
-    const uint32_t base = buf * B_BUF;
+    const uint32_t base = ((i - c0) & 1) * BUF;
+    // prefetch the next caption into the other buffer (read last iteration,
+    // released by the barrier that ended it)
+    if (i + 1 < c1)
+      bwd_stage<MODE>(base ^ BUF, Whi, Wlo, Chi, Clo, tok, (long long)b * B_cap + i + 1, i + 1,
+                      wid, lane);
     if (active) {
-      const int len = lens[i];
-      // ---- [S^T ; dA2^T] = [W ; dC] R_tile^T  (M = 64 tokens, N = 32 regions)
+      const uint32_t tk = base + NIMG * B_XIMG;
+      // ---- [S^T ; Q^T] = [W ; C] R_tile^T  (M = 64 tokens, N = 32 regions)
       f32x16 A0, A1;
 #pragma unroll
       for (int q = 0; q < 16; ++q) A0[q] = A1[q] = 0.f;
@@ -492,16 +693,26 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
         mma<MODE>(A1, c_hi, c_lo, Rh[s], Rl[s]);
       }
       // ---- softmax forward recompute + both softmax backwards (registers)
-      const bool rvalid = r < NREG;
+      float zinv[16], alpha[16], beta[16], sig[16], valid[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int t = acc_row(q, h);
+        const uint4 v0 = lds_ld16(tk + t * 32);
+        zinv[q] = __uint_as_float(v0.x);
+        alpha[q] = __uint_as_float(v0.y);
+        beta[q] = __uint_as_float(v0.z);
+        sig[q] = __uint_as_float(v0.w);
+        valid[q] = lds_ldf(tk + t * 32 + 16);
+      }
       float m = -INFINITY;
 #pragma unroll
       for (int q = 0; q < 16; ++q)
-        if (acc_row(q, h) < len) m = fmaxf(m, A0[q]);
+        if (valid[q] != 0.f) m = fmaxf(m, A0[q]);
       m = fmaxf(m, __shfl_xor(m, 32));
       float a1[16], sum = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        a1[q] = acc_row(q, h) < len ? __expf(A0[q] - m) : 0.f;
+        a1[q] = valid[q] != 0.f ? __expf(A0[q] - m) : 0.f;
         sum += a1[q];
       }
       sum += __shfl_xor(sum, 32);
@@ -509,25 +720,26 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
       float a2[16], da1[16], rho = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int t = acc_row(q, h);
         a1[q] *= inv;
-        const bool ok = rvalid && t < len;
-        const float zinv = lds_ldf(base + 2 * B_XIMG + t * 4);
-        const float sig = lds_ldf(base + 2 * B_XIMG + 128 + t * 4);
-        a2[q] = ok ? __expf(g1 * a1[q]) * zinv : 0.f;
-        da1[q] = g1 * a2[q] * (A1[q] - sig);
+        a2[q] = rvalid ? __expf(g1 * a1[q]) * zinv[q] : 0.f;
+        const float da2 = alpha[q] * A0[q] + beta[q] * A1[q];
+        da1[q] = g1 * a2[q] * (da2 - sig[q]);
         rho += a1[q] * da1[q];
       }
       rho += __shfl_xor(rho, 32);
-      float ds[16];
+      float mw[16], mc[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) ds[q] = rvalid ? a1[q] * (da1[q] - rho) : 0.f;
-      // ---- A fragments of M = [dS | A2] (accumulator-as-operand, k permuted)
+      for (int q = 0; q < 16; ++q) {
+        const float ds = rvalid ? a1[q] * (da1[q] - rho) : 0.f;
+        mw[q] = ds + alpha[q] * a2[q];
+        mc[q] = beta[q] * a2[q];
+      }
+      // ---- A fragments of M = [dS + alpha A2 | beta A2] (accumulator-as-operand)
       bf16x8 Mh[4], Ml[4];
-      frag8<MODE>(ds, Mh[0], Ml[0]);
-      frag8<MODE>(ds + 8, Mh[1], Ml[1]);
-      frag8<MODE>(a2, Mh[2], Ml[2]);
-      frag8<MODE>(a2 + 8, Mh[3], Ml[3]);
+      frag8<MODE>(mw, Mh[0], Ml[0]);
+      frag8<MODE>(mw + 8, Mh[1], Ml[1]);
+      frag8<MODE>(mc, Mh[2], Ml[2]);
+      frag8<MODE>(mc + 8, Mh[3], Ml[3]);
       // ---- dR_tile[r][d] += sum_k M[r][k] X[k][d]
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) {
@@ -544,9 +756,7 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
         }
       }
     }
-    if (i + 1 < c1)
-      bwd_stage(buf ^ 1, Whi, Wlo, Cbuf, stats, Wnorm, lens, dlogits, ld, b, i + 1, B_cap, g2,
-                g3, eps, tid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   if (!active) return;
@@ -598,25 +808,29 @@ int tgfr_prep_rows(const float* x, long long s_item, long long s_row, long long 
 int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, const float* Wnorm, const int* lens, int B_img, int B_cap,
                 int img_offset, float gamma1, float gamma2, float gamma3, float eps,
-                float* logits, int ld_logits, float* stats, float* Cout, float* att,
-                int att_T, int mode, void* stream) {
+                float* logits, int ld_logits, float* stats, uint16_t* Chi, uint16_t* Clo,
+                float* att, int att_T, int mode, void* stream) {
   if (B_img <= 0 || B_cap <= 0 || ld_logits < B_cap) return 1001;
   const int grid = ((B_cap + 3) / 4) * B_img;
   auto* s = (hipStream_t)stream;
   static bool once = [] {
     allow_lds(wr_fwd_kernel<MODE_SPLIT>, F_LDS);
     allow_lds(wr_fwd_kernel<MODE_BF16>, F_LDS);
+    allow_lds(wr_fwd_res_kernel, FR_LDS);
     return true;
   }();
   (void)once;
   if (mode == MODE_SPLIT)
     hipLaunchKernelGGL(wr_fwd_kernel<MODE_SPLIT>, dim3(grid), dim3(256), F_LDS, s, Rhi, Rlo,
                        Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1, gamma2, gamma3,
-                       eps, logits, ld_logits, (float4*)stats, Cout, att, att_T);
-  else if (mode == MODE_BF16)
-    hipLaunchKernelGGL(wr_fwd_kernel<MODE_BF16>, dim3(grid), dim3(256), F_LDS, s, Rhi, Rlo,
-                       Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1, gamma2, gamma3,
-                       eps, logits, ld_logits, (float4*)stats, Cout, att, att_T);
+                       eps, logits, ld_logits, (float4*)stats, Chi, Clo, att, att_T);
+  else if (mode == MODE_BF16) {
+    // R resident in LDS; caption chunks sized for >= ~256 workgroups
+    const int n_chunks = max(1, min((B_cap + 3) / 4, (256 + B_img - 1) / B_img));
+    hipLaunchKernelGGL(wr_fwd_res_kernel, dim3(n_chunks * B_img), dim3(256), FR_LDS, s, Rhi,
+                       Whi, Wnorm, lens, B_img, B_cap, n_chunks, img_offset, gamma1, gamma2,
+                       gamma3, eps, logits, ld_logits, (float4*)stats, Chi, att, att_T);
+  }
   else
     return 1002;
   return (int)hipGetLastError();
@@ -625,25 +839,30 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, const float* Wnorm, const int* lens, int B_img, int B_cap,
                 int n_chunks, float gamma1, float gamma2, float gamma3, float eps,
-                const float* dlogits, int ld, const float* stats, const float* Cbuf,
-                float* slab, int mode, void* stream) {
+                const float* dlogits, int ld, const float* stats, const uint16_t* Chi,
+                const uint16_t* Clo, float* tok_ws, float* slab, int mode, void* stream) {
   if (B_img <= 0 || B_cap <= 0 || n_chunks <= 0 || n_chunks > B_cap) return 1001;
-  const int grid = n_chunks * 2 * B_img;
+  if (mode == MODE_SPLIT && (!Rlo || !Wlo || !Clo)) return 1001;
   auto* s = (hipStream_t)stream;
   static bool once = [] {
-    allow_lds(wr_bwd_kernel<MODE_SPLIT>, B_LDS);
-    allow_lds(wr_bwd_kernel<MODE_BF16>, B_LDS);
+    allow_lds(wr_bwd_kernel<MODE_SPLIT>, BwdCfg<MODE_SPLIT>::LDS);
+    allow_lds(wr_bwd_kernel<MODE_BF16>, BwdCfg<MODE_BF16>::LDS);
     return true;
   }();
   (void)once;
+  const long long pairs = (long long)B_img * B_cap;
+  hipLaunchKernelGGL(wr_tok_kernel, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, s,
+                     (const float4*)stats, Wnorm, lens, dlogits, ld, B_img, B_cap, gamma2,
+                     gamma3, eps, tok_ws);
+  const int grid = n_chunks * 2 * B_img;
   if (mode == MODE_SPLIT)
-    hipLaunchKernelGGL(wr_bwd_kernel<MODE_SPLIT>, dim3(grid), dim3(256), B_LDS, s, Rhi, Rlo,
-                       Whi, Wlo, Wnorm, lens, B_img, B_cap, n_chunks, gamma1, gamma2, gamma3,
-                       eps, dlogits, ld, (const float4*)stats, Cbuf, slab);
+    hipLaunchKernelGGL(wr_bwd_kernel<MODE_SPLIT>, dim3(grid), dim3(256),
+                       BwdCfg<MODE_SPLIT>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
+                       gamma1, tok_ws, Chi, Clo, slab);
   else if (mode == MODE_BF16)
-    hipLaunchKernelGGL(wr_bwd_kernel<MODE_BF16>, dim3(grid), dim3(256), B_LDS, s, Rhi, Rlo,
-                       Whi, Wlo, Wnorm, lens, B_img, B_cap, n_chunks, gamma1, gamma2, gamma3,
-                       eps, dlogits, ld, (const float4*)stats, Cbuf, slab);
+    hipLaunchKernelGGL(wr_bwd_kernel<MODE_BF16>, dim3(grid), dim3(256),
+                       BwdCfg<MODE_BF16>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
+                       gamma1, tok_ws, Chi, Clo, slab);
   else
     return 1002;
   return (int)hipGetLastError();
@@ -658,7 +877,9 @@ int tgfr_wr_reduce(const float* slab, int n_chunks, int B_img, float* out, long 
   return (int)hipGetLastError();
 }
 
-int tgfr_wr_lds_bytes(int which) { return which == 0 ? F_LDS : B_LDS; }
+int tgfr_wr_lds_bytes(int which) {
+  return which == 0 ? F_LDS : which == 1 ? BwdCfg<MODE_SPLIT>::LDS : FR_LDS;
+}
 
 int tgfr_version(void) { return 100; }
 

@@ -85,31 +85,36 @@ class WordRegionLogits(torch.autograd.Function):
                                        want_norms=True)
         logits = torch.empty(b_img, b_cap, dtype=torch.float32, device=dev)
         stats = torch.empty(b_img, b_cap, TPAD, 4, dtype=torch.float32, device=dev)
-        cbuf = torch.empty(b_img, b_cap, TPAD, D, dtype=torch.float32, device=dev)
+        m = _mode(mode)
+        # C for the backward: bf16 hi (+lo in fp32 mode), chunk-major [pair][32][32][8]
+        c_hi = torch.empty(b_img, b_cap, 32, TPAD, 8, dtype=torch.int16, device=dev)
+        c_lo = torch.empty_like(c_hi) if m == MODES["fp32"] else None
         att = torch.zeros(b_img, att_T, NREG, dtype=torch.float32, device=dev) \
             if att_T else None
-        m = _mode(mode)
         call("tgfr_wr_fwd", ptr(r_hi), ptr(r_lo), ptr(w_hi), ptr(w_lo), ptr(w_norm),
              ptr(lens), b_img, b_cap, img_offset, gamma1, gamma2, gamma3, eps,
-             ptr(logits), b_cap, ptr(stats), ptr(cbuf), ptr(att), att_T, m,
+             ptr(logits), b_cap, ptr(stats), ptr(c_hi), ptr(c_lo), ptr(att), att_T, m,
              _hip.stream())
-        ctx.save_for_backward(r_hi, r_lo, w_hi, w_lo, w_norm, lens, stats, cbuf)
+        ctx.save_for_backward(r_hi, r_lo, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo)
         ctx.cfg = (gamma1, gamma2, gamma3, eps, m, img_features.shape)
         ctx.mark_non_differentiable(*([att] if att is not None else []))
         return (logits, att) if att is not None else logits
 
     @staticmethod
     def backward(ctx, dlogits, *unused):
-        r_hi, r_lo, w_hi, w_lo, w_norm, lens, stats, cbuf = ctx.saved_tensors
+        r_hi, r_lo, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo = ctx.saved_tensors
         gamma1, gamma2, gamma3, eps, m, shape = ctx.cfg
         b_img, b_cap = stats.shape[0], stats.shape[1]
         dlogits = dlogits.float().contiguous()
         chunks = bwd_chunks(b_img, b_cap)
         slab = torch.empty(chunks, b_img, RPAD, D, dtype=torch.float32,
                            device=dlogits.device)
-        call("tgfr_wr_bwd", ptr(r_hi), ptr(r_lo), ptr(w_hi), ptr(w_lo), ptr(w_norm),
-             ptr(lens), b_img, b_cap, chunks, gamma1, gamma2, gamma3, eps,
-             ptr(dlogits), b_cap, ptr(stats), ptr(cbuf), ptr(slab), m, _hip.stream())
+        tok = torch.empty(b_img, b_cap, TPAD, 8, dtype=torch.float32, device=dlogits.device)
+        split = m == MODES["fp32"]
+        call("tgfr_wr_bwd", ptr(r_hi), ptr(r_lo) if split else None, ptr(w_hi),
+             ptr(w_lo) if split else None, ptr(w_norm), ptr(lens), b_img, b_cap, chunks,
+             gamma1, gamma2, gamma3, eps, ptr(dlogits), b_cap, ptr(stats), ptr(c_hi),
+             ptr(c_lo), ptr(tok), ptr(slab), m, _hip.stream())
         d_reg = torch.empty(b_img, NREG, D, dtype=torch.float32, device=dlogits.device)
         call("tgfr_wr_reduce", ptr(slab), chunks, b_img, ptr(d_reg), NREG * D, D, 1, 0,
              _hip.stream())

@@ -137,6 +137,35 @@ int tgfr_attn_softmax(const float* S, float* P, float* lse, long long rows, int 
 int tgfr_attn_softmax_bwd(const float* P, const float* dP, float* dS, long long rows, int n,
                           long long ld, float scale, void* stream);
 
+/* y = x / max(|x|, eps) per row (F.normalize; ProjectionHead models/models.py:119,
+ * ArcMarginProduct models/metrics.py:44); inv_norm[row] = 1 / max(|x|, eps). */
+int tgfr_l2norm_rows(const float* x, long long ldx, int rows, int d, float eps, float* y,
+                     long long ldy, float* inv_norm, void* stream);
+
+/* dx = (dy - y (y.dy)) * inv_norm (rows with |x| <= eps: dx = dy / eps). */
+int tgfr_l2norm_rows_bwd(const float* dy, long long lddy, const float* y, long long ldy,
+                         const float* inv_norm, int rows, int d, float eps, float* dx,
+                         long long lddx, void* stream);
+
+/* ArcMarginProduct margin (models/metrics.py:45-57) on a [rows x cols] cosine
+ * matrix: out = s * (label column ? phi(cos) : cos). */
+int tgfr_arc_margin(const float* cosv, const long long* label, int rows, int cols, float s,
+                    float m, int easy, float* out, void* stream);
+
+/* d cos from d out for tgfr_arc_margin. */
+int tgfr_arc_margin_bwd(const float* cosv, const long long* label, const float* dout, int rows,
+                        int cols, float s, float m, int easy, float* dcos, void* stream);
+
+/* FocalLoss (models/losses.py:313-325): logp = mean_b CE(L_b, label_b),
+ * loss[0] = (1 - exp(-logp))^gamma * logp; ws receives rows + 1 floats
+ * (row LSE, logp) for the backward. */
+int tgfr_focal_ce(const float* L, int rows, int cols, const long long* label, float gamma,
+                  float* ws, float* loss, void* stream);
+
+/* dL = gscale[0] * dloss/dlogp * (softmax(L_b) - onehot) / rows. */
+int tgfr_focal_ce_bwd(const float* L, int rows, int cols, const long long* label, float gamma,
+                      const float* ws, const float* gscale, float* dL, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

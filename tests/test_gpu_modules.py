@@ -137,3 +137,48 @@ def test_words_loss_module(gpu):
     np.testing.assert_allclose(att[2][0].cpu().numpy(), g["att_diag"][2], atol=1e-4)
     (l0 + l1).backward()
     assert _relerr(r.grad, g["d_img"]) < 2e-3
+
+
+def test_arc_margin_and_focal(gpu):
+    """ArcMarginProduct (metrics.py:17-60) + FocalLoss (losses.py:313-325):
+    fused kernels vs the oracle / the reference fixture, values and grads."""
+    from oracle import tgfr_oracle as O
+    from text_guided_face_recognition_amd.models.losses import FocalLoss
+    from text_guided_face_recognition_amd.models.metrics import ArcMarginProduct
+    torch.manual_seed(3)
+    x = torch.randn(16, 256)
+    head = ArcMarginProduct(256, 300, s=30, m=0.5).to(gpu)
+    w = head.weight.detach().cpu().clone()
+    lab = torch.randint(0, 300, (16,))
+    xo, wo = x.clone().requires_grad_(), w.clone().requires_grad_()
+    ref = O.focal_loss(O.arc_margin(xo, wo, lab, s=30, m=0.5), lab)
+    ref.backward()
+    xg = x.to(gpu).requires_grad_()
+    out = FocalLoss(gamma=2)(head(xg, lab.to(gpu)), lab.to(gpu))
+    out.backward()
+    assert abs(out.item() - ref.item()) < 1e-4 * max(1.0, abs(ref.item()))
+    assert _relerr(xg.grad, xo.grad.numpy()) < 1e-3
+    assert _relerr(head.weight.grad, wo.grad.numpy()) < 1e-3
+
+    g = load_golden("focal_loss_b8")
+    lg = t(g["logits"]).to(gpu).requires_grad_()
+    fl = FocalLoss(gamma=2)(lg, t(g["target"]).to(gpu))
+    fl.backward()
+    assert abs(fl.item() - float(g["loss"])) < 1e-5
+    assert _relerr(lg.grad, g["d_logits"]) < 1e-4
+
+
+def test_l2norm_rows(gpu):
+    from text_guided_face_recognition_amd import kernels as K
+    torch.manual_seed(4)
+    x = torch.randn(37, 256)
+    x[5] = 1e-14                       # clamped row: y = x / eps
+    xo = x.clone().requires_grad_()
+    y_ref = torch.nn.functional.normalize(xo, dim=-1)
+    probe = torch.randn_like(x)
+    (y_ref * probe).sum().backward()
+    xg = x.to(gpu).requires_grad_()
+    y = K.l2norm_rows(xg)
+    (y * probe.to(gpu)).sum().backward()
+    torch.testing.assert_close(y.cpu(), y_ref.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(xg.grad.cpu(), xo.grad, rtol=1e-4, atol=1e-4)

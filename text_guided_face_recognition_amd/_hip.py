@@ -37,6 +37,12 @@ SIGNATURES = {
     "tgfr_ce_grad": [P, L, I, I, I, F, P, P, P, P, F, F, P, L, P],
     "tgfr_bgemm": [P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, F, I, P, I, I, L, I, P],
     "tgfr_attn_softmax": [P, P, P, L, I, L, F, P],
+    "tgfr_l2norm_rows": [P, L, I, I, F, P, L, P, P],
+    "tgfr_l2norm_rows_bwd": [P, L, P, L, P, I, I, F, P, L, P],
+    "tgfr_arc_margin": [P, P, I, I, F, F, I, P, P],
+    "tgfr_arc_margin_bwd": [P, P, P, I, I, F, F, I, P, P],
+    "tgfr_focal_ce": [P, I, I, P, F, P, P, P],
+    "tgfr_focal_ce_bwd": [P, I, I, P, F, P, P, P, P],
     "tgfr_attn_softmax_bwd": [P, P, P, L, I, L, F, P],
 }
 

@@ -1,0 +1,215 @@
+// Fused elementwise/reduction kernels for the heads around the hot path.
+//
+//   l2norm_rows      y = x / max(|x|, eps) per row       (F.normalize, ProjectionHead
+//                    models/models.py:112-120; ArcMargin models/metrics.py:44)
+//   l2norm_rows_bwd  dx = (dy - y (y.dy)) / max(|x|, eps)   (|x| > eps; else dy / eps)
+//   arc_margin       logits = s * (onehot * phi(cos) + (1 - onehot) * cos) with
+//                    phi = cos m - sin m, sin = sqrt(clamp(1 - cos^2, 0, 1)),
+//                    phi = where(cos > th, phi, cos - mm)   (models/metrics.py:45-57)
+//   arc_margin_bwd   d cos from d logits (the where/clamp branches as torch takes them)
+//   focal_ce         logp = mean_b CE(logits_b, y_b); loss = (1 - e^-logp)^gamma logp
+//                    (FocalLoss, models/losses.py:313-325)
+//   focal_ce_bwd     dlogits = g * dloss/dlogp * (softmax - onehot) / B
+// Each replaces 10-25 PyTorch launches per call with one.
+#include "tgfr_common.h"
+
+using namespace tgfr;
+
+namespace {
+
+// one wave per row
+__global__ __launch_bounds__(256) void l2norm_rows_kernel(const float* __restrict__ x, long long ldx,
+                                                          int rows, int d, float eps,
+                                                          float* __restrict__ y, long long ldy,
+                                                          float* __restrict__ inv_norm) {
+  const long long row = blockIdx.x * 4LL + threadIdx.x / WAVE;
+  const int lane = threadIdx.x % WAVE;
+  if (row >= rows) return;
+  const float* xr = x + row * ldx;
+  float ss = 0.f;
+  for (int c = lane; c < d; c += WAVE) ss += xr[c] * xr[c];
+  ss = wave_sum(ss);
+  const float inv = 1.f / fmaxf(sqrtf(ss), eps);
+  float* yr = y + row * ldy;
+  for (int c = lane; c < d; c += WAVE) yr[c] = xr[c] * inv;
+  if (lane == 0) inv_norm[row] = inv;
+}
+
+__global__ __launch_bounds__(256) void l2norm_rows_bwd_kernel(
+    const float* __restrict__ dy, long long lddy, const float* __restrict__ y, long long ldy,
+    const float* __restrict__ inv_norm, int rows, int d, float eps, float* __restrict__ dx,
+    long long lddx) {
+  const long long row = blockIdx.x * 4LL + threadIdx.x / WAVE;
+  const int lane = threadIdx.x % WAVE;
+  if (row >= rows) return;
+  const float* g = dy + row * lddy;
+  const float* yr = y + row * ldy;
+  const float inv = inv_norm[row];
+  // clamped rows (|x| <= eps) are y = x / eps: a plain scaling, no projection
+  const bool clamped = inv >= 1.f / eps;
+  float dot = 0.f;
+  for (int c = lane; c < d; c += WAVE) dot += yr[c] * g[c];
+  dot = clamped ? 0.f : wave_sum(dot);
+  float* o = dx + row * lddx;
+  for (int c = lane; c < d; c += WAVE) o[c] = (g[c] - yr[c] * dot) * inv;
+}
+
+__global__ __launch_bounds__(256) void arc_margin_kernel(const float* __restrict__ cosv,
+                                                         const long long* __restrict__ label,
+                                                         int rows, int cols, float s, float cos_m,
+                                                         float sin_m, float th, float mm,
+                                                         int easy, float* __restrict__ out) {
+  const long long e = blockIdx.x * 256LL + threadIdx.x;
+  if (e >= (long long)rows * cols) return;
+  const int b = e / cols, c = e % cols;
+  const float cv = cosv[e];
+  float v = cv;
+  if (c == label[b]) {
+    const float sine = sqrtf(fminf(fmaxf(1.f - cv * cv, 0.f), 1.f));
+    const float phi = cv * cos_m - sine * sin_m;
+    v = easy ? (cv > 0.f ? phi : cv) : (cv > th ? phi : cv - mm);
+  }
+  out[e] = v * s;
+}
+
+__global__ __launch_bounds__(256) void arc_margin_bwd_kernel(const float* __restrict__ cosv,
+                                                             const long long* __restrict__ label,
+                                                             const float* __restrict__ dout,
+                                                             int rows, int cols, float s,
+                                                             float cos_m, float sin_m, float th,
+                                                             int easy, float* __restrict__ dcos) {
+  const long long e = blockIdx.x * 256LL + threadIdx.x;
+  if (e >= (long long)rows * cols) return;
+  const int b = e / cols, c = e % cols;
+  const float g = dout[e] * s;
+  float d = g;
+  if (c == label[b]) {
+    const float cv = cosv[e];
+    const bool use_phi = easy ? cv > 0.f : cv > th;
+    if (use_phi) {
+      const float one_m = 1.f - cv * cv;
+      const float sine = sqrtf(fminf(fmaxf(one_m, 0.f), 1.f));
+      // d sine / d cos = -cos / sine inside the clamp range, 0 outside
+      const float dsine = (one_m >= 0.f && one_m <= 1.f) ? -cv / sine : 0.f;
+      d = g * (cos_m - sin_m * dsine);
+    }
+  }
+  dcos[e] = d;
+}
+
+// one block: waves loop over rows; ws[b] = row LSE, ws[rows] = logp
+__global__ __launch_bounds__(1024) void focal_ce_kernel(const float* __restrict__ L, int rows,
+                                                        int cols, const long long* __restrict__ label,
+                                                        float gamma, float* __restrict__ ws,
+                                                        float* __restrict__ loss) {
+  __shared__ float red[16];
+  const int wid = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
+  float acc = 0.f;
+  for (int b = wid; b < rows; b += 16) {
+    const float* r = L + (long long)b * cols;
+    float m = -INFINITY;
+    for (int c = lane; c < cols; c += WAVE) m = fmaxf(m, r[c]);
+    m = wave_max(m);
+    float sum = 0.f;
+    for (int c = lane; c < cols; c += WAVE) sum += __expf(r[c] - m);
+    sum = wave_sum(sum);
+    const float lse = m + __logf(sum);
+    if (lane == 0) {
+      ws[b] = lse;
+      acc += lse - r[label[b]];
+    }
+  }
+  if (lane == 0) red[wid] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < 16; ++k) t += red[k];
+    const float logp = t / rows;
+    const float p = __expf(-logp);
+    ws[rows] = logp;
+    loss[0] = powf(1.f - p, gamma) * logp;
+  }
+}
+
+__global__ __launch_bounds__(256) void focal_ce_bwd_kernel(const float* __restrict__ L, int rows,
+                                                           int cols,
+                                                           const long long* __restrict__ label,
+                                                           float gamma,
+                                                           const float* __restrict__ ws,
+                                                           const float* __restrict__ gscale,
+                                                           float* __restrict__ dL) {
+  const long long e = blockIdx.x * 256LL + threadIdx.x;
+  if (e >= (long long)rows * cols) return;
+  const int b = e / cols, c = e % cols;
+  const float logp = ws[rows];
+  const float p = __expf(-logp);
+  const float q = 1.f - p;
+  // d/dlogp [(1 - e^-logp)^gamma logp] = q^gamma + gamma q^(gamma-1) p logp
+  float dfl = powf(q, gamma);
+  if (gamma != 0.f) dfl += gamma * powf(q, gamma - 1.f) * p * logp;
+  const float g = (gscale ? gscale[0] : 1.f) * dfl / rows;
+  const float sm = __expf(L[e] - ws[b]);
+  dL[e] = g * (sm - (c == label[b] ? 1.f : 0.f));
+}
+
+}  // namespace
+
+extern "C" {
+
+int tgfr_l2norm_rows(const float* x, long long ldx, int rows, int d, float eps, float* y,
+                     long long ldy, float* inv_norm, void* stream) {
+  if (rows <= 0 || d <= 0) return 1001;
+  hipLaunchKernelGGL(l2norm_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0,
+                     (hipStream_t)stream, x, ldx, rows, d, eps, y, ldy, inv_norm);
+  return (int)hipGetLastError();
+}
+
+int tgfr_l2norm_rows_bwd(const float* dy, long long lddy, const float* y, long long ldy,
+                         const float* inv_norm, int rows, int d, float eps, float* dx,
+                         long long lddx, void* stream) {
+  if (rows <= 0 || d <= 0) return 1001;
+  hipLaunchKernelGGL(l2norm_rows_bwd_kernel, dim3((rows + 3) / 4), dim3(256), 0,
+                     (hipStream_t)stream, dy, lddy, y, ldy, inv_norm, rows, d, eps, dx, lddx);
+  return (int)hipGetLastError();
+}
+
+int tgfr_arc_margin(const float* cosv, const long long* label, int rows, int cols, float s,
+                    float m, int easy, float* out, void* stream) {
+  if (rows <= 0 || cols <= 0) return 1001;
+  const long long n = (long long)rows * cols;
+  const float PI = 3.14159265358979323846f;
+  hipLaunchKernelGGL(arc_margin_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, cosv, label, rows, cols, s, cosf(m), sinf(m),
+                     cosf(PI - m), sinf(PI - m) * m, easy, out);
+  return (int)hipGetLastError();
+}
+
+int tgfr_arc_margin_bwd(const float* cosv, const long long* label, const float* dout, int rows,
+                        int cols, float s, float m, int easy, float* dcos, void* stream) {
+  if (rows <= 0 || cols <= 0) return 1001;
+  const long long n = (long long)rows * cols;
+  const float PI = 3.14159265358979323846f;
+  hipLaunchKernelGGL(arc_margin_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, cosv, label, dout, rows, cols, s, cosf(m), sinf(m),
+                     cosf(PI - m), easy, dcos);
+  return (int)hipGetLastError();
+}
+
+int tgfr_focal_ce(const float* L, int rows, int cols, const long long* label, float gamma,
+                  float* ws, float* loss, void* stream) {
+  if (rows <= 0 || cols <= 0) return 1001;
+  hipLaunchKernelGGL(focal_ce_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, L, rows,
+                     cols, label, gamma, ws, loss);
+  return (int)hipGetLastError();
+}
+
+int tgfr_focal_ce_bwd(const float* L, int rows, int cols, const long long* label, float gamma,
+                      const float* ws, const float* gscale, float* dL, void* stream) {
+  if (rows <= 0 || cols <= 0) return 1001;
+  const long long n = (long long)rows * cols;
+  hipLaunchKernelGGL(focal_ce_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, L, rows, cols, label, gamma, ws, gscale, dL);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

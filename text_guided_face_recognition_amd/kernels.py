@@ -354,3 +354,98 @@ class AttentionCore(torch.autograd.Function):
 
 def attention_core(qr, kr, v, scale, mode="fp32"):
     return AttentionCore.apply(qr, kr, v, scale, mode)
+
+
+# ---------------------------------------------------------------- heads ---
+class L2NormRows(torch.autograd.Function):
+    """F.normalize(x, p=2, dim=-1, eps) in one kernel each way."""
+
+    @staticmethod
+    def forward(ctx, x, eps):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).float().contiguous()
+        rows, d = x2.shape
+        y = torch.empty_like(x2)
+        inv = torch.empty(rows, dtype=torch.float32, device=x2.device)
+        call("tgfr_l2norm_rows", ptr(x2), d, rows, d, float(eps), ptr(y), d, ptr(inv),
+             _hip.stream())
+        ctx.save_for_backward(y, inv)
+        ctx.cfg = (float(eps), shape)
+        return y.reshape(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, inv = ctx.saved_tensors
+        eps, shape = ctx.cfg
+        rows, d = y.shape
+        dy2 = dy.reshape(rows, d).float().contiguous()
+        dx = torch.empty_like(y)
+        call("tgfr_l2norm_rows_bwd", ptr(dy2), d, ptr(y), d, ptr(inv), rows, d, eps, ptr(dx),
+             d, _hip.stream())
+        return dx.reshape(shape), None
+
+
+def l2norm_rows(x, eps=1e-12):
+    return L2NormRows.apply(x, eps)
+
+
+class ArcMargin(torch.autograd.Function):
+    """The margin part of ArcMarginProduct on a cosine matrix (metrics.py:45-57)."""
+
+    @staticmethod
+    def forward(ctx, cosine, label, s, m, easy):
+        cosine = cosine.float().contiguous()
+        label = label.to(torch.int64).contiguous()
+        rows, cols = cosine.shape
+        out = torch.empty_like(cosine)
+        call("tgfr_arc_margin", ptr(cosine), ptr(label), rows, cols, float(s), float(m),
+             int(easy), ptr(out), _hip.stream())
+        ctx.save_for_backward(cosine, label)
+        ctx.cfg = (float(s), float(m), int(easy))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        cosine, label = ctx.saved_tensors
+        s, m, easy = ctx.cfg
+        rows, cols = cosine.shape
+        dout = dout.float().contiguous()
+        dcos = torch.empty_like(cosine)
+        call("tgfr_arc_margin_bwd", ptr(cosine), ptr(label), ptr(dout), rows, cols, s, m,
+             easy, ptr(dcos), _hip.stream())
+        return dcos, None, None, None, None
+
+
+def arc_margin(cosine, label, s, m, easy_margin=False):
+    return ArcMargin.apply(cosine, label, s, m, easy_margin)
+
+
+class FocalCE(torch.autograd.Function):
+    """FocalLoss(gamma)(logits, target) (losses.py:313-325)."""
+
+    @staticmethod
+    def forward(ctx, logits, target, gamma):
+        logits = logits.float().contiguous()
+        target = target.to(torch.int64).contiguous()
+        rows, cols = logits.shape
+        ws = torch.empty(rows + 1, dtype=torch.float32, device=logits.device)
+        loss = torch.empty(1, dtype=torch.float32, device=logits.device)
+        call("tgfr_focal_ce", ptr(logits), rows, cols, ptr(target), float(gamma), ptr(ws),
+             ptr(loss), _hip.stream())
+        ctx.save_for_backward(logits, target, ws)
+        ctx.gamma = float(gamma)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, target, ws = ctx.saved_tensors
+        rows, cols = logits.shape
+        g = g.float().contiguous()
+        dl = torch.empty_like(logits)
+        call("tgfr_focal_ce_bwd", ptr(logits), rows, cols, ptr(target), ctx.gamma, ptr(ws),
+             ptr(g), ptr(dl), _hip.stream())
+        return dl, None, None
+
+
+def focal_ce(logits, target, gamma):
+    return FocalCE.apply(logits, target, gamma)

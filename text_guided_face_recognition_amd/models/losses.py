@@ -7,7 +7,7 @@ runs in the gfx950 kernels of libtgfr_hip.so (see kernels.py):
   sent_loss    models/losses.py:19-57    cosine-logit kernel (class mask) + CE
   global_loss  models/losses.py:329-351  cosine-logit kernel + CE
   ClipLoss     models/losses.py:268-309  dot-product logits + CE
-  FocalLoss    models/losses.py:313-325  identity head, plain PyTorch (out of scope)
+  FocalLoss    models/losses.py:313-325  fused focal-CE kernel (identity head)
 
 Extra knobs ride on ``args`` so the call sites stay identical:
   args.precision   "fp32" (split-bf16 MFMA, parity mode; default) or "bf16"
@@ -141,15 +141,13 @@ class ClipLoss(nn.Module):
 
 
 class FocalLoss(nn.Module):
-    """losses.py:313-325 (identity head; stays PyTorch)."""
+    """losses.py:313-325: (1 - e^-logp)^gamma * logp of the batch-mean CE,
+    one fused kernel each way (kernels.FocalCE)."""
 
     def __init__(self, gamma=0, eps=1e-7):
         super().__init__()
         self.gamma = gamma
         self.eps = eps
-        self.ce = nn.CrossEntropyLoss()
 
     def forward(self, input, target):
-        logp = self.ce(input, target)
-        p = torch.exp(-logp)
-        return ((1 - p) ** self.gamma * logp).mean()
+        return K.focal_ce(input, target, self.gamma)

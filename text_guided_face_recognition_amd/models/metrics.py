@@ -1,7 +1,7 @@
 """ArcMarginProduct (models/metrics.py:17-60): the identity head that runs
-after the hot path every step.  Its cosine GEMM runs
-on the split-bf16 MFMA GEMM kernel (kernels.linear_rows); the margin and the
-one-hot (CUDA-only in the reference, :53) are device-side PyTorch ops."""
+after the hot path every step.  Row normalisation,
+the cosine GEMM (split-bf16 MFMA) and the margin (with the one-hot that is
+CUDA-only in the reference, :53) each run as one gfx950 kernel."""
 from __future__ import annotations
 
 import math
@@ -33,14 +33,8 @@ class ArcMarginProduct(nn.Module):
         self.precision = "fp32"
 
     def forward(self, input, label):
-        cosine = K.linear_rows(F.normalize(input), F.normalize(self.weight),
+        # cos = normalize(x) normalize(W)^T on the split-bf16 MFMA GEMM, then the
+        # fused margin kernel (the reference's 15 elementwise ops, :45-57)
+        cosine = K.linear_rows(K.l2norm_rows(input), K.l2norm_rows(self.weight),
                                mode=self.precision)
-        sine = torch.sqrt((1.0 - torch.pow(cosine, 2)).clamp(0, 1))
-        phi = cosine * self.cos_m - sine * self.sin_m
-        if self.easy_margin:
-            phi = torch.where(cosine > 0, phi, cosine)
-        else:
-            phi = torch.where(cosine > self.th, phi, cosine - self.mm)
-        one_hot = torch.zeros_like(cosine)
-        one_hot.scatter_(1, label.view(-1, 1).long(), 1)
-        return ((one_hot * phi) + ((1.0 - one_hot) * cosine)) * self.s
+        return K.arc_margin(cosine, label, self.s, self.m, self.easy_margin)

@@ -35,7 +35,7 @@ class ProjectionHead(nn.Module):
 
     def forward(self, x):
         y = K.linear_rows(x, self.projection.weight, self.projection.bias, mode=self.precision)
-        return F.normalize(y, p=2, dim=-1)
+        return K.l2norm_rows(y)
 
 
 class IMIM(nn.Module):

@@ -157,14 +157,33 @@ int tgfr_arc_margin_bwd(const float* cosv, const long long* label, const float* 
                         int cols, float s, float m, int easy, float* dcos, void* stream);
 
 /* FocalLoss (models/losses.py:313-325): logp = mean_b CE(L_b, label_b),
- * loss[0] = (1 - exp(-logp))^gamma * logp; ws receives rows + 1 floats
- * (row LSE, logp) for the backward. */
+ * loss[0] = (1 - exp(-logp))^gamma * logp; ws receives 2 * rows + 1 floats
+ * (row LSE [rows], logp, row NLL [rows]) for the backward. */
 int tgfr_focal_ce(const float* L, int rows, int cols, const long long* label, float gamma,
                   float* ws, float* loss, void* stream);
 
 /* dL = gscale[0] * dloss/dlogp * (softmax(L_b) - onehot) / rows. */
 int tgfr_focal_ce_bwd(const float* L, int rows, int cols, const long long* label, float gamma,
                       const float* ws, const float* gscale, float* dL, void* stream);
+
+/* ---- per-sample LayerNorm (IMIM ln, models/models.py:388 / :401) -----------
+ * x [rows][E] (row-contiguous, E % 4 == 0, 16-B aligned), affine w, b [E].
+ * y = (x - mean_r) / sqrt(var_r + eps) * w + b with biased var_r, as
+ * nn.LayerNorm([C, H, W]).  ws: tgfr_ln_ws_floats(rows, E, 1) floats; the
+ * forward leaves mean/rstd in it for the backward (pass the same ws). */
+int tgfr_ln_ws_floats(int rows, long long E, int backward, long long* out);
+int tgfr_ln_fwd(const float* x, int rows, long long E, const float* w, const float* b, float eps,
+                float* y, float* ws, void* stream);
+/* dx, dw = sum_r dy xhat, db = sum_r dy (fixed-order reductions). */
+int tgfr_ln_bwd(const float* dy, const float* x, int rows, long long E, const float* w,
+                float* ws, float* dx, float* dw, float* db, void* stream);
+
+/* Bias gradient of a row-wise linear map: db[c] = sum_r dy[r][c].  With y
+ * (the ReLU output) the ReLU mask is applied first and the masked gradient is
+ * written to dym (both set or both NULL).  ws: ceil(rows / 256) * cols floats. */
+int tgfr_bias_grad(const float* dy, long long lddy, int rows, int cols, const float* y,
+                   long long ldy, float* dym, long long lddm, float* db, float* ws,
+                   void* stream);
 
 #ifdef __cplusplus
 }

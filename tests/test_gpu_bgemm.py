@@ -1,0 +1,66 @@
+"""bgemm (csrc/tgfr_attn.hip) against torch fp32 matmul for every operand
+layout the kernel stages (k-contiguous, m/n-contiguous, strided gathers),
+ragged tile edges, split-K, bias/ReLU/accumulate epilogues and both modes.
+Tolerance: fp32 (split-bf16) 2e-5 x sqrt(K) relative to max |C|; bf16 1e-2."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _operand(rows, cols, lay, dev, gen):
+    """[rows, cols] fp32 view with the requested unit-stride axis."""
+    if lay == "row":                     # unit stride on cols
+        return torch.randn(rows, cols, generator=gen).to(dev)
+    if lay == "col":                     # unit stride on rows
+        return torch.randn(cols, rows, generator=gen).to(dev).t()
+    # neither axis unit-stride
+    return torch.randn(rows, 2 * cols, generator=gen).to(dev)[:, ::2]
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+@pytest.mark.parametrize("la", ["row", "col", "any"])
+@pytest.mark.parametrize("lb", ["row", "col", "any"])
+def test_layouts(gpu, mode, la, lb):
+    from text_guided_face_recognition_amd import kernels as K
+    gen = torch.Generator().manual_seed(11)
+    m, n, k = 77, 130, 203                      # ragged in every dimension
+    a = _operand(m, k, la, gpu, gen)
+    b = _operand(k, n, lb, gpu, gen)
+    c = K.bgemm(a.unsqueeze(0), b.unsqueeze(0), mode=mode)[0]
+    ref = a.double() @ b.double()
+    err = (c.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < (2e-5 if mode == "fp32" else 1e-2), err
+
+
+@pytest.mark.parametrize("lay", ["row", "col"])
+def test_split_k_and_batch(gpu, lay):
+    from text_guided_face_recognition_amd import kernels as K
+    gen = torch.Generator().manual_seed(12)
+    a = torch.stack([_operand(40, 3000, lay, gpu, gen) for _ in range(3)])
+    b = torch.stack([_operand(3000, 96, lay, gpu, gen) for _ in range(3)])
+    for ks in (1, 7, 13):
+        c = K.bgemm(a, b, mode="fp32", ksplit=ks)
+        ref = a.double() @ b.double()
+        err = (c.double() - ref).abs().max().item() / ref.abs().max().item()
+        assert err < 1e-5, (ks, err)
+
+
+def test_epilogues(gpu):
+    from text_guided_face_recognition_amd import kernels as K
+    gen = torch.Generator().manual_seed(13)
+    a = _operand(65, 64, "col", gpu, gen).unsqueeze(0)
+    b = _operand(64, 33, "row", gpu, gen).unsqueeze(0)
+    bias = torch.randn(33, generator=gen).to(gpu)
+    ref = torch.relu(0.5 * (a[0].double() @ b[0].double()) + bias.double())
+    c = K.bgemm(a, b, alpha=0.5, bias=bias, relu=True)[0]
+    torch.testing.assert_close(c.double(), ref, rtol=1e-4, atol=2e-4)
+    acc = torch.randn(1, 65, 33, generator=gen).to(gpu)
+    ref2 = acc[0].double() + a[0].double() @ b[0].double()
+    K.bgemm(a, b, out=acc, accumulate=True)
+    torch.testing.assert_close(acc[0].double(), ref2, rtol=1e-4, atol=2e-4)
+    # transposed (column-major) output
+    out = torch.empty(33, 65, device=gpu).t().unsqueeze(0)
+    K.bgemm(a, b, out=out)
+    torch.testing.assert_close(out[0].double(), a[0].double() @ b[0].double(),
+                               rtol=1e-4, atol=2e-4)

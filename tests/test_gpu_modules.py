@@ -182,3 +182,23 @@ def test_l2norm_rows(gpu):
     (y * probe.to(gpu)).sum().backward()
     torch.testing.assert_close(y.cpu(), y_ref.detach(), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(xg.grad.cpu(), xo.grad, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("rows,shape", [(64, (196, 256)), (3, (36, 6, 6)), (1, (4,))])
+def test_layer_norm_rows(gpu, rows, shape):
+    """Per-sample LayerNorm kernel vs torch fp32 F.layer_norm (values, dx, dw, db)."""
+    from text_guided_face_recognition_amd import kernels as K
+    gen = torch.Generator().manual_seed(5)
+    x = (torch.randn(rows, *shape, generator=gen) * 3 + 1.5)
+    w = torch.randn(*shape, generator=gen)
+    b = torch.randn(*shape, generator=gen)
+    probe = torch.randn(rows, *shape, generator=gen)
+    xs = [x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()]
+    ref = torch.nn.functional.layer_norm(xs[0], shape, xs[1], xs[2], 1e-5)
+    (ref * probe).sum().backward()
+    xg = [x.to(gpu).requires_grad_(), w.to(gpu).requires_grad_(), b.to(gpu).requires_grad_()]
+    y = K.layer_norm_rows(*xg, 1e-5)
+    (y * probe.to(gpu)).sum().backward()
+    torch.testing.assert_close(y.detach().cpu(), ref.detach(), rtol=1e-4, atol=1e-4)
+    for a, r in zip(xg, xs):
+        assert _relerr(a.grad, r.grad.numpy()) < 1e-4

@@ -44,6 +44,10 @@ SIGNATURES = {
     "tgfr_focal_ce": [P, I, I, P, F, P, P, P],
     "tgfr_focal_ce_bwd": [P, I, I, P, F, P, P, P, P],
     "tgfr_attn_softmax_bwd": [P, P, P, L, I, L, F, P],
+    "tgfr_ln_ws_floats": [I, L, I, P],
+    "tgfr_bias_grad": [P, L, I, I, P, L, P, L, P, P, P],
+    "tgfr_ln_fwd": [P, I, L, P, P, F, P, P, P],
+    "tgfr_ln_bwd": [P, P, I, L, P, P, P, P, P, P],
 }
 
 

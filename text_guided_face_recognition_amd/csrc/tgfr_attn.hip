@@ -19,45 +19,93 @@ using namespace tgfr;
 namespace {
 
 constexpr int BM = 64, BN = 64, BK = 32;
-constexpr int HALF = 64 * 64;                 // bytes of one [64][32] bf16 tile
+constexpr int HALF = 64 * 64;                 // bytes of one 64x32 bf16 tile
 constexpr int STAGE = 4 * HALF;               // A hi, A lo, B hi, B lo
 
-// [64 rows][32 k] bf16 tile with 64-B rows; chunk swizzle keeps the
-// ds_read_b128 lane groups conflict-free.
+// Operand layouts: LAY_K = k-contiguous (unit k stride), LAY_MN = m- (or n-)
+// contiguous, LAY_ANY = neither (scalar gathers).  Each layout is staged in
+// the LDS layout its global reads coalesce into:
+//   LAY_K / LAY_ANY  [64 mn][32 k]  64-B rows, read with ds_read_b128
+//   LAY_MN           [32 k][64 mn] 128-B rows, read with ds_read_b64_tr_b16
+// so a transposed operand costs neither a copy nor uncoalesced loads.
+enum { LAY_K = 0, LAY_MN = 1, LAY_ANY = 2 };
+
+// [64 mn][32 k]: 16-B chunk swizzle keeps ds_read_b128 lane groups conflict-free.
 __device__ __forceinline__ uint32_t toff(int row, int chunk) {
   return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
+}
+// [32 k][64 mn]: rows 2 apart land 64 B apart, so the 4 rows of one
+// transposed read hit disjoint banks.
+__device__ __forceinline__ uint32_t moff(int krow, int chunk) {
+  return krow * 128 + ((chunk ^ (((krow >> 1) & 1) << 2)) << 4);
 }
 
 struct Frag8 {
   float v[8];
 };
 
-// Load 8 consecutive-k elements of row `row` (a tile row) into f.
-__device__ __forceinline__ void load8(Frag8& f, const float* base, long long s_row,
-                                      long long s_k, int row, int k0, int rows, int K) {
-  const bool vec = (s_k == 1) && (((uintptr_t)(base + row * s_row + k0) & 15) == 0) &&
-                   (k0 + 8 <= K) && (row < rows);
-  if (vec) {
-    const float4 a = *(const float4*)(base + row * s_row + k0);
-    const float4 b = *(const float4*)(base + row * s_row + k0 + 4);
-    f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w;
-    f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
-  } else {
+// Staging role of thread tid for one 64x32 operand tile:
+//   LAY_K/ANY: mn row tid/4, k 8*(tid%4) .. +7
+//   LAY_MN:    k row tid/8,  mn 8*(tid%8) .. +7
+template <int LAY>
+__device__ __forceinline__ void load_tile(Frag8& f, const float* base, long long s_mn,
+                                          long long s_k, int tid, int k0, int mn_lim, int K) {
+  if constexpr (LAY == LAY_MN) {
+    const int k = k0 + (tid >> 3), mn = (tid & 7) * 8;
+    const float* p = base + (long long)k * s_k + mn;
+    if (k < K && mn + 8 <= mn_lim && (((uintptr_t)p & 15) == 0)) {
+      const float4 a = *(const float4*)p;
+      const float4 b = *(const float4*)(p + 4);
+      f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w;
+      f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
+    } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      f.v[e] = (row < rows && k0 + e < K) ? base[row * s_row + (k0 + e) * s_k] : 0.f;
+      for (int e = 0; e < 8; ++e) f.v[e] = (k < K && mn + e < mn_lim) ? p[e] : 0.f;
+    }
+  } else {
+    const int row = tid >> 2, k = k0 + (tid & 3) * 8;
+    const float* p = base + (long long)row * s_mn + (long long)k * s_k;
+    if (LAY == LAY_K && row < mn_lim && k + 8 <= K && (((uintptr_t)p & 15) == 0)) {
+      const float4 a = *(const float4*)p;
+      const float4 b = *(const float4*)(p + 4);
+      f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w;
+      f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        f.v[e] = (row < mn_lim && k + e < K) ? p[(long long)e * s_k] : 0.f;
+    }
   }
 }
 
-template <int MODE>
-__device__ __forceinline__ void store8(uint32_t off_hi, const Frag8& f) {
+template <int MODE, int LAY>
+__device__ __forceinline__ void store_tile(uint32_t base, const Frag8& f, int tid) {
   bf16x8 hi, lo;
   frag8<MODE>(f.v, hi, lo);
-  lds_st16(off_hi, __builtin_bit_cast(uint4, hi));
-  if (MODE == MODE_SPLIT) lds_st16(off_hi + HALF, __builtin_bit_cast(uint4, lo));
+  const uint32_t off =
+      base + (LAY == LAY_MN ? moff(tid >> 3, tid & 7) : toff(tid >> 2, tid & 3));
+  lds_st16(off, __builtin_bit_cast(uint4, hi));
+  if (MODE == MODE_SPLIT) lds_st16(off + HALF, __builtin_bit_cast(uint4, lo));
 }
 
-template <int MODE>
+// MFMA operand fragment: lane (lr, h) gets element [mn = mn0 + lr][k = 16 s + 8 h .. +7].
+template <int LAY>
+__device__ __forceinline__ bf16x8 frag_read(uint32_t base, int mn0, int s, int lane) {
+  if constexpr (LAY == LAY_MN) {
+    // 16-lane group g: mn block 16 (g & 1), k rows 16 s + 8 (g >> 1) (+4);
+    // lane 4q+p addresses k row q, mn columns 4p .. 4p+3
+    const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
+    const int col = mn0 + 16 * (g & 1) + 4 * p;
+    const int kr = 16 * s + 8 * (g >> 1) + q;
+    const uint32_t a = base + moff(kr, col >> 3) + (col & 7) * 2;
+    const uint32_t b = base + moff(kr + 4, col >> 3) + (col & 7) * 2;
+    return join_tr(lds_tr4(a), lds_tr4(b));
+  } else {
+    return as_bf8(lds_ld16(base + toff(mn0 + (lane & 31), 2 * s + (lane >> 5))));
+  }
+}
+
+template <int MODE, int LA, int LB>
 __global__ __launch_bounds__(256) void bgemm_kernel(
     const float* __restrict__ A, long long sAb, long long sAm, long long sAk,
     const float* __restrict__ B, long long sBb, long long sBk, long long sBn,
@@ -80,48 +128,41 @@ __global__ __launch_bounds__(256) void bgemm_kernel(
     }
     return;
   }
-  A += (long long)kb * sAk;
-  B += (long long)kb * sBk;
   const int tid = threadIdx.x, wid = tid / WAVE, lane = tid % WAVE;
   const int lr = lane & 31, h = lane >> 5;
   const int wm = wid >> 1, wn = wid & 1;
-  const float* Ab = A + bt * sAb + m0 * sAm;
-  const float* Bb = B + bt * sBb + n0 * sBn;
-  // staging role: tile row = tid / 4, 8-k chunk = tid % 4
-  const int srow = tid >> 2, sch = tid & 3;
+  const float* Ab = A + bt * sAb + m0 * sAm + (long long)kb * sAk;
+  const float* Bb = B + bt * sBb + n0 * sBn + (long long)kb * sBk;
   Frag8 fa, fb;
   f32x16 acc;
 #pragma unroll
   for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 
   const int nk = (K + BK - 1) / BK;
-  load8(fa, Ab, sAm, sAk, srow, sch * 8, M - m0, K);
-  load8(fb, Bb, sBn, sBk, srow, sch * 8, N - n0, K);
-  store8<MODE>(toff(srow, sch), fa);
-  store8<MODE>(2 * HALF + toff(srow, sch), fb);
+  load_tile<LA>(fa, Ab, sAm, sAk, tid, 0, M - m0, K);
+  load_tile<LB>(fb, Bb, sBn, sBk, tid, 0, N - n0, K);
+  store_tile<MODE, LA>(0, fa, tid);
+  store_tile<MODE, LB>(2 * HALF, fb, tid);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const uint32_t sb = (kt & 1) * STAGE;
     if (kt + 1 < nk) {
-      const int k0 = (kt + 1) * BK + sch * 8;
-      load8(fa, Ab, sAm, sAk, srow, k0, M - m0, K);
-      load8(fb, Bb, sBn, sBk, srow, k0, N - n0, K);
+      load_tile<LA>(fa, Ab, sAm, sAk, tid, (kt + 1) * BK, M - m0, K);
+      load_tile<LB>(fb, Bb, sBn, sBk, tid, (kt + 1) * BK, N - n0, K);
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int ch = 2 * s + h;
-      const uint32_t ao = sb + toff(32 * wm + lr, ch);
-      const uint32_t bo = sb + 2 * HALF + toff(32 * wn + lr, ch);
-      const bf16x8 ahi = as_bf8(lds_ld16(ao));
-      const bf16x8 bhi = as_bf8(lds_ld16(bo));
-      const bf16x8 alo = MODE == MODE_SPLIT ? as_bf8(lds_ld16(ao + HALF)) : ahi;
-      const bf16x8 blo = MODE == MODE_SPLIT ? as_bf8(lds_ld16(bo + HALF)) : bhi;
+      const bf16x8 ahi = frag_read<LA>(sb, 32 * wm, s, lane);
+      const bf16x8 bhi = frag_read<LB>(sb + 2 * HALF, 32 * wn, s, lane);
+      const bf16x8 alo = MODE == MODE_SPLIT ? frag_read<LA>(sb + HALF, 32 * wm, s, lane) : ahi;
+      const bf16x8 blo =
+          MODE == MODE_SPLIT ? frag_read<LB>(sb + 3 * HALF, 32 * wn, s, lane) : bhi;
       mma<MODE>(acc, ahi, alo, bhi, blo);
     }
     if (kt + 1 < nk) {
       const uint32_t nb = ((kt + 1) & 1) * STAGE;
-      store8<MODE>(nb + toff(srow, sch), fa);
-      store8<MODE>(nb + 2 * HALF + toff(srow, sch), fb);
+      store_tile<MODE, LA>(nb, fa, tid);
+      store_tile<MODE, LB>(nb + 2 * HALF, fb, tid);
     }
     __syncthreads();
   }
@@ -190,18 +231,26 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
                int mode, void* stream) {
   if (batch <= 0 || M <= 0 || N <= 0 || K <= 0 || ksplit <= 0) return 1001;
   if (ksplit > 1 && (bias || relu || accumulate)) return 1001;
+  if (mode != MODE_SPLIT && mode != MODE_BF16) return 1002;
   const dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch * ksplit);
   auto* s = (hipStream_t)stream;
-  if (mode == MODE_SPLIT)
-    hipLaunchKernelGGL(bgemm_kernel<MODE_SPLIT>, grid, dim3(256), 2 * STAGE, s, A, sAb, sAm,
-                       sAk, B, sBb, sBk, sBn, C, sCb, sCm, sCn, M, N, K, alpha, accumulate,
-                       bias, relu, ksplit, sCsplit);
-  else if (mode == MODE_BF16)
-    hipLaunchKernelGGL(bgemm_kernel<MODE_BF16>, grid, dim3(256), 2 * STAGE, s, A, sAb, sAm,
-                       sAk, B, sBb, sBk, sBn, C, sCb, sCm, sCn, M, N, K, alpha, accumulate,
-                       bias, relu, ksplit, sCsplit);
-  else
-    return 1002;
+  const int la = sAk == 1 ? LAY_K : sAm == 1 ? LAY_MN : LAY_ANY;
+  const int lb = sBk == 1 ? LAY_K : sBn == 1 ? LAY_MN : LAY_ANY;
+  using Fn = void (*)(const float*, long long, long long, long long, const float*, long long,
+                      long long, long long, float*, long long, long long, long long, int, int,
+                      int, float, int, const float*, int, int, long long);
+#define TGFR_BG(MD, A_, B_) &bgemm_kernel<MD, A_, B_>
+#define TGFR_BG_ROW(MD, A_) TGFR_BG(MD, A_, LAY_K), TGFR_BG(MD, A_, LAY_MN), TGFR_BG(MD, A_, LAY_ANY)
+  static const Fn table[2][3][3] = {
+      {{TGFR_BG_ROW(MODE_BF16, LAY_K)}, {TGFR_BG_ROW(MODE_BF16, LAY_MN)},
+       {TGFR_BG_ROW(MODE_BF16, LAY_ANY)}},
+      {{TGFR_BG_ROW(MODE_SPLIT, LAY_K)}, {TGFR_BG_ROW(MODE_SPLIT, LAY_MN)},
+       {TGFR_BG_ROW(MODE_SPLIT, LAY_ANY)}}};
+#undef TGFR_BG_ROW
+#undef TGFR_BG
+  hipLaunchKernelGGL(table[mode][la][lb], grid, dim3(256), 2 * STAGE, s, A, sAb, sAm, sAk, B,
+                     sBb, sBk, sBn, C, sCb, sCm, sCn, M, N, K, alpha, accumulate, bias, relu,
+                     ksplit, sCsplit);
   return (int)hipGetLastError();
 }
 

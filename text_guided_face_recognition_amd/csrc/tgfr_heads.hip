@@ -8,8 +8,12 @@
 //                    phi = where(cos > th, phi, cos - mm)   (models/metrics.py:45-57)
 //   arc_margin_bwd   d cos from d logits (the where/clamp branches as torch takes them)
 //   focal_ce         logp = mean_b CE(logits_b, y_b); loss = (1 - e^-logp)^gamma logp
+//                    (a block per row, then a fixed-order mean: deterministic)
 //                    (FocalLoss, models/losses.py:313-325)
 //   focal_ce_bwd     dlogits = g * dloss/dlogp * (softmax - onehot) / B
+//   bias_grad        db = column sums of dy (after the ReLU mask y > 0 when given,
+//                    writing the masked dy for the weight/input GEMMs): the
+//                    nn.Linear / 1x1-conv bias gradient, fixed-order reduction
 // Each replaces 10-25 PyTorch launches per call with one.
 #include "tgfr_common.h"
 
@@ -97,34 +101,45 @@ __global__ __launch_bounds__(256) void arc_margin_bwd_kernel(const float* __rest
   dcos[e] = d;
 }
 
-// one block: waves loop over rows; ws[b] = row LSE, ws[rows] = logp
-__global__ __launch_bounds__(1024) void focal_ce_kernel(const float* __restrict__ L, int rows,
-                                                        int cols, const long long* __restrict__ label,
-                                                        float gamma, float* __restrict__ ws,
-                                                        float* __restrict__ loss) {
-  __shared__ float red[16];
+// one block per row: ws[b] = row LSE, ws[rows + 1 + b] = row NLL
+__global__ __launch_bounds__(256) void focal_rows_kernel(const float* __restrict__ L, int cols,
+                                                         const long long* __restrict__ label,
+                                                         int rows, float* __restrict__ ws) {
+  __shared__ float red[4];
+  const int b = blockIdx.x, wid = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
+  const float* r = L + (long long)b * cols;
+  float m = -INFINITY;
+  for (int c = threadIdx.x; c < cols; c += 256) m = fmaxf(m, r[c]);
+  m = wave_max(m);
+  if (lane == 0) red[wid] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int c = threadIdx.x; c < cols; c += 256) sum += __expf(r[c] - m);
+  sum = wave_sum(sum);
+  if (lane == 0) red[wid] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float lse = m + __logf(red[0] + red[1] + red[2] + red[3]);
+    ws[b] = lse;
+    ws[rows + 1 + b] = lse - r[label[b]];
+  }
+}
+
+// ws[rows] = logp = mean NLL (fixed-order sum); loss = (1 - e^-logp)^gamma logp
+__global__ __launch_bounds__(256) void focal_final_kernel(int rows, float gamma,
+                                                          float* __restrict__ ws,
+                                                          float* __restrict__ loss) {
+  __shared__ float red[4];
   const int wid = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
   float acc = 0.f;
-  for (int b = wid; b < rows; b += 16) {
-    const float* r = L + (long long)b * cols;
-    float m = -INFINITY;
-    for (int c = lane; c < cols; c += WAVE) m = fmaxf(m, r[c]);
-    m = wave_max(m);
-    float sum = 0.f;
-    for (int c = lane; c < cols; c += WAVE) sum += __expf(r[c] - m);
-    sum = wave_sum(sum);
-    const float lse = m + __logf(sum);
-    if (lane == 0) {
-      ws[b] = lse;
-      acc += lse - r[label[b]];
-    }
-  }
+  for (int b = threadIdx.x; b < rows; b += 256) acc += ws[rows + 1 + b];
+  acc = wave_sum(acc);
   if (lane == 0) red[wid] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
-    float t = 0.f;
-    for (int k = 0; k < 16; ++k) t += red[k];
-    const float logp = t / rows;
+    const float logp = (red[0] + red[1] + red[2] + red[3]) / rows;
     const float p = __expf(-logp);
     ws[rows] = logp;
     loss[0] = powf(1.f - p, gamma) * logp;
@@ -150,6 +165,43 @@ __global__ __launch_bounds__(256) void focal_ce_bwd_kernel(const float* __restri
   const float g = (gscale ? gscale[0] : 1.f) * dfl / rows;
   const float sm = __expf(L[e] - ws[b]);
   dL[e] = g * (sm - (c == label[b] ? 1.f : 0.f));
+}
+
+constexpr int BG_ROWS = 256;   // rows per partial-sum block of bias_grad
+
+// grid (ceil(cols / 64), ceil(rows / BG_ROWS)); block = 64 columns x 4 row lanes
+__global__ __launch_bounds__(256) void bias_grad_part_kernel(
+    const float* __restrict__ dy, long long lddy, int rows, int cols, const float* __restrict__ y,
+    long long ldy, float* __restrict__ dym, long long lddm, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int r0 = blockIdx.y * BG_ROWS, r1 = min(rows, r0 + BG_ROWS);
+  float acc = 0.f;
+  if (c < cols) {
+    for (int r = r0 + ry; r < r1; r += 4) {
+      float v = dy[(long long)r * lddy + c];
+      if (y) {
+        v = y[(long long)r * ldy + c] > 0.f ? v : 0.f;
+        dym[(long long)r * lddm + c] = v;
+      }
+      acc += v;
+    }
+  }
+  red[ry][tx] = acc;
+  __syncthreads();
+  if (ry == 0 && c < cols)
+    part[(long long)blockIdx.y * cols + c] = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+}
+
+__global__ __launch_bounds__(256) void bias_grad_final_kernel(const float* __restrict__ part,
+                                                              int nparts, int cols,
+                                                              float* __restrict__ db) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float a = 0.f;
+  for (int k = 0; k < nparts; ++k) a += part[(long long)k * cols + c];
+  db[c] = a;
 }
 
 }  // namespace
@@ -198,8 +250,9 @@ int tgfr_arc_margin_bwd(const float* cosv, const long long* label, const float* 
 int tgfr_focal_ce(const float* L, int rows, int cols, const long long* label, float gamma,
                   float* ws, float* loss, void* stream) {
   if (rows <= 0 || cols <= 0) return 1001;
-  hipLaunchKernelGGL(focal_ce_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, L, rows,
-                     cols, label, gamma, ws, loss);
+  auto* st = (hipStream_t)stream;
+  hipLaunchKernelGGL(focal_rows_kernel, dim3(rows), dim3(256), 0, st, L, cols, label, rows, ws);
+  hipLaunchKernelGGL(focal_final_kernel, dim3(1), dim3(256), 0, st, rows, gamma, ws, loss);
   return (int)hipGetLastError();
 }
 
@@ -209,6 +262,21 @@ int tgfr_focal_ce_bwd(const float* L, int rows, int cols, const long long* label
   const long long n = (long long)rows * cols;
   hipLaunchKernelGGL(focal_ce_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, L, rows, cols, label, gamma, ws, gscale, dL);
+  return (int)hipGetLastError();
+}
+
+// ws: ceil(rows / 256) * cols floats.  y (ReLU output) and dym are both set
+// or both NULL.
+int tgfr_bias_grad(const float* dy, long long lddy, int rows, int cols, const float* y,
+                   long long ldy, float* dym, long long lddm, float* db, float* ws,
+                   void* stream) {
+  if (rows <= 0 || cols <= 0 || (!y) != (!dym)) return 1001;
+  const int nparts = (rows + BG_ROWS - 1) / BG_ROWS;
+  auto* st = (hipStream_t)stream;
+  hipLaunchKernelGGL(bias_grad_part_kernel, dim3((cols + 63) / 64, nparts), dim3(256), 0, st, dy,
+                     lddy, rows, cols, y, ldy, dym, lddm, ws);
+  hipLaunchKernelGGL(bias_grad_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, st, ws,
+                     nparts, cols, db);
   return (int)hipGetLastError();
 }
 

@@ -6,6 +6,8 @@ in a HIP graph.  There is no CPU fallback: CPU tensors raise.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _hip
@@ -298,17 +300,30 @@ class LinearRows(torch.autograd.Function):
         x2, w, y = ctx.saved_tensors
         relu, mode, has_bias, shape, wshape = ctx.cfg
         dy = dy.reshape(-1, w.shape[0]).float()
-        if relu:
-            dy = dy * (y > 0)
+        if dy.stride(1) != 1:
+            dy = dy.contiguous()
         dx = dw = db = None
+        want_db = has_bias and ctx.needs_input_grad[2]
+        if relu or want_db:
+            rows, cols = dy.shape
+            ws = torch.empty(-(-rows // 256) * cols, dtype=torch.float32, device=dy.device)
+            db = torch.empty(cols, dtype=torch.float32, device=dy.device)
+            dym = torch.empty_like(dy) if relu else None
+            call("tgfr_bias_grad", ptr(dy), dy.stride(0), rows, cols, ptr(y),
+                 y.stride(0) if relu else 0, ptr(dym), dym.stride(0) if relu else 0, ptr(db),
+                 ptr(ws), _hip.stream())
+            if relu:
+                dy = dym
+            if not want_db:
+                db = None
         if ctx.needs_input_grad[0]:
-            dx = bgemm(dy.unsqueeze(0), w.unsqueeze(0), mode=mode)[0].reshape(shape)
+            mb = -(-dy.shape[0] // 64) * -(-w.shape[1] // 64)
+            dx = bgemm(dy.unsqueeze(0), w.unsqueeze(0), mode=mode,
+                       ksplit=_ksplit(w.shape[0], mb))[0].reshape(shape)
         if ctx.needs_input_grad[1]:
             mb = -(-w.shape[0] // 64) * -(-w.shape[1] // 64)
             dw = bgemm(dy.t().unsqueeze(0), x2.unsqueeze(0), mode=mode,
                        ksplit=_ksplit(x2.shape[0], mb))[0].reshape(wshape)
-        if has_bias and ctx.needs_input_grad[2]:
-            db = dy.sum(0)
         return dx, dw, db, None, None
 
 
@@ -317,43 +332,111 @@ def linear_rows(x, weight, bias=None, relu=False, mode="fp32"):
 
 
 class AttentionCore(torch.autograd.Function):
-    """O = softmax(scale * Qr Kr^T) V per sample (fusion_nets.py:103-115).
+    """O = softmax(scale * Qr Kr^T) V per sample (fusion_nets.py:103-115) on
+    packed projections, so the backward writes dQr/dKr/dV straight into the
+    column slices of one packed gradient (no zero-fill + add per slice).
 
-    qr, kr: [N, HW, C'] (query role = key_proj(x), key role = query_proj(y));
-    v: [N, HW, C].  Returns O [N, HW, C].
+    px [N, HW, Cx] holds Qr in columns [0, cq) and V in [cv, Cx); Kr is
+    columns [ck, ck + cq) of py [N, HW, Cy], or of px when py is None
+    (self-attention).  Returns O [N, HW, Cx - cv].
     """
 
     @staticmethod
-    def forward(ctx, qr, kr, v, scale, mode):
-        qr, kr, v = qr.float(), kr.float(), v.float()
+    def forward(ctx, px, py, cq, ck, cv, scale, mode):
+        px = px.float()
+        ky = px if py is None else py.float()
+        qr, kr, v = px[..., :cq], ky[..., ck:ck + cq], px[..., cv:]
         nb, hw, _ = qr.shape
         s = bgemm(qr, kr.transpose(1, 2), mode=mode)
         p = torch.empty_like(s)
         call("tgfr_attn_softmax", ptr(s), ptr(p), None, nb * hw, hw, hw, float(scale),
              _hip.stream())
         o = bgemm(p, v, mode=mode)
-        ctx.save_for_backward(qr, kr, v, p)
-        ctx.cfg = (float(scale), mode)
+        ctx.save_for_backward(px, None if py is None else ky, p)
+        ctx.cfg = (float(scale), mode, cq, ck, cv)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qr, kr, v, p = ctx.saved_tensors
-        scale, mode = ctx.cfg
+        px, py, p = ctx.saved_tensors
+        scale, mode, cq, ck, cv = ctx.cfg
+        ky = px if py is None else py
+        qr, kr, v = px[..., :cq], ky[..., ck:ck + cq], px[..., cv:]
         do = do.float()
         nb, hw, _ = qr.shape
         dp = bgemm(do, v.transpose(1, 2), mode=mode)
         ds = torch.empty_like(dp)
         call("tgfr_attn_softmax_bwd", ptr(p), ptr(dp), ptr(ds), nb * hw, hw, hw, scale,
              _hip.stream())
-        dqr = bgemm(ds, kr, mode=mode)
-        dkr = bgemm(ds.transpose(1, 2), qr, mode=mode)
-        dv = bgemm(p.transpose(1, 2), do, mode=mode)
-        return dqr, dkr, dv, None, None
+        dpx = torch.empty_like(px)
+        dky = dpx if py is None else torch.empty_like(py)
+        if py is None:
+            covered = ck == cq and cv == 2 * cq
+        else:
+            covered = cv == cq and ck == 0 and cq == py.shape[-1]
+        if not covered:
+            dpx.zero_()
+            if py is not None:
+                dky.zero_()
+        bgemm(ds, kr, out=dpx[..., :cq], mode=mode)
+        bgemm(ds.transpose(1, 2), qr, out=dky[..., ck:ck + cq], mode=mode)
+        bgemm(p.transpose(1, 2), do, out=dpx[..., cv:], mode=mode)
+        return dpx, (None if py is None else dky), None, None, None, None, None
 
 
-def attention_core(qr, kr, v, scale, mode="fp32"):
-    return AttentionCore.apply(qr, kr, v, scale, mode)
+def attention_core(px, py, cq, ck, cv, scale, mode="fp32"):
+    return AttentionCore.apply(px, py, cq, ck, cv, scale, mode)
+
+
+# ------------------------------------------------------------ layer norm ---
+def _aligned(t):
+    t = t.float().contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+def ln_ws_floats(rows, e, backward=True):
+    out = (ctypes.c_longlong * 1)()
+    rc = _hip.lib().tgfr_ln_ws_floats(int(rows), int(e), int(backward), ctypes.addressof(out))
+    if rc != 0:
+        raise RuntimeError(f"tgfr_ln_ws_floats failed with code {rc}")
+    return int(out[0])
+
+
+class LayerNormRows(torch.autograd.Function):
+    """Per-sample LayerNorm over all trailing elements with an elementwise
+    affine of the same shape (nn.LayerNorm([C, H, W]), models.py:388/:401)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        rows = x.shape[0]
+        x2 = _aligned(x.reshape(rows, -1))
+        e = x2.shape[1]
+        assert weight.numel() == e and bias.numel() == e
+        w, b = _aligned(weight.reshape(-1)), _aligned(bias.reshape(-1))
+        ws = torch.empty(ln_ws_floats(rows, e), dtype=torch.float32, device=x.device)
+        y = torch.empty_like(x2)
+        call("tgfr_ln_fwd", ptr(x2), rows, e, ptr(w), ptr(b), float(eps), ptr(y), ptr(ws),
+             _hip.stream())
+        ctx.save_for_backward(x2, w, ws)
+        ctx.shapes = (x.shape, weight.shape)
+        return y.reshape(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, ws = ctx.saved_tensors
+        xshape, wshape = ctx.shapes
+        rows, e = x2.shape
+        dy = _aligned(dy.reshape(rows, e))
+        dx = torch.empty_like(x2)
+        dw = torch.empty(e, dtype=torch.float32, device=x2.device)
+        db = torch.empty_like(dw)
+        call("tgfr_ln_bwd", ptr(dy), ptr(x2), rows, e, ptr(w), ptr(ws), ptr(dx), ptr(dw),
+             ptr(db), _hip.stream())
+        return dx.reshape(xshape), dw.reshape(wshape), db.reshape(wshape), None
+
+
+def layer_norm_rows(x, weight, bias, eps=1e-5):
+    return LayerNormRows.apply(x, weight, bias, eps)
 
 
 # ---------------------------------------------------------------- heads ---
@@ -428,7 +511,7 @@ class FocalCE(torch.autograd.Function):
         logits = logits.float().contiguous()
         target = target.to(torch.int64).contiguous()
         rows, cols = logits.shape
-        ws = torch.empty(rows + 1, dtype=torch.float32, device=logits.device)
+        ws = torch.empty(2 * rows + 1, dtype=torch.float32, device=logits.device)
         loss = torch.empty(1, dtype=torch.float32, device=logits.device)
         call("tgfr_focal_ce", ptr(logits), rows, cols, ptr(target), float(gamma), ptr(ws),
              ptr(loss), _hip.stream())

@@ -51,21 +51,19 @@ class SelfAttention(nn.Module):
     def forward_cl(self, x_cl, y_cl):
         """Channels-last core: x_cl, y_cl [N, HW, C] -> [N, HW, C]."""
         mode = self.precision
+        cq = self.key_proj.weight.shape[0]
         if y_cl is x_cl:
+            # packed [Qr | Kr | V] = x [key_proj | query_proj | value_proj]^T
             w = torch.cat([self._w(self.key_proj), self._w(self.query_proj),
                            self._w(self.value_proj)], 0)
             b = torch.cat([self.key_proj.bias, self.query_proj.bias, self.value_proj.bias])
-            proj = K.linear_rows(x_cl, w, b, mode=mode)
-            cq = self.key_proj.weight.shape[0]
-            qr, kr, v = proj[..., :cq], proj[..., cq:2 * cq], proj[..., 2 * cq:]
-        else:
-            w = torch.cat([self._w(self.key_proj), self._w(self.value_proj)], 0)
-            b = torch.cat([self.key_proj.bias, self.value_proj.bias])
-            proj = K.linear_rows(x_cl, w, b, mode=mode)
-            cq = self.key_proj.weight.shape[0]
-            qr, v = proj[..., :cq], proj[..., cq:]
-            kr = K.linear_rows(y_cl, self._w(self.query_proj), self.query_proj.bias, mode=mode)
-        return K.attention_core(qr, kr, v, 1.0 / float(self.sqrt_dim), self.precision)
+            px = K.linear_rows(x_cl, w, b, mode=mode)
+            return K.attention_core(px, None, cq, cq, 2 * cq, 1.0 / float(self.sqrt_dim), mode)
+        w = torch.cat([self._w(self.key_proj), self._w(self.value_proj)], 0)
+        b = torch.cat([self.key_proj.bias, self.value_proj.bias])
+        px = K.linear_rows(x_cl, w, b, mode=mode)                     # [Qr | V]
+        py = K.linear_rows(y_cl, self._w(self.query_proj), self.query_proj.bias, mode=mode)
+        return K.attention_core(px, py, cq, 0, cq, 1.0 / float(self.sqrt_dim), mode)
 
     def forward(self, x, y):
         n, c, h, w = y.shape

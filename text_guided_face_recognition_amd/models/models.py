@@ -63,7 +63,7 @@ class IMIM(nn.Module):
         # the channels-last [B, HW, C] rows, with the affine maps permuted
         wt = self.ln.weight.permute(1, 2, 0).reshape(h * w, c)
         bs = self.ln.bias.permute(1, 2, 0).reshape(h * w, c)
-        z = F.layer_norm(z, (h * w, c), wt, bs, self.ln.eps)
+        z = K.layer_norm_rows(z, wt, bs, self.ln.eps)
         z = K.linear_rows(z, self.conv1x1_1.weight, self.conv1x1_1.bias, relu=True,
                           mode=self.precision)
         z = K.linear_rows(z, self.conv1x1_2.weight, self.conv1x1_2.bias, relu=True,

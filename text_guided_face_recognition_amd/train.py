@@ -80,7 +80,7 @@ class Train:
         # :219-222
         self.optimizer_cls = torch.optim.SGD(
             list(self.image_cls.parameters()) + list(self.text_cls.parameters()),
-            lr=0.1, momentum=0.9, weight_decay=5e-5)
+            lr=0.1, momentum=0.9, weight_decay=5e-5, fused=device.type == "cuda")
 
     def step(self, batch):
         args, ctx = self.args, self.ctx
@@ -128,12 +128,12 @@ class Fusion:
             set_precision(m, args.precision)
         self.criterion = FocalLoss(gamma=2)                        # :92-96
         self.optimizer_cls = torch.optim.SGD(self.metric_fc.parameters(), lr=0.1,
-                                             weight_decay=5e-4)    # :119-130
+                                             weight_decay=5e-4,
+                                             fused=device.type == "cuda")   # :119-130
         self.optimizer_head = torch.optim.Adam(
             list(self.image_head.parameters()) + list(self.fusion_net.parameters()),
             weight_decay=5e-5, lr=args.lr_head,
-            capturable=device.type == "cuda",
-                                               fused=device.type == "cuda")                      # :137-139
+            capturable=device.type == "cuda", fused=device.type == "cuda")   # :137-139
 
     def step(self, batch):
         g, local, words, sent, class_ids = batch

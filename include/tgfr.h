@@ -99,9 +99,12 @@ int tgfr_cos_logits_bwd(const float* g, long long gs0, long long gs1, const floa
 
 /* Row log-sum-exp and column (max, sum exp) partials of a [n_r x n_c] block;
  * col_lse (nullable) also receives the column LSE of this block alone (the
- * single-process case, where no exchange is needed). */
+ * single-process case, where no exchange is needed).  With loss set (needs
+ * col_lse and one zeroed counters word, left zeroed) the launch also computes
+ * what tgfr_ce_loss would (row_offset, inv_n as there). */
 int tgfr_ce_stats(const float* L, long long ld, int n_r, int n_c, float* row_lse,
-                  float* col_max, float* col_sum, float* col_lse, void* stream);
+                  float* col_max, float* col_sum, float* col_lse, int row_offset, float inv_n,
+                  float* loss, unsigned* counters, void* stream);
 
 /* loss[0] = inv_n * sum_b (row_lse[b] - L[b][b+off]), loss[1] = inv_n * sum_b
  * (col_lse[b+off] - L[b][b+off]): this rank's share of nn.CrossEntropyLoss on
@@ -120,14 +123,16 @@ int tgfr_ce_grad(const float* L, long long ld, int n_r, int n_c, int row_offset,
  * products of SelfAttention (models/fusion_nets.py:103, :115), the 1x1-conv /
  * Linear projections of IMIM and FCFM (models/models.py:386-404), and their
  * backward.  bias (nullable, per column) and relu form the epilogue.  With
- * ksplit > 1 the K range is split over ksplit blocks, each writing its own
- * slab at C + k*sCsplit (deterministic split-K; the caller sums the slabs);
- * bias/relu/accumulate require ksplit == 1. */
+ * ksplit > 1 the K range is split over ksplit blocks per 64x64 output tile;
+ * each stores a partial tile to slab (ksplit * tiles * 4096 floats, tiles =
+ * batch * ceil(M/64) * ceil(N/64)) and the tile's last-arriving block sums the
+ * partials in slice order (deterministic) and applies the epilogue.
+ * counters: >= tiles zeroed uint32 words, left zeroed on return. */
 int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, const float* B,
                long long sBb, long long sBk, long long sBn, float* C, long long sCb,
                long long sCm, long long sCn, int batch, int M, int N, int K, float alpha,
-               int accumulate, const float* bias, int relu, int ksplit, long long sCsplit,
-               int mode, void* stream);
+               int accumulate, const float* bias, int relu, int ksplit, float* slab,
+               unsigned* counters, int mode, void* stream);
 
 /* P = softmax(scale * S) per row (models/fusion_nets.py:103-106), optional LSE. */
 int tgfr_attn_softmax(const float* S, float* P, float* lse, long long rows, int n, long long ld,
@@ -158,9 +163,10 @@ int tgfr_arc_margin_bwd(const float* cosv, const long long* label, const float* 
 
 /* FocalLoss (models/losses.py:313-325): logp = mean_b CE(L_b, label_b),
  * loss[0] = (1 - exp(-logp))^gamma * logp; ws receives 2 * rows + 1 floats
- * (row LSE [rows], logp, row NLL [rows]) for the backward. */
+ * (row LSE [rows], logp, row NLL [rows]) for the backward; counters: 1 zeroed
+ * word (left zeroed). */
 int tgfr_focal_ce(const float* L, int rows, int cols, const long long* label, float gamma,
-                  float* ws, float* loss, void* stream);
+                  float* ws, unsigned* counters, float* loss, void* stream);
 
 /* dL = gscale[0] * dloss/dlogp * (softmax(L_b) - onehot) / rows. */
 int tgfr_focal_ce_bwd(const float* L, int rows, int cols, const long long* label, float gamma,
@@ -180,10 +186,20 @@ int tgfr_ln_bwd(const float* dy, const float* x, int rows, long long E, const fl
 
 /* Bias gradient of a row-wise linear map: db[c] = sum_r dy[r][c].  With y
  * (the ReLU output) the ReLU mask is applied first and the masked gradient is
- * written to dym (both set or both NULL).  ws: ceil(rows / 256) * cols floats. */
+ * written to dym (both set or both NULL).  ws: ceil(rows / 256) * cols floats;
+ * counters: ceil(cols / 64) zeroed words (left zeroed). */
 int tgfr_bias_grad(const float* dy, long long lddy, int rows, int cols, const float* y,
                    long long ldy, float* dym, long long lddm, float* db, float* ws,
-                   void* stream);
+                   unsigned* counters, void* stream);
+
+/* Weighted sums of scalar device losses: out[j] = sum_i W[j][i] * *losses[i]
+ * (losses: host array of n <= 16 device pointers; W: host [m][n], m <= 4).
+ * Row 0 is the training objective; tgfr_loss_mix_bwd gives its gradient
+ * dloss[i] = g[0] * W[0][i].  Replaces the trainer's chain of scalar ops
+ * (src/train_encoders_bert.py:279-323). */
+int tgfr_loss_mix(int n, const float* const* losses, int m, const float* W, float* out,
+                  void* stream);
+int tgfr_loss_mix_bwd(const float* g, int n, const float* W, float* dloss, void* stream);
 
 #ifdef __cplusplus
 }

@@ -32,20 +32,22 @@ SIGNATURES = {
     "tgfr_wr_lds_bytes": [I],
     "tgfr_cos_logits": [P, L, P, L, I, I, I, I, F, F, I, P, I, P, L, P],
     "tgfr_cos_logits_bwd": [P, L, L, P, L, P, L, I, I, I, I, F, F, P, L, P],
-    "tgfr_ce_stats": [P, L, I, I, P, P, P, P, P],
+    "tgfr_ce_stats": [P, L, I, I, P, P, P, P, I, F, P, P, P],
     "tgfr_ce_loss": [P, L, I, I, F, P, P, P, P],
     "tgfr_ce_grad": [P, L, I, I, I, F, P, P, P, P, F, F, P, L, P],
-    "tgfr_bgemm": [P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, F, I, P, I, I, L, I, P],
+    "tgfr_bgemm": [P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, F, I, P, I, I, P, P, I, P],
     "tgfr_attn_softmax": [P, P, P, L, I, L, F, P],
     "tgfr_l2norm_rows": [P, L, I, I, F, P, L, P, P],
     "tgfr_l2norm_rows_bwd": [P, L, P, L, P, I, I, F, P, L, P],
     "tgfr_arc_margin": [P, P, I, I, F, F, I, P, P],
     "tgfr_arc_margin_bwd": [P, P, P, I, I, F, F, I, P, P],
-    "tgfr_focal_ce": [P, I, I, P, F, P, P, P],
+    "tgfr_focal_ce": [P, I, I, P, F, P, P, P, P],
     "tgfr_focal_ce_bwd": [P, I, I, P, F, P, P, P, P],
     "tgfr_attn_softmax_bwd": [P, P, P, L, I, L, F, P],
     "tgfr_ln_ws_floats": [I, L, I, P],
-    "tgfr_bias_grad": [P, L, I, I, P, L, P, L, P, P, P],
+    "tgfr_loss_mix": [I, P, I, P, P, P],
+    "tgfr_loss_mix_bwd": [P, I, P, P, P],
+    "tgfr_bias_grad": [P, L, I, I, P, L, P, L, P, P, P, P],
     "tgfr_ln_fwd": [P, I, L, P, P, F, P, P, P],
     "tgfr_ln_bwd": [P, P, I, L, P, P, P, P, P, P],
 }
@@ -107,6 +109,22 @@ class KernelTimer:
             ms = [s.elapsed_time(e) for s, e in evs]
             out[name] = (len(ms), sum(ms) / len(ms))
         return out
+
+
+_counters = {}
+N_COUNTERS = 1 << 20
+
+
+def counters(device):
+    """Per-device zeroed uint32 words for the kernels' in-launch last-arriver
+    hand-offs; every kernel leaves the words it used at zero again, and calls
+    on one stream run one at a time, so all calls share the buffer."""
+    key = torch.device(device).index
+    buf = _counters.get(key)
+    if buf is None:
+        buf = torch.zeros(N_COUNTERS, dtype=torch.int32, device=device)
+        _counters[key] = buf
+    return buf
 
 
 def call(name, *args):

@@ -111,23 +111,13 @@ __global__ __launch_bounds__(256) void bgemm_kernel(
     const float* __restrict__ B, long long sBb, long long sBk, long long sBn,
     float* __restrict__ Cm, long long sCb, long long sCm, long long sCn, int M, int N, int Kfull,
     float alpha, int accumulate, const float* __restrict__ bias, int relu, int ksplit,
-    long long sCsplit) {
+    float* __restrict__ slab, unsigned* __restrict__ counters) {
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int bt = blockIdx.z / ksplit, kz = blockIdx.z % ksplit;
-  // split-K: this block reduces k in [kb, kb + K) into its own output slab
+  // split-K: this block reduces k in [kb, kb + K) (possibly empty)
   const int kc = ((Kfull + ksplit - 1) / ksplit + BK - 1) / BK * BK;
   const int kb = kz * kc;
-  const int K = min(Kfull - kb, kc);
-  if (K <= 0) {
-    // empty tail slice: its slab must still hold zeros
-    const int n = n0 + 32 * (threadIdx.x / WAVE & 1) + (threadIdx.x & 31);
-    float* Cb = Cm + bt * sCb + kz * sCsplit;
-    for (int q = 0; q < 16; ++q) {
-      const int m = m0 + 32 * ((threadIdx.x / WAVE) >> 1) + acc_row(q, (threadIdx.x & 63) >> 5);
-      if (m < M && n < N) Cb[m * sCm + n * sCn] = 0.f;
-    }
-    return;
-  }
+  const int K = max(0, min(Kfull - kb, kc));
   const int tid = threadIdx.x, wid = tid / WAVE, lane = tid % WAVE;
   const int lr = lane & 31, h = lane >> 5;
   const int wm = wid >> 1, wn = wid & 1;
@@ -139,10 +129,12 @@ __global__ __launch_bounds__(256) void bgemm_kernel(
   for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 
   const int nk = (K + BK - 1) / BK;
-  load_tile<LA>(fa, Ab, sAm, sAk, tid, 0, M - m0, K);
-  load_tile<LB>(fb, Bb, sBn, sBk, tid, 0, N - n0, K);
-  store_tile<MODE, LA>(0, fa, tid);
-  store_tile<MODE, LB>(2 * HALF, fb, tid);
+  if (nk > 0) {
+    load_tile<LA>(fa, Ab, sAm, sAk, tid, 0, M - m0, K);
+    load_tile<LB>(fb, Bb, sBn, sBk, tid, 0, N - n0, K);
+    store_tile<MODE, LA>(0, fa, tid);
+    store_tile<MODE, LB>(2 * HALF, fb, tid);
+  }
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const uint32_t sb = (kt & 1) * STAGE;
@@ -166,9 +158,29 @@ __global__ __launch_bounds__(256) void bgemm_kernel(
     }
     __syncthreads();
   }
+  if (ksplit > 1) {
+    // every K slice stores its tile slab (lane-major, 64 B per lane); the last
+    // arriving slice of the tile sums all slabs in slice order (deterministic)
+    const long long tile = ((long long)bt * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    float4* mine = (float4*)(slab + ((tile * ksplit + kz) * 256 + tid) * 16);
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      mine[v] = make_float4(acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]);
+    if (!last_arrival(counters + tile, ksplit, (int*)(g_smem + 2 * STAGE))) return;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    for (int z = 0; z < ksplit; ++z) {
+      const float4* src = (const float4*)(slab + ((tile * ksplit + z) * 256 + tid) * 16);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float4 t = src[v];
+        acc[4 * v] += t.x; acc[4 * v + 1] += t.y; acc[4 * v + 2] += t.z; acc[4 * v + 3] += t.w;
+      }
+    }
+  }
   const int n = n0 + 32 * wn + lr;
   if (n >= N) return;
-  float* Cb = Cm + bt * sCb + kz * sCsplit;
+  float* Cb = Cm + bt * sCb;
   const float bn = bias ? bias[n] : 0.f;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -227,10 +239,10 @@ extern "C" {
 int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, const float* B,
                long long sBb, long long sBk, long long sBn, float* C, long long sCb,
                long long sCm, long long sCn, int batch, int M, int N, int K, float alpha,
-               int accumulate, const float* bias, int relu, int ksplit, long long sCsplit,
-               int mode, void* stream) {
+               int accumulate, const float* bias, int relu, int ksplit, float* slab,
+               unsigned* counters, int mode, void* stream) {
   if (batch <= 0 || M <= 0 || N <= 0 || K <= 0 || ksplit <= 0) return 1001;
-  if (ksplit > 1 && (bias || relu || accumulate)) return 1001;
+  if (ksplit > 1 && (!slab || !counters)) return 1001;
   if (mode != MODE_SPLIT && mode != MODE_BF16) return 1002;
   const dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch * ksplit);
   auto* s = (hipStream_t)stream;
@@ -238,7 +250,7 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
   const int lb = sBk == 1 ? LAY_K : sBn == 1 ? LAY_MN : LAY_ANY;
   using Fn = void (*)(const float*, long long, long long, long long, const float*, long long,
                       long long, long long, float*, long long, long long, long long, int, int,
-                      int, float, int, const float*, int, int, long long);
+                      int, float, int, const float*, int, int, float*, unsigned*);
 #define TGFR_BG(MD, A_, B_) &bgemm_kernel<MD, A_, B_>
 #define TGFR_BG_ROW(MD, A_) TGFR_BG(MD, A_, LAY_K), TGFR_BG(MD, A_, LAY_MN), TGFR_BG(MD, A_, LAY_ANY)
   static const Fn table[2][3][3] = {
@@ -248,9 +260,9 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
        {TGFR_BG_ROW(MODE_SPLIT, LAY_ANY)}}};
 #undef TGFR_BG_ROW
 #undef TGFR_BG
-  hipLaunchKernelGGL(table[mode][la][lb], grid, dim3(256), 2 * STAGE, s, A, sAb, sAm, sAk, B,
-                     sBb, sBk, sBn, C, sCb, sCm, sCn, M, N, K, alpha, accumulate, bias, relu,
-                     ksplit, sCsplit);
+  hipLaunchKernelGGL(table[mode][la][lb], grid, dim3(256), 2 * STAGE + 16, s, A, sAb, sAm, sAk,
+                     B, sBb, sBk, sBn, C, sCb, sCm, sCn, M, N, K, alpha, accumulate, bias, relu,
+                     ksplit, slab, counters);
   return (int)hipGetLastError();
 }
 

@@ -8,6 +8,8 @@
 //                a [rows x cols] logit block; rows are this rank's images,
 //                columns the global caption list, so column partials from all
 //                ranks combine into the global column LSE (one tiny exchange).
+//                With the column LSE final in-launch (one rank), the last block
+//                also forms the losses below (one launch per forward).
 //   ce_loss      loss0 = mean_b CE(row b, label b+off) and
 //                loss1 = mean_i CE(col i, label i) restricted to this rank's
 //                diagonal entries (nn.CrossEntropyLoss, losses.py:52-53,131-132).
@@ -98,42 +100,13 @@ __global__ __launch_bounds__(256) void cos_logits_bwd_kernel(
   dx[b * lddx + tid] = acc;
 }
 
-__global__ __launch_bounds__(256) void ce_stats_kernel(const float* __restrict__ L, long long ld,
-                                                       int n_r, int n_c,
-                                                       float* __restrict__ row_lse,
-                                                       float* __restrict__ col_max,
-                                                       float* __restrict__ col_sum,
-                                                       float* __restrict__ col_lse) {
-  // blockIdx.y == 0: rows (one wave per row); == 1: columns (one thread per column)
-  if (blockIdx.y == 0) {
-    const int row = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
-    if (row >= n_r) return;
-    float m = -INFINITY;
-    for (int c = lane; c < n_c; c += WAVE) m = fmaxf(m, L[row * ld + c]);
-    m = wave_max(m);
-    float s = 0.f;
-    for (int c = lane; c < n_c; c += WAVE) s += __expf(L[row * ld + c] - m);
-    s = wave_sum(s);
-    if (lane == 0) row_lse[row] = m + __logf(s);
-  } else {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= n_c) return;
-    float m = -INFINITY;
-    for (int r = 0; r < n_r; ++r) m = fmaxf(m, L[r * ld + c]);
-    float s = 0.f;
-    for (int r = 0; r < n_r; ++r) s += __expf(L[r * ld + c] - m);
-    col_max[c] = m;
-    col_sum[c] = s;
-    if (col_lse) col_lse[c] = m + __logf(s);
-  }
-}
-
-__global__ __launch_bounds__(256) void ce_loss_kernel(const float* __restrict__ L, long long ld,
-                                                      int n_r, int row_offset, float inv_n,
-                                                      const float* __restrict__ row_lse,
-                                                      const float* __restrict__ col_lse,
-                                                      float* __restrict__ loss) {
-  __shared__ float red[8];
+// Sums of (row LSE - diagonal logit) and (column LSE - diagonal logit) over
+// this rank's rows: loss[0], loss[1] (times inv_n).
+__device__ __forceinline__ void ce_loss_block(const float* __restrict__ L, long long ld, int n_r,
+                                              int row_offset, float inv_n,
+                                              const float* __restrict__ row_lse,
+                                              const float* __restrict__ col_lse,
+                                              float* __restrict__ loss, float* red) {
   float l0 = 0.f, l1 = 0.f;
   for (int b = threadIdx.x; b < n_r; b += 256) {
     const int c = row_offset + b;
@@ -143,6 +116,7 @@ __global__ __launch_bounds__(256) void ce_loss_kernel(const float* __restrict__ 
   }
   l0 = wave_sum(l0);
   l1 = wave_sum(l1);
+  __syncthreads();
   if (threadIdx.x % WAVE == 0) {
     red[threadIdx.x / WAVE] = l0;
     red[4 + threadIdx.x / WAVE] = l1;
@@ -152,6 +126,58 @@ __global__ __launch_bounds__(256) void ce_loss_kernel(const float* __restrict__ 
     loss[0] = (red[0] + red[1] + red[2] + red[3]) * inv_n;
     loss[1] = (red[4] + red[5] + red[6] + red[7]) * inv_n;
   }
+}
+
+// blockIdx.y == 0: rows, == 1: columns; one wave per row / column.  With
+// `loss` set (single rank: col_lse is final here) the last block also forms
+// the two losses, so the forward is one launch.
+__global__ __launch_bounds__(256) void ce_stats_kernel(const float* __restrict__ L, long long ld,
+                                                       int n_r, int n_c,
+                                                       float* __restrict__ row_lse,
+                                                       float* __restrict__ col_max,
+                                                       float* __restrict__ col_sum,
+                                                       float* __restrict__ col_lse,
+                                                       int row_offset, float inv_n,
+                                                       float* __restrict__ loss,
+                                                       unsigned* __restrict__ counter) {
+  __shared__ float red[9];
+  const int lane = threadIdx.x % WAVE;
+  const int idx = blockIdx.x * 4 + threadIdx.x / WAVE;
+  if (blockIdx.y == 0) {
+    if (idx < n_r) {
+      float m = -INFINITY;
+      for (int c = lane; c < n_c; c += WAVE) m = fmaxf(m, L[idx * ld + c]);
+      m = wave_max(m);
+      float s = 0.f;
+      for (int c = lane; c < n_c; c += WAVE) s += __expf(L[idx * ld + c] - m);
+      s = wave_sum(s);
+      if (lane == 0) row_lse[idx] = m + __logf(s);
+    }
+  } else if (idx < n_c) {
+    float m = -INFINITY;
+    for (int r = lane; r < n_r; r += WAVE) m = fmaxf(m, L[r * ld + idx]);
+    m = wave_max(m);
+    float s = 0.f;
+    for (int r = lane; r < n_r; r += WAVE) s += __expf(L[r * ld + idx] - m);
+    s = wave_sum(s);
+    if (lane == 0) {
+      col_max[idx] = m;
+      col_sum[idx] = s;
+      if (col_lse) col_lse[idx] = m + __logf(s);
+    }
+  }
+  if (!loss) return;
+  if (!last_arrival(counter, gridDim.x * gridDim.y, (int*)&red[8])) return;
+  ce_loss_block(L, ld, n_r, row_offset, inv_n, row_lse, col_lse, loss, red);
+}
+
+__global__ __launch_bounds__(256) void ce_loss_kernel(const float* __restrict__ L, long long ld,
+                                                      int n_r, int row_offset, float inv_n,
+                                                      const float* __restrict__ row_lse,
+                                                      const float* __restrict__ col_lse,
+                                                      float* __restrict__ loss) {
+  __shared__ float red[8];
+  ce_loss_block(L, ld, n_r, row_offset, inv_n, row_lse, col_lse, loss, red);
 }
 
 __global__ __launch_bounds__(256) void ce_grad_kernel(const float* __restrict__ L, long long ld,
@@ -199,11 +225,13 @@ int tgfr_cos_logits_bwd(const float* g, long long gs0, long long gs1, const floa
 }
 
 int tgfr_ce_stats(const float* L, long long ld, int n_r, int n_c, float* row_lse,
-                  float* col_max, float* col_sum, float* col_lse, void* stream) {
-  if (n_r <= 0 || n_c <= 0) return 1001;
-  const int gx = max((n_r + 3) / 4, (n_c + 255) / 256);
+                  float* col_max, float* col_sum, float* col_lse, int row_offset, float inv_n,
+                  float* loss, unsigned* counters, void* stream) {
+  if (n_r <= 0 || n_c <= 0 || (loss && (!col_lse || !counters))) return 1001;
+  const int gx = max((n_r + 3) / 4, (n_c + 3) / 4);
   hipLaunchKernelGGL(ce_stats_kernel, dim3(gx, 2), dim3(256), 0, (hipStream_t)stream, L, ld,
-                     n_r, n_c, row_lse, col_max, col_sum, col_lse);
+                     n_r, n_c, row_lse, col_max, col_sum, col_lse, row_offset, inv_n, loss,
+                     counters);
   return (int)hipGetLastError();
 }
 

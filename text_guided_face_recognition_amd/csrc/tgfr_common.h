@@ -164,6 +164,35 @@ __device__ __forceinline__ int rs16_index(int lr) {
          ((lr >> 1) & 1);
 }
 
+// In-launch "last arriver" hand-off (the split-K counter recipe of
+// cdna_hip_programming.md 5 item 2 / 6 Guideline 16): every block stores its
+// partials with plain stores, drains, and lane 0 releases at agent scope
+// before taking a ticket; the block drawing expected-1 acquires, resets the
+// counter for the next launch and returns true in all its threads.  Correct
+// for any placement of the blocks over XCDs.  `flag` is an LDS word of the
+// kernel's (single) shared array.
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__device__ __forceinline__ bool last_arrival(unsigned* cnt, unsigned expected, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t =
+        __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == expected - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store((gu32*)cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
 // Row index inside a 32x32 MFMA accumulator tile for register q of wave half h.
 __device__ __forceinline__ constexpr int acc_row(int q, int h) {
   return (q & 3) + 8 * (q >> 2) + 4 * h;

@@ -8,9 +8,12 @@
 //                    phi = where(cos > th, phi, cos - mm)   (models/metrics.py:45-57)
 //   arc_margin_bwd   d cos from d logits (the where/clamp branches as torch takes them)
 //   focal_ce         logp = mean_b CE(logits_b, y_b); loss = (1 - e^-logp)^gamma logp
-//                    (a block per row, then a fixed-order mean: deterministic)
+//                    (a block per row; the last block takes the row-order mean)
 //                    (FocalLoss, models/losses.py:313-325)
 //   focal_ce_bwd     dlogits = g * dloss/dlogp * (softmax - onehot) / B
+//   loss_mix         out[j] = sum_i W[j][i] * loss_i for the trainer's scalar
+//                    losses (one launch instead of a chain of scalar ops);
+//   loss_mix_bwd     dloss_i = g * W[0][i]
 //   bias_grad        db = column sums of dy (after the ReLU mask y > 0 when given,
 //                    writing the masked dy for the weight/input GEMMs): the
 //                    nn.Linear / 1x1-conv bias gradient, fixed-order reduction
@@ -101,11 +104,15 @@ __global__ __launch_bounds__(256) void arc_margin_bwd_kernel(const float* __rest
   dcos[e] = d;
 }
 
-// one block per row: ws[b] = row LSE, ws[rows + 1 + b] = row NLL
-__global__ __launch_bounds__(256) void focal_rows_kernel(const float* __restrict__ L, int cols,
-                                                         const long long* __restrict__ label,
-                                                         int rows, float* __restrict__ ws) {
-  __shared__ float red[4];
+// one block per row: ws[b] = row LSE, ws[rows + 1 + b] = row NLL; the last
+// block forms ws[rows] = logp = mean NLL (row order) and the focal loss
+__global__ __launch_bounds__(256) void focal_ce_kernel(const float* __restrict__ L, int cols,
+                                                       const long long* __restrict__ label,
+                                                       int rows, float gamma,
+                                                       float* __restrict__ ws,
+                                                       unsigned* __restrict__ counter,
+                                                       float* __restrict__ loss) {
+  __shared__ float red[5];
   const int b = blockIdx.x, wid = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
   const float* r = L + (long long)b * cols;
   float m = -INFINITY;
@@ -125,17 +132,11 @@ __global__ __launch_bounds__(256) void focal_rows_kernel(const float* __restrict
     ws[b] = lse;
     ws[rows + 1 + b] = lse - r[label[b]];
   }
-}
-
-// ws[rows] = logp = mean NLL (fixed-order sum); loss = (1 - e^-logp)^gamma logp
-__global__ __launch_bounds__(256) void focal_final_kernel(int rows, float gamma,
-                                                          float* __restrict__ ws,
-                                                          float* __restrict__ loss) {
-  __shared__ float red[4];
-  const int wid = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
+  if (!last_arrival(counter, rows, (int*)&red[4])) return;
   float acc = 0.f;
-  for (int b = threadIdx.x; b < rows; b += 256) acc += ws[rows + 1 + b];
+  for (int k = threadIdx.x; k < rows; k += 256) acc += ws[rows + 1 + k];
   acc = wave_sum(acc);
+  __syncthreads();
   if (lane == 0) red[wid] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -169,39 +170,61 @@ __global__ __launch_bounds__(256) void focal_ce_bwd_kernel(const float* __restri
 
 constexpr int BG_ROWS = 256;   // rows per partial-sum block of bias_grad
 
-// grid (ceil(cols / 64), ceil(rows / BG_ROWS)); block = 64 columns x 4 row lanes
-__global__ __launch_bounds__(256) void bias_grad_part_kernel(
+// grid (ceil(cols / 64), ceil(rows / BG_ROWS)); block = 64 columns x 4 row
+// lanes.  Each block stores its column partials; the last block of a column
+// group sums the group's partials in block order.
+template <bool RELU>
+__global__ __launch_bounds__(256) void bias_grad_kernel(
     const float* __restrict__ dy, long long lddy, int rows, int cols, const float* __restrict__ y,
-    long long ldy, float* __restrict__ dym, long long lddm, float* __restrict__ part) {
-  __shared__ float red[4][64];
+    long long ldy, float* __restrict__ dym, long long lddm, float* __restrict__ part,
+    unsigned* __restrict__ counters, float* __restrict__ db) {
+  __shared__ float red[4 * 64 + 1];
   const int tx = threadIdx.x & 63, ry = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   const int r0 = blockIdx.y * BG_ROWS, r1 = min(rows, r0 + BG_ROWS);
   float acc = 0.f;
   if (c < cols) {
+#pragma unroll 4
     for (int r = r0 + ry; r < r1; r += 4) {
       float v = dy[(long long)r * lddy + c];
-      if (y) {
+      if constexpr (RELU) {
         v = y[(long long)r * ldy + c] > 0.f ? v : 0.f;
         dym[(long long)r * lddm + c] = v;
       }
       acc += v;
     }
   }
-  red[ry][tx] = acc;
+  red[ry * 64 + tx] = acc;
   __syncthreads();
   if (ry == 0 && c < cols)
-    part[(long long)blockIdx.y * cols + c] = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+    part[(long long)blockIdx.y * cols + c] = red[tx] + red[64 + tx] + red[128 + tx] + red[192 + tx];
+  if (!last_arrival(counters + blockIdx.x, gridDim.y, (int*)&red[256])) return;
+  float a = 0.f;
+  if (c < cols)
+    for (int k = ry; k < (int)gridDim.y; k += 4) a += part[(long long)k * cols + c];
+  red[ry * 64 + tx] = a;
+  __syncthreads();
+  if (ry == 0 && c < cols) db[c] = red[tx] + red[64 + tx] + red[128 + tx] + red[192 + tx];
 }
 
-__global__ __launch_bounds__(256) void bias_grad_final_kernel(const float* __restrict__ part,
-                                                              int nparts, int cols,
-                                                              float* __restrict__ db) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  float a = 0.f;
-  for (int k = 0; k < nparts; ++k) a += part[(long long)k * cols + c];
-  db[c] = a;
+constexpr int MIX_N = 16, MIX_M = 4;
+struct MixArgs {
+  const float* loss[MIX_N];
+  float w[MIX_M][MIX_N];
+};
+
+__global__ void loss_mix_kernel(MixArgs a, int n, int m, float* __restrict__ out) {
+  const int j = threadIdx.x;
+  if (j >= m) return;
+  float acc = 0.f;
+  for (int i = 0; i < n; ++i) acc += a.w[j][i] * *a.loss[i];
+  out[j] = acc;
+}
+
+__global__ void loss_mix_bwd_kernel(const float* __restrict__ g, MixArgs a, int n,
+                                    float* __restrict__ dloss) {
+  const int i = threadIdx.x;
+  if (i < n) dloss[i] = g[0] * a.w[0][i];
 }
 
 }  // namespace
@@ -248,11 +271,10 @@ int tgfr_arc_margin_bwd(const float* cosv, const long long* label, const float* 
 }
 
 int tgfr_focal_ce(const float* L, int rows, int cols, const long long* label, float gamma,
-                  float* ws, float* loss, void* stream) {
-  if (rows <= 0 || cols <= 0) return 1001;
-  auto* st = (hipStream_t)stream;
-  hipLaunchKernelGGL(focal_rows_kernel, dim3(rows), dim3(256), 0, st, L, cols, label, rows, ws);
-  hipLaunchKernelGGL(focal_final_kernel, dim3(1), dim3(256), 0, st, rows, gamma, ws, loss);
+                  float* ws, unsigned* counters, float* loss, void* stream) {
+  if (rows <= 0 || cols <= 0 || !counters) return 1001;
+  hipLaunchKernelGGL(focal_ce_kernel, dim3(rows), dim3(256), 0, (hipStream_t)stream, L, cols,
+                     label, rows, gamma, ws, counters, loss);
   return (int)hipGetLastError();
 }
 
@@ -265,18 +287,44 @@ int tgfr_focal_ce_bwd(const float* L, int rows, int cols, const long long* label
   return (int)hipGetLastError();
 }
 
-// ws: ceil(rows / 256) * cols floats.  y (ReLU output) and dym are both set
-// or both NULL.
+// ws: ceil(rows / 256) * cols floats; counters: ceil(cols / 64) zeroed words.
+// y (ReLU output) and dym are both set or both NULL.
 int tgfr_bias_grad(const float* dy, long long lddy, int rows, int cols, const float* y,
                    long long ldy, float* dym, long long lddm, float* db, float* ws,
-                   void* stream) {
-  if (rows <= 0 || cols <= 0 || (!y) != (!dym)) return 1001;
-  const int nparts = (rows + BG_ROWS - 1) / BG_ROWS;
+                   unsigned* counters, void* stream) {
+  if (rows <= 0 || cols <= 0 || (!y) != (!dym) || !counters) return 1001;
+  const dim3 grid((cols + 63) / 64, (rows + BG_ROWS - 1) / BG_ROWS);
   auto* st = (hipStream_t)stream;
-  hipLaunchKernelGGL(bias_grad_part_kernel, dim3((cols + 63) / 64, nparts), dim3(256), 0, st, dy,
-                     lddy, rows, cols, y, ldy, dym, lddm, ws);
-  hipLaunchKernelGGL(bias_grad_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, st, ws,
-                     nparts, cols, db);
+  if (y)
+    hipLaunchKernelGGL(bias_grad_kernel<true>, grid, dim3(256), 0, st, dy, lddy, rows, cols, y,
+                       ldy, dym, lddm, ws, counters, db);
+  else
+    hipLaunchKernelGGL(bias_grad_kernel<false>, grid, dim3(256), 0, st, dy, lddy, rows, cols, y,
+                       ldy, dym, lddm, ws, counters, db);
+  return (int)hipGetLastError();
+}
+
+// losses: host array of n device pointers (n <= 16); W: host [m][n] row-major
+// (m <= 4).  out[j] = sum_i W[j][i] * *losses[i].
+int tgfr_loss_mix(int n, const float* const* losses, int m, const float* W, float* out,
+                  void* stream) {
+  if (n <= 0 || n > MIX_N || m <= 0 || m > MIX_M || !losses || !W) return 1001;
+  MixArgs a = {};
+  for (int i = 0; i < n; ++i) {
+    a.loss[i] = losses[i];
+    for (int j = 0; j < m; ++j) a.w[j][i] = W[j * n + i];
+  }
+  hipLaunchKernelGGL(loss_mix_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a, n, m, out);
+  return (int)hipGetLastError();
+}
+
+// dloss[i] = g[0] * W[0][i] (W as for tgfr_loss_mix; only row 0 is read).
+int tgfr_loss_mix_bwd(const float* g, int n, const float* W, float* dloss, void* stream) {
+  if (n <= 0 || n > MIX_N || !W) return 1001;
+  MixArgs a = {};
+  for (int i = 0; i < n; ++i) a.w[0][i] = W[i];
+  hipLaunchKernelGGL(loss_mix_bwd_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, g, a, n,
+                     dloss);
   return (int)hipGetLastError();
 }
 

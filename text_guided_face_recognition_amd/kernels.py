@@ -209,14 +209,20 @@ class ContrastiveCE(torch.autograd.Function):
         dev = logits.device
         row_lse = torch.empty(n_r, dtype=torch.float32, device=dev)
         part = torch.empty(2, n_c, dtype=torch.float32, device=dev)
-        local_lse = torch.empty(n_c, dtype=torch.float32, device=dev) if group is None else None
-        call("tgfr_ce_stats", ptr(logits), n_c, n_r, n_c, ptr(row_lse), ptr(part[0]),
-             ptr(part[1]), ptr(local_lse), _hip.stream())
-        col_lse = local_lse if group is None else exchange_col_partials(part, group)
         loss = torch.empty(2, dtype=torch.float32, device=dev)
         inv_n = 1.0 / float(n_global)
-        call("tgfr_ce_loss", ptr(logits), n_c, n_r, int(row_offset), inv_n, ptr(row_lse),
-             ptr(col_lse), ptr(loss), _hip.stream())
+        if group is None:
+            # one launch: stats, final column LSE and both losses
+            col_lse = torch.empty(n_c, dtype=torch.float32, device=dev)
+            call("tgfr_ce_stats", ptr(logits), n_c, n_r, n_c, ptr(row_lse), ptr(part[0]),
+                 ptr(part[1]), ptr(col_lse), int(row_offset), inv_n, ptr(loss),
+                 ptr(_hip.counters(dev)), _hip.stream())
+        else:
+            call("tgfr_ce_stats", ptr(logits), n_c, n_r, n_c, ptr(row_lse), ptr(part[0]),
+                 ptr(part[1]), None, 0, 0.0, None, None, _hip.stream())
+            col_lse = exchange_col_partials(part, group)
+            call("tgfr_ce_loss", ptr(logits), n_c, n_r, int(row_offset), inv_n, ptr(row_lse),
+                 ptr(col_lse), ptr(loss), _hip.stream())
         ctx.save_for_backward(logits, row_lse, col_lse)
         ctx.cfg = (int(row_offset), inv_n)
         return loss[0], loss[1]
@@ -246,30 +252,23 @@ def bgemm(a, b, out=None, alpha=1.0, accumulate=False, mode="fp32", bias=None,
           relu=False, ksplit=1):
     """out[n] = epi(alpha * a[n] @ b[n] (+ out[n]) + bias) for 3-D fp32 tensors of
     any strides (transposed views cost nothing: strides are passed through).
-    ksplit > 1 splits K over blocks into slabs that are summed afterwards."""
+    ksplit > 1 splits K over blocks; the partial tiles are summed in-launch."""
     assert a.dim() == 3 and b.dim() == 3 and a.shape[0] == b.shape[0]
     assert a.shape[2] == b.shape[1] and a.dtype == b.dtype == torch.float32
     nb, m, k = a.shape
     n = b.shape[2]
-    if ksplit > 1:
-        slab = torch.empty(ksplit, nb, m, n, dtype=torch.float32, device=a.device)
-        call("tgfr_bgemm", ptr(a), a.stride(0), a.stride(1), a.stride(2), ptr(b),
-             b.stride(0), b.stride(1), b.stride(2), ptr(slab), m * n, n, 1, nb, m, n, k,
-             float(alpha), 0, None, 0, int(ksplit), nb * m * n, _mode(mode), _hip.stream())
-        red = slab.sum(0)
-        if out is None:
-            return red
-        if accumulate:
-            out.add_(red)
-        else:
-            out.copy_(red)
-        return out
     if out is None:
         out = torch.empty(nb, m, n, dtype=torch.float32, device=a.device)
+    slab = cnt = None
+    if ksplit > 1:
+        tiles = nb * -(-m // 64) * -(-n // 64)
+        assert tiles <= _hip.N_COUNTERS
+        slab = torch.empty(ksplit * tiles * 4096, dtype=torch.float32, device=a.device)
+        cnt = _hip.counters(a.device)
     call("tgfr_bgemm", ptr(a), a.stride(0), a.stride(1), a.stride(2), ptr(b), b.stride(0),
          b.stride(1), b.stride(2), ptr(out), out.stride(0), out.stride(1), out.stride(2),
-         nb, m, n, k, float(alpha), int(accumulate), ptr(bias), int(relu), 1, 0,
-         _mode(mode), _hip.stream())
+         nb, m, n, k, float(alpha), int(accumulate), ptr(bias), int(relu), int(ksplit),
+         ptr(slab), ptr(cnt), _mode(mode), _hip.stream())
     return out
 
 
@@ -311,7 +310,7 @@ class LinearRows(torch.autograd.Function):
             dym = torch.empty_like(dy) if relu else None
             call("tgfr_bias_grad", ptr(dy), dy.stride(0), rows, cols, ptr(y),
                  y.stride(0) if relu else 0, ptr(dym), dym.stride(0) if relu else 0, ptr(db),
-                 ptr(ws), _hip.stream())
+                 ptr(ws), ptr(_hip.counters(dy.device)), _hip.stream())
             if relu:
                 dy = dym
             if not want_db:
@@ -514,7 +513,7 @@ class FocalCE(torch.autograd.Function):
         ws = torch.empty(2 * rows + 1, dtype=torch.float32, device=logits.device)
         loss = torch.empty(1, dtype=torch.float32, device=logits.device)
         call("tgfr_focal_ce", ptr(logits), rows, cols, ptr(target), float(gamma), ptr(ws),
-             ptr(loss), _hip.stream())
+             ptr(_hip.counters(logits.device)), ptr(loss), _hip.stream())
         ctx.save_for_backward(logits, target, ws)
         ctx.gamma = float(gamma)
         return loss[0]
@@ -532,3 +531,41 @@ class FocalCE(torch.autograd.Function):
 
 def focal_ce(logits, target, gamma):
     return FocalCE.apply(logits, target, gamma)
+
+
+# ------------------------------------------------------------- loss mix ---
+class LossMix(torch.autograd.Function):
+    """(total, report) = (W[0] . losses, W[1:] . losses) in one launch; only
+    total carries a gradient (dloss_i = g W[0][i], one launch)."""
+
+    @staticmethod
+    def forward(ctx, weights, *losses):
+        n, m = len(losses), len(weights)
+        dev = losses[0].device
+        ptrs = (ctypes.c_void_p * n)(*[ptr(l.float()) for l in losses])
+        w = (ctypes.c_float * (n * m))(*[float(x) for row in weights for x in row])
+        out = torch.empty(m, dtype=torch.float32, device=dev)
+        call("tgfr_loss_mix", n, ctypes.addressof(ptrs), m, ctypes.addressof(w), ptr(out),
+             _hip.stream())
+        ctx.w0 = [float(x) for x in weights[0]]
+        ctx.set_materialize_grads(False)
+        total, report = out[0], out[1:]
+        ctx.mark_non_differentiable(report)
+        return total, report
+
+    @staticmethod
+    def backward(ctx, g, _unused):
+        n = len(ctx.w0)
+        if g is None:
+            return (None,) * (n + 1)
+        g = g.float().contiguous()
+        w = (ctypes.c_float * n)(*ctx.w0)
+        d = torch.empty(n, dtype=torch.float32, device=g.device)
+        call("tgfr_loss_mix_bwd", ptr(g), n, ctypes.addressof(w), ptr(d), _hip.stream())
+        return (None,) + tuple(d[i] for i in range(n))
+
+
+def loss_mix(losses, weights):
+    """weights: m rows of len(losses) floats; returns (total [], report [m-1])."""
+    return LossMix.apply(tuple(tuple(r) for r in weights), *losses)
+

@@ -23,6 +23,7 @@ from __future__ import annotations
 import torch
 from torch.nn.parallel import DistributedDataParallel as DDP
 
+from . import kernels as K
 from .dist import DistContext
 from .models.fusion_nets import Working, set_precision
 from .models.losses import FocalLoss, global_loss, sent_loss, words_loss
@@ -92,7 +93,7 @@ class Train:
         words_g = ctx.gather_rows(words.transpose(1, 2)).transpose(1, 2)
         sent_g = ctx.gather_rows(sent)
         cls_g = ctx.gather_rows(class_ids)
-        labels = torch.arange(ctx.n_global, device=g.device)
+        labels = self._labels(ctx.n_global, g.device)
 
         img_features, words_features = self.image_head(g, local)   # :265
         self.optimizer_head.zero_grad(set_to_none=True)
@@ -100,17 +101,28 @@ class Train:
 
         w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
         s0, s1 = sent_loss(img_features, sent_g, labels, cls_g, b, args)
-        damsm = w0 + w1 + s0 + s1                                  # :279
         tid = self.ident_loss(self.text_cls(sent, class_ids), class_ids)      # :293-294
         iid = self.ident_loss(self.image_cls(img_features, class_ids), class_ids)
         cl = global_loss(img_features, sent_g, args=args)          # :310
-        contrastive = damsm + args.lambda_clip * cl
-        total = ctx.world * contrastive + args.lambda_id * (tid + iid)
+        # total = world * (damsm + lambda_clip * cl) + lambda_id * (tid + iid)
+        # (:279, :316-323) and the logged terms, as one launch each way
+        wd, wi = float(ctx.world), float(args.lambda_id)
+        total, report = K.loss_mix(
+            (w0, w1, s0, s1, cl, tid, iid),
+            [(wd, wd, wd, wd, wd * args.lambda_clip, wi, wi),     # objective
+             (1, 1, 1, 1, 0, 0, 0),                               # damsm
+             (0, 0, 0, 0, 1, 0, 0),                               # clip
+             (0, 0, 0, 0, 0, wi, wi)])                            # ident
         total.backward()                                           # :323
         self.optimizer_head.step()
         self.optimizer_cls.step()
-        return {"damsm": damsm.detach(), "clip": cl.detach(),
-                "ident": (args.lambda_id * (tid + iid)).detach()}
+        return {"damsm": report[0], "clip": report[1], "ident": report[2]}
+
+    def _labels(self, n, device):
+        lab = getattr(self, "_lab", None)
+        if lab is None or lab.numel() != n or lab.device != device:
+            lab = self._lab = torch.arange(n, device=device)
+        return lab
 
 
 class Fusion:

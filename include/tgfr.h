@@ -125,8 +125,9 @@ int tgfr_ce_grad(const float* L, long long ld, int n_r, int n_c, int row_offset,
  * backward.  bias (nullable, per column) and relu form the epilogue.  With
  * ksplit > 1 the K range is split over ksplit blocks per 64x64 output tile;
  * each stores a partial tile to slab (ksplit * tiles * 4096 floats, tiles =
- * batch * ceil(M/64) * ceil(N/64)) and the tile's last-arriving block sums the
- * partials in slice order (deterministic) and applies the epilogue.
+ * batch * ceil(M/64) * ceil(N/64)); the partials are summed in slice order
+ * (deterministic) and the epilogue applied by the tile's last-arriving block
+ * (ksplit <= 4) or by a second, chip-wide launch (ksplit > 4).
  * counters: >= tiles zeroed uint32 words, left zeroed on return. */
 int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, const float* B,
                long long sBb, long long sBk, long long sBn, float* C, long long sCb,

@@ -30,6 +30,11 @@ constexpr int STAGE = 4 * HALF;               // A hi, A lo, B hi, B lo
 // so a transposed operand costs neither a copy nor uncoalesced loads.
 enum { LAY_K = 0, LAY_MN = 1, LAY_ANY = 2 };
 
+// Split-K partial tiles are combined in-launch by the last-arriving slice only
+// while the serial slab read stays small (<= 4 x 16 KB per tile); beyond that a
+// chip-wide reduce launch is cheaper.
+constexpr int KSPLIT_INLAUNCH = 4;
+
 // [64 mn][32 k]: 16-B chunk swizzle keeps ds_read_b128 lane groups conflict-free.
 __device__ __forceinline__ uint32_t toff(int row, int chunk) {
   return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
@@ -159,13 +164,15 @@ __global__ __launch_bounds__(256) void bgemm_kernel(
     __syncthreads();
   }
   if (ksplit > 1) {
-    // every K slice stores its tile slab (lane-major, 64 B per lane); the last
-    // arriving slice of the tile sums all slabs in slice order (deterministic)
+    // every K slice stores its tile slab (lane-major, 64 B per lane); with few
+    // slices the last arriving slice of the tile sums all slabs in slice order
+    // (deterministic), otherwise bgemm_reduce_kernel does it chip-wide
     const long long tile = ((long long)bt * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     float4* mine = (float4*)(slab + ((tile * ksplit + kz) * 256 + tid) * 16);
 #pragma unroll
     for (int v = 0; v < 4; ++v)
       mine[v] = make_float4(acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]);
+    if (ksplit > KSPLIT_INLAUNCH) return;
     if (!last_arrival(counters + tile, ksplit, (int*)(g_smem + 2 * STAGE))) return;
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = 0.f;
@@ -190,6 +197,40 @@ __global__ __launch_bounds__(256) void bgemm_kernel(
       float v = alpha * acc[q] + bn;
       if (accumulate) v += *o;
       *o = relu ? fmaxf(v, 0.f) : v;
+    }
+  }
+}
+
+// Chip-wide split-K combine: one thread per (tile, lane, 4-register group);
+// slabs summed in slice order, then the bgemm epilogue.
+__global__ __launch_bounds__(256) void bgemm_reduce_kernel(
+    const float* __restrict__ slab, int ksplit, int mt, int nt, long long n_tiles, float* Cm,
+    long long sCb, long long sCm, long long sCn, int M, int N, float alpha, int accumulate,
+    const float* __restrict__ bias, int relu) {
+  const long long e = blockIdx.x * 256LL + threadIdx.x;
+  if (e >= n_tiles * 1024) return;
+  const long long tile = e >> 10;
+  const int r = (int)(e & 1023), tid = r >> 2, v = r & 3;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int z = 0; z < ksplit; ++z) {
+    const float4 t = ((const float4*)(slab + ((tile * ksplit + z) * 256 + tid) * 16))[v];
+    a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w;
+  }
+  const int tn = (int)(tile % nt), tm = (int)((tile / nt) % mt), bt = (int)(tile / ((long long)nt * mt));
+  const int wid = tid / WAVE, lane = tid % WAVE, wm = wid >> 1, wn = wid & 1;
+  const int n = tn * BN + 32 * wn + (lane & 31);
+  if (n >= N) return;
+  const float bn = bias ? bias[n] : 0.f;
+  const float vals[4] = {a.x, a.y, a.z, a.w};
+  float* Cb = Cm + bt * sCb;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = tm * BM + 32 * wm + acc_row(4 * v + j, lane >> 5);
+    if (m < M) {
+      float* o = Cb + m * sCm + n * sCn;
+      float val = alpha * vals[j] + bn;
+      if (accumulate) val += *o;
+      *o = relu ? fmaxf(val, 0.f) : val;
     }
   }
 }
@@ -263,6 +304,12 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
   hipLaunchKernelGGL(table[mode][la][lb], grid, dim3(256), 2 * STAGE + 16, s, A, sAb, sAm, sAk,
                      B, sBb, sBk, sBn, C, sCb, sCm, sCn, M, N, K, alpha, accumulate, bias, relu,
                      ksplit, slab, counters);
+  if (ksplit > KSPLIT_INLAUNCH) {
+    const long long tiles = (long long)grid.x * grid.y * batch;
+    hipLaunchKernelGGL(bgemm_reduce_kernel, dim3((unsigned)((tiles * 1024 + 255) / 256)),
+                       dim3(256), 0, s, slab, ksplit, (int)grid.y, (int)grid.x, tiles, C, sCb,
+                       sCm, sCn, M, N, alpha, accumulate, bias, relu);
+  }
   return (int)hipGetLastError();
 }
 

@@ -273,10 +273,12 @@ def bgemm(a, b, out=None, alpha=1.0, accumulate=False, mode="fp32", bias=None,
 
 
 def _ksplit(k, mn_blocks):
-    """Split-K factor that gives >= ~512 blocks for a long-K, small-output GEMM."""
-    if k < 1024 or mn_blocks >= 256:
+    """Split-K factor giving ~512 blocks to a small-output GEMM, with K slices
+    of at least 128 (K < 2048) or 256 elements."""
+    if mn_blocks >= 256 or k < 256:
         return 1
-    return int(max(1, min(k // 256, -(-512 // mn_blocks))))
+    chunk = 128 if k < 2048 else 256
+    return int(max(1, min(k // chunk, -(-512 // mn_blocks))))
 
 
 class LinearRows(torch.autograd.Function):
@@ -288,8 +290,10 @@ class LinearRows(torch.autograd.Function):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).float()
         w = weight.reshape(weight.shape[0], -1).float()
+        mb = -(-x2.shape[0] // 64) * -(-w.shape[0] // 64)
         y = bgemm(x2.unsqueeze(0), w.t().unsqueeze(0), mode=mode,
-                  bias=None if bias is None else bias.float().contiguous(), relu=relu)[0]
+                  bias=None if bias is None else bias.float().contiguous(), relu=relu,
+                  ksplit=_ksplit(x2.shape[1], mb))[0]
         ctx.save_for_backward(x2, w, y if relu else None)
         ctx.cfg = (relu, mode, bias is not None, shape, weight.shape)
         return y.reshape(*shape[:-1], w.shape[0])

@@ -1,7 +1,9 @@
 """Per-kernel breakdown of one graph-replayed train step from a rocprofv3
 kernel trace (tools/profile_round.sh output).
 
-    python tools/step_breakdown.py <bench_kernel_trace.csv> [--list]
+    python tools/step_breakdown.py <bench_kernel_trace.csv> [--list] [--step K]
+
+K indexes the word-region forward launches (one per step); default -3.
 """
 import collections
 import csv
@@ -9,12 +11,12 @@ import re
 import sys
 
 
-def main(path, listing=False):
+def main(path, listing=False, which=-3):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if "wr_fwd" in r["Kernel_Name"]]
-    step = rows[idx[-3]:idx[-2]]
-    t0, t1 = int(step[0]["Start_Timestamp"]), int(rows[idx[-2]]["Start_Timestamp"])
+    step = rows[idx[which]:idx[which + 1]]
+    t0, t1 = int(step[0]["Start_Timestamp"]), int(rows[idx[which + 1]]["Start_Timestamp"])
     fam = collections.defaultdict(lambda: [0, 0.0])
     for i, r in enumerate(step):
         n = r["Kernel_Name"]
@@ -43,4 +45,5 @@ def main(path, listing=False):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], "--list" in sys.argv)
+    k = sys.argv.index("--step") if "--step" in sys.argv else None
+    main(sys.argv[1], "--list" in sys.argv, int(sys.argv[k + 1]) if k else -3)

@@ -123,12 +123,13 @@ int tgfr_ce_grad(const float* L, long long ld, int n_r, int n_c, int row_offset,
  * products of SelfAttention (models/fusion_nets.py:103, :115), the 1x1-conv /
  * Linear projections of IMIM and FCFM (models/models.py:386-404), and their
  * backward.  bias (nullable, per column) and relu form the epilogue.  With
- * ksplit > 1 the K range is split over ksplit blocks per 64x64 output tile;
- * each stores a partial tile to slab (ksplit * tiles * 4096 floats, tiles =
- * batch * ceil(M/64) * ceil(N/64)); the partials are summed in slice order
- * (deterministic) and the epilogue applied by the tile's last-arriving block
+ * ksplit > 1 the K range is split over ksplit blocks per output tile; each
+ * stores its partial tile to slab (at least ksplit * batch * ceil(M/128)*128 *
+ * ceil(N/128)*128 floats) and the partials are summed in slice order
+ * (deterministic) before the epilogue, by the tile's last-arriving block
  * (ksplit <= 4) or by a second, chip-wide launch (ksplit > 4).
- * counters: >= tiles zeroed uint32 words, left zeroed on return. */
+ * counters: >= batch * ceil(M/64) * ceil(N/64) zeroed uint32 words, left
+ * zeroed on return. */
 int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, const float* B,
                long long sBb, long long sBk, long long sBn, float* C, long long sCb,
                long long sCm, long long sCn, int batch, int M, int N, int K, float alpha,

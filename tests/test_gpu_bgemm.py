@@ -64,3 +64,30 @@ def test_epilogues(gpu):
     K.bgemm(a, b, out=out)
     torch.testing.assert_close(out[0].double(), a[0].double() @ b[0].double(),
                                rtol=1e-4, atol=2e-4)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+@pytest.mark.parametrize("shape", [
+    (76, 132, 204, 1),        # ragged tiles, 64x64 DMA path
+    (4100, 1028, 96, 1),      # 128x128 tiles
+    (12548, 256, 68, 1),      # 128x64 tiles
+    (196, 196, 256, 8),       # batched attention-like products
+])
+@pytest.mark.parametrize("la,lb", [("row", "col"), ("col", "row"), ("row", "row"),
+                                   ("col", "col")])
+def test_dma_path_configs(gpu, mode, shape, la, lb):
+    """Shapes whose operands the DMA path fetches (16-B quads along the unit
+    axis), across the tile configurations the launcher picks."""
+    from text_guided_face_recognition_amd import kernels as K
+    m, n, k, nb = shape
+    gen = torch.Generator().manual_seed(14)
+    a = torch.stack([_operand(m, k, la, gpu, gen) for _ in range(nb)])
+    b = torch.stack([_operand(k, n, lb, gpu, gen) for _ in range(nb)])
+    if la == "col":
+        a = a.transpose(1, 2).contiguous().transpose(1, 2)
+    if lb == "col":
+        b = b.transpose(1, 2).contiguous().transpose(1, 2)
+    c = K.bgemm(a, b, mode=mode)
+    ref = a.double() @ b.double()
+    err = (c.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < (2e-5 if mode == "fp32" else 1e-2), err

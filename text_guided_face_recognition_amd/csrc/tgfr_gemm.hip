@@ -1,0 +1,523 @@
+// Batched GEMM for the IMIM / FCFM heads and the attention products
+// (models/fusion_nets.py:103, :115; models/models.py:386-404; the 1x1 convs,
+// Linear layers and their backward):
+//
+//   C[b] = epi(alpha * A[b] B[b] (+ C[b]) + bias),  epi = optional ReLU,
+//
+// fp32 operands of ANY element strides (every transpose of the backward is a
+// stride swap), fp32 accumulation on v_mfma_f32_32x32x16_bf16, operands
+// carried as bf16 (MODE_BF16) or as a bf16 hi/lo pair (MODE_SPLIT, ~fp32).
+//
+// Two kernels:
+//   bgemm_glds  the main path.  fp32 tiles go global -> LDS by global_load_lds
+//               (no staging registers) through an NS-deep ring, so NS-1 tiles
+//               are in flight while one is computed; the bf16 (hi/lo)
+//               conversion happens at fragment-read time.  Per operand the LDS
+//               image follows the operand's unit-stride axis:
+//                 LAY_K   [rows][32 k]  128-B rows, 16-B quads XOR-swizzled by
+//                         row so the two ds_read_b128 of a fragment are
+//                         conflict-free
+//                 LAY_MN  [32 k][rows] (unit stride along m / n), read with 8
+//                         ds_read_b32 per fragment (consecutive lanes =
+//                         consecutive banks)
+//               Block tile (64 WM) x (64 WN), 4 waves in 2 x 2, each wave
+//               (32 WM) x (32 WN) = WM x WN accumulators; the host picks the
+//               largest tile that still fills the chip.  Block ids are remapped
+//               so the tiles that share an A row block run on one XCD (L2).
+//   bgemm_regs  register-staged fallback for operands the DMA cannot fetch
+//               (no unit-stride axis, 16-B misalignment, ragged quads).
+//
+// Split-K: each K slice stores its partial tile to a slab; the slices are
+// summed in slice order (deterministic) by the tile's last-arriving slice
+// (few slices) or by one chip-wide reduce launch (many slices).
+#include "tgfr_common.h"
+
+using namespace tgfr;
+
+namespace {
+
+constexpr int BK = 32;
+enum { LAY_K = 0, LAY_MN = 1, LAY_ANY = 2 };
+constexpr int KSPLIT_INLAUNCH = 4;
+
+__device__ __attribute__((aligned(16))) float g_zero16[4] = {0.f, 0.f, 0.f, 0.f};
+
+struct Frag8 {
+  float v[8];
+};
+
+// ------------------------------------------------------------- epilogues ---
+// Stores one 32x32 accumulator (rows m0.., cols n0..) with the bgemm epilogue.
+__device__ __forceinline__ void store_acc(const f32x16& acc, float* Cb, long long sCm,
+                                          long long sCn, int m0, int n0, int M, int N,
+                                          float alpha, int accumulate, const float* bias,
+                                          int relu, int lane) {
+  const int n = n0 + (lane & 31);
+  if (n >= N) return;
+  const float bn = bias ? bias[n] : 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int m = m0 + acc_row(q, lane >> 5);
+    if (m < M) {
+      float* o = Cb + m * sCm + n * sCn;
+      float v = alpha * acc[q] + bn;
+      if (accumulate) v += *o;
+      *o = relu ? fmaxf(v, 0.f) : v;
+    }
+  }
+}
+
+// Slab of one split-K slice: the tile in natural [TM][TN] order.
+__device__ __forceinline__ void store_slab(const f32x16& acc, float* tile_slab, int TN, int mm0,
+                                           int nn0, int lane) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q)
+    tile_slab[(mm0 + acc_row(q, lane >> 5)) * TN + nn0 + (lane & 31)] = acc[q];
+}
+__device__ __forceinline__ void sum_slabs(f32x16& acc, const float* slab0, long long slab_stride,
+                                          int ksplit, int TN, int mm0, int nn0, int lane) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  for (int z = 0; z < ksplit; ++z) {
+    const float* t = slab0 + z * slab_stride;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] += t[(mm0 + acc_row(q, lane >> 5)) * TN + nn0 + (lane & 31)];
+  }
+}
+
+// Chip-wide split-K combine: thread = (tile, row, 4 columns); slabs summed in
+// slice order, then the epilogue.
+__global__ __launch_bounds__(256) void bgemm_reduce_kernel(
+    const float* __restrict__ slab, int ksplit, int TM, int TN, int mt, int nt, long long n_tiles,
+    float* Cm, long long sCb, long long sCm, long long sCn, int M, int N, float alpha,
+    int accumulate, const float* __restrict__ bias, int relu) {
+  const int per_tile = TM * TN / 4;
+  const long long e = blockIdx.x * 256LL + threadIdx.x;
+  if (e >= n_tiles * per_tile) return;
+  const long long tile = e / per_tile;
+  const int r = (int)(e % per_tile), mm = r / (TN / 4), nn = (r % (TN / 4)) * 4;
+  const float4* src = (const float4*)(slab + tile * ksplit * (long long)(TM * TN) + mm * TN + nn);
+  const long long zs = TM * TN / 4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+  for (int z = 0; z < ksplit; ++z) {
+    const float4 t = src[z * zs];
+    a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w;
+  }
+  const int tn = (int)(tile % nt), tm = (int)((tile / nt) % mt);
+  const int bt = (int)(tile / ((long long)nt * mt));
+  const int m = tm * TM + mm;
+  if (m >= M) return;
+  float* Cb = Cm + bt * sCb + m * sCm;
+  const float vals[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = tn * TN + nn + j;
+    if (n < N) {
+      float* o = Cb + n * sCn;
+      float v = alpha * vals[j] + (bias ? bias[n] : 0.f);
+      if (accumulate) v += *o;
+      *o = relu ? fmaxf(v, 0.f) : v;
+    }
+  }
+}
+
+// ------------------------------------------------------- glds main path ---
+// LDS image of one fp32 operand tile (R rows x 32 k) per layout.
+template <int LAY, int R>
+struct Img {
+  static constexpr int BYTES = R * BK * 4;
+  static constexpr int PIECES = BYTES / 1024;     // one wave instruction = 1 KiB
+};
+
+// Quad swizzle of the [rows][32 k] fp32 image: 16 consecutive rows of one
+// logical quad hit 16 distinct (row parity, quad) bank groups.
+__device__ __forceinline__ int kswz(int row, int q) { return q ^ ((row >> 1) & 7); }
+
+// Issue this wave's share of the DMA pieces of one operand tile.
+// base: element (mn = 0, k = 0) of the tile; mn_lim / k_lim: valid extents.
+template <int LAY, int R>
+__device__ __forceinline__ void issue_tile(const float* base, long long s_mn, long long s_k,
+                                           int mn_lim, int k_lim, uint32_t lds_off, int wid,
+                                           int lane) {
+  constexpr int P = Img<LAY, R>::PIECES;
+#pragma unroll
+  for (int p = wid; p < P; p += 4) {
+    const float* src;
+    if constexpr (LAY == LAY_K) {
+      const int row = p * 8 + (lane >> 3);
+      const int q = kswz(row, lane & 7);
+      const bool ok = row < mn_lim && 4 * q < k_lim;
+      src = ok ? base + row * s_mn + 4 * q : g_zero16;
+    } else {
+      constexpr int ROWB = R * 4;                 // bytes per k row
+      const int byte = p * 1024 + lane * 16;
+      const int kr = byte / ROWB, mn = (byte % ROWB) / 4;
+      const bool ok = mn < mn_lim && kr < k_lim;
+      src = ok ? base + kr * s_k + mn : g_zero16;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(lds_base() + lds_off + p * 1024),
+                                     16, 0, 0);
+  }
+}
+
+// Fragment (lane: row mn0 + lane%32, k = 16 s + 8 (lane/32) .. +7) as fp32.
+template <int LAY, int R>
+__device__ __forceinline__ void read_frag(Frag8& f, uint32_t off, int mn0, int s, int lane) {
+  const int row = mn0 + (lane & 31), k0 = 16 * s + 8 * (lane >> 5);
+  if constexpr (LAY == LAY_K) {
+    const int q = k0 >> 2;
+    const float4 a = __builtin_bit_cast(float4, lds_ld16(off + row * 128 + (kswz(row, q) << 4)));
+    const float4 b =
+        __builtin_bit_cast(float4, lds_ld16(off + row * 128 + (kswz(row, q + 1) << 4)));
+    f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w;
+    f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f.v[j] = lds_ldf(off + (k0 + j) * (R * 4) + row * 4);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int MODE, int LA, int LB, int WM, int WN, int NS>
+__global__ __launch_bounds__(256) void bgemm_glds_kernel(
+    const float* __restrict__ A, long long sAb, long long sAm, long long sAk,
+    const float* __restrict__ B, long long sBb, long long sBk, long long sBn,
+    float* __restrict__ Cm, long long sCb, long long sCm, long long sCn, int M, int N, int Kfull,
+    float alpha, int accumulate, const float* __restrict__ bias, int relu, int ksplit,
+    float* __restrict__ slab, unsigned* __restrict__ counters) {
+  constexpr int TM = 64 * WM, TN = 64 * WN;
+  constexpr int SA = Img<LA, TM>::BYTES, SB = Img<LB, TN>::BYTES, STG = SA + SB;
+  constexpr int PER = (Img<LA, TM>::PIECES + Img<LB, TN>::PIECES) / 4;   // DMA ops / wave / stage
+  // XCD-aware tile order: consecutive work ids (same A row block) share an L2
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int w = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
+  const int tn = w % gx, tm = w / gx;
+  const int n0 = tn * TN, m0 = tm * TM;
+  const int bt = blockIdx.z / ksplit, kz = blockIdx.z % ksplit;
+  const int kc = ((Kfull + ksplit - 1) / ksplit + BK - 1) / BK * BK;
+  const int kb = kz * kc;
+  const int K = max(0, min(Kfull - kb, kc));
+  const int tid = threadIdx.x, wid = tid / WAVE, lane = tid % WAVE;
+  const int wm = wid >> 1, wn = wid & 1;
+  const float* Ab = A + bt * sAb + m0 * sAm + (long long)kb * sAk;
+  const float* Bb = B + bt * sBb + n0 * sBn + (long long)kb * sBk;
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  const int nk = (K + BK - 1) / BK;
+  auto issue = [&](int kt) {
+    const uint32_t o = (kt % NS) * STG;
+    const int k0 = kt * BK;
+    issue_tile<LA, TM>(Ab + (long long)k0 * sAk, sAm, sAk, M - m0, K - k0, o, wid, lane);
+    issue_tile<LB, TN>(Bb + (long long)k0 * sBk, sBn, sBk, N - n0, K - k0, o + SA, wid, lane);
+  };
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st)
+    if (st < nk) issue(st);
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's pieces of tile kt have landed once at most (NS-2) younger
+    // stages are outstanding; the barrier makes every wave's pieces visible
+    // and retires the reads of tile kt-1, whose buffer is refilled next
+    if (kt + NS - 2 < nk) wait_vm<(NS - 2) * PER>();
+    else wait_vm<0>();
+    __syncthreads();
+    if (kt + NS - 1 < nk) issue(kt + NS - 1);
+    const uint32_t o = (kt % NS) * STG;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 bh[WN], bl[WN];
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        Frag8 f;
+        read_frag<LB, TN>(f, o + SA, wn * 32 * WN + 32 * j, s, lane);
+        frag8<MODE>(f.v, bh[j], bl[j]);
+      }
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        Frag8 f;
+        bf16x8 ah, al;
+        read_frag<LA, TM>(f, o, wm * 32 * WM + 32 * i, s, lane);
+        frag8<MODE>(f.v, ah, al);
+#pragma unroll
+        for (int j = 0; j < WN; ++j) mma<MODE>(acc[i][j], ah, al, bh[j], bl[j]);
+      }
+    }
+  }
+
+  if (ksplit > 1) {
+    const long long tile = ((long long)bt * gy + tm) * gx + tn;
+    float* mine = slab + (tile * ksplit + kz) * (long long)(TM * TN);
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+        store_slab(acc[i][j], mine, TN, wm * 32 * WM + 32 * i, wn * 32 * WN + 32 * j, lane);
+    if (ksplit > KSPLIT_INLAUNCH) return;
+    if (!last_arrival(counters + tile, ksplit, (int*)(g_smem + NS * STG))) return;
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+        sum_slabs(acc[i][j], slab + tile * ksplit * (long long)(TM * TN), TM * TN, ksplit, TN,
+                  wm * 32 * WM + 32 * i, wn * 32 * WN + 32 * j, lane);
+  }
+  float* Cb = Cm + bt * sCb;
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+      store_acc(acc[i][j], Cb, sCm, sCn, m0 + wm * 32 * WM + 32 * i, n0 + wn * 32 * WN + 32 * j,
+                M, N, alpha, accumulate, bias, relu, lane);
+}
+
+// ------------------------------------------------- register-staged path ---
+constexpr int HALF = 64 * 64;                 // bytes of one 64x32 bf16 tile
+constexpr int STAGE = 4 * HALF;               // A hi, A lo, B hi, B lo
+
+// [64 mn][32 k] bf16: 16-B chunk swizzle keeps ds_read_b128 lane groups conflict-free.
+__device__ __forceinline__ uint32_t toff(int row, int chunk) {
+  return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
+}
+// [32 k][64 mn] bf16: rows 2 apart land 64 B apart, so the 4 rows of one
+// transposed read hit disjoint banks.
+__device__ __forceinline__ uint32_t moff(int krow, int chunk) {
+  return krow * 128 + ((chunk ^ (((krow >> 1) & 1) << 2)) << 4);
+}
+
+// Staging role of thread tid for one 64x32 operand tile:
+//   LAY_K/ANY: mn row tid/4, k 8*(tid%4) .. +7
+//   LAY_MN:    k row tid/8,  mn 8*(tid%8) .. +7
+template <int LAY>
+__device__ __forceinline__ void load_tile(Frag8& f, const float* base, long long s_mn,
+                                          long long s_k, int tid, int k0, int mn_lim, int K) {
+  if constexpr (LAY == LAY_MN) {
+    const int k = k0 + (tid >> 3), mn = (tid & 7) * 8;
+    const float* p = base + (long long)k * s_k + mn;
+    if (k < K && mn + 8 <= mn_lim && (((uintptr_t)p & 15) == 0)) {
+      const float4 a = *(const float4*)p;
+      const float4 b = *(const float4*)(p + 4);
+      f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w;
+      f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f.v[e] = (k < K && mn + e < mn_lim) ? p[e] : 0.f;
+    }
+  } else {
+    const int row = tid >> 2, k = k0 + (tid & 3) * 8;
+    const float* p = base + (long long)row * s_mn + (long long)k * s_k;
+    if (LAY == LAY_K && row < mn_lim && k + 8 <= K && (((uintptr_t)p & 15) == 0)) {
+      const float4 a = *(const float4*)p;
+      const float4 b = *(const float4*)(p + 4);
+      f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w;
+      f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        f.v[e] = (row < mn_lim && k + e < K) ? p[(long long)e * s_k] : 0.f;
+    }
+  }
+}
+
+template <int MODE, int LAY>
+__device__ __forceinline__ void store_tile(uint32_t base, const Frag8& f, int tid) {
+  bf16x8 hi, lo;
+  frag8<MODE>(f.v, hi, lo);
+  const uint32_t off =
+      base + (LAY == LAY_MN ? moff(tid >> 3, tid & 7) : toff(tid >> 2, tid & 3));
+  lds_st16(off, __builtin_bit_cast(uint4, hi));
+  if (MODE == MODE_SPLIT) lds_st16(off + HALF, __builtin_bit_cast(uint4, lo));
+}
+
+// MFMA operand fragment: lane (lr, h) gets element [mn = mn0 + lr][k = 16 s + 8 h .. +7].
+template <int LAY>
+__device__ __forceinline__ bf16x8 frag_read(uint32_t base, int mn0, int s, int lane) {
+  if constexpr (LAY == LAY_MN) {
+    // 16-lane group g: mn block 16 (g & 1), k rows 16 s + 8 (g >> 1) (+4);
+    // lane 4q+p addresses k row q, mn columns 4p .. 4p+3
+    const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
+    const int col = mn0 + 16 * (g & 1) + 4 * p;
+    const int kr = 16 * s + 8 * (g >> 1) + q;
+    const uint32_t a = base + moff(kr, col >> 3) + (col & 7) * 2;
+    const uint32_t b = base + moff(kr + 4, col >> 3) + (col & 7) * 2;
+    return join_tr(lds_tr4(a), lds_tr4(b));
+  } else {
+    return as_bf8(lds_ld16(base + toff(mn0 + (lane & 31), 2 * s + (lane >> 5))));
+  }
+}
+
+template <int MODE, int LA, int LB>
+__global__ __launch_bounds__(256) void bgemm_regs_kernel(
+    const float* __restrict__ A, long long sAb, long long sAm, long long sAk,
+    const float* __restrict__ B, long long sBb, long long sBk, long long sBn,
+    float* __restrict__ Cm, long long sCb, long long sCm, long long sCn, int M, int N, int Kfull,
+    float alpha, int accumulate, const float* __restrict__ bias, int relu, int ksplit,
+    float* __restrict__ slab, unsigned* __restrict__ counters) {
+  const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+  const int bt = blockIdx.z / ksplit, kz = blockIdx.z % ksplit;
+  const int kc = ((Kfull + ksplit - 1) / ksplit + BK - 1) / BK * BK;
+  const int kb = kz * kc;
+  const int K = max(0, min(Kfull - kb, kc));
+  const int tid = threadIdx.x, wid = tid / WAVE, lane = tid % WAVE;
+  const int wm = wid >> 1, wn = wid & 1;
+  const float* Ab = A + bt * sAb + m0 * sAm + (long long)kb * sAk;
+  const float* Bb = B + bt * sBb + n0 * sBn + (long long)kb * sBk;
+  Frag8 fa, fb;
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+
+  const int nk = (K + BK - 1) / BK;
+  if (nk > 0) {
+    load_tile<LA>(fa, Ab, sAm, sAk, tid, 0, M - m0, K);
+    load_tile<LB>(fb, Bb, sBn, sBk, tid, 0, N - n0, K);
+    store_tile<MODE, LA>(0, fa, tid);
+    store_tile<MODE, LB>(2 * HALF, fb, tid);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const uint32_t sb = (kt & 1) * STAGE;
+    if (kt + 1 < nk) {
+      load_tile<LA>(fa, Ab, sAm, sAk, tid, (kt + 1) * BK, M - m0, K);
+      load_tile<LB>(fb, Bb, sBn, sBk, tid, (kt + 1) * BK, N - n0, K);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 ahi = frag_read<LA>(sb, 32 * wm, s, lane);
+      const bf16x8 bhi = frag_read<LB>(sb + 2 * HALF, 32 * wn, s, lane);
+      const bf16x8 alo = MODE == MODE_SPLIT ? frag_read<LA>(sb + HALF, 32 * wm, s, lane) : ahi;
+      const bf16x8 blo =
+          MODE == MODE_SPLIT ? frag_read<LB>(sb + 3 * HALF, 32 * wn, s, lane) : bhi;
+      mma<MODE>(acc, ahi, alo, bhi, blo);
+    }
+    if (kt + 1 < nk) {
+      const uint32_t nb = ((kt + 1) & 1) * STAGE;
+      store_tile<MODE, LA>(nb, fa, tid);
+      store_tile<MODE, LB>(nb + 2 * HALF, fb, tid);
+    }
+    __syncthreads();
+  }
+  if (ksplit > 1) {
+    const long long tile = ((long long)bt * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    store_slab(acc, slab + (tile * ksplit + kz) * 4096LL, 64, 32 * wm, 32 * wn, lane);
+    if (ksplit > KSPLIT_INLAUNCH) return;
+    if (!last_arrival(counters + tile, ksplit, (int*)(g_smem + 2 * STAGE))) return;
+    sum_slabs(acc, slab + tile * ksplit * 4096LL, 4096, ksplit, 64, 32 * wm, 32 * wn, lane);
+  }
+  store_acc(acc, Cm + bt * sCb, sCm, sCn, m0 + 32 * wm, n0 + 32 * wn, M, N, alpha, accumulate,
+            bias, relu, lane);
+}
+
+using GemmFn = void (*)(const float*, long long, long long, long long, const float*, long long,
+                        long long, long long, float*, long long, long long, long long, int, int,
+                        int, float, int, const float*, int, int, float*, unsigned*);
+
+template <int MODE, int LA, int LB>
+GemmFn glds_fn(int cfg) {
+  switch (cfg) {
+    case 0: return &bgemm_glds_kernel<MODE, LA, LB, 1, 1, 4>;
+    case 1: return &bgemm_glds_kernel<MODE, LA, LB, 2, 1, 3>;
+    case 2: return &bgemm_glds_kernel<MODE, LA, LB, 1, 2, 3>;
+    default: return &bgemm_glds_kernel<MODE, LA, LB, 2, 2, 3>;
+  }
+}
+constexpr int CFG_WM[4] = {1, 2, 1, 2}, CFG_WN[4] = {1, 1, 2, 2}, CFG_NS[4] = {4, 3, 3, 3};
+
+template <int MODE>
+GemmFn pick_glds(int la, int lb, int cfg) {
+  if (la == LAY_K)
+    return lb == LAY_K ? glds_fn<MODE, LAY_K, LAY_K>(cfg) : glds_fn<MODE, LAY_K, LAY_MN>(cfg);
+  return lb == LAY_K ? glds_fn<MODE, LAY_MN, LAY_K>(cfg) : glds_fn<MODE, LAY_MN, LAY_MN>(cfg);
+}
+
+template <int MODE>
+GemmFn pick_regs(int la, int lb) {
+  static const GemmFn t[3][3] = {
+      {&bgemm_regs_kernel<MODE, LAY_K, LAY_K>, &bgemm_regs_kernel<MODE, LAY_K, LAY_MN>,
+       &bgemm_regs_kernel<MODE, LAY_K, LAY_ANY>},
+      {&bgemm_regs_kernel<MODE, LAY_MN, LAY_K>, &bgemm_regs_kernel<MODE, LAY_MN, LAY_MN>,
+       &bgemm_regs_kernel<MODE, LAY_MN, LAY_ANY>},
+      {&bgemm_regs_kernel<MODE, LAY_ANY, LAY_K>, &bgemm_regs_kernel<MODE, LAY_ANY, LAY_MN>,
+       &bgemm_regs_kernel<MODE, LAY_ANY, LAY_ANY>}};
+  return t[la][lb];
+}
+
+bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// Can the DMA fetch this operand as whole 16-B quads?
+bool dma_ok(const float* p, int lay, long long sb, long long s_mn, long long s_k, int mn, int k,
+            int batch) {
+  if (lay == LAY_ANY || !al16(p) || (batch > 1 && (sb & 3))) return false;
+  if (lay == LAY_K) return (s_mn & 3) == 0 && (k & 3) == 0;
+  return (s_k & 3) == 0 && (mn & 3) == 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, const float* B,
+               long long sBb, long long sBk, long long sBn, float* C, long long sCb,
+               long long sCm, long long sCn, int batch, int M, int N, int K, float alpha,
+               int accumulate, const float* bias, int relu, int ksplit, float* slab,
+               unsigned* counters, int mode, void* stream) {
+  if (batch <= 0 || M <= 0 || N <= 0 || K <= 0 || ksplit <= 0) return 1001;
+  if (ksplit > 1 && (!slab || !counters)) return 1001;
+  if (mode != MODE_SPLIT && mode != MODE_BF16) return 1002;
+  auto* s = (hipStream_t)stream;
+  const int la = sAk == 1 ? LAY_K : sAm == 1 ? LAY_MN : LAY_ANY;
+  const int lb = sBk == 1 ? LAY_K : sBn == 1 ? LAY_MN : LAY_ANY;
+  const bool dma = dma_ok(A, la, sAb, sAm, sAk, M, K, batch) &&
+                   dma_ok(B, lb, sBb, sBn, sBk, N, K, batch);
+  int TM = 64, TN = 64;
+  dim3 grid;
+  if (dma) {
+    // largest tile that still gives >= 256 blocks (one per CU)
+    int cfg = 0;
+    for (int c = 3; c >= 1; --c) {
+      const long long blocks = (long long)((M + 64 * CFG_WM[c] - 1) / (64 * CFG_WM[c])) *
+                               ((N + 64 * CFG_WN[c] - 1) / (64 * CFG_WN[c])) * batch * ksplit;
+      if (blocks >= 256) { cfg = c; break; }
+    }
+    TM = 64 * CFG_WM[cfg];
+    TN = 64 * CFG_WN[cfg];
+    grid = dim3((N + TN - 1) / TN, (M + TM - 1) / TM, batch * ksplit);
+    const int stg = (TM + TN) * BK * 4;
+    const int lds = CFG_NS[cfg] * stg + 16;
+    GemmFn fn = mode == MODE_SPLIT ? pick_glds<MODE_SPLIT>(la, lb, cfg)
+                                   : pick_glds<MODE_BF16>(la, lb, cfg);
+    static bool lds_set[2][2][2][4];
+    bool& done = lds_set[mode][la][lb][cfg];
+    if (!done) {
+      hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      done = true;
+    }
+    hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, A, sAb, sAm, sAk, B, sBb, sBk, sBn, C, sCb,
+                       sCm, sCn, M, N, K, alpha, accumulate, bias, relu, ksplit, slab, counters);
+  } else {
+    grid = dim3((N + 63) / 64, (M + 63) / 64, batch * ksplit);
+    GemmFn fn = mode == MODE_SPLIT ? pick_regs<MODE_SPLIT>(la, lb) : pick_regs<MODE_BF16>(la, lb);
+    hipLaunchKernelGGL(fn, grid, dim3(256), 2 * STAGE + 16, s, A, sAb, sAm, sAk, B, sBb, sBk,
+                       sBn, C, sCb, sCm, sCn, M, N, K, alpha, accumulate, bias, relu, ksplit,
+                       slab, counters);
+  }
+  if (ksplit > KSPLIT_INLAUNCH) {
+    const long long tiles = (long long)grid.x * grid.y * batch;
+    hipLaunchKernelGGL(bgemm_reduce_kernel,
+                       dim3((unsigned)((tiles * (TM * TN / 4) + 255) / 256)), dim3(256), 0, s,
+                       slab, ksplit, TM, TN, (int)grid.y, (int)grid.x, tiles, C, sCb, sCm, sCn,
+                       M, N, alpha, accumulate, bias, relu);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -261,9 +261,9 @@ def bgemm(a, b, out=None, alpha=1.0, accumulate=False, mode="fp32", bias=None,
         out = torch.empty(nb, m, n, dtype=torch.float32, device=a.device)
     slab = cnt = None
     if ksplit > 1:
-        tiles = nb * -(-m // 64) * -(-n // 64)
-        assert tiles <= _hip.N_COUNTERS
-        slab = torch.empty(ksplit * tiles * 4096, dtype=torch.float32, device=a.device)
+        assert nb * -(-m // 64) * -(-n // 64) <= _hip.N_COUNTERS
+        padded = nb * (-(-m // 128) * 128) * (-(-n // 128) * 128)
+        slab = torch.empty(ksplit * padded, dtype=torch.float32, device=a.device)
         cnt = _hip.counters(a.device)
     call("tgfr_bgemm", ptr(a), a.stride(0), a.stride(1), a.stride(2), ptr(b), b.stride(0),
          b.stride(1), b.stride(2), ptr(out), out.stride(0), out.stride(1), out.stride(2),

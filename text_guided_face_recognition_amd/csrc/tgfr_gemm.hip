@@ -32,6 +32,8 @@
 // (few slices) or by one chip-wide reduce launch (many slices).
 #include "tgfr_common.h"
 
+#include <stdlib.h>
+
 using namespace tgfr;
 
 namespace {
@@ -134,6 +136,29 @@ struct Img {
 // logical quad hit 16 distinct (row parity, quad) bank groups.
 __device__ __forceinline__ int kswz(int row, int q) { return q ^ ((row >> 1) & 7); }
 
+// One 16-B-per-lane global -> LDS DMA (global_load_lds_dwordx4) to LDS byte
+// offset lds_off (wave-uniform) + 16 * lane.  Issued from inline asm so that
+// hipcc does not see an LDS write pending on the VM counter: with the builtin
+// it drains every DMA (vmcnt(0)) before the next ds_read and before each
+// barrier, which serialises the ring.  The kernel orders the DMA by counted
+// vmcnt waits + raw barriers itself (cdna_hip_programming.md, pipelining
+// across barriers).
+__device__ __forceinline__ void glds16(const float* src, uint32_t lds_off) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(lds_base() + lds_off));
+  // s_nop: one wait state between the M0 write and the LDS DMA that reads it
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src),
+               "s"(m0)
+               : "memory", "m0");
+}
+
+// Retire this wave's DMA down to N outstanding ops and its LDS reads, then
+// meet the other waves.  One asm statement: nothing moves across it.
+template <int N>
+__device__ __forceinline__ void ring_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
 // Issue this wave's share of the DMA pieces of one operand tile.
 // base: element (mn = 0, k = 0) of the tile; mn_lim / k_lim: valid extents.
 template <int LAY, int R>
@@ -156,8 +181,7 @@ __device__ __forceinline__ void issue_tile(const float* base, long long s_mn, lo
       const bool ok = mn < mn_lim && kr < k_lim;
       src = ok ? base + kr * s_k + mn : g_zero16;
     }
-    __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(lds_base() + lds_off + p * 1024),
-                                     16, 0, 0);
+    glds16(src, lds_off + p * 1024);
   }
 }
 
@@ -178,10 +202,6 @@ __device__ __forceinline__ void read_frag(Frag8& f, uint32_t off, int mn0, int s
   }
 }
 
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 template <int MODE, int LA, int LB, int WM, int WN, int NS>
 __global__ __launch_bounds__(256) void bgemm_glds_kernel(
@@ -228,9 +248,8 @@ __global__ __launch_bounds__(256) void bgemm_glds_kernel(
     // this wave's pieces of tile kt have landed once at most (NS-2) younger
     // stages are outstanding; the barrier makes every wave's pieces visible
     // and retires the reads of tile kt-1, whose buffer is refilled next
-    if (kt + NS - 2 < nk) wait_vm<(NS - 2) * PER>();
-    else wait_vm<0>();
-    __syncthreads();
+    if (kt + NS - 2 < nk) ring_barrier<(NS - 2) * PER>();
+    else ring_barrier<0>();
     if (kt + NS - 1 < nk) issue(kt + NS - 1);
     const uint32_t o = (kt % NS) * STG;
 #pragma unroll
@@ -427,10 +446,10 @@ GemmFn glds_fn(int cfg) {
     case 0: return &bgemm_glds_kernel<MODE, LA, LB, 1, 1, 4>;
     case 1: return &bgemm_glds_kernel<MODE, LA, LB, 2, 1, 3>;
     case 2: return &bgemm_glds_kernel<MODE, LA, LB, 1, 2, 3>;
-    default: return &bgemm_glds_kernel<MODE, LA, LB, 2, 2, 3>;
+    default: return &bgemm_glds_kernel<MODE, LA, LB, 2, 2, 4>;
   }
 }
-constexpr int CFG_WM[4] = {1, 2, 1, 2}, CFG_WN[4] = {1, 1, 2, 2}, CFG_NS[4] = {4, 3, 3, 3};
+constexpr int CFG_WM[4] = {1, 2, 1, 2}, CFG_WN[4] = {1, 1, 2, 2}, CFG_NS[4] = {4, 3, 3, 4};
 
 template <int MODE>
 GemmFn pick_glds(int la, int lb, int cfg) {
@@ -481,12 +500,18 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
   int TM = 64, TN = 64;
   dim3 grid;
   if (dma) {
-    // largest tile that still gives >= 256 blocks (one per CU)
+    // largest tile that still gives >= 2 blocks per CU (TGFR_GEMM_CFG forces
+    // one, for tuning)
+    static const int forced = getenv("TGFR_GEMM_CFG") ? atoi(getenv("TGFR_GEMM_CFG")) : -1;
     int cfg = 0;
-    for (int c = 3; c >= 1; --c) {
-      const long long blocks = (long long)((M + 64 * CFG_WM[c] - 1) / (64 * CFG_WM[c])) *
-                               ((N + 64 * CFG_WN[c] - 1) / (64 * CFG_WN[c])) * batch * ksplit;
-      if (blocks >= 256) { cfg = c; break; }
+    if (forced >= 0 && forced < 4) {
+      cfg = forced;
+    } else {
+      for (int c = 3; c >= 1; --c) {
+        const long long blocks = (long long)((M + 64 * CFG_WM[c] - 1) / (64 * CFG_WM[c])) *
+                                 ((N + 64 * CFG_WN[c] - 1) / (64 * CFG_WN[c])) * batch * ksplit;
+        if (blocks >= 512) { cfg = c; break; }
+      }
     }
     TM = 64 * CFG_WM[cfg];
     TN = 64 * CFG_WN[cfg];

@@ -203,6 +203,24 @@ int tgfr_loss_mix(int n, const float* const* losses, int m, const float* W, floa
                   void* stream);
 int tgfr_loss_mix_bwd(const float* g, int n, const float* W, float* dloss, void* stream);
 
+/* ---- IMIM input BatchNorm folded into the q/k/v projection --------------
+ * (models/models.py:397-398 -> models/fusion_nets.py:97-99)
+ * tgfr_bn_fwd_cl: x [N][C][HW] -> xhat [N][HW][C] = (x - mean) * rstd with
+ * batch statistics (training: biased var for the normalisation, unbiased for
+ * running_var, momentum update, *nbt += 1; each buffer nullable) or running
+ * statistics (training == 0).  mean, rstd [C] are outputs. */
+int tgfr_bn_fwd_cl(const float* x, int N, int C, int HW, float eps, float momentum,
+                   int training, float* running_mean, float* running_var, long long* nbt,
+                   float* mean, float* rstd, float* xhat, void* stream);
+/* Wf = W diag(gamma), bf = b + W beta (W [O][C]; b nullable). */
+int tgfr_bn_fold(const float* W, const float* b, int O, int C, const float* gamma,
+                 const float* beta, float* Wf, float* bf, void* stream);
+/* From G = dY^T xhat [O][C] and s = colsum(dY) [O]: dW = G diag(gamma) +
+ * s beta^T, dgamma = sum_o W .* G, dbeta = sum_o W .* s (fixed-order sums). */
+int tgfr_bn_unfold(const float* G, const float* s, const float* W, int O, int C,
+                   const float* gamma, const float* beta, float* dW, float* dgamma, float* dbeta,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -46,6 +46,9 @@ SIGNATURES = {
     "tgfr_attn_softmax_bwd": [P, P, P, L, I, L, F, P],
     "tgfr_ln_ws_floats": [I, L, I, P],
     "tgfr_loss_mix": [I, P, I, P, P, P],
+    "tgfr_bn_fwd_cl": [P, I, I, I, F, F, I, P, P, P, P, P, P, P],
+    "tgfr_bn_fold": [P, P, I, I, P, P, P, P, P],
+    "tgfr_bn_unfold": [P, P, P, I, I, P, P, P, P, P, P],
     "tgfr_loss_mix_bwd": [P, I, P, P, P],
     "tgfr_bias_grad": [P, L, I, I, P, L, P, L, P, P, P, P],
     "tgfr_ln_fwd": [P, I, L, P, P, F, P, P, P],

@@ -1,0 +1,180 @@
+// IMIM's input BatchNorm folded into the packed q/k/v projection that follows
+// it (models/models.py:386-404 then models/fusion_nets.py:97-99):
+//
+//   z  = bn_img(img)                    training: batch statistics over (N, H, W)
+//   px = z^T [key; query; value]^T + b  (three 1x1 convs on the same map)
+//
+// is computed as px = xhat W'^T + b' with xhat = (x - mean) rstd (channels
+// last) and W' = W diag(gamma), b' = b + W beta, so the normalised map is never
+// transposed back and the affine costs nothing.  The backward needs only
+// G = dpx^T xhat (the projection's weight-gradient GEMM) and s = colsum(dpx):
+//   dW = G diag(gamma) + s beta^T,  dgamma_c = sum_o W[o,c] G[o,c],
+//   dbeta_c = sum_o W[o,c] s_o.
+//
+//   bn_stats      per channel: two-pass mean / biased var over N x HW, rstd;
+//                 running_mean/var update with the unbiased var (momentum), and
+//                 num_batches_tracked += 1 (nn.BatchNorm2d training semantics)
+//   bn_norm_cl    xhat[n][hw][c] = (x[n][c][hw] - mean_c) rstd_c, an LDS-tiled
+//                 NCHW -> channels-last transpose
+//   bn_fold       W' = W diag(gamma), b' = b + W beta
+//   bn_unfold     dW, dgamma, dbeta from G and s (fixed-order column sums)
+#include "tgfr_common.h"
+
+using namespace tgfr;
+
+namespace {
+
+// grid C; 256 threads.  x[n][c][hw].
+__global__ __launch_bounds__(256) void bn_stats_kernel(
+    const float* __restrict__ x, int N, int C, int HW, float eps, float momentum, int training,
+    float* __restrict__ running_mean, float* __restrict__ running_var,
+    long long* __restrict__ nbt, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  __shared__ float red[4];
+  const int c = blockIdx.x, tid = threadIdx.x, wid = tid / WAVE, lane = tid % WAVE;
+  if (!training) {
+    if (tid == 0) {
+      mean_out[c] = running_mean[c];
+      rstd_out[c] = rsqrtf(running_var[c] + eps);
+    }
+    return;
+  }
+  const long long cnt = (long long)N * HW;
+  float s = 0.f;
+  for (long long i = tid; i < cnt; i += 256) {
+    const int n = (int)(i / HW), hw = (int)(i % HW);
+    s += x[((long long)n * C + c) * HW + hw];
+  }
+  s = wave_sum(s);
+  if (lane == 0) red[wid] = s;
+  __syncthreads();
+  const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)cnt;
+  __syncthreads();
+  float m2 = 0.f;
+  for (long long i = tid; i < cnt; i += 256) {
+    const int n = (int)(i / HW), hw = (int)(i % HW);
+    const float d = x[((long long)n * C + c) * HW + hw] - mean;
+    m2 += d * d;
+  }
+  m2 = wave_sum(m2);
+  if (lane == 0) red[wid] = m2;
+  __syncthreads();
+  if (tid == 0) {
+    const float var = (red[0] + red[1] + red[2] + red[3]) / (float)cnt;
+    mean_out[c] = mean;
+    rstd_out[c] = rsqrtf(var + eps);
+    if (running_mean) {
+      const float unbiased = cnt > 1 ? var * (float)cnt / (float)(cnt - 1) : var;
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+    }
+    if (nbt && c == 0) nbt[0] += 1;
+  }
+}
+
+// grid (ceil(C / 64), N); 256 threads; LDS [64][HW + 1] floats.
+__global__ __launch_bounds__(256) void bn_norm_cl_kernel(const float* __restrict__ x, int C,
+                                                         int HW, const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd,
+                                                         float* __restrict__ y) {
+  extern __shared__ float tile[];
+  const int c0 = blockIdx.x * 64, n = blockIdx.y, tid = threadIdx.x;
+  const int cn = min(64, C - c0), ld = HW + 1;
+  const float* xs = x + ((long long)n * C + c0) * HW;
+  for (int i = tid; i < cn * HW; i += 256) {
+    const int cc = i / HW, hw = i % HW;
+    tile[cc * ld + hw] = (xs[i] - mean[c0 + cc]) * rstd[c0 + cc];
+  }
+  __syncthreads();
+  float* ys = y + (long long)n * HW * C + c0;
+  for (int i = tid; i < cn * HW; i += 256) {
+    const int hw = i / cn, cc = i % cn;
+    ys[(long long)hw * C + cc] = tile[cc * ld + hw];
+  }
+}
+
+// one wave per output row o
+__global__ __launch_bounds__(256) void bn_fold_kernel(const float* __restrict__ W,
+                                                      const float* __restrict__ b, int O, int C,
+                                                      const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta,
+                                                      float* __restrict__ Wf,
+                                                      float* __restrict__ bf) {
+  const int o = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
+  if (o >= O) return;
+  float acc = 0.f;
+  for (int c = lane; c < C; c += WAVE) {
+    const float w = W[(long long)o * C + c];
+    Wf[(long long)o * C + c] = w * gamma[c];
+    acc += w * beta[c];
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) bf[o] = (b ? b[o] : 0.f) + acc;
+}
+
+// grid ceil(C / 64); block = 64 columns x 4 row lanes.
+__global__ __launch_bounds__(256) void bn_unfold_kernel(
+    const float* __restrict__ G, const float* __restrict__ s, const float* __restrict__ W, int O,
+    int C, const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dW,
+    float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float red[2][4][64];
+  const int tx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float ag = 0.f, ab = 0.f;
+  if (c < C) {
+    const float g = gamma[c], bt = beta[c];
+    for (int o = ry; o < O; o += 4) {
+      const long long e = (long long)o * C + c;
+      const float gv = G[e], w = W[e];
+      dW[e] = gv * g + s[o] * bt;
+      ag += w * gv;
+      ab += w * s[o];
+    }
+  }
+  red[0][ry][tx] = ag;
+  red[1][ry][tx] = ab;
+  __syncthreads();
+  if (ry == 0 && c < C) {
+    dgamma[c] = red[0][0][tx] + red[0][1][tx] + red[0][2][tx] + red[0][3][tx];
+    dbeta[c] = red[1][0][tx] + red[1][1][tx] + red[1][2][tx] + red[1][3][tx];
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int tgfr_bn_fwd_cl(const float* x, int N, int C, int HW, float eps, float momentum,
+                   int training, float* running_mean, float* running_var, long long* nbt,
+                   float* mean, float* rstd, float* xhat, void* stream) {
+  if (N <= 0 || C <= 0 || HW <= 0 || (64 * (HW + 1) * 4 > 160 * 1024)) return 1001;
+  if (!training && (!running_mean || !running_var)) return 1001;
+  auto* st = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(C), dim3(256), 0, st, x, N, C, HW, eps, momentum,
+                     training, running_mean, running_var, nbt, mean, rstd);
+  const int lds = 64 * (HW + 1) * 4;
+  if (lds > 64 * 1024)
+    hipFuncSetAttribute((const void*)bn_norm_cl_kernel,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL(bn_norm_cl_kernel, dim3((C + 63) / 64, N), dim3(256), lds, st, x, C, HW,
+                     mean, rstd, xhat);
+  return (int)hipGetLastError();
+}
+
+int tgfr_bn_fold(const float* W, const float* b, int O, int C, const float* gamma,
+                 const float* beta, float* Wf, float* bf, void* stream) {
+  if (O <= 0 || C <= 0) return 1001;
+  hipLaunchKernelGGL(bn_fold_kernel, dim3((O + 3) / 4), dim3(256), 0, (hipStream_t)stream, W, b,
+                     O, C, gamma, beta, Wf, bf);
+  return (int)hipGetLastError();
+}
+
+int tgfr_bn_unfold(const float* G, const float* s, const float* W, int O, int C,
+                   const float* gamma, const float* beta, float* dW, float* dgamma, float* dbeta,
+                   void* stream) {
+  if (O <= 0 || C <= 0) return 1001;
+  hipLaunchKernelGGL(bn_unfold_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)stream,
+                     G, s, W, O, C, gamma, beta, dW, dgamma, dbeta);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

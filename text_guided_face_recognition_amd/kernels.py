@@ -391,6 +391,88 @@ def attention_core(px, py, cq, ck, cv, scale, mode="fp32"):
     return AttentionCore.apply(px, py, cq, ck, cv, scale, mode)
 
 
+# ------------------------------------------------- batch norm -> linear ---
+class BNLinear(torch.autograd.Function):
+    """y[n, hw] = W bn(x)[n, :, hw] + b for x [N, C, H, W] (NCHW), returned
+    channels-last [N, HW, O]: nn.BatchNorm2d followed by a 1x1 projection
+    (IMIM bn_img -> SelfAttention q/k/v, models/models.py:397-398), with the BN
+    affine folded into the projection (tgfr_bn.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, weight, bias, bn, training, mode):
+        n, c, h, w_ = x.shape
+        hw, o = h * w_, weight.shape[0]
+        x = x.float().contiguous()
+        dev = x.device
+        mean = torch.empty(c, dtype=torch.float32, device=dev)
+        rstd = torch.empty_like(mean)
+        xhat = torch.empty(n, hw, c, dtype=torch.float32, device=dev)
+        track = training and bn.track_running_stats and bn.running_mean is not None
+        if training and track and bn.momentum is None:
+            raise NotImplementedError("cumulative-average BatchNorm (momentum=None)")
+        use_batch = training or bn.running_mean is None
+        call("tgfr_bn_fwd_cl", ptr(x), n, c, hw, float(bn.eps),
+             float(bn.momentum or 0.0), int(use_batch),
+             ptr(bn.running_mean) if (track or not use_batch) else None,
+             ptr(bn.running_var) if (track or not use_batch) else None,
+             ptr(bn.num_batches_tracked) if track else None, ptr(mean), ptr(rstd), ptr(xhat),
+             _hip.stream())
+        w2 = weight.reshape(o, c).float().contiguous()
+        g = gamma.float().contiguous()
+        wf = torch.empty_like(w2)
+        bf = torch.empty(o, dtype=torch.float32, device=dev)
+        call("tgfr_bn_fold", ptr(w2), ptr(None if bias is None else bias.float().contiguous()),
+             o, c, ptr(g), ptr(beta.float().contiguous()), ptr(wf), ptr(bf), _hip.stream())
+        rows = n * hw
+        mb = -(-rows // 64) * -(-o // 64)
+        y = bgemm(xhat.view(1, rows, c), wf.t().unsqueeze(0), bias=bf, mode=mode,
+                  ksplit=_ksplit(c, mb))[0]
+        ctx.save_for_backward(xhat, w2, wf, g, beta.float().contiguous(), rstd)
+        ctx.cfg = (mode, bias is not None, x.shape, weight.shape, use_batch)
+        return y.view(n, hw, o)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xhat, w2, wf, g, bt, rstd = ctx.saved_tensors
+        mode, has_bias, xshape, wshape, use_batch = ctx.cfg
+        n, hw, c = xhat.shape
+        o = w2.shape[0]
+        rows = n * hw
+        dp = dy.reshape(rows, o).float()
+        if dp.stride(1) != 1 or dp.stride(0) != o:
+            dp = dp.contiguous()
+        dev = dp.device
+        s = torch.empty(o, dtype=torch.float32, device=dev)
+        ws = torch.empty(-(-rows // 256) * o, dtype=torch.float32, device=dev)
+        call("tgfr_bias_grad", ptr(dp), o, rows, o, None, 0, None, 0, ptr(s), ptr(ws),
+             ptr(_hip.counters(dev)), _hip.stream())
+        mb = -(-o // 64) * -(-c // 64)
+        gm = bgemm(dp.t().unsqueeze(0), xhat.view(1, rows, c), mode=mode,
+                   ksplit=_ksplit(rows, mb))[0]
+        dw = torch.empty_like(w2)
+        dgamma = torch.empty(c, dtype=torch.float32, device=dev)
+        dbeta = torch.empty_like(dgamma)
+        call("tgfr_bn_unfold", ptr(gm), ptr(s), ptr(w2), o, c, ptr(g), ptr(bt), ptr(dw),
+             ptr(dgamma), ptr(dbeta), _hip.stream())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            # d xhat = dp W'; BN input gradient (only when the map itself is trained)
+            dxh = bgemm(dp.unsqueeze(0), wf.unsqueeze(0), mode=mode)[0].view(n, hw, c)
+            if use_batch:
+                m1 = dxh.mean((0, 1))
+                m2 = (dxh * xhat).mean((0, 1))
+                dxh = dxh - m1 - xhat * m2
+            dx = (dxh * rstd).permute(0, 2, 1).reshape(xshape)
+        return (dx, dgamma, dbeta, dw.reshape(wshape), s if has_bias else None, None, None,
+                None)
+
+
+def bn_linear(x, bn, weight, bias, mode="fp32"):
+    """BatchNorm2d `bn` (its training flag and running buffers) then the
+    projection; returns [N, HW, O]."""
+    return BNLinear.apply(x, bn.weight, bn.bias, weight, bias, bn, bn.training, mode)
+
+
 # ------------------------------------------------------------ layer norm ---
 def _aligned(t):
     t = t.float().contiguous()

@@ -48,17 +48,27 @@ class SelfAttention(nn.Module):
     def _w(self, conv):
         return conv.weight.reshape(conv.weight.shape[0], -1)
 
+    def packed_self(self):
+        """[key_proj; query_proj; value_proj] as one [2 C' + C, C] weight and
+        bias: the query role, key role and value of self-attention."""
+        w = torch.cat([self._w(self.key_proj), self._w(self.query_proj),
+                       self._w(self.value_proj)], 0)
+        b = torch.cat([self.key_proj.bias, self.query_proj.bias, self.value_proj.bias])
+        return w, b
+
+    def core_self(self, px):
+        """Attention on packed [Qr | Kr | V] rows [N, HW, 2 C' + C]."""
+        cq = self.key_proj.weight.shape[0]
+        return K.attention_core(px, None, cq, cq, 2 * cq, 1.0 / float(self.sqrt_dim),
+                                self.precision)
+
     def forward_cl(self, x_cl, y_cl):
         """Channels-last core: x_cl, y_cl [N, HW, C] -> [N, HW, C]."""
         mode = self.precision
         cq = self.key_proj.weight.shape[0]
         if y_cl is x_cl:
-            # packed [Qr | Kr | V] = x [key_proj | query_proj | value_proj]^T
-            w = torch.cat([self._w(self.key_proj), self._w(self.query_proj),
-                           self._w(self.value_proj)], 0)
-            b = torch.cat([self.key_proj.bias, self.query_proj.bias, self.value_proj.bias])
-            px = K.linear_rows(x_cl, w, b, mode=mode)
-            return K.attention_core(px, None, cq, cq, 2 * cq, 1.0 / float(self.sqrt_dim), mode)
+            w, b = self.packed_self()
+            return self.core_self(K.linear_rows(x_cl, w, b, mode=mode))
         w = torch.cat([self._w(self.key_proj), self._w(self.value_proj)], 0)
         b = torch.cat([self.key_proj.bias, self.value_proj.bias])
         px = K.linear_rows(x_cl, w, b, mode=mode)                     # [Qr | V]

@@ -57,8 +57,10 @@ class IMIM(nn.Module):
 
     def forward(self, img):
         n, c, h, w = img.shape
-        z = _cl(self.bn_img(img))                       # [B, HW, C]
-        z = self.sa.forward_cl(z, z)
+        # bn_img folded into the packed q/k/v projection of the self-attention
+        wq, bq = self.sa.packed_self()
+        px = K.bn_linear(img, self.bn_img, wq, bq, mode=self.precision)   # [B, HW, 3C]
+        z = self.sa.core_self(px)
         # LayerNorm over (C, H, W) of each sample == over the last two dims of
         # the channels-last [B, HW, C] rows, with the affine maps permuted
         wt = self.ln.weight.permute(1, 2, 0).reshape(h * w, c)

@@ -175,15 +175,18 @@ int tgfr_focal_ce_bwd(const float* L, int rows, int cols, const long long* label
                       const float* ws, const float* gscale, float* dL, void* stream);
 
 /* ---- per-sample LayerNorm (IMIM ln, models/models.py:388 / :401) -----------
- * x [rows][E] (row-contiguous, E % 4 == 0, 16-B aligned), affine w, b [E].
+ * x [rows][E] (row-contiguous, E % 4 == 0, 16-B aligned), affine w, b of E
+ * elements: indexed like a row (ch == 0), or stored channel-major [ch][E/ch]
+ * for rows laid out [E/ch][ch] (ch > 0, ch % 4 == 0): LayerNorm([C, H, W])
+ * weights applied to channels-last rows without permuted copies.
  * y = (x - mean_r) / sqrt(var_r + eps) * w + b with biased var_r, as
- * nn.LayerNorm([C, H, W]).  ws: tgfr_ln_ws_floats(rows, E, 1) floats; the
- * forward leaves mean/rstd in it for the backward (pass the same ws). */
+ * nn.LayerNorm.  ws: tgfr_ln_ws_floats(rows, E, 1) floats; the forward leaves
+ * mean/rstd in it for the backward (pass the same ws). */
 int tgfr_ln_ws_floats(int rows, long long E, int backward, long long* out);
 int tgfr_ln_fwd(const float* x, int rows, long long E, const float* w, const float* b, float eps,
-                float* y, float* ws, void* stream);
+                int ch, float* y, float* ws, void* stream);
 /* dx, dw = sum_r dy xhat, db = sum_r dy (fixed-order reductions). */
-int tgfr_ln_bwd(const float* dy, const float* x, int rows, long long E, const float* w,
+int tgfr_ln_bwd(const float* dy, const float* x, int rows, long long E, const float* w, int ch,
                 float* ws, float* dx, float* dw, float* db, void* stream);
 
 /* Bias gradient of a row-wise linear map: db[c] = sum_r dy[r][c].  With y
@@ -216,10 +219,11 @@ int tgfr_bn_fwd_cl(const float* x, int N, int C, int HW, float eps, float moment
 int tgfr_bn_fold(const float* W, const float* b, int O, int C, const float* gamma,
                  const float* beta, float* Wf, float* bf, void* stream);
 /* From G = dY^T xhat [O][C] and s = colsum(dY) [O]: dW = G diag(gamma) +
- * s beta^T, dgamma = sum_o W .* G, dbeta = sum_o W .* s (fixed-order sums). */
+ * s beta^T, dgamma = sum_o W .* G, dbeta = sum_o W .* s (fixed-order sums).
+ * ws: 2 * ceil(O / 64) * C floats; counters: ceil(C / 64) zeroed words. */
 int tgfr_bn_unfold(const float* G, const float* s, const float* W, int O, int C,
                    const float* gamma, const float* beta, float* dW, float* dgamma, float* dbeta,
-                   void* stream);
+                   float* ws, unsigned* counters, void* stream);
 
 #ifdef __cplusplus
 }

@@ -245,3 +245,29 @@ def test_bn_linear_fold(gpu, training):
     torch.testing.assert_close(bn_g.running_mean.cpu(), bn.running_mean, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(bn_g.running_var.cpu(), bn.running_var, rtol=1e-5, atol=1e-6)
     assert int(bn_g.num_batches_tracked) == int(bn.num_batches_tracked)
+
+
+def test_layer_norm_rows_channel_major_affine(gpu):
+    """IMIM layout: channels-last rows [HW, C] with the reference's [C, H, W]
+    affine maps read in place (ch = C)."""
+    from text_guided_face_recognition_amd import kernels as K
+    gen = torch.Generator().manual_seed(7)
+    n, c, h, w = 4, 24, 5, 6
+    x = torch.randn(n, c, h, w, generator=gen) * 2 - 1
+    wt = torch.randn(c, h, w, generator=gen)
+    bs = torch.randn(c, h, w, generator=gen)
+    probe = torch.randn(n, c, h, w, generator=gen)
+    xs = [x.clone().requires_grad_(), wt.clone().requires_grad_(), bs.clone().requires_grad_()]
+    ref = torch.nn.functional.layer_norm(xs[0], (c, h, w), xs[1], xs[2], 1e-5)
+    (ref * probe).sum().backward()
+    x_cl = x.permute(0, 2, 3, 1).reshape(n, h * w, c).contiguous().to(gpu).requires_grad_()
+    wg, bg = wt.to(gpu).requires_grad_(), bs.to(gpu).requires_grad_()
+    y = K.layer_norm_rows(x_cl, wg, bg, 1e-5, ch=c)
+    p_cl = probe.permute(0, 2, 3, 1).reshape(n, h * w, c).to(gpu)
+    (y * p_cl).sum().backward()
+    ref_cl = ref.detach().permute(0, 2, 3, 1).reshape(n, h * w, c)
+    torch.testing.assert_close(y.detach().cpu(), ref_cl, rtol=1e-4, atol=1e-4)
+    dx_ref = xs[0].grad.permute(0, 2, 3, 1).reshape(n, h * w, c)
+    assert _relerr(x_cl.grad, dx_ref.numpy()) < 1e-4
+    assert _relerr(wg.grad, xs[1].grad.numpy()) < 1e-4
+    assert _relerr(bg.grad, xs[2].grad.numpy()) < 1e-4

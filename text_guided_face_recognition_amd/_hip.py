@@ -48,11 +48,11 @@ SIGNATURES = {
     "tgfr_loss_mix": [I, P, I, P, P, P],
     "tgfr_bn_fwd_cl": [P, I, I, I, F, F, I, P, P, P, P, P, P, P],
     "tgfr_bn_fold": [P, P, I, I, P, P, P, P, P],
-    "tgfr_bn_unfold": [P, P, P, I, I, P, P, P, P, P, P],
+    "tgfr_bn_unfold": [P, P, P, I, I, P, P, P, P, P, P, P, P],
     "tgfr_loss_mix_bwd": [P, I, P, P, P],
     "tgfr_bias_grad": [P, L, I, I, P, L, P, L, P, P, P, P],
-    "tgfr_ln_fwd": [P, I, L, P, P, F, P, P, P],
-    "tgfr_ln_bwd": [P, P, I, L, P, P, P, P, P, P],
+    "tgfr_ln_fwd": [P, I, L, P, P, F, I, P, P, P],
+    "tgfr_ln_bwd": [P, P, I, L, P, I, P, P, P, P, P],
 }
 
 

@@ -24,7 +24,8 @@ using namespace tgfr;
 
 namespace {
 
-// grid C; 256 threads.  x[n][c][hw].
+// grid C; 256 threads.  x[n][c][hw]: thread t owns positions hw = t, t+256,
+// ... of every sample, so each load instruction reads HW-contiguous floats.
 __global__ __launch_bounds__(256) void bn_stats_kernel(
     const float* __restrict__ x, int N, int C, int HW, float eps, float momentum, int training,
     float* __restrict__ running_mean, float* __restrict__ running_var,
@@ -39,10 +40,12 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(
     return;
   }
   const long long cnt = (long long)N * HW;
+  const float* xc = x + (long long)c * HW;
+  const long long sn = (long long)C * HW;
   float s = 0.f;
-  for (long long i = tid; i < cnt; i += 256) {
-    const int n = (int)(i / HW), hw = (int)(i % HW);
-    s += x[((long long)n * C + c) * HW + hw];
+  for (int hw = tid; hw < HW; hw += 256) {
+#pragma unroll 8
+    for (int n = 0; n < N; ++n) s += xc[n * sn + hw];
   }
   s = wave_sum(s);
   if (lane == 0) red[wid] = s;
@@ -50,10 +53,12 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(
   const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)cnt;
   __syncthreads();
   float m2 = 0.f;
-  for (long long i = tid; i < cnt; i += 256) {
-    const int n = (int)(i / HW), hw = (int)(i % HW);
-    const float d = x[((long long)n * C + c) * HW + hw] - mean;
-    m2 += d * d;
+  for (int hw = tid; hw < HW; hw += 256) {
+#pragma unroll 8
+    for (int n = 0; n < N; ++n) {
+      const float d = xc[n * sn + hw] - mean;
+      m2 += d * d;
+    }
   }
   m2 = wave_sum(m2);
   if (lane == 0) red[wid] = m2;
@@ -111,31 +116,48 @@ __global__ __launch_bounds__(256) void bn_fold_kernel(const float* __restrict__ 
   if (lane == 0) bf[o] = (b ? b[o] : 0.f) + acc;
 }
 
-// grid ceil(C / 64); block = 64 columns x 4 row lanes.
+// grid (ceil(C / 64), ceil(O / 64)); block = 64 columns x 4 row lanes over a
+// 64-row chunk.  dW is elementwise; the dgamma / dbeta column partials of the
+// chunks are combined by the last chunk of each column group (chunk order).
+constexpr int UF_ROWS = 64;
 __global__ __launch_bounds__(256) void bn_unfold_kernel(
     const float* __restrict__ G, const float* __restrict__ s, const float* __restrict__ W, int O,
     int C, const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dW,
-    float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  __shared__ float red[2][4][64];
+    float* __restrict__ part, unsigned* __restrict__ counters, float* __restrict__ dgamma,
+    float* __restrict__ dbeta) {
+  __shared__ float red[2 * 4 * 64 + 1];
   const int tx = threadIdx.x & 63, ry = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
+  const int o0 = blockIdx.y * UF_ROWS, o1 = min(O, o0 + UF_ROWS);
   float ag = 0.f, ab = 0.f;
   if (c < C) {
     const float g = gamma[c], bt = beta[c];
-    for (int o = ry; o < O; o += 4) {
+#pragma unroll 4
+    for (int o = o0 + ry; o < o1; o += 4) {
       const long long e = (long long)o * C + c;
-      const float gv = G[e], w = W[e];
-      dW[e] = gv * g + s[o] * bt;
+      const float gv = G[e], w = W[e], so = s[o];
+      dW[e] = gv * g + so * bt;
       ag += w * gv;
-      ab += w * s[o];
+      ab += w * so;
     }
   }
-  red[0][ry][tx] = ag;
-  red[1][ry][tx] = ab;
+  red[ry * 64 + tx] = ag;
+  red[256 + ry * 64 + tx] = ab;
   __syncthreads();
   if (ry == 0 && c < C) {
-    dgamma[c] = red[0][0][tx] + red[0][1][tx] + red[0][2][tx] + red[0][3][tx];
-    dbeta[c] = red[1][0][tx] + red[1][1][tx] + red[1][2][tx] + red[1][3][tx];
+    float* pp = part + ((long long)blockIdx.y * C + c) * 2;
+    pp[0] = red[tx] + red[64 + tx] + red[128 + tx] + red[192 + tx];
+    pp[1] = red[256 + tx] + red[320 + tx] + red[384 + tx] + red[448 + tx];
+  }
+  if (!last_arrival(counters + blockIdx.x, gridDim.y, (int*)&red[512])) return;
+  if (ry == 0 && c < C) {
+    float a = 0.f, b = 0.f;
+    for (int k = 0; k < (int)gridDim.y; ++k) {
+      a += part[((long long)k * C + c) * 2];
+      b += part[((long long)k * C + c) * 2 + 1];
+    }
+    dgamma[c] = a;
+    dbeta[c] = b;
   }
 }
 
@@ -168,12 +190,14 @@ int tgfr_bn_fold(const float* W, const float* b, int O, int C, const float* gamm
   return (int)hipGetLastError();
 }
 
+// ws: 2 * ceil(O / 64) * C floats; counters: ceil(C / 64) zeroed words.
 int tgfr_bn_unfold(const float* G, const float* s, const float* W, int O, int C,
                    const float* gamma, const float* beta, float* dW, float* dgamma, float* dbeta,
-                   void* stream) {
-  if (O <= 0 || C <= 0) return 1001;
-  hipLaunchKernelGGL(bn_unfold_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)stream,
-                     G, s, W, O, C, gamma, beta, dW, dgamma, dbeta);
+                   float* ws, unsigned* counters, void* stream) {
+  if (O <= 0 || C <= 0 || !ws || !counters) return 1001;
+  hipLaunchKernelGGL(bn_unfold_kernel, dim3((C + 63) / 64, (O + UF_ROWS - 1) / UF_ROWS),
+                     dim3(256), 0, (hipStream_t)stream, G, s, W, O, C, gamma, beta, dW, ws,
+                     counters, dgamma, dbeta);
   return (int)hipGetLastError();
 }
 

@@ -49,6 +49,27 @@ __device__ __forceinline__ void mma(f32x16& acc, const bf16x8& ahi, const bf16x8
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc, 0, 0, 0);
 }
 
+// mma<MODE> with the accumulator pinned to AGPRs ("+a"): for accumulators
+// that live across a loop (the word-region backward's dR), where hipcc would
+// otherwise keep them in VGPRs and copy them to / from AGPRs around every
+// MFMA chain.  Only MFMAs touch these registers until the caller reads them
+// back (after mfma_drain()).
+template <int MODE>
+__device__ __forceinline__ void mma_agpr(f32x16& acc, const bf16x8& ahi, const bf16x8& alo,
+                                         const bf16x8& bhi, const bf16x8& blo) {
+  if constexpr (MODE == MODE_SPLIT) {
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(alo), "v"(bhi));
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(ahi), "v"(blo));
+  }
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(ahi), "v"(bhi));
+}
+// Wait states before anything but an MFMA reads an mma_agpr accumulator
+// (a 32x32x16 MFMA's result latency; the hazard recognizer does not see
+// through inline asm).
+__device__ __forceinline__ void mfma_drain() {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+}
+
 __device__ __forceinline__ bf16x8 as_bf8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
 
 // 8 fp32 values -> bf16x8 hi (and lo when split).
@@ -101,6 +122,29 @@ __device__ __forceinline__ s16x4 lds_tr4(uint32_t off) {
 __device__ __forceinline__ bf16x8 join_tr(s16x4 a, s16x4 b) {
   s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
   return __builtin_bit_cast(bf16x8, v);
+}
+
+// One 16-B-per-lane global -> LDS DMA (global_load_lds_dwordx4) to LDS byte
+// offset lds_off (wave-uniform) + 16 * lane.  Issued from inline asm so that
+// hipcc does not see an LDS write pending on the VM counter: with the builtin
+// it drains every DMA (vmcnt(0)) before the next ds_read and before each
+// barrier, which serialises the ring.  The kernel orders the DMA by counted
+// vmcnt waits + raw barriers itself (cdna_hip_programming.md, pipelining
+// across barriers).
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds_off) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(lds_base() + lds_off));
+  // s_nop: one wait state between the M0 write and the LDS DMA that reads it
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src),
+               "s"(m0)
+               : "memory", "m0");
+}
+
+// Retire this wave's DMA down to N outstanding ops and its LDS reads, then
+// meet the other waves.  One asm statement: nothing moves across it.
+template <int N>
+__device__ __forceinline__ void ring_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
 // Bijective XCD-aware remap of a 1-D grid: blocks L and L+8 run on one XCD,

@@ -136,29 +136,6 @@ struct Img {
 // logical quad hit 16 distinct (row parity, quad) bank groups.
 __device__ __forceinline__ int kswz(int row, int q) { return q ^ ((row >> 1) & 7); }
 
-// One 16-B-per-lane global -> LDS DMA (global_load_lds_dwordx4) to LDS byte
-// offset lds_off (wave-uniform) + 16 * lane.  Issued from inline asm so that
-// hipcc does not see an LDS write pending on the VM counter: with the builtin
-// it drains every DMA (vmcnt(0)) before the next ds_read and before each
-// barrier, which serialises the ring.  The kernel orders the DMA by counted
-// vmcnt waits + raw barriers itself (cdna_hip_programming.md, pipelining
-// across barriers).
-__device__ __forceinline__ void glds16(const float* src, uint32_t lds_off) {
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(lds_base() + lds_off));
-  // s_nop: one wait state between the M0 write and the LDS DMA that reads it
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src),
-               "s"(m0)
-               : "memory", "m0");
-}
-
-// Retire this wave's DMA down to N outstanding ops and its LDS reads, then
-// meet the other waves.  One asm statement: nothing moves across it.
-template <int N>
-__device__ __forceinline__ void ring_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-
 // Issue this wave's share of the DMA pieces of one operand tile.
 // base: element (mn = 0, k = 0) of the tile; mn_lim / k_lim: valid extents.
 template <int LAY, int R>

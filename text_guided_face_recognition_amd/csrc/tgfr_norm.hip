@@ -30,6 +30,20 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return red[0] + red[1] + red[2] + red[3];
 }
 
+// The affine map w, b is indexed like x's rows ([E]) or, with ch > 0, stored
+// channel-major [ch][E / ch] while x's rows are [E / ch][ch] (IMIM's
+// LayerNorm([C, H, W]) on channels-last rows: no permuted copies of w, b).
+__device__ __forceinline__ long long aidx(long long e, int ch, long long E) {
+  return ch ? (e % ch) * (E / ch) + e / ch : e;
+}
+// 4 consecutive elements 4 i4 .. +3 (ch % 4 == 0 keeps them in one position)
+__device__ __forceinline__ float4 aff4(const float* __restrict__ a, long long i4, int ch,
+                                       long long E) {
+  if (!ch) return ((const float4*)a)[i4];
+  const long long e = i4 * 4, n = E / ch, c = e % ch, p = e / ch;
+  return make_float4(a[c * n + p], a[(c + 1) * n + p], a[(c + 2) * n + p], a[(c + 3) * n + p]);
+}
+
 struct Slice {
   long long lo, hi;
 };
@@ -85,7 +99,7 @@ __global__ __launch_bounds__(NT) void ln_apply_kernel(const float* __restrict__ 
                                                       const float* __restrict__ bias, float eps,
                                                       const float* __restrict__ part,
                                                       float* __restrict__ stats, int rows,
-                                                      float* __restrict__ y) {
+                                                      int ch, float* __restrict__ y) {
   const int b = blockIdx.y;
   float mean, rstd;
   ln_stats(part, E, S, b, eps, mean, rstd);
@@ -96,10 +110,8 @@ __global__ __launch_bounds__(NT) void ln_apply_kernel(const float* __restrict__ 
   const long long n4 = E / 4;
   const float4* x4 = (const float4*)(x + (long long)b * E);
   float4* y4 = (float4*)(y + (long long)b * E);
-  const float4* w4 = (const float4*)w;
-  const float4* b4 = (const float4*)bias;
   for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n4; i += gridDim.x * (long long)NT) {
-    const float4 v = x4[i], ww = w4[i], bb = b4[i];
+    const float4 v = x4[i], ww = aff4(w, i, ch, E), bb = aff4(bias, i, ch, E);
     y4[i] = make_float4((v.x - mean) * rstd * ww.x + bb.x, (v.y - mean) * rstd * ww.y + bb.y,
                         (v.z - mean) * rstd * ww.z + bb.z, (v.w - mean) * rstd * ww.w + bb.w);
   }
@@ -110,7 +122,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_part_kernel(const float* __restrict
                                                          const float* __restrict__ x, long long E,
                                                          int S, const float* __restrict__ w,
                                                          const float* __restrict__ stats, int rows,
-                                                         float* __restrict__ part) {
+                                                         int ch, float* __restrict__ part) {
   __shared__ float red[4];
   const int b = blockIdx.y, s = blockIdx.x;
   const Slice sl = slice_of(E, S, s);
@@ -119,7 +131,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_part_kernel(const float* __restrict
   const float* gr = dy + (long long)b * E;
   float sg = 0.f, sgx = 0.f;
   for (long long e = sl.lo + threadIdx.x; e < sl.hi; e += NT) {
-    const float g = gr[e] * w[e];
+    const float g = gr[e] * w[aidx(e, ch, E)];
     sg += g;
     sgx += g * (xr[e] - mean) * rstd;
   }
@@ -136,7 +148,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_part_kernel(const float* __restrict
 __global__ __launch_bounds__(NT) void ln_bwd_dx_kernel(
     const float* __restrict__ dy, const float* __restrict__ x, long long E, int S,
     const float* __restrict__ w, const float* __restrict__ stats, int rows,
-    const float* __restrict__ part, int per_group, float* __restrict__ dx,
+    const float* __restrict__ part, int per_group, int ch, float* __restrict__ dx,
     float* __restrict__ dwp, float* __restrict__ dbp) {
   __shared__ float coef[3][64];
   const int g0 = blockIdx.y * per_group, g1 = min(rows, g0 + per_group);
@@ -154,7 +166,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_dx_kernel(
   __syncthreads();
   const long long i = blockIdx.x * (long long)NT + threadIdx.x;
   if (i >= E / 4) return;
-  const float4 ww = ((const float4*)w)[i];
+  const float4 ww = aff4(w, i, ch, E);
   float4 dw = make_float4(0.f, 0.f, 0.f, 0.f), db = dw;
   for (int b = g0; b < g1; ++b) {
     const float mean = stats[b], rstd = coef[0][b - g0];
@@ -175,7 +187,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_dx_kernel(
 
 __global__ __launch_bounds__(NT) void ln_bwd_dw_kernel(const float* __restrict__ dwp,
                                                        const float* __restrict__ dbp, long long E,
-                                                       int groups, float* __restrict__ dw,
+                                                       int groups, int ch, float* __restrict__ dw,
                                                        float* __restrict__ db) {
   const long long e = blockIdx.x * (long long)NT + threadIdx.x;
   if (e >= E) return;
@@ -184,8 +196,9 @@ __global__ __launch_bounds__(NT) void ln_bwd_dw_kernel(const float* __restrict__
     a += dwp[k * E + e];
     c += dbp[k * E + e];
   }
-  dw[e] = a;
-  db[e] = c;
+  const long long t = aidx(e, ch, E);
+  dw[t] = a;
+  db[t] = c;
 }
 
 int slices_for(int rows, long long E) {
@@ -211,8 +224,9 @@ int tgfr_ln_ws_floats(int rows, long long E, int backward, long long* out) {
 }
 
 int tgfr_ln_fwd(const float* x, int rows, long long E, const float* w, const float* b, float eps,
-                float* y, float* ws, void* stream) {
-  if (rows <= 0 || E <= 0 || (E & 3) || rows > 65535) return 1001;
+                int ch, float* y, float* ws, void* stream) {
+  if (rows <= 0 || E <= 0 || (E & 3) || rows > 65535 || ch < 0 || (ch && (ch & 3 || E % ch)))
+    return 1001;
   const int S = slices_for(rows, E);
   float* part = ws;
   float* stats = ws + (long long)rows * S * 2;
@@ -220,13 +234,14 @@ int tgfr_ln_fwd(const float* x, int rows, long long E, const float* w, const flo
   hipLaunchKernelGGL(ln_part_kernel, dim3(S, rows), dim3(NT), 0, st, x, E, S, part);
   const long long blocks = std::min<long long>((E / 4 + NT - 1) / NT, 64);
   hipLaunchKernelGGL(ln_apply_kernel, dim3((unsigned)blocks, rows), dim3(NT), 0, st, x, E, S, w,
-                     b, eps, part, stats, rows, y);
+                     b, eps, part, stats, rows, ch, y);
   return (int)hipGetLastError();
 }
 
-int tgfr_ln_bwd(const float* dy, const float* x, int rows, long long E, const float* w,
+int tgfr_ln_bwd(const float* dy, const float* x, int rows, long long E, const float* w, int ch,
                 float* ws, float* dx, float* dw, float* db, void* stream) {
-  if (rows <= 0 || E <= 0 || (E & 3) || rows > 65535) return 1001;
+  if (rows <= 0 || E <= 0 || (E & 3) || rows > 65535 || ch < 0 || (ch && (ch & 3 || E % ch)))
+    return 1001;
   const int S = slices_for(rows, E);
   const int per = 8, groups = (rows + per - 1) / per;
   float* part = ws;
@@ -236,11 +251,11 @@ int tgfr_ln_bwd(const float* dy, const float* x, int rows, long long E, const fl
   auto* st = (hipStream_t)stream;
   // the forward's slice moments are no longer needed: reuse their slots
   hipLaunchKernelGGL(ln_bwd_part_kernel, dim3(S, rows), dim3(NT), 0, st, dy, x, E, S, w, stats,
-                     rows, part);
+                     rows, ch, part);
   hipLaunchKernelGGL(ln_bwd_dx_kernel, dim3((unsigned)((E / 4 + NT - 1) / NT), groups),
-                     dim3(NT), 0, st, dy, x, E, S, w, stats, rows, part, per, dx, dwp, dbp);
+                     dim3(NT), 0, st, dy, x, E, S, w, stats, rows, part, per, ch, dx, dwp, dbp);
   hipLaunchKernelGGL(ln_bwd_dw_kernel, dim3((unsigned)((E + NT - 1) / NT)), dim3(NT), 0, st,
-                     dwp, dbp, E, groups, dw, db);
+                     dwp, dbp, E, groups, ch, dw, db);
   return (int)hipGetLastError();
 }
 

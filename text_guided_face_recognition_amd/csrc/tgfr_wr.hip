@@ -21,8 +21,9 @@
 //               waves: 8 d-chunks for S^T = W R^T, then 7 region chunks for
 //               C^T = R^T E^T.  Writes logits, per-token stats and C.
 //   wr_bwd      workgroup = (image, 4 region tiles, caption chunk), one wave
-//               per 32-region tile, all waves on the same caption.  Per
-//               caption it stages X = [W; dC] in LDS and computes
+//               per 32-region tile, all waves on the same caption.  Captions
+//               stream through an LDS ring (global_load_lds, 3 in flight in
+//               bf16 mode).  Per caption it stages X = [W; C] and computes
 //               [S^T; dA2^T] = X R_tile^T, the two softmax backwards in
 //               registers, and dR_tile += [dS | A2] X.  Writes partial slabs.
 //   wr_reduce   sums the caption-chunk slabs into dR (caller's strides).
@@ -588,12 +589,23 @@ template <int MODE>
 struct BwdCfg {
   static constexpr int NIMG = MODE == MODE_SPLIT ? 2 : 1;
   static constexpr int BUF = NIMG * B_XIMG + B_TOK;
-  static constexpr int LDS = 2 * BUF;
+  // caption ring: NB buffers, NB-1 captions in flight while one is computed
+  static constexpr int NB = 2;
+  // bf16: each wave's R tile (32 x 256 bf16) lives in LDS instead of 64
+  // VGPRs, which keeps the caption loop's live set inside the VGPR file (no
+  // AGPR shuttling); split mode keeps hi/lo R fragments in registers.
+  static constexpr bool R_LDS = MODE == MODE_BF16;
+  static constexpr int R_BASE = NB * BUF;
+  static constexpr int R_TILE = 32 * D * 2;
+  static constexpr int LDS = NB * BUF + (R_LDS ? 4 * R_TILE : 0);
+  static constexpr int PER = 8 * NIMG + 1;     // DMA ops per wave per caption
 };
 
-// Stage caption i of image b into LDS buffer `base` with global_load_lds:
-// pure copies (no registers), swizzled source addresses so the lane-linear
-// LDS writes land in the swizzled image.
+// Stage caption i of image b into LDS buffer `base`: pure global -> LDS DMA
+// (no registers), swizzled source addresses so the lane-linear LDS writes land
+// in the swizzled image.  Every wave issues BwdCfg::PER ops (the token table is
+// written by all four waves with identical bytes) so the ring's counted vmcnt
+// waits are the same in every wave.
 template <int MODE>
 __device__ __forceinline__ void bwd_stage(uint32_t base, const uint16_t* Whi, const uint16_t* Wlo,
                                           const uint16_t* Chi, const uint16_t* Clo,
@@ -601,6 +613,7 @@ __device__ __forceinline__ void bwd_stage(uint32_t base, const uint16_t* Whi, co
                                           int lane) {
   constexpr int NIMG = BwdCfg<MODE>::NIMG;
   // 32 one-KiB pieces per image: piece p covers rows 4*(p%16)..+3 of half p/16
+#pragma unroll
   for (int k = wid; k < 32 * NIMG; k += 4) {
     const int img = k / 32, p = k % 32;
     const int half = p / 16;
@@ -612,15 +625,9 @@ __device__ __forceinline__ void bwd_stage(uint32_t base, const uint16_t* Whi, co
       src = (img ? Wlo : Whi) + ((long long)i * TPAD + row) * D + c * 8;
     else
       src = (img ? Clo : Chi) + ((pair * 32 + c) * 32 + (row - 32)) * 8;
-    __builtin_amdgcn_global_load_lds((const void*)src,
-                                     (LDS_AS void*)(lds_base() + base + img * B_XIMG +
-                                                    half * (64 * 256) + 4 * (p % 16) * 256),
-                                     16, 0, 0);
+    glds16(src, base + img * B_XIMG + half * (64 * 256) + 4 * (p % 16) * 256);
   }
-  if (wid == 3)
-    __builtin_amdgcn_global_load_lds((const void*)(tok + pair * TPAD * 8 + lane * 4),
-                                     (LDS_AS void*)(lds_base() + base + NIMG * B_XIMG), 16, 0,
-                                     0);
+  glds16(tok + pair * TPAD * 8 + lane * 4, base + NIMG * B_XIMG);
 }
 
 template <int MODE>
@@ -638,20 +645,40 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
   const int tg = rem / n_chunks, chunk = rem % n_chunks;
   const int per = (B_cap + n_chunks - 1) / n_chunks;
   const int c0 = chunk * per, c1 = min(B_cap, c0 + per);
-  const int tid = threadIdx.x, wid = tid / WAVE, lane = tid % WAVE;
+  // wave index as a scalar: `active` below is then a uniform branch, so the
+  // dR accumulators stay in place across it
+  const int tid = threadIdx.x, lane = tid % WAVE;
+  const int wid = __builtin_amdgcn_readfirstlane(tid / WAVE);
   const int lr = lane & 31, h = lane >> 5;
   const int rt = tg * 4 + wid;
   const bool active = rt < NRT;
   const int r = rt * 32 + lr;
   const bool rvalid = active && r < NREG;
 
-  // R tile as B-operand fragments: lane (r, h), k-step s -> d = 16 s + 8 h
-  bf16x8 Rh[16], Rl[16];
-  const long long roff_ = ((long long)b * RPAD + (active ? r : 0)) * D;
+  // R tile as B-operand fragments: lane (r, h), k-step s -> d = 16 s + 8 h.
+  // bf16: staged once into this wave's LDS tile [32 rows][512 B], 16-B chunks
+  // XOR-swizzled by row (chunk c of row r at c ^ (r & 15)); rof[] holds the
+  // per-lane part of the fragment address (+ (s >> 3) * 256 B).
+  constexpr bool R_LDS = BwdCfg<MODE>::R_LDS;
+  bf16x8 Rh[R_LDS ? 1 : 16], Rl[R_LDS ? 1 : 16];
+  uint32_t rof[8];
+  const uint32_t rtile = BwdCfg<MODE>::R_BASE + wid * BwdCfg<MODE>::R_TILE;
+  if constexpr (R_LDS) {
+    const uint16_t* src = Rhi + ((long long)b * RPAD + (active ? rt * 32 : 0)) * D;
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    Rh[s] = as_bf8(*(const uint4*)(Rhi + roff_ + s * 16 + h * 8));
-    Rl[s] = MODE == MODE_SPLIT ? as_bf8(*(const uint4*)(Rlo + roff_ + s * 16 + h * 8)) : Rh[s];
+    for (int p = 0; p < 16; ++p) {
+      const int row = 2 * p + (lane >> 5), pc = lane & 31;
+      glds16(src + row * D + ((pc ^ (row & 15)) << 3), rtile + p * 1024);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rof[k] = rtile + lr * 512 + (((2 * k + h) ^ (lr & 15)) << 4);
+  } else {
+    const long long roff_ = ((long long)b * RPAD + (active ? r : 0)) * D;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      Rh[s] = as_bf8(*(const uint4*)(Rhi + roff_ + s * 16 + h * 8));
+      Rl[s] = MODE == MODE_SPLIT ? as_bf8(*(const uint4*)(Rlo + roff_ + s * 16 + h * 8)) : Rh[s];
+    }
   }
   f32x16 dR[8];
 #pragma unroll
@@ -659,21 +686,49 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
 #pragma unroll
     for (int q = 0; q < 16; ++q) dR[j][q] = 0.f;
 
-  if (c0 < c1) {
-    bwd_stage<MODE>(0, Whi, Wlo, Chi, Clo, tok, (long long)b * B_cap + c0, c0, wid, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
+  constexpr int NB = BwdCfg<MODE>::NB, PER = BwdCfg<MODE>::PER;
+  // R fragments must have landed before the ring's counted waits start
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int j = 0; j < NB - 1; ++j)
+    if (c0 + j < c1)
+      bwd_stage<MODE>(j * BUF, Whi, Wlo, Chi, Clo, tok, (long long)b * B_cap + c0 + j, c0 + j,
+                      wid, lane);
 
   const int g16 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  // Per-lane parts of the swizzled X-image addresses (xoff), so each LDS read
+  // in the caption loop is one register + an immediate offset:
+  //   row reads (GEMM1), W row lr / C row 32+lr, 16-d step s:
+  //     xoff = (s >> 3) * 16 KiB + [C: 8 KiB] + g1o[s & 7]
+  //   transposed reads (GEMM2), k block ks, d tile dt, half b of the 8 rows:
+  //     xoff = (dt >> 2) * 16 KiB + ((ks >> 1) * 32 + (ks & 1) * 16) * 256 + g2o[b][dt & 3]
+  uint32_t g1o[8], g2o[2][4];
+  {
+    const int sw1 = ((lr & 3) << 2) | ((lr >> 2) & 3);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g1o[k] = lr * 256 + (((2 * k + h) ^ sw1) << 4);
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd)
+        g2o[bb][dd] = (4 * h + q4 + 8 * bb) * 256 + ((dd ^ q4) << 6) +
+                      (((2 * (g16 & 1) + (p4 >> 1)) ^ ((h + 2 * bb) & 3)) << 4) + (p4 & 1) * 8;
+  }
   for (int i = c0; i < c1; ++i) {
-    const uint32_t base = ((i - c0) & 1) * BUF;
-    // prefetch the next caption into the other buffer (read last iteration,
-    // released by the barrier that ended it)
-    if (i + 1 < c1)
-      bwd_stage<MODE>(base ^ BUF, Whi, Wlo, Chi, Clo, tok, (long long)b * B_cap + i + 1, i + 1,
-                      wid, lane);
-    if (active) {
+    const int it = i - c0;
+    const uint32_t base = (it % NB) * BUF;
+    // caption i has landed once at most NB-2 younger captions are in flight;
+    // the barrier publishes every wave's pieces and retires the reads of
+    // caption i-1, whose buffer is refilled next
+    if (i + NB - 2 < c1) ring_barrier<(NB - 2) * PER>();
+    else ring_barrier<0>();
+    if (i + NB - 1 < c1)
+      bwd_stage<MODE>(((it + NB - 1) % NB) * BUF, Whi, Wlo, Chi, Clo, tok,
+                      (long long)b * B_cap + i + NB - 1, i + NB - 1, wid, lane);
+    // Every wave computes, the inactive tile-7 wave too (its rows are masked
+    // to zero and never stored): a branch here makes hipcc move the dR
+    // accumulators between AGPRs and VGPRs around it every caption.
+    {
       const uint32_t tk = base + NIMG * B_XIMG;
       // ---- [S^T ; Q^T] = [W ; C] R_tile^T  (M = 64 tokens, N = 32 regions)
       f32x16 A0, A1;
@@ -681,58 +736,65 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
       for (int q = 0; q < 16; ++q) A0[q] = A1[q] = 0.f;
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
-        const int col = s * 16 + h * 8;
-        const bf16x8 w_hi = as_bf8(lds_ld16(base + xoff(lr, col)));
-        const bf16x8 c_hi = as_bf8(lds_ld16(base + xoff(32 + lr, col)));
+        const uint32_t ow = base + g1o[s & 7] + (s >> 3) * (64 * 256);
+        const bf16x8 w_hi = as_bf8(lds_ld16(ow));
+        const bf16x8 c_hi = as_bf8(lds_ld16(ow + 32 * 256));
         bf16x8 w_lo = w_hi, c_lo = c_hi;
         if (MODE == MODE_SPLIT) {
-          w_lo = as_bf8(lds_ld16(base + B_XIMG + xoff(lr, col)));
-          c_lo = as_bf8(lds_ld16(base + B_XIMG + xoff(32 + lr, col)));
+          w_lo = as_bf8(lds_ld16(ow + B_XIMG));
+          c_lo = as_bf8(lds_ld16(ow + B_XIMG + 32 * 256));
         }
-        mma<MODE>(A0, w_hi, w_lo, Rh[s], Rl[s]);
-        mma<MODE>(A1, c_hi, c_lo, Rh[s], Rl[s]);
+        bf16x8 rh, rl;
+        if constexpr (R_LDS) {
+          rh = rl = as_bf8(lds_ld16(rof[s & 7] + (s >> 3) * 256));
+        } else {
+          rh = Rh[s];
+          rl = Rl[s];
+        }
+        mma<MODE>(A0, w_hi, w_lo, rh, rl);
+        mma<MODE>(A1, c_hi, c_lo, rh, rl);
       }
-      // ---- softmax forward recompute + both softmax backwards (registers)
-      float zinv[16], alpha[16], beta[16], sig[16], valid[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int t = acc_row(q, h);
-        const uint4 v0 = lds_ld16(tk + t * 32);
-        zinv[q] = __uint_as_float(v0.x);
-        alpha[q] = __uint_as_float(v0.y);
-        beta[q] = __uint_as_float(v0.z);
-        sig[q] = __uint_as_float(v0.w);
-        valid[q] = lds_ldf(tk + t * 32 + 16);
-      }
+      // sched_barrier fences keep the scheduler from hoisting the LDS reads of
+      // later phases (their results would pin registers across the softmax)
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- softmax forward recompute + both softmax backwards (registers).
+      // Token scalars are re-read from the LDS table in each pass instead of
+      // being held (keeps the live set small: no spills); a token is valid
+      // iff its 1/Z entry is non-zero.
       float m = -INFINITY;
 #pragma unroll
       for (int q = 0; q < 16; ++q)
-        if (valid[q] != 0.f) m = fmaxf(m, A0[q]);
+        if (lds_ldf(tk + acc_row(q, h) * 32) != 0.f) m = fmaxf(m, A0[q]);
       m = fmaxf(m, __shfl_xor(m, 32));
       float a1[16], sum = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        a1[q] = valid[q] != 0.f ? __expf(A0[q] - m) : 0.f;
+        a1[q] = lds_ldf(tk + acc_row(q, h) * 32) != 0.f ? __expf(A0[q] - m) : 0.f;
         sum += a1[q];
       }
       sum += __shfl_xor(sum, 32);
       const float inv = 1.f / sum;
-      float a2[16], da1[16], rho = 0.f;
+      float da1[16], rho = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
+        const uint4 v = lds_ld16(tk + acc_row(q, h) * 32);   // {1/Z, alpha, beta, sigma}
         a1[q] *= inv;
-        a2[q] = rvalid ? __expf(g1 * a1[q]) * zinv[q] : 0.f;
-        const float da2 = alpha[q] * A0[q] + beta[q] * A1[q];
-        da1[q] = g1 * a2[q] * (da2 - sig[q]);
+        const float a2 = rvalid ? __expf(g1 * a1[q]) * __uint_as_float(v.x) : 0.f;
+        const float da2 = __uint_as_float(v.y) * A0[q] + __uint_as_float(v.z) * A1[q];
+        da1[q] = g1 * a2 * (da2 - __uint_as_float(v.w));
         rho += a1[q] * da1[q];
+        A1[q] = a2;                                          // A1 now holds A2
       }
       rho += __shfl_xor(rho, 32);
+      __builtin_amdgcn_sched_barrier(0);
       float mw[16], mc[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
+        const uint4 v = lds_ld16(tk + acc_row(q, h) * 32);
+        const float alpha = __uint_as_float(v.y), beta = __uint_as_float(v.z);
         const float ds = rvalid ? a1[q] * (da1[q] - rho) : 0.f;
-        mw[q] = ds + alpha[q] * a2[q];
-        mc[q] = beta[q] * a2[q];
+        mw[q] = ds + alpha * A1[q];
+        mc[q] = beta * A1[q];
       }
       // ---- A fragments of M = [dS + alpha A2 | beta A2] (accumulator-as-operand)
       bf16x8 Mh[4], Ml[4];
@@ -740,26 +802,26 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
       frag8<MODE>(mw + 8, Mh[1], Ml[1]);
       frag8<MODE>(mc, Mh[2], Ml[2]);
       frag8<MODE>(mc + 8, Mh[3], Ml[3]);
+      __builtin_amdgcn_sched_barrier(0);
       // ---- dR_tile[r][d] += sum_k M[r][k] X[k][d]
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) {
+        if (dt == 2 || dt == 4 || dt == 6) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
-          const int rb = (ks >> 1) * 32 + (ks & 1) * 16 + 4 * h;
-          const int col = dt * 32 + 16 * (g16 & 1) + 4 * p4;
-          const uint32_t o0 = base + xoff(rb + q4, col), o1 = base + xoff(rb + 8 + q4, col);
+          const uint32_t kb = base + (dt >> 2) * (64 * 256) + ((ks >> 1) * 32 + (ks & 1) * 16) * 256;
+          const uint32_t o0 = kb + g2o[0][dt & 3], o1 = kb + g2o[1][dt & 3];
           const bf16x8 xh = join_tr(lds_tr4(o0), lds_tr4(o1));
           const bf16x8 xl = MODE == MODE_SPLIT
                                 ? join_tr(lds_tr4(o0 + B_XIMG), lds_tr4(o1 + B_XIMG))
                                 : xh;
-          mma<MODE>(dR[dt], Mh[ks], Ml[ks], xh, xl);
+          mma_agpr<MODE>(dR[dt], Mh[ks], Ml[ks], xh, xl);
         }
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
   if (!active) return;
+  mfma_drain();
   float* dst = slab + (((long long)chunk * B_img + b) * RPAD + rt * 32) * D;
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt)

@@ -7,6 +7,7 @@ in a HIP graph.  There is no CPU fallback: CPU tensors raise.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -58,8 +59,10 @@ def words_view(words_emb, n_words):
 
 
 def bwd_chunks(b_img, b_cap):
-    """Caption chunks for the backward grid (>= ~512 workgroups)."""
-    want = max(1, -(-512 // (2 * b_img)))
+    """Caption chunks for the backward grid: ~one workgroup per CU (the kernel
+    runs one 256-thread workgroup per CU), fewer slabs to reduce."""
+    per_cu = int(os.environ.get("TGFR_BWD_BLOCKS", "256"))
+    want = max(1, -(-per_cu // (2 * b_img)))
     return max(1, min(b_cap, want))
 
 
@@ -452,8 +455,9 @@ class BNLinear(torch.autograd.Function):
         dw = torch.empty_like(w2)
         dgamma = torch.empty(c, dtype=torch.float32, device=dev)
         dbeta = torch.empty_like(dgamma)
+        uws = torch.empty(2 * -(-o // 64) * c, dtype=torch.float32, device=dev)
         call("tgfr_bn_unfold", ptr(gm), ptr(s), ptr(w2), o, c, ptr(g), ptr(bt), ptr(dw),
-             ptr(dgamma), ptr(dbeta), _hip.stream())
+             ptr(dgamma), ptr(dbeta), ptr(uws), ptr(_hip.counters(dev)), _hip.stream())
         dx = None
         if ctx.needs_input_grad[0]:
             # d xhat = dp W'; BN input gradient (only when the map itself is trained)
@@ -489,10 +493,12 @@ def ln_ws_floats(rows, e, backward=True):
 
 class LayerNormRows(torch.autograd.Function):
     """Per-sample LayerNorm over all trailing elements with an elementwise
-    affine of the same shape (nn.LayerNorm([C, H, W]), models.py:388/:401)."""
+    affine of the same size (nn.LayerNorm([C, H, W]), models.py:388/:401).
+    ch > 0: x rows are channels-last [HW, ch] while weight/bias keep the
+    reference's [ch, H, W] layout (read in place, no permuted copies)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, eps):
+    def forward(ctx, x, weight, bias, eps, ch):
         rows = x.shape[0]
         x2 = _aligned(x.reshape(rows, -1))
         e = x2.shape[1]
@@ -500,28 +506,28 @@ class LayerNormRows(torch.autograd.Function):
         w, b = _aligned(weight.reshape(-1)), _aligned(bias.reshape(-1))
         ws = torch.empty(ln_ws_floats(rows, e), dtype=torch.float32, device=x.device)
         y = torch.empty_like(x2)
-        call("tgfr_ln_fwd", ptr(x2), rows, e, ptr(w), ptr(b), float(eps), ptr(y), ptr(ws),
-             _hip.stream())
+        call("tgfr_ln_fwd", ptr(x2), rows, e, ptr(w), ptr(b), float(eps), int(ch), ptr(y),
+             ptr(ws), _hip.stream())
         ctx.save_for_backward(x2, w, ws)
-        ctx.shapes = (x.shape, weight.shape)
+        ctx.shapes = (x.shape, weight.shape, int(ch))
         return y.reshape(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
         x2, w, ws = ctx.saved_tensors
-        xshape, wshape = ctx.shapes
+        xshape, wshape, ch = ctx.shapes
         rows, e = x2.shape
         dy = _aligned(dy.reshape(rows, e))
         dx = torch.empty_like(x2)
         dw = torch.empty(e, dtype=torch.float32, device=x2.device)
         db = torch.empty_like(dw)
-        call("tgfr_ln_bwd", ptr(dy), ptr(x2), rows, e, ptr(w), ptr(ws), ptr(dx), ptr(dw),
+        call("tgfr_ln_bwd", ptr(dy), ptr(x2), rows, e, ptr(w), ch, ptr(ws), ptr(dx), ptr(dw),
              ptr(db), _hip.stream())
-        return dx.reshape(xshape), dw.reshape(wshape), db.reshape(wshape), None
+        return dx.reshape(xshape), dw.reshape(wshape), db.reshape(wshape), None, None
 
 
-def layer_norm_rows(x, weight, bias, eps=1e-5):
-    return LayerNormRows.apply(x, weight, bias, eps)
+def layer_norm_rows(x, weight, bias, eps=1e-5, ch=0):
+    return LayerNormRows.apply(x, weight, bias, eps, ch)
 
 
 # ---------------------------------------------------------------- heads ---

@@ -61,11 +61,9 @@ class IMIM(nn.Module):
         wq, bq = self.sa.packed_self()
         px = K.bn_linear(img, self.bn_img, wq, bq, mode=self.precision)   # [B, HW, 3C]
         z = self.sa.core_self(px)
-        # LayerNorm over (C, H, W) of each sample == over the last two dims of
-        # the channels-last [B, HW, C] rows, with the affine maps permuted
-        wt = self.ln.weight.permute(1, 2, 0).reshape(h * w, c)
-        bs = self.ln.bias.permute(1, 2, 0).reshape(h * w, c)
-        z = K.layer_norm_rows(z, wt, bs, self.ln.eps)
+        # LayerNorm over (C, H, W) of each sample == over the channels-last
+        # [HW, C] rows; the [C, H, W] affine maps are read channel-major in place
+        z = K.layer_norm_rows(z, self.ln.weight, self.ln.bias, self.ln.eps, ch=c)
         z = K.linear_rows(z, self.conv1x1_1.weight, self.conv1x1_1.bias, relu=True,
                           mode=self.precision)
         z = K.linear_rows(z, self.conv1x1_2.weight, self.conv1x1_2.bias, relu=True,

@@ -47,6 +47,9 @@ def main(b=64, nw=30, mode="fp32", iters=20):
 
 
 if __name__ == "__main__":
+    if "--bf16-only" in sys.argv:
+        main(mode="bf16", iters=3)
+        sys.exit(0)
     for mode in ("fp32", "bf16"):
         main(mode=mode)
         main(b=256, mode=mode)

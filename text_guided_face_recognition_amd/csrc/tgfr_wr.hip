@@ -363,8 +363,8 @@ __device__ __forceinline__ uint32_t roff(int row, int col) {
   return (col >> 7) * (RPAD * 256) + row * 256 + ((((col & 127) >> 3) ^ sw) << 4) + (col & 7) * 2;
 }
 constexpr int FR_IMG = RPAD * D * 2;                 // 114688
-constexpr int FR_OFF_ET = FR_IMG;                    // per-wave E^T tile, bf16 [32][32]
-constexpr int FR_OFF_TOK = FR_OFF_ET + 4 * 2048;
+constexpr int FR_OFF_ET = FR_IMG;                    // per-wave E^T tiles, 2 x bf16 [32][32]
+constexpr int FR_OFF_TOK = FR_OFF_ET + 4 * 4096;
 constexpr int FR_LDS = FR_OFF_TOK + 4 * 256;
 
 __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
@@ -396,8 +396,26 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  const uint32_t et = FR_OFF_ET + wid * 2048;
+  const uint32_t et = FR_OFF_ET + wid * 4096;
   const uint32_t tok = FR_OFF_TOK + wid * 256;
+  // Per-lane parts of the swizzled R-image addresses (roff), so every LDS read
+  // below is one register + an immediate:
+  //   GEMM1 row reads, region tile j, 16-d step s:
+  //     roff = (s >> 3) * RPAD * 256 + j * 32 * 256 + f1o[s & 7]
+  //   GEMM2 transposed reads, region block 16 s of tile j, d tile dt, half b:
+  //     roff = (dt >> 2) * RPAD * 256 + (j * 32 + 16 s) * 256 + f2o[b][dt & 3]
+  uint32_t f1o[8], f2o[2][4];
+  {
+    const int sw1 = ((lr & 3) << 2) | ((lr >> 2) & 3);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f1o[k] = lr * 256 + (((2 * k + h) ^ sw1) << 4);
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd)
+        f2o[bb][dd] = (8 * h + q4 + 4 * bb) * 256 + ((dd ^ q4) << 6) +
+                      (((2 * (g16 & 1) + (p4 >> 1)) ^ ((2 * h + bb) & 3)) << 4) + (p4 & 1) * 8;
+  }
 
   for (int i = c0 + wid; i < c1; i += 4) {
     bf16x8 Wc[16];
@@ -415,37 +433,77 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
     for (int s = 0; s < 16; ++s) {
 #pragma unroll
       for (int j = 0; j < NRT; ++j) {
-        const bf16x8 bb = as_bf8(lds_ld16(roff(j * 32 + lr, s * 16 + h * 8)));
+        const bf16x8 bb = as_bf8(lds_ld16(f1o[s & 7] + (s >> 3) * (RPAD * 256) + j * 32 * 256));
         S[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Wc[s], bb, S[j], 0, 0, 0);
       }
     }
-    // ---- softmax over words per region; E overwrites S; per-token Z and N
+    // ---- per region tile j: softmax over words (E overwrites S, per-token Z
+    // and N accumulate), E^T through this wave's LDS (double-buffered), then
+    // C^T[d][t] += R[r][d] E[t][r] for the tile.  One unrolled sequence, so the
+    // MFMAs of tile j overlap the softmax VALU work of tile j+1.
+    // Padding words / regions are excluded by an additive -1e30 bias (exp2
+    // underflows to 0) instead of per-element selects; exps are exp2 with the
+    // log2(e) factor folded into one fma.
+    constexpr float L2E = 1.4426950408889634f;
+    float tb[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tb[q] = acc_row(q, h) < len ? 0.f : -1e30f;
     float zp[16], np[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) zp[q] = np[q] = 0.f;
+    f32x16 C[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) C[j][q] = 0.f;
 #pragma unroll
     for (int j = 0; j < NRT; ++j) {
-      const bool rvalid = j * 32 + lr < NREG;
-      float m = -INFINITY;
+      const float rb = j * 32 + lr < NREG ? 0.f : -1e30f;
+      float sm[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q)
-        if (acc_row(q, h) < len) m = fmaxf(m, S[j][q]);
-      m = fmaxf(m, __shfl_xor(m, 32));
-      float p[16], sum = 0.f;
+      for (int q = 0; q < 16; ++q) sm[q] = S[j][q] + tb[q];
+      float m = sm[0];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) m = __builtin_fmaxf(m, sm[q]);
+      m = __builtin_fmaxf(m, __shfl_xor(m, 32));
+      const float ml = m * L2E;
+      float sum = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        p[q] = acc_row(q, h) < len ? __expf(S[j][q] - m) : 0.f;
-        sum += p[q];
+        sm[q] = __builtin_amdgcn_exp2f(fmaf(sm[q], L2E, -ml));
+        sum += sm[q];
       }
       sum += __shfl_xor(sum, 32);
-      const float inv = 1.f / sum;
+      const float k = g1 * L2E * __builtin_amdgcn_rcpf(sum);
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const bool ok = rvalid && acc_row(q, h) < len;
-        const float e = ok ? __expf(g1 * (p[q] * inv)) : 0.f;
+        const float e = __builtin_amdgcn_exp2f(fmaf(sm[q], k, tb[q] + rb));
         zp[q] += e;
-        np[q] += e * S[j][q];
+        np[q] = fmaf(e, S[j][q], np[q]);
         S[j][q] = e;
+      }
+      // E^T tile j (bf16) -> LDS; DS instructions of one wave execute in order,
+      // so the transposed reads below see these writes
+      const uint32_t etj = et + (j & 1) * 2048;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint16_t hh[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) hh[kk] = bf_bits(S[j][4 * g + kk]);
+        lds_st8(etj + lr * 64 + (8 * g + 4 * h) * 2,
+                make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3])));
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int rbk = 16 * s + 8 * h;
+        const uint32_t eo = etj + (rbk + q4) * 64 + (16 * (g16 & 1) + 4 * p4) * 2;
+        const bf16x8 bb = join_tr(lds_tr4(eo), lds_tr4(eo + 4 * 64));
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          const uint32_t kb = (dt >> 2) * (RPAD * 256) + (j * 32 + 16 * s) * 256;
+          const bf16x8 aa = join_tr(lds_tr4(kb + f2o[0][dt & 3]), lds_tr4(kb + f2o[1][dt & 3]));
+          C[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aa, bb, C[dt], 0, 0, 0);
+        }
       }
     }
     const float zr = rs16(zp, lr), nr = rs16(np, lr);
@@ -463,41 +521,8 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
         for (int q = 0; q < 16; ++q) {
           const int tt = acc_row(q, h), r = j * 32 + lr;
           if (tt < len && tt < att_T && r < NREG)
-            dst[tt * NREG + r] = S[j][q] / lds_ldf(tok + tt * 4);
+            dst[tt * NREG + r] = S[j][q] * __builtin_amdgcn_rcpf(lds_ldf(tok + tt * 4));
         }
-    }
-    // ---- GEMM2: C^T[d][t] = R[r][d] E[t][r], region tile by tile
-    f32x16 C[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) C[j][q] = 0.f;
-#pragma unroll
-    for (int j = 0; j < NRT; ++j) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint16_t hh[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) hh[k] = bf_bits(S[j][4 * g + k]);
-        lds_st8(et + lr * 64 + (8 * g + 4 * h) * 2,
-                make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3])));
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int rb = 16 * s + 8 * h;
-        const uint32_t eo = et + (rb + q4) * 64 + (16 * (g16 & 1) + 4 * p4) * 2;
-        const bf16x8 bb = join_tr(lds_tr4(eo), lds_tr4(eo + 4 * 64));
-        const int r0 = j * 32 + rb + q4;
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-          const int col = dt * 32 + 16 * (g16 & 1) + 4 * p4;
-          const bf16x8 aa = join_tr(lds_tr4(roff(r0, col)), lds_tr4(roff(r0 + 4, col)));
-          C[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aa, bb, C[dt], 0, 0, 0);
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     // ---- per-token epilogue (lane t = lr)
     const int t = lr;
@@ -761,19 +786,23 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
       // Token scalars are re-read from the LDS table in each pass instead of
       // being held (keeps the live set small: no spills); a token is valid
       // iff its 1/Z entry is non-zero.
-      float m = -INFINITY;
+      // invalid tokens -> -1e30 once (exp underflows to 0; their alpha and beta
+      // are exactly 0, so alpha * A0 stays 0 below): no selects in the max/exp
 #pragma unroll
       for (int q = 0; q < 16; ++q)
-        if (lds_ldf(tk + acc_row(q, h) * 32) != 0.f) m = fmaxf(m, A0[q]);
-      m = fmaxf(m, __shfl_xor(m, 32));
+        if (lds_ldf(tk + acc_row(q, h) * 32) == 0.f) A0[q] = -1e30f;
+      float m = A0[0];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) m = __builtin_fmaxf(m, A0[q]);
+      m = __builtin_fmaxf(m, __shfl_xor(m, 32));
       float a1[16], sum = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        a1[q] = lds_ldf(tk + acc_row(q, h) * 32) != 0.f ? __expf(A0[q] - m) : 0.f;
+        a1[q] = __expf(A0[q] - m);
         sum += a1[q];
       }
       sum += __shfl_xor(sum, 32);
-      const float inv = 1.f / sum;
+      const float inv = __builtin_amdgcn_rcpf(sum);
       float da1[16], rho = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -806,7 +835,6 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
       // ---- dR_tile[r][d] += sum_k M[r][k] X[k][d]
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) {
-        if (dt == 2 || dt == 4 || dt == 6) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           const uint32_t kb = base + (dt >> 2) * (64 * 256) + ((ks >> 1) * 32 + (ks & 1) * 16) * 256;

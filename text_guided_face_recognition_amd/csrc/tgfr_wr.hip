@@ -417,11 +417,17 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
                       (((2 * (g16 & 1) + (p4 >> 1)) ^ ((2 * h + bb) & 3)) << 4) + (p4 & 1) * 8;
   }
 
-  for (int i = c0 + wid; i < c1; i += 4) {
-    bf16x8 Wc[16];
+  // this wave's captions i = c0 + wid, +4, ...; the next caption's words are
+  // loaded into Wc after the current caption's last MFMA, so the load latency
+  // hides behind its epilogue
+  bf16x8 Wc[16];
+  auto load_w = [&](int ii) {
 #pragma unroll
     for (int s = 0; s < 16; ++s)
-      Wc[s] = as_bf8(*(const uint4*)(Whi + ((long long)i * TPAD + lr) * D + s * 16 + h * 8));
+      Wc[s] = as_bf8(*(const uint4*)(Whi + ((long long)ii * TPAD + lr) * D + s * 16 + h * 8));
+  };
+  if (c0 + wid < c1) load_w(c0 + wid);
+  for (int i = c0 + wid; i < c1; i += 4) {
     const int len = lens[i];
     // ---- GEMM1: S^T[t][r] = W[t][d] R[r][d]
     f32x16 S[NRT];
@@ -524,6 +530,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
             dst[tt * NREG + r] = S[j][q] * __builtin_amdgcn_rcpf(lds_ldf(tok + tt * 4));
         }
     }
+    if (i + 4 < c1) load_w(i + 4);
     // ---- per-token epilogue (lane t = lr)
     const int t = lr;
     float csq = 0.f;

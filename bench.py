@@ -84,10 +84,27 @@ def time_steps(trainer, batch, ctx, steps, warmup):
 
 
 def kernel_profile(trainer, batch, steps):
+    """Per-ABI-call HIP-event timings over eager steps, plus back-to-back
+    replays of the word<->region kernels' first calls; returns (summary, timer)."""
     from text_guided_face_recognition_amd._hip import KernelTimer
-    with KernelTimer() as kt:
+    with KernelTimer(replay=("tgfr_wr_fwd", "tgfr_wr_bwd")) as kt:
         run_steps(trainer, batch, steps)
-    return kt.summary()
+    return kt.summary(), kt
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC passes of the
+    latest round (profiles/rNN/pmc.json, written by tools/summarize_profile.py
+    from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench
+    config; FETCH_SIZE doubled per MI355X_MICROARCH.md 'HBM').  None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                          "profiles", "r*", "pmc.json")))
+    if not files:
+        return None
+    data = json.load(open(files[-1]))
+    entry = data.get("kernels", {}).get(kernel)
+    return None if entry is None else entry.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(args, n_words):
@@ -191,7 +208,7 @@ def main():
         return GraphedStep(tr, batch) if use_graph else tr
 
     trainer = build(args.precision)
-    prof = kernel_profile(trainer, batch, max(3, min(args.steps, 10)))
+    prof, ktimer = kernel_profile(trainer, batch, max(3, min(args.steps, 10)))
     elapsed, out = time_steps(runner(trainer), batch, ctx, args.steps, args.warmup)
     n = ctx.world
     pairs = n * args.batch * args.steps
@@ -200,7 +217,7 @@ def main():
     alt = None
     if args.alt_precision and args.alt_precision != args.precision:
         tr2 = build(args.alt_precision)
-        prof2 = kernel_profile(tr2, batch, max(3, min(args.steps, 10)))
+        prof2, _ = kernel_profile(tr2, batch, max(3, min(args.steps, 10)))
         e2, _ = time_steps(runner(tr2), batch, ctx, args.steps, args.warmup)
         alt = {"precision": args.alt_precision, "value": round(pairs / e2, 2),
                "ms_per_step": round(e2 / args.steps * 1000, 4),
@@ -217,11 +234,15 @@ def main():
     flops = {"tgfr_wr_fwd": 4 * R * D * n_words * pair_count,
              "tgfr_wr_bwd": 6 * R * D * n_words * pair_count}
     dominant = max((k for k in prof if k in flops), key=lambda k: prof[k][1])
-    dom_ms = prof[dominant][1]
+    # the dominant kernel's launch duration: HIP events around 20 back-to-back
+    # re-launches with the step's own arguments (inside the step, while its
+    # buffers are alive), on the stream it runs on
+    dom_ms = ktimer.replayed[dominant]
     achieved = flops[dominant] / (dom_ms * 1e-3) / 1e12
     roofline = {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 2),
                 "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                "traffic": pmc_traffic(dominant),
                 "avg_launch_ms": round(dom_ms, 4),
                 "flop_per_launch": flops[dominant]}
 

@@ -61,16 +61,19 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 float* logits, int ld_logits, float* stats, uint16_t* Chi, uint16_t* Clo,
                 float* att, int att_T, int mode, void* stream);
 
-/* Backward of tgfr_wr_fwd w.r.t. the image regions given dL/dlogits: writes
- * n_chunks partial slabs [n_chunks][B_img][224][256] (one per caption chunk);
- * tok_ws is a caller workspace of B_img*B_cap*32*8 floats (per-token backward
- * scalars).  The text side is detached in the reference
- * (utils/dataset_utils.py:42). */
+/* Backward of tgfr_wr_fwd w.r.t. the image regions given dL/dlogits, in two
+ * launches.  tgfr_wr_bwd_tok: per-(pair, token) scalars from the forward
+ * stats and dlogits into tok_ws (B_img*B_cap*32*8 floats).  tgfr_wr_bwd: the
+ * fused recompute + both softmax backwards + dR GEMM; writes n_chunks partial
+ * slabs [n_chunks][B_img][224][256] (one per caption chunk).  The text side
+ * is detached in the reference (utils/dataset_utils.py:42). */
+int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const int* lens, int B_img,
+                    int B_cap, float gamma2, float gamma3, float eps, const float* dlogits,
+                    int ld, float* tok_ws, void* stream);
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
-                const uint16_t* Wlo, const float* Wnorm, const int* lens, int B_img, int B_cap,
-                int n_chunks, float gamma1, float gamma2, float gamma3, float eps,
-                const float* dlogits, int ld, const float* stats, const uint16_t* Chi,
-                const uint16_t* Clo, float* tok_ws, float* slab, int mode, void* stream);
+                const uint16_t* Wlo, int B_img, int B_cap, int n_chunks, float gamma1,
+                const float* tok_ws, const uint16_t* Chi, const uint16_t* Clo, float* slab,
+                int mode, void* stream);
 
 /* dR[b][r][d] (caller strides; r < 196) = (+)= sum over chunks of the slabs. */
 int tgfr_wr_reduce(const float* slab, int n_chunks, int B_img, float* out, long long s_b,

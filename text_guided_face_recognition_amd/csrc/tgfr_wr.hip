@@ -933,11 +933,21 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   return (int)hipGetLastError();
 }
 
+int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const int* lens, int B_img,
+                    int B_cap, float gamma2, float gamma3, float eps, const float* dlogits,
+                    int ld, float* tok_ws, void* stream) {
+  if (B_img <= 0 || B_cap <= 0 || ld < B_cap) return 1001;
+  const long long pairs = (long long)B_img * B_cap;
+  hipLaunchKernelGGL(wr_tok_kernel, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, (const float4*)stats, Wnorm, lens, dlogits, ld, B_img,
+                     B_cap, gamma2, gamma3, eps, tok_ws);
+  return (int)hipGetLastError();
+}
+
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
-                const uint16_t* Wlo, const float* Wnorm, const int* lens, int B_img, int B_cap,
-                int n_chunks, float gamma1, float gamma2, float gamma3, float eps,
-                const float* dlogits, int ld, const float* stats, const uint16_t* Chi,
-                const uint16_t* Clo, float* tok_ws, float* slab, int mode, void* stream) {
+                const uint16_t* Wlo, int B_img, int B_cap, int n_chunks, float gamma1,
+                const float* tok_ws, const uint16_t* Chi, const uint16_t* Clo, float* slab,
+                int mode, void* stream) {
   if (B_img <= 0 || B_cap <= 0 || n_chunks <= 0 || n_chunks > B_cap) return 1001;
   if (mode == MODE_SPLIT && (!Rlo || !Wlo || !Clo)) return 1001;
   auto* s = (hipStream_t)stream;
@@ -947,10 +957,6 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
     return true;
   }();
   (void)once;
-  const long long pairs = (long long)B_img * B_cap;
-  hipLaunchKernelGGL(wr_tok_kernel, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, s,
-                     (const float4*)stats, Wnorm, lens, dlogits, ld, B_img, B_cap, gamma2,
-                     gamma3, eps, tok_ws);
   const int grid = n_chunks * 2 * B_img;
   if (mode == MODE_SPLIT)
     hipLaunchKernelGGL(wr_bwd_kernel<MODE_SPLIT>, dim3(grid), dim3(256),

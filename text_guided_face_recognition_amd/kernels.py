@@ -116,10 +116,11 @@ class WordRegionLogits(torch.autograd.Function):
                            device=dlogits.device)
         tok = torch.empty(b_img, b_cap, TPAD, 8, dtype=torch.float32, device=dlogits.device)
         split = m == MODES["fp32"]
+        call("tgfr_wr_bwd_tok", ptr(stats), ptr(w_norm), ptr(lens), b_img, b_cap, gamma2,
+             gamma3, eps, ptr(dlogits), b_cap, ptr(tok), _hip.stream())
         call("tgfr_wr_bwd", ptr(r_hi), ptr(r_lo) if split else None, ptr(w_hi),
-             ptr(w_lo) if split else None, ptr(w_norm), ptr(lens), b_img, b_cap, chunks,
-             gamma1, gamma2, gamma3, eps, ptr(dlogits), b_cap, ptr(stats), ptr(c_hi),
-             ptr(c_lo), ptr(tok), ptr(slab), m, _hip.stream())
+             ptr(w_lo) if split else None, b_img, b_cap, chunks, gamma1, ptr(tok),
+             ptr(c_hi), ptr(c_lo) if split else None, ptr(slab), m, _hip.stream())
         d_reg = torch.empty(b_img, NREG, D, dtype=torch.float32, device=dlogits.device)
         call("tgfr_wr_reduce", ptr(slab), chunks, b_img, ptr(d_reg), NREG * D, D, 1, 0,
              _hip.stream())

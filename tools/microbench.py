@@ -35,11 +35,10 @@ def main(b=64, nw=30, mode="fp32", iters=20):
     ms = e0.elapsed_time(e1) / iters
     flop = 10 * 196 * 256 * nw * b * b
     from text_guided_face_recognition_amd._hip import KernelTimer
-    with KernelTimer() as kt:
+    with KernelTimer(replay=("tgfr_wr_fwd", "tgfr_wr_bwd")) as kt:
         for _ in range(5):
             step()
-    ks = kt.summary()
-    fwd, bwd = ks["tgfr_wr_fwd"][1], ks["tgfr_wr_bwd"][1]
+    fwd, bwd = kt.replayed["tgfr_wr_fwd"], kt.replayed["tgfr_wr_bwd"]
     f_tf = 4 * 196 * 256 * nw * b * b / fwd / 1e9
     b_tf = 6 * 196 * 256 * nw * b * b / bwd / 1e9
     print(f"mode={mode} B={b} T={nw}: {ms:.3f} ms/step  {flop / ms / 1e9:.1f} TFLOP/s algorithmic"

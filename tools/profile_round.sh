@@ -3,9 +3,11 @@
 #   1. kernel trace + stats of the default bench command (graph replay)
 #   2. FETCH_SIZE and 3. WRITE_SIZE PMC passes (separate: TCC slot limits),
 #      eager launches, few steps.
+# Then, here: python tools/summarize_profile.py gpurun_out/prof_<round> profiles/<round>
+# Usage: bash tools/profile_round.sh <round>   (default r01)
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/prof_r1
+OUT=gpurun_out/prof_${1:-r01}
 mkdir -p $OUT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench \
   -- python3 bench.py --steps 20 --warmup 5 --no-cpu --alt-precision "" > $OUT/trace.log 2>&1

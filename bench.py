@@ -202,7 +202,7 @@ def main():
     batch = synthetic_batch(args.batch, n_words, dev, seed=100 + 1000 * ctx.rank)
     batch = batch[:4] + (batch[4] % 4500,)
 
-    use_graph = not args.eager and not ctx.active
+    use_graph = not args.eager
 
     def runner(tr):
         return GraphedStep(tr, batch) if use_graph else tr

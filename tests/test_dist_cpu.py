@@ -1,6 +1,7 @@
 """CPU, world_size 2 over gloo: the rank-major row ownership, the text-side
-all-gather and the column log-sum-exp exchange of the contrastive CE
-reproduce the single-process global-batch quantities."""
+all-gather (one packed collective for mixed dtypes), the column log-sum-exp
+exchange of the contrastive CE, the flat gradient all-reduce and the initial
+parameter broadcast reproduce the single-process global-batch quantities."""
 import os
 import socket
 
@@ -49,6 +50,29 @@ def _worker(rank, world, port, q):
         ok_loss = torch.allclose(tot, ref, atol=1e-5)
         one = combine_col_partials(part.unsqueeze(0))
         ok_single = torch.allclose(one, torch.logsumexp(mine, 0), atol=1e-5)
+        # packed text gather: fp32 words [B, T, D], fp32 sentences, int64 ids
+        words = torch.randn(world * b_l, 4, 6)
+        sent = torch.randn(world * b_l, 6)
+        ids = torch.randint(0, 10 ** 12, (world * b_l,))
+        rows = slice(ctx.row_offset, ctx.row_offset + b_l)
+        gw, gs, gi = ctx.gather_text(words[rows].transpose(1, 2), sent[rows], ids[rows])
+        ok_gather = ok_gather and torch.equal(gw, words.transpose(1, 2)) and \
+            torch.equal(gs, sent) and torch.equal(gi, ids) and gi.dtype == torch.int64
+        # broadcast of rank 0's parameters, then the summed flat gradient
+        torch.manual_seed(1 + rank)                     # different init per rank
+        lin = torch.nn.Linear(6, 3)
+        ctx.broadcast_params(list(lin.parameters()))
+        torch.manual_seed(1)
+        ref_lin = torch.nn.Linear(6, 3)
+        ok_bcast = all(torch.equal(a, b) for a, b in zip(lin.parameters(),
+                                                         ref_lin.parameters()))
+        x = torch.randn(world * b_l, 6)
+        lin(x[rows]).pow(2).sum().backward()
+        ctx.reduce_grads(list(lin.parameters()))
+        ref_lin(x).pow(2).sum().backward()
+        ok_grad = all(torch.allclose(a.grad, b.grad, atol=1e-5)
+                      for a, b in zip(lin.parameters(), ref_lin.parameters()))
+        ok_gather = ok_gather and ok_bcast and ok_grad
         q.put((rank, ok_gather, ok_lse, ok_loss, ok_single, ctx.n_global))
     finally:
         dist.destroy_process_group()

@@ -20,16 +20,36 @@ def _port():
         return s.getsockname()[1]
 
 
+def _run(worker, out, **extra_env):
+    env = dict(os.environ, TGFR_DIST_BACKEND="gloo", OMP_NUM_THREADS="4", TGFR_DP_OUT=out,
+               **extra_env)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=2", "--master-addr=127.0.0.1", f"--master-port={_port()}",
+           os.path.join(ROOT, "tests", worker)]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env,
+                         cwd=ROOT)
+    ranks = "\n".join(l for l in res.stderr.splitlines() if l.startswith("[rank"))
+    assert res.returncode == 0, res.stdout[-2000:] + ranks[-6000:] + res.stderr[-1500:]
+
+
 def test_dp_world2_matches_global(gpu, tmp_path):
     import json
     out = str(tmp_path / "dp")
-    env = dict(os.environ, TGFR_DIST_BACKEND="gloo", OMP_NUM_THREADS="4", TGFR_DP_OUT=out)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           "--nproc-per-node=2", "--master-addr=127.0.0.1", f"--master-port={_port()}",
-           os.path.join(ROOT, "tests", "dp_worker.py")]
-    res = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env,
-                         cwd=ROOT)
-    assert res.returncode == 0, res.stdout[-3000:] + res.stderr[-3000:]
+    _run("dp_worker.py", out)
     for rank in range(2):
         r = json.load(open(f"{out}.{rank}"))
         assert r["err_loss"] < 1e-4 and r["err_r"] < 1e-4 and r["err_i"] < 1e-4, r
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_dp_graphed_train_step(gpu, tmp_path, precision):
+    """2 ranks: the stage-1 step replayed as graphs cut at its collectives
+    equals eager stepping, and the replicas stay identical."""
+    import json
+    out = str(tmp_path / "dpt")
+    _run("dp_train_worker.py", out, TGFR_DP_PRECISION=precision)
+    for rank in range(2):
+        r = json.load(open(f"{out}.{rank}"))
+        # text gather, 3 column exchanges, gradient all-reduce -> 6 graphs
+        assert r["segments"] == 6, r
+        assert r["err_out"] < 1e-4 and r["err_par"] < 1e-5 and r["err_rank"] == 0.0, r

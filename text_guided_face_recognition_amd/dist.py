@@ -14,6 +14,13 @@ its own images and gathers only what the contrastive denominators need:
 Rank r owns global rows [r*B_l, (r+1)*B_l) (rank-major), the same order the
 reference's gathered batch has, so the summed per-rank losses equal the
 single-process global-batch losses.
+
+Every collective goes through ``all_gather_cat`` / ``all_reduce_sum_``.  While
+a ``StepCapture`` is recording a step, each of them closes the HIP graph being
+captured, runs the collective eagerly on static buffers (and remembers it), and
+opens the next graph, so a distributed step replays as
+``graph, collective, graph, collective, ..., graph`` with no host work besides
+the launches (train.GraphedStep).
 """
 from __future__ import annotations
 
@@ -21,6 +28,61 @@ import os
 
 import torch
 import torch.distributed as dist
+
+_CAPTURE = None
+
+
+def active_capture():
+    return _CAPTURE
+
+
+class StepCapture:
+    """A step captured as a chain of HIP graphs cut at its collectives.
+
+    Graphs share one memory pool, so tensors made in one segment stay valid in
+    the next; the collectives between them run on buffers allocated during the
+    capture (static addresses), replayed in the captured order."""
+
+    def __init__(self):
+        self.graphs = []
+        self.collectives = []
+        self.pool = torch.cuda.graph_pool_handle()
+        self.stream = torch.cuda.Stream()
+
+    def _begin(self):
+        g = torch.cuda.CUDAGraph()
+        g.capture_begin(pool=self.pool)
+        self.graphs.append(g)
+
+    def cut(self, fn):
+        """Close the current graph, run collective `fn` now and at every
+        replay between this graph and the next, open the next graph."""
+        self.graphs[-1].capture_end()
+        fn()
+        self.collectives.append(fn)
+        self._begin()
+
+    def capture(self, step, *args):
+        """Record `step(*args)` (on a side stream); returns its outputs, whose
+        storage the replays rewrite."""
+        global _CAPTURE
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            self._begin()
+            _CAPTURE = self
+            try:
+                out = step(*args)
+            finally:
+                _CAPTURE = None
+                self.graphs[-1].capture_end()
+        torch.cuda.current_stream().wait_stream(self.stream)
+        return out
+
+    def replay(self):
+        for i, g in enumerate(self.graphs):
+            g.replay()
+            if i < len(self.collectives):
+                self.collectives[i]()
 
 
 class DistContext:
@@ -56,33 +118,102 @@ class DistContext:
 
     def sum(self, t):
         if self.active:
-            if dist.get_backend(self.group) == "gloo" and t.is_cuda:
-                c = t.detach().cpu()
-                dist.all_reduce(c, group=self.group)
-                return c.to(t.device)
-            t = t.clone()
-            dist.all_reduce(t, group=self.group)
+            t = t.detach().clone()
+            all_reduce_sum_(t, self.group)
         return t
+
+    def gather_text(self, *tensors):
+        """All-gather several equally-batched tensors (any dtypes) along dim 0
+        with ONE collective: their bytes are packed per rank, gathered, and
+        unpacked rank-major."""
+        if not self.active:
+            return tensors
+        flat = [t.contiguous().view(torch.uint8).reshape(t.shape[0], -1) for t in tensors]
+        widths = [f.shape[1] for f in flat]
+        packed = torch.cat(flat, 1)
+        allp = all_gather_cat(packed, self.group)
+        outs, c = [], 0
+        for t, w in zip(tensors, widths):
+            part = allp[:, c:c + w].contiguous().view(t.dtype)
+            outs.append(part.reshape((allp.shape[0],) + tuple(t.shape[1:])))
+            c += w
+        return tuple(outs)
+
+    def reduce_grads(self, params):
+        """Sum the gradients of `params` over ranks in one all-reduce of a flat
+        buffer (the DDP replacement: losses are pre-weighted so that the SUM is
+        the global-batch gradient); p.grad become views of the reduced buffer."""
+        if not self.active:
+            return
+        ps = [p for p in params if p.grad is not None]
+        if not ps:
+            return
+        flat = torch.cat([p.grad.reshape(-1) for p in ps])
+        all_reduce_sum_(flat, self.group)
+        off = 0
+        for p in ps:
+            n = p.numel()
+            p.grad = flat[off:off + n].view_as(p)
+            off += n
+
+    def broadcast_params(self, params):
+        """Rank 0's initial parameters to every rank (DDP's construction-time
+        broadcast)."""
+        if not self.active:
+            return
+        with torch.no_grad():
+            for p in params:
+                if dist.get_backend(self.group) == "gloo" and p.is_cuda:
+                    c = p.detach().cpu()
+                    dist.broadcast(c, 0, group=self.group)
+                    p.copy_(c)
+                else:
+                    dist.broadcast(p.data, 0, group=self.group)
+
+
+def _run_or_cut(fn):
+    if _CAPTURE is not None:
+        _CAPTURE.cut(fn)
+    else:
+        fn()
 
 
 def all_gather_cat(t, group=None):
-    """all_gather + concatenate along dim 0.  RCCL gathers device tensors in
-    place; gloo (CPU tests) only gathers host tensors, so it stages through host
-    memory."""
+    """all_gather + concatenate along dim 0 into a fresh tensor.  RCCL gathers
+    device tensors in place; gloo (CPU tests) only gathers host tensors, so it
+    stages through host memory.  Capture-aware (StepCapture)."""
     t = t.contiguous()
     world = dist.get_world_size(group)
-    if dist.get_backend(group) == "gloo" and t.is_cuda:
-        parts = [torch.empty_like(t, device="cpu") for _ in range(world)]
-        dist.all_gather(parts, t.cpu(), group=group)
-        return torch.cat(parts, 0).to(t.device)
-    if dist.get_backend(group) == "gloo":
-        parts = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(parts, t, group=group)
-        return torch.cat(parts, 0)
     out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
                       device=t.device)
-    dist.all_gather_into_tensor(out, t, group=group)
+    gloo = dist.get_backend(group) == "gloo"
+
+    def run():
+        if gloo:
+            src = t.cpu() if t.is_cuda else t
+            parts = [torch.empty_like(src) for _ in range(world)]
+            dist.all_gather(parts, src, group=group)
+            out.copy_(torch.cat(parts, 0))
+        else:
+            dist.all_gather_into_tensor(out, t, group=group)
+    _run_or_cut(run)
     return out
+
+
+def all_reduce_sum_(t, group=None):
+    """In-place SUM all-reduce (gloo stages device tensors through host
+    memory).  Capture-aware (StepCapture)."""
+    gloo = dist.get_backend(group) == "gloo"
+
+    def run():
+        if gloo and t.is_cuda:
+            c = t.cpu()
+            dist.all_reduce(c, group=group)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, group=group)
+    _run_or_cut(run)
+    return t
 
 
 def init_from_env(backend=None):

@@ -13,18 +13,19 @@ sentence [B,256], class ids) as device tensors.  ``synthetic_batch`` makes
 them with the shapes and statistics SURVEY.md 8(d) prescribes.
 
 One process per GPU: pass a DistContext; text features and class ids are
-all-gathered so every contrastive denominator sees the global batch, the
-contrastive losses are this rank's contributions (scaled by the world size
-before backward so DDP's gradient mean equals the global-batch gradient), and
-the identity losses are per-rank means (DDP's mean is the global mean).
+all-gathered (one collective) so every contrastive denominator sees the global
+batch.  Gradients are summed over ranks by one flat all-reduce
+(DistContext.reduce_grads, in place of DDP), so the contrastive losses -- this
+rank's contributions to the global-batch losses -- enter with weight 1 and the
+per-rank-mean identity losses with weight 1/world: the summed gradient is the
+reference's global-batch gradient.  Initial parameters are broadcast from
+rank 0.
 """
 from __future__ import annotations
 
 import torch
-from torch.nn.parallel import DistributedDataParallel as DDP
-
 from . import kernels as K
-from .dist import DistContext
+from .dist import DistContext, StepCapture
 from .models.fusion_nets import Working, set_precision
 from .models.losses import FocalLoss, global_loss, sent_loss, words_loss
 from .models.metrics import ArcMarginProduct
@@ -48,14 +49,6 @@ def synthetic_batch(b, n_words, device, seed, n_ids=10000):
             cls.to(**to))
 
 
-def _ddp(m, ctx):
-    if not ctx.active:
-        return m
-    dev = next(m.parameters()).device
-    ids = [dev.index] if dev.type == "cuda" else None
-    return DDP(m, device_ids=ids)
-
-
 class Train:
     """Stage-1 BERT trainer step (src/train_encoders_bert.py)."""
 
@@ -63,15 +56,16 @@ class Train:
         self.args = args
         self.ctx = ctx or DistContext()
         args.return_att_maps = False
-        self.image_head = _ddp(ImageHeading(args).to(device), self.ctx)
-        self.image_cls = _ddp(ArcMarginProduct(args.aux_feat_dim_per_granularity,
-                                               args.num_classes, s=30, m=0.5).to(device),
-                              self.ctx)
-        self.text_cls = _ddp(ArcMarginProduct(args.aux_feat_dim_per_granularity,
-                                              args.num_classes, s=35, m=0.5).to(device),
-                             self.ctx)
+        self.image_head = ImageHeading(args).to(device)
+        self.image_cls = ArcMarginProduct(args.aux_feat_dim_per_granularity,
+                                          args.num_classes, s=30, m=0.5).to(device)
+        self.text_cls = ArcMarginProduct(args.aux_feat_dim_per_granularity,
+                                         args.num_classes, s=35, m=0.5).to(device)
         for m in (self.image_head, self.image_cls, self.text_cls):
             set_precision(m, args.precision)
+        self.params = [p for m in (self.image_head, self.image_cls, self.text_cls)
+                       for p in m.parameters()]
+        self.ctx.broadcast_params(self.params)
         self.ident_loss = FocalLoss(gamma=2)
         # :212 (text_head params would join here; the text side is frozen input)
         self.optimizer_head = torch.optim.Adam(self.image_head.parameters(),
@@ -90,9 +84,8 @@ class Train:
         ctx.set_batch(b)
         args.dist = ctx
         # text side: all-gathered global batch (detached, as in the reference)
-        words_g = ctx.gather_rows(words.transpose(1, 2)).transpose(1, 2)
-        sent_g = ctx.gather_rows(sent)
-        cls_g = ctx.gather_rows(class_ids)
+        words_g, sent_g, cls_g = ctx.gather_text(words.transpose(1, 2), sent, class_ids)
+        words_g = words_g.transpose(1, 2)
         labels = self._labels(ctx.n_global, g.device)
 
         img_features, words_features = self.image_head(g, local)   # :265
@@ -104,16 +97,19 @@ class Train:
         tid = self.ident_loss(self.text_cls(sent, class_ids), class_ids)      # :293-294
         iid = self.ident_loss(self.image_cls(img_features, class_ids), class_ids)
         cl = global_loss(img_features, sent_g, args=args)          # :310
-        # total = world * (damsm + lambda_clip * cl) + lambda_id * (tid + iid)
-        # (:279, :316-323) and the logged terms, as one launch each way
-        wd, wi = float(ctx.world), float(args.lambda_id)
+        # total = damsm + lambda_clip * cl + lambda_id / world * (tid + iid)
+        # (:279, :316-323; see the module docstring for the 1/world) and the
+        # logged terms, as one launch each way
+        wi = float(args.lambda_id)
+        wo = wi / ctx.world
         total, report = K.loss_mix(
             (w0, w1, s0, s1, cl, tid, iid),
-            [(wd, wd, wd, wd, wd * args.lambda_clip, wi, wi),     # objective
+            [(1, 1, 1, 1, args.lambda_clip, wo, wo),              # objective
              (1, 1, 1, 1, 0, 0, 0),                               # damsm
              (0, 0, 0, 0, 1, 0, 0),                               # clip
              (0, 0, 0, 0, 0, wi, wi)])                            # ident
         total.backward()                                           # :323
+        ctx.reduce_grads(self.params)
         self.optimizer_head.step()
         self.optimizer_cls.step()
         return {"damsm": report[0], "clip": report[1], "ident": report[2]}
@@ -131,13 +127,14 @@ class Fusion:
     def __init__(self, args, device, ctx=None):
         self.args = args
         self.ctx = ctx or DistContext()
-        self.image_head = _ddp(ImageHeading(args).to(device), self.ctx)
-        self.fusion_net = _ddp(Working(args.aux_feat_dim_per_granularity).to(device),
-                               self.ctx)
-        self.metric_fc = _ddp(ArcMarginProduct(640, args.num_classes, s=30, m=0.5).to(device),
-                              self.ctx)
+        self.image_head = ImageHeading(args).to(device)
+        self.fusion_net = Working(args.aux_feat_dim_per_granularity).to(device)
+        self.metric_fc = ArcMarginProduct(640, args.num_classes, s=30, m=0.5).to(device)
         for m in (self.image_head, self.fusion_net, self.metric_fc):
             set_precision(m, args.precision)
+        self.params = [p for m in (self.image_head, self.fusion_net, self.metric_fc)
+                       for p in m.parameters()]
+        self.ctx.broadcast_params(self.params)
         self.criterion = FocalLoss(gamma=2)                        # :92-96
         self.optimizer_cls = torch.optim.SGD(self.metric_fc.parameters(), lr=0.1,
                                              weight_decay=5e-4,
@@ -157,18 +154,24 @@ class Fusion:
         self.optimizer_cls.zero_grad(set_to_none=True)
         self.optimizer_head.zero_grad(set_to_none=True)
         loss = self.criterion(output, class_ids)                   # :232
-        loss.backward()
+        # replicas only: per-rank mean losses, summed gradients -> scale 1/world
+        (loss if self.ctx.world == 1 else loss / self.ctx.world).backward()
+        self.ctx.reduce_grads(self.params)
         self.optimizer_cls.step()
         self.optimizer_head.step()
         return {"loss": loss.detach()}
 
 
 class GraphedStep:
-    """A whole train step (forward, backward, optimiser) captured into one HIP
-    graph: the host launches one graph per step instead of ~370 kernels.
+    """A whole train step (forward, backward, optimiser) captured as HIP
+    graphs: one graph on a single GPU; with a process group, a chain of graphs
+    cut at the step's collectives (text all-gather, one column-partial
+    all-gather per contrastive loss, the gradient all-reduce), which replay in
+    order with the collectives between them (dist.StepCapture).  The host
+    launches a few graphs per step instead of ~370 kernels.
 
     The batch tensors are static: copy the next batch into them (``load``)
-    before each replay.  Single-process only (DDP's hooks are not captured).
+    before each replay.
     """
 
     def __init__(self, trainer, batch, warmup=3):
@@ -179,9 +182,8 @@ class GraphedStep:
             for _ in range(warmup):
                 trainer.step(batch)
         torch.cuda.current_stream().wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.out = trainer.step(batch)
+        self.capture = StepCapture()
+        self.out = self.capture.capture(trainer.step, batch)
 
     def load(self, batch):
         for dst, src in zip(self.batch, batch):
@@ -191,5 +193,5 @@ class GraphedStep:
     def step(self, batch=None):
         if batch is not None:
             self.load(batch)
-        self.graph.replay()
+        self.capture.replay()
         return self.out

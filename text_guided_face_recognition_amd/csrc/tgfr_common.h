@@ -38,6 +38,12 @@ __device__ __forceinline__ void split2(float x, uint16_t& hi, uint16_t& lo) {
 __device__ __forceinline__ uint32_t pack2(uint16_t a, uint16_t b) {
   return (uint32_t)a | ((uint32_t)b << 16);
 }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// Two fp32 -> packed bf16x2 (a in the low half) by one v_cvt_pk_bf16_f32.
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
 
 template <int MODE>
 __device__ __forceinline__ void mma(f32x16& acc, const bf16x8& ahi, const bf16x8& alo,
@@ -164,6 +170,21 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
   return v;
 }
+// v combined with the same register of lane l ^ 32 by v_permlane32_swap (a
+// VALU op; no LDS round trip as with ds_bpermute).  After the swap, lanes
+// 0-31 hold (own, partner) in (r[0], r[1]) and lanes 32-63 (partner, own), so
+// a symmetric op of r[0] and r[1] is the pair's result in every lane.
+__device__ __forceinline__ float xhalf_sum(float v) {
+  const int u = __float_as_int(v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __int_as_float(r[0]) + __int_as_float(r[1]);
+}
+__device__ __forceinline__ float xhalf_max(float v) {
+  const int u = __float_as_int(v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_fmaxf(__int_as_float(r[0]), __int_as_float(r[1]));
+}
+
 // Reduce over the 32 lanes of each wave half (lanes differing in bits 0..4).
 __device__ __forceinline__ float half_sum(float v) {
 #pragma unroll

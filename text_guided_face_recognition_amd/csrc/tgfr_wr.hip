@@ -27,6 +27,8 @@
 //               [S^T; dA2^T] = X R_tile^T, the two softmax backwards in
 //               registers, and dR_tile += [dS | A2] X.  Writes partial slabs.
 //   wr_reduce   sums the caption-chunk slabs into dR (caller's strides).
+#include <stdlib.h>
+
 #include "tgfr_common.h"
 
 using namespace tgfr;
@@ -131,14 +133,18 @@ __device__ __forceinline__ void fwd_store_chunk(const StageRegs& s, int c, int b
   }
 }
 
-// C (the normalised weighted context, attention.py:41) for the backward, as
-// bf16 hi (+lo) in chunk-major order Cq[pair][c][t][8] (c = d / 8): lane
-// (t, h) holds d = 32 dt + 8 g + 4 h + 0..3, so each store instruction
-// writes 512 contiguous bytes and every 16-B chunk (8 consecutive d of one
-// token) is contiguous for the backward's global_load_lds gather.
+// C-hat = Z * C (the UNnormalised weighted context sum_r E[t,r] R_r, attention.py:41
+// before the 1/Z of the softmax) for the backward, as bf16 hi (+lo) in
+// chunk-major order Cq[pair][c][t][8] (c = d / 8): lane (t, h) holds
+// d = 32 dt + 8 g + 4 h + 0..3, so each store instruction writes 512
+// contiguous bytes and every 16-B chunk (8 consecutive d of one token) is
+// contiguous for the backward's global_load_lds gather.  The backward folds
+// 1/Z into its per-token scalars (wr_tok_kernel), so no per-element scaling
+// here.  Rows of padding tokens are whatever the kernel's E gives them
+// (finite); the backward multiplies them by zero scalars.
 template <int MODE>
 __device__ __forceinline__ void store_cq(uint16_t* Chi, uint16_t* Clo, long long pair, int t,
-                                         int h, bool tvalid, float zinv, const f32x16 (&C)[8]) {
+                                         int h, const f32x16 (&C)[8]) {
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
@@ -146,8 +152,8 @@ __device__ __forceinline__ void store_cq(uint16_t* Chi, uint16_t* Clo, long long
       uint16_t hh[4], ll[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float v = tvalid ? C[dt][4 * g + k] * zinv : 0.f;
-        split2(v, hh[k], ll[k]);
+        if constexpr (MODE == MODE_SPLIT) split2(C[dt][4 * g + k], hh[k], ll[k]);
+        else hh[k] = bf_bits(C[dt][4 * g + k]);
       }
       const long long o = ((pair * 32 + (4 * dt + g)) * 32 + t) * 8 + 4 * h;
       *(uint2*)(Chi + o) = make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3]));
@@ -336,7 +342,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_kernel(
   if (lane == 0) logits[(long long)b * ld_logits + i] = g3 * __logf(ex);
   if (stats && h == 0)
     stats[pair * TPAD + t] = tvalid ? make_float4(Z, n, cn, cosv) : make_float4(0.f, 0.f, 0.f, 0.f);
-  if (Chi) store_cq<MODE>(Chi, Clo, pair, t, h, tvalid, zinv, C);
+  if (Chi) store_cq<MODE>(Chi, Clo, pair, t, h, C);
   if (att && b + img_offset == i) {
     // attention map of the matching pair: A2[t][r] = E[t][r] / Z_t
     float* dst = att + (long long)b * att_T * NREG;
@@ -554,7 +560,314 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
     if (stats && h == 0)
       stats[pair * TPAD + t] =
           tvalid ? make_float4(Z, n, cn, cosv) : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (Chi) store_cq<MODE_BF16>(Chi, nullptr, pair, t, h, tvalid, zinv, C);
+    if (Chi) store_cq<MODE_BF16>(Chi, nullptr, pair, t, h, C);
+  }
+}
+
+// ------------------------------------- fwd, bf16, R resident, pipelined ---
+// Same work split, R image (LDS, roff swizzle) and outputs as
+// wr_fwd_res_kernel, restructured so that the matrix core and the VALU work
+// at the same time (one wave per SIMD: nothing else hides a stall).
+//
+// Per caption the 7 region tiles run as a software pipeline of 224 MFMA
+// "slots" whose order is fixed in the source (sched_barrier after each slot):
+//   stage 0     GEMM1(tile 1)                          | softmax(tile 0)
+//   stage 1..5  GEMM1(tile j+1) and GEMM2(tile j-1)    | softmax(tile j)
+//   stage 6     GEMM2(tile 5)                          | softmax(tile 6)
+//   stage 7     GEMM2(tile 6) and the NEXT caption's GEMM1(tile 0)
+// GEMM1 = S^T = bias + W R^T (16 MFMAs per tile, inline asm, VGPR results
+// read by the softmax); GEMM2 = C^T += R^T E^T (16 per tile, accumulators in
+// AGPRs).  Every slot issues the LDS reads of the slot three ahead (R rows /
+// R^T blocks are caption-independent, so the stream runs on across caption
+// seams) and one chunk (~4 ops, at most two exp) of the softmax VALU, so
+// each MFMA gap carries ~5 issue slots of other work (MI355X_MICROARCH.md,
+// 'single-issue instructions HIDDEN per MFMA gap').
+// Per element the VALU does: exp2(fma) (softmax over words), a sum, mul +
+// exp2 (E = exp(g1 A1)), the Z / N accumulations and the bf16 pack -- no
+// selects: padding words enter GEMM1's accumulator as a -1e30 bias (their
+// E is then exp(0) = 1, which only feeds their own -- unused -- token
+// statistics and C-hat rows); padding regions (tile 6) get an additive
+// -1e30 inside the second exp2.  Outputs: logits, stats {Z, n, |C|, cos},
+// C-hat (store_cq).  No attention maps (the host uses wr_fwd_res_kernel for
+// those).
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// MFMA -> VALU read of an asm MFMA's result: the 32x32x16 result latency (the
+// hazard recognizer does not see into inline asm).  The operand ties the wait
+// to the chain; not volatile, so it does not pin the LDS reads around it.
+__device__ __forceinline__ void mfma_result_wait(f32x16& acc) {
+  asm("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(acc));
+}
+
+// slot decode of a 32-slot stage: G1 x4, (G2 G1) x12, G2 x4
+__device__ __forceinline__ constexpr bool s32_is_g1(int m) {
+  return m < 4 || (m < 28 && ((m - 4) & 1));
+}
+__device__ __forceinline__ constexpr int s32_idx(int m) {
+  return m < 4 ? m : m < 28 ? ((m - 4) & 1 ? 4 + (m - 4) / 2 : (m - 4) / 2) : 12 + (m - 28);
+}
+
+struct FwdSlot {
+  int kind;  // 0: GEMM1, 1: GEMM2
+  int tile;  // region tile; GEMM1 of tile 0 is the next caption's
+  int idx;   // GEMM1: k-step 0..15; GEMM2: 8 * s + dt
+};
+// the caption's 224 slots in issue order
+__device__ __forceinline__ constexpr FwdSlot fwd_slot(int n) {
+  if (n < 16) return {0, 1, n};
+  if (n < 176) {
+    const int j = 1 + (n - 16) / 32, m = (n - 16) % 32;
+    return s32_is_g1(m) ? FwdSlot{0, j + 1, s32_idx(m)} : FwdSlot{1, j - 1, s32_idx(m)};
+  }
+  if (n < 192) return {1, 5, n - 176};
+  const int m = n - 192;
+  return s32_is_g1(m) ? FwdSlot{0, 0, s32_idx(m)} : FwdSlot{1, 6, s32_idx(m)};
+}
+
+__global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
+    const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi,
+    const float* __restrict__ Wnorm, const int* __restrict__ lens, int B_img, int B_cap,
+    int n_chunks, float g1, float g2, float g3, float eps, float* __restrict__ logits,
+    int ld_logits, float4* __restrict__ stats, uint16_t* __restrict__ Chi) {
+  const int work = xcd_remap(blockIdx.x, n_chunks * B_img);
+  const int b = work / n_chunks, chunk = work % n_chunks;
+  const int per = (B_cap + n_chunks - 1) / n_chunks;
+  const int c0 = chunk * per, c1 = min(B_cap, c0 + per);
+  const int tid = threadIdx.x, lane = tid % WAVE;
+  const int wid = __builtin_amdgcn_readfirstlane(tid / WAVE);
+  const int lr = lane & 31, h = lane >> 5;
+  const int g16 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+
+  {
+    const uint16_t* src = Rhi + (long long)b * RPAD * D;
+    for (int piece = wid; piece < FR_IMG / 1024; piece += 4) {
+      const int o = piece * 1024 + lane * 16;
+      const int half = o / (RPAD * 256), rem = o % (RPAD * 256);
+      const int row = rem / 256, pc = (rem % 256) / 16;
+      const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
+      const int col = half * 128 + ((pc ^ sw) << 3);
+      __builtin_amdgcn_global_load_lds((const void*)(src + row * D + col),
+                                       (LDS_AS void*)(lds_base() + piece * 1024), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  int i = c0 + wid;
+  if (i >= c1) return;
+
+  const uint32_t et = FR_OFF_ET + wid * 4096;
+  const uint32_t tok = FR_OFF_TOK + wid * 256;
+  // per-lane parts of the swizzled R-image addresses (roff); the d >= 128
+  // half has its own bases so every read is base + immediate
+  uint32_t f1o[2][8], f2o[2][2][4];
+  {
+    const int sw1 = ((lr & 3) << 2) | ((lr >> 2) & 3);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      f1o[0][k] = lr * 256 + (((2 * k + h) ^ sw1) << 4);
+      f1o[1][k] = f1o[0][k] + RPAD * 256;
+    }
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd) {
+        f2o[0][bb][dd] = (8 * h + q4 + 4 * bb) * 256 + ((dd ^ q4) << 6) +
+                         (((2 * (g16 & 1) + (p4 >> 1)) ^ ((2 * h + bb) & 3)) << 4) +
+                         (p4 & 1) * 8;
+        f2o[1][bb][dd] = f2o[0][bb][dd] + RPAD * 256;
+      }
+  }
+  // E^T fragment (B operand of GEMM2), k block s of the wave's buffer etb
+  const uint32_t eo_lane = (8 * h + q4) * 64 + (16 * (g16 & 1) + 4 * p4) * 2;
+  constexpr float L2E = 1.4426950408889634f;
+  const float kg = g1 * L2E;
+  const float rb6 = lr < NREG - 6 * 32 ? 0.f : -1e30f;   // padding regions of tile 6
+
+  bf16x8 Wc[16];
+  auto load_w = [&](int ii) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      Wc[s] = as_bf8(*(const uint4*)(Whi + ((long long)ii * TPAD + lr) * D + s * 16 + h * 8));
+  };
+  auto token_bias = [&](int ii) {
+    const int len = lens[ii];
+    f32x16 tb;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tb[q] = acc_row(q, h) < len ? 0.f : -1e30f;
+    return tb;
+  };
+  // LDS operand reads, 4-deep ring indexed by slot
+  u32x4 rd[4];
+  auto issue_read = [&](const FwdSlot sl, u32x4& dst) {
+    if (sl.kind == 0) {
+      const int s = sl.idx;
+      dst = __builtin_bit_cast(u32x4, lds_ld16(f1o[s >> 3][s & 7] + sl.tile * 32 * 256));
+    } else {
+      const int s = sl.idx >> 3, dt = sl.idx & 7;
+      const uint32_t kb = (sl.tile * 32 + 16 * s) * 256;
+      const s16x4 a = lds_tr4(kb + f2o[dt >> 2][0][dt & 3]);
+      const s16x4 c = lds_tr4(kb + f2o[dt >> 2][1][dt & 3]);
+      dst = __builtin_bit_cast(u32x4, join_tr(a, c));
+    }
+  };
+  auto read_e = [&](uint32_t etb, int s) {
+    const uint32_t eo = etb + eo_lane + s * 16 * 64;
+    return join_tr(lds_tr4(eo), lds_tr4(eo + 4 * 64));
+  };
+
+  f32x16 C[8];
+  float zp[16], np[16], p[16];
+  uint32_t pk[8];
+  float ma[5], mm, kk;
+  // softmax chunk c (0..31) of the tile in S (region tile j), E^T -> etb
+  auto sm_chunk = [&](int c, int j, const f32x16& S, uint32_t etb) {
+    if (c == 0) {
+      ma[0] = max3f(S[0], S[1], S[2]);
+      ma[1] = max3f(S[3], S[4], S[5]);
+    } else if (c == 1) {
+      ma[2] = max3f(S[6], S[7], S[8]);
+      ma[3] = max3f(S[9], S[10], S[11]);
+    } else if (c == 2) {
+      ma[4] = max3f(S[12], S[13], S[14]);
+      ma[0] = max3f(ma[0], ma[1], ma[2]);
+    } else if (c == 3) {
+      mm = -L2E * xhalf_max(max3f(ma[0], max3f(ma[3], ma[4], S[15]), ma[0]));
+    } else if (c < 12) {
+      const int q = 2 * (c - 4);
+      p[q] = __builtin_amdgcn_exp2f(fmaf(S[q], L2E, mm));
+      p[q + 1] = __builtin_amdgcn_exp2f(fmaf(S[q + 1], L2E, mm));
+    } else if (c == 12) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ma[q] = p[q] + p[q + 8];
+    } else if (c == 13) {
+      ma[0] += p[4] + p[12];
+      ma[1] += p[5] + p[13];
+    } else if (c == 14) {
+      ma[2] += p[6] + p[14];
+      ma[3] += p[7] + p[15];
+    } else if (c == 15) {
+      kk = kg * __builtin_amdgcn_rcpf(xhalf_sum((ma[0] + ma[1]) + (ma[2] + ma[3])));
+    } else {
+      const int q = c - 16;
+      const float e = __builtin_amdgcn_exp2f(j == 6 ? fmaf(p[q], kk, rb6) : p[q] * kk);
+      zp[q] += e;
+      np[q] = fmaf(e, S[q], np[q]);
+      p[q] = e;
+      if (q & 1) pk[q >> 1] = pk_bf16(p[q - 1], p[q]);
+      if ((q & 3) == 3) {
+        const int g = q >> 2;
+        lds_st8(etb + lr * 64 + (8 * g + 4 * h) * 2, make_uint2(pk[2 * g], pk[2 * g + 1]));
+      }
+    }
+  };
+
+  // ---- prologue: first caption's words, GEMM1 of its tile 0, first reads
+  load_w(i);
+  f32x16 S[7];           // S[j]: GEMM1 result of tile j (only two live at a time)
+  {
+    const f32x16 tb0 = token_bias(i);
+    f32x16 acc;
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3"
+        : "=&v"(acc) : "v"(Wc[0]), "v"(as_bf8(lds_ld16(f1o[0][0]))), "v"(tb0));
+#pragma unroll
+    for (int s = 1; s < 16; ++s)
+      asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
+          : "+v"(acc) : "v"(Wc[s]), "v"(as_bf8(lds_ld16(f1o[s >> 3][s & 7]))));
+    mfma_result_wait(acc);
+    S[0] = acc;
+  }
+#pragma unroll
+  for (int n = 0; n < 3; ++n) issue_read(fwd_slot(n), rd[n]);
+
+  for (; i < c1; i += 4) {
+    const int len = lens[i];
+    const int inext = min(i + 4, c1 - 1);   // the last caption recomputes itself
+    const f32x16 tb = token_bias(i);
+    const f32x16 tbn = token_bias(inext);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) zp[q] = np[q] = 0.f;
+    bf16x8 eb[2];
+#pragma clang loop unroll(full)
+    for (int n = 0; n < 224; ++n) {
+      const FwdSlot sl = fwd_slot(n);
+      // stage / slot-in-stage
+      const int stage = n < 16 ? 0 : n < 176 ? 1 + (n - 16) / 32 : n < 192 ? 6 : 7;
+      const int m = n < 16 ? n : n < 176 ? (n - 16) % 32 : n < 192 ? n - 176 : n - 192;
+      // E^T fragments of the tile GEMM2 consumes in this stage
+      const int g2tile = stage - 1;
+      if (stage >= 1 && m == 0) eb[0] = read_e(et + (g2tile & 1) * 2048, 0);
+      if (stage >= 1 && m == (stage == 6 ? 4 : 10)) eb[1] = read_e(et + (g2tile & 1) * 2048, 1);
+      // ---- the MFMA of this slot
+      const u32x4 opnd = rd[n & 3];
+      if (sl.kind == 0) {
+        const int s = sl.idx, j = sl.tile;
+        const bf16x8 w = Wc[s];
+        if (s == 0) {
+          asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3"
+              : "=&v"(S[j]) : "v"(w), "v"(__builtin_bit_cast(bf16x8, opnd)),
+                "v"(j == 0 ? tbn : tb));
+        } else {
+          asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
+              : "+v"(S[j]) : "v"(w), "v"(__builtin_bit_cast(bf16x8, opnd)));
+        }
+        if (s == 15 && j == 1) mfma_result_wait(S[1]);   // read in the next slot's stage
+      } else {
+        const int s = sl.idx >> 3, dt = sl.idx & 7;
+        const bf16x8 a = __builtin_bit_cast(bf16x8, opnd);
+        if (sl.tile == 0 && s == 0)
+          C[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, eb[0], (f32x16){}, 0, 0, 0);
+        else
+          C[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, eb[s], C[dt], 0, 0, 0);
+      }
+      // ---- reads of the slot three ahead (wrapping into the next caption)
+      issue_read(fwd_slot((n + 3) % 224), rd[(n + 3) & 3]);
+      // ---- the softmax VALU of this slot
+      if (stage <= 6) {
+        const int j = stage;                       // softmax tile
+        const uint32_t etb = et + (j & 1) * 2048;
+        if (stage == 0 || stage == 6) {
+          sm_chunk(2 * m, j, S[j], etb);
+          sm_chunk(2 * m + 1, j, S[j], etb);
+        } else {
+          sm_chunk(m, j, S[j], etb);
+        }
+      }
+      // the next caption's words, once GEMM1 of tile 6 is issued
+      if (n == 176) load_w(inext);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- Z and N per token: reduce-scatter over the region lanes -> LDS
+    {
+      const float zr = rs16(zp, lr), nr = rs16(np, lr);
+      const int t = acc_row(rs16_index(lr), h);
+      lds_stf(tok + t * 4, zr);
+      lds_stf(tok + 128 + t * 4, nr);
+    }
+    // ---- per-token epilogue (lane t = lr; both halves hold the same token)
+    const int t = lr;
+    float csq = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) csq = fmaf(C[dt][q], C[dt][q], csq);
+    csq = xhalf_sum(csq);
+    const float Z = lds_ldf(tok + t * 4);
+    const float nhat = lds_ldf(tok + 128 + t * 4);
+    const bool tvalid = t < len;
+    const float zinv = __builtin_amdgcn_rcpf(Z);
+    const float cn = sqrtf(csq) * zinv;
+    const float n_ = nhat * zinv;
+    const float u = Wnorm[(long long)i * TPAD + t];
+    const float cosv = n_ / fmaxf(u * cn, eps);
+    const float ex = half_sum(tvalid ? __expf(g2 * cosv) : 0.f);
+    const long long pair = (long long)b * B_cap + i;
+    logits[(long long)b * ld_logits + i] = g3 * __logf(ex);
+    stats[pair * TPAD + t] =
+        tvalid ? make_float4(Z, n_, cn, cosv) : make_float4(0.f, 0.f, 0.f, 0.f);
+    store_cq<MODE_BF16>(Chi, nullptr, pair, t, h, C);
   }
 }
 
@@ -563,8 +876,9 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
 //   dcos_t = g3 * dlogit * g2 * softmax_t(g2 cos)            (losses.py:107-122)
 //   dC_t   = alpha_t W_t + beta_t C_t                          (d cos / d C_t)
 //   sigma_t = sum_r A2[t,r] dA2[t,r] = dC_t . C_t               (softmax-2 bwd)
-// stored as 8 floats {1/Z, alpha, beta, sigma, valid, 0, 0, 0} so one 1-KiB
-// global_load_lds stages a caption's table.
+// stored as 8 floats {1/Z, alpha, beta/Z, sigma, valid, 0, 0, 0} (beta/Z: the
+// forward stores C-hat = Z C) so one 1-KiB global_load_lds stages a caption's
+// table.
 __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ stats,
                                                      const float* __restrict__ Wnorm,
                                                      const int* __restrict__ lens,
@@ -596,7 +910,7 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
     }
     o[0] = 1.f / st.x;
     o[1] = alpha;
-    o[2] = beta;
+    o[2] = beta * o[0];     // applied to C-hat = Z C (store_cq)
     o[3] = alpha * n + beta * cn * cn;
     o[4] = 1.f;
   }
@@ -914,6 +1228,7 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
     allow_lds(wr_fwd_kernel<MODE_SPLIT>, F_LDS);
     allow_lds(wr_fwd_kernel<MODE_BF16>, F_LDS);
     allow_lds(wr_fwd_res_kernel, FR_LDS);
+    allow_lds(wr_fwd_pipe_kernel, FR_LDS);
     return true;
   }();
   (void)once;
@@ -924,9 +1239,16 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   else if (mode == MODE_BF16) {
     // R resident in LDS; caption chunks sized for >= ~256 workgroups
     const int n_chunks = max(1, min((B_cap + 3) / 4, (256 + B_img - 1) / B_img));
-    hipLaunchKernelGGL(wr_fwd_res_kernel, dim3(n_chunks * B_img), dim3(256), FR_LDS, s, Rhi,
-                       Whi, Wnorm, lens, B_img, B_cap, n_chunks, img_offset, gamma1, gamma2,
-                       gamma3, eps, logits, ld_logits, (float4*)stats, Chi, att, att_T);
+    static const bool pipe = !getenv("TGFR_WR_FWD_RES");
+    if (pipe && !att && stats && Chi)
+      hipLaunchKernelGGL(wr_fwd_pipe_kernel, dim3(n_chunks * B_img), dim3(256), FR_LDS, s,
+                         Rhi, Whi, Wnorm, lens, B_img, B_cap, n_chunks, gamma1, gamma2, gamma3,
+                         eps, logits, ld_logits, (float4*)stats, Chi);
+    else
+      hipLaunchKernelGGL(wr_fwd_res_kernel, dim3(n_chunks * B_img), dim3(256), FR_LDS, s,
+                         Rhi, Whi, Wnorm, lens, B_img, B_cap, n_chunks, img_offset, gamma1,
+                         gamma2, gamma3, eps, logits, ld_logits, (float4*)stats, Chi, att,
+                         att_T);
   }
   else
     return 1002;

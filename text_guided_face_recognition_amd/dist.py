@@ -85,9 +85,23 @@ class StepCapture:
                 self.collectives[i]()
 
 
+class ReplicaGroup:
+    """A stand-in process group for ONE process that plays rank 0 of `world`
+    identical replicas (bench.py --simulate-world): gathers repeat the local
+    tensor, sums multiply it by `world`.  It reproduces the per-GPU work of a
+    `world`-GPU step (B_l images against B_l * world captions) on one device;
+    it moves no bytes between devices, so it says nothing about collectives."""
+
+    def __init__(self, world):
+        self.world = int(world)
+
+
 class DistContext:
     def __init__(self, group=None):
-        if dist.is_available() and dist.is_initialized():
+        if isinstance(group, ReplicaGroup):
+            self.group = group
+            self.rank, self.world = 0, group.world
+        elif dist.is_available() and dist.is_initialized():
             # an explicit handle: None means "not distributed" to the kernels
             self.group = group if group is not None else dist.group.WORLD
             self.rank = dist.get_rank(self.group)
@@ -97,6 +111,11 @@ class DistContext:
             self.rank, self.world = 0, 1
         self.active = self.world > 1
         self.b_local = None
+
+    @property
+    def multiprocess(self):
+        """True when other processes take part (a real process group)."""
+        return self.active and not isinstance(self.group, ReplicaGroup)
 
     def set_batch(self, b_local):
         self.b_local = int(b_local)
@@ -161,6 +180,8 @@ class DistContext:
         broadcast)."""
         if not self.active:
             return
+        if isinstance(self.group, ReplicaGroup):
+            return
         with torch.no_grad():
             for p in params:
                 if dist.get_backend(self.group) == "gloo" and p.is_cuda:
@@ -183,13 +204,17 @@ def all_gather_cat(t, group=None):
     device tensors in place; gloo (CPU tests) only gathers host tensors, so it
     stages through host memory.  Capture-aware (StepCapture)."""
     t = t.contiguous()
-    world = dist.get_world_size(group)
+    replica = isinstance(group, ReplicaGroup)
+    world = group.world if replica else dist.get_world_size(group)
     out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
                       device=t.device)
-    gloo = dist.get_backend(group) == "gloo"
+    gloo = not replica and dist.get_backend(group) == "gloo"
 
     def run():
-        if gloo:
+        if replica:
+            out.view((world,) + tuple(t.shape)).copy_(t.unsqueeze(0).expand(
+                (world,) + tuple(t.shape)))
+        elif gloo:
             src = t.cpu() if t.is_cuda else t
             parts = [torch.empty_like(src) for _ in range(world)]
             dist.all_gather(parts, src, group=group)
@@ -203,10 +228,13 @@ def all_gather_cat(t, group=None):
 def all_reduce_sum_(t, group=None):
     """In-place SUM all-reduce (gloo stages device tensors through host
     memory).  Capture-aware (StepCapture)."""
-    gloo = dist.get_backend(group) == "gloo"
+    replica = isinstance(group, ReplicaGroup)
+    gloo = not replica and dist.get_backend(group) == "gloo"
 
     def run():
-        if gloo and t.is_cuda:
+        if replica:
+            t.mul_(group.world)
+        elif gloo and t.is_cuda:
             c = t.cpu()
             dist.all_reduce(c, group=group)
             t.copy_(c)

@@ -37,13 +37,13 @@ extern "C" {
 int tgfr_version(void);
 
 /* fp32 rows (element (item,row,col) at x[item*s_item + row*s_row + col*s_col])
- * -> bf16 hi/lo [n_items][rows_pad][256] with rows >= min(n_rows, lens[item])
- * zeroed, plus optional fp32 row L2 norms [n_items][rows_pad].  Feeds the
- * word<->region kernels with R (image regions, models/models.py:401-404) and
- * W (words, models/models.py:231). */
+ * -> bf16 hi/lo of scale*x [n_items][rows_pad][256] with rows >=
+ * min(n_rows, lens[item]) zeroed, plus optional fp32 L2 norms of the unscaled
+ * rows [n_items][rows_pad].  Feeds the word<->region kernels with R (image
+ * regions, models/models.py:401-404) and W (words, models/models.py:231). */
 int tgfr_prep_rows(const float* x, long long s_item, long long s_row, long long s_col,
                    int n_items, int n_rows, int n_cols, int rows_pad, const int* lens,
-                   uint16_t* hi, uint16_t* lo, float* norms, void* stream);
+                   float scale, uint16_t* hi, uint16_t* lo, float* norms, void* stream);
 
 /* Forward of words_loss's similarity matrix for all (image b, caption i) pairs:
  * replaces the per-caption loop of models/losses.py:73-122 together with
@@ -53,13 +53,20 @@ int tgfr_prep_rows(const float* x, long long s_item, long long s_row, long long 
  * and the weighted context C (attention.py:41) as bf16 hi (Chi) and, in
  * mode 1, lo (Clo) in chunk-major order [pair][32 chunks of 8 d][32 t][8],
  * for the backward; att (nullable) receives A2 [b][t][196] for the matching
- * pair i == b + img_offset (the att_maps of losses.py:97).  Mode 0 keeps the
- * image's R resident in LDS (Rlo/Wlo unused, may be NULL). */
+ * pair i == b + img_offset (the att_maps of losses.py:97).  Wnorm: |W_t|
+ * [B_cap][32].  Mode 0 keeps the image's R resident in LDS (Rlo/Wlo unused, may
+ * be NULL) and takes the words scaled by log2(e) (Whi = bf16(log2(e) W),
+ * tgfr_prep_rows scale).  bounded = 1 (with Rnorm = |R_r| [B_img][224]) lets
+ * the mode-0 forward shift every caption's scores by max|W| max|R| instead of
+ * a running max (exact while that product is < 43, e.g. the unit-norm
+ * BERT-path features); otherwise the exact-max kernel runs.  C is stored
+ * unnormalised (C-hat = Z C); tgfr_wr_bwd_tok folds the 1/Z back in. */
 int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
-                const uint16_t* Wlo, const float* Wnorm, const int* lens, int B_img, int B_cap,
+                const uint16_t* Wlo, const float* Wnorm, const float* Rnorm, const int* lens,
+                int B_img, int B_cap,
                 int img_offset, float gamma1, float gamma2, float gamma3, float eps,
                 float* logits, int ld_logits, float* stats, uint16_t* Chi, uint16_t* Clo,
-                float* att, int att_T, int mode, void* stream);
+                float* att, int att_T, int bounded, int mode, void* stream);
 
 /* Backward of tgfr_wr_fwd w.r.t. the image regions given dL/dlogits, in two
  * launches.  tgfr_wr_bwd_tok: per-(pair, token) scalars from the forward

@@ -185,6 +185,11 @@ __device__ __forceinline__ float xhalf_max(float v) {
   return __builtin_fmaxf(__int_as_float(r[0]), __int_as_float(r[1]));
 }
 
+__device__ __forceinline__ float half_max(float v) {
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
+  return v;
+}
 // Reduce over the 32 lanes of each wave half (lanes differing in bits 0..4).
 __device__ __forceinline__ float half_sum(float v) {
 #pragma unroll

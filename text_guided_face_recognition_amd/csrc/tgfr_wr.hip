@@ -44,7 +44,7 @@ constexpr int NRT = 7;         // region tiles
 // ----------------------------------------------------------------- prep ---
 __global__ __launch_bounds__(256) void prep_rows_kernel(
     const float* __restrict__ x, long long s_item, long long s_row, long long s_col,
-    int n_items, int n_rows, int rows_pad, const int* __restrict__ lens,
+    int n_items, int n_rows, int rows_pad, const int* __restrict__ lens, float scale,
     uint16_t* __restrict__ hi, uint16_t* __restrict__ lo, float* __restrict__ norms) {
   const int wave = (blockIdx.x * 256 + threadIdx.x) / WAVE;
   const int lane = threadIdx.x % WAVE;
@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256) void prep_rows_kernel(
   }
   uint16_t h[4], l[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) split2(v[k], h[k], l[k]);
+  for (int k = 0; k < 4; ++k) split2(scale * v[k], h[k], l[k]);
   const long long o = ((long long)item * rows_pad + row) * D + lane * 4;
   *(uint2*)(hi + o) = make_uint2(pack2(h[0], h[1]), pack2(h[2], h[3]));
   *(uint2*)(lo + o) = make_uint2(pack2(l[0], l[1]), pack2(l[2], l[3]));
@@ -144,7 +144,7 @@ __device__ __forceinline__ void fwd_store_chunk(const StageRegs& s, int c, int b
 // (finite); the backward multiplies them by zero scalars.
 template <int MODE>
 __device__ __forceinline__ void store_cq(uint16_t* Chi, uint16_t* Clo, long long pair, int t,
-                                         int h, const f32x16 (&C)[8]) {
+                                         int h, const f32x16* C) {
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_kernel(
 }
 
 // ------------------------------------------------ fwd, bf16, R resident ---
-// bf16 mode only: the image's R (224 x 256 bf16 = 112 KB) stays in LDS for the
+// bf16 mode only (words scaled by log2(e) as for wr_fwd_pipe_kernel): the image's R (224 x 256 bf16 = 112 KB) stays in LDS for the
 // whole workgroup, so R is read from L2 once per (image, caption chunk)
 // instead of once per 4 captions.  Image layout: 2 halves x [224 rows][128
 // cols], 256-B rows, 16-B chunks XOR-swizzled by row -> both the row reads of
@@ -478,11 +478,11 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
 #pragma unroll
       for (int q = 1; q < 16; ++q) m = __builtin_fmaxf(m, sm[q]);
       m = __builtin_fmaxf(m, __shfl_xor(m, 32));
-      const float ml = m * L2E;
+      const float ml = m;        // scores are log2(e)-scaled (W' = log2(e) W)
       float sum = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        sm[q] = __builtin_amdgcn_exp2f(fmaf(sm[q], L2E, -ml));
+        sm[q] = __builtin_amdgcn_exp2f(sm[q] - ml);
         sum += sm[q];
       }
       sum += __shfl_xor(sum, 32);
@@ -546,7 +546,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
       for (int q = 0; q < 16; ++q) csq += C[dt][q] * C[dt][q];
     csq += __shfl_xor(csq, 32);
     const float Z = lds_ldf(tok + t * 4);
-    const float nhat = lds_ldf(tok + 128 + t * 4);
+    const float nhat = lds_ldf(tok + 128 + t * 4) * (1.f / L2E);
     const bool tvalid = t < len;
     const float zinv = 1.f / Z;
     const float cn = sqrtf(csq) * zinv;
@@ -569,27 +569,34 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
 // wr_fwd_res_kernel, restructured so that the matrix core and the VALU work
 // at the same time (one wave per SIMD: nothing else hides a stall).
 //
-// Per caption the 7 region tiles run as a software pipeline of 224 MFMA
+// Per caption the 7 region tiles run as a software pipeline of 238 MFMA
 // "slots" whose order is fixed in the source (sched_barrier after each slot):
 //   stage 0     GEMM1(tile 1)                          | softmax(tile 0)
 //   stage 1..5  GEMM1(tile j+1) and GEMM2(tile j-1)    | softmax(tile j)
 //   stage 6     GEMM2(tile 5)                          | softmax(tile 6)
 //   stage 7     GEMM2(tile 6) and the NEXT caption's GEMM1(tile 0)
-// GEMM1 = S^T = bias + W R^T (16 MFMAs per tile, inline asm, VGPR results
-// read by the softmax); GEMM2 = C^T += R^T E^T (16 per tile, accumulators in
-// AGPRs).  Every slot issues the LDS reads of the slot three ahead (R rows /
-// R^T blocks are caption-independent, so the stream runs on across caption
-// seams) and one chunk (~4 ops, at most two exp) of the softmax VALU, so
-// each MFMA gap carries ~5 issue slots of other work (MI355X_MICROARCH.md,
+// GEMM1 = S'^T = init + W' R^T (16 MFMAs per tile, inline asm, VGPR results
+// read by the softmax); GEMM2 = C^T += R^T E^T (16 per tile) plus Z^T +=
+// 1^T E^T (2 per tile: the softmax-2 denominators come out of the matrix
+// core, no per-element adds or cross-lane sums), accumulators in AGPRs.
+// Every slot issues the LDS reads of the slot three ahead (R rows / R^T
+// blocks are caption-independent, so the stream runs on across caption
+// seams) and one chunk (~4 VALU, at most two exp) of the softmax, so each
+// MFMA gap carries ~5 issue slots of other work (MI355X_MICROARCH.md,
 // 'single-issue instructions HIDDEN per MFMA gap').
-// Per element the VALU does: exp2(fma) (softmax over words), a sum, mul +
-// exp2 (E = exp(g1 A1)), the Z / N accumulations and the bf16 pack -- no
-// selects: padding words enter GEMM1's accumulator as a -1e30 bias (their
-// E is then exp(0) = 1, which only feeds their own -- unused -- token
-// statistics and C-hat rows); padding regions (tile 6) get an additive
-// -1e30 inside the second exp2.  Outputs: logits, stats {Z, n, |C|, cos},
-// C-hat (store_cq).  No attention maps (the host uses wr_fwd_res_kernel for
-// those).
+//
+// Words come in scaled by log2(e) (W' = log2(e) W, tgfr_prep_rows scale), and
+// GEMM1's accumulator starts at init[t] = bias[t] - log2(e) c with c =
+// max_t |W_t| * max_r |R_r| >= every score of the caption: the softmax over
+// words is then p = exp2(S'^T) directly (no max, no subtraction; exact in
+// real arithmetic, the shift cancels in the normalisation; no term can
+// overflow, and a region's sum cannot underflow while 2c < 87 -- c = 1 for
+// the L2-normalised BERT-path features, models/models.py:212,403).  The host
+// routes other inputs to wr_fwd_res_kernel (exact running max).  Padding
+// words carry bias -1e30 (p = 0; their E = exp(0) = 1 only feeds their own
+// unused statistics and C-hat rows); padding regions (tile 6) get -1e30
+// inside the second exp2.  Outputs: logits, stats {Z, n, |C|, cos}, C-hat
+// (store_cq).  No attention maps (the host uses wr_fwd_res_kernel for those).
 __device__ __forceinline__ float max3f(float a, float b, float c) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -602,36 +609,44 @@ __device__ __forceinline__ void mfma_result_wait(f32x16& acc) {
   asm("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(acc));
 }
 
-// slot decode of a 32-slot stage: G1 x4, (G2 G1) x12, G2 x4
-__device__ __forceinline__ constexpr bool s32_is_g1(int m) {
+// slot decode of a 34-slot stage: G1 x4, (G2 G1) x12, G2 x6
+__device__ __forceinline__ constexpr bool s34_is_g1(int m) {
   return m < 4 || (m < 28 && ((m - 4) & 1));
 }
-__device__ __forceinline__ constexpr int s32_idx(int m) {
+__device__ __forceinline__ constexpr int s34_idx(int m) {
   return m < 4 ? m : m < 28 ? ((m - 4) & 1 ? 4 + (m - 4) / 2 : (m - 4) / 2) : 12 + (m - 28);
 }
 
 struct FwdSlot {
-  int kind;  // 0: GEMM1, 1: GEMM2
-  int tile;  // region tile; GEMM1 of tile 0 is the next caption's
-  int idx;   // GEMM1: k-step 0..15; GEMM2: 8 * s + dt
+  int kind;   // 0: GEMM1, 1: GEMM2
+  int tile;   // region tile; GEMM1 of tile 0 is the next caption's
+  int idx;    // GEMM1: k-step 0..15; GEMM2: 0..17 (see g2_dt)
+  int stage;  // 0..7
+  int m;      // slot within the stage
 };
-// the caption's 224 slots in issue order
+constexpr int FWD_SLOTS = 16 + 5 * 34 + 18 + 34;
+// the caption's slots in issue order
 __device__ __forceinline__ constexpr FwdSlot fwd_slot(int n) {
-  if (n < 16) return {0, 1, n};
-  if (n < 176) {
-    const int j = 1 + (n - 16) / 32, m = (n - 16) % 32;
-    return s32_is_g1(m) ? FwdSlot{0, j + 1, s32_idx(m)} : FwdSlot{1, j - 1, s32_idx(m)};
+  if (n < 16) return {0, 1, n, 0, n};
+  if (n < 186) {
+    const int j = 1 + (n - 16) / 34, m = (n - 16) % 34;
+    return s34_is_g1(m) ? FwdSlot{0, j + 1, s34_idx(m), j, m}
+                        : FwdSlot{1, j - 1, s34_idx(m), j, m};
   }
-  if (n < 192) return {1, 5, n - 176};
-  const int m = n - 192;
-  return s32_is_g1(m) ? FwdSlot{0, 0, s32_idx(m)} : FwdSlot{1, 6, s32_idx(m)};
+  if (n < 204) return {1, 5, n - 186, 6, n - 186};
+  const int m = n - 204;
+  return s34_is_g1(m) ? FwdSlot{0, 0, s34_idx(m), 7, m} : FwdSlot{1, 6, s34_idx(m), 7, m};
 }
+// GEMM2 index v -> k block s (16 regions) and d tile (8 = the Z row of ones)
+__device__ __forceinline__ constexpr int g2_s(int v) { return v < 9 ? 0 : 1; }
+__device__ __forceinline__ constexpr int g2_dt(int v) { return v < 9 ? v : v - 9; }
 
 __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi,
-    const float* __restrict__ Wnorm, const int* __restrict__ lens, int B_img, int B_cap,
-    int n_chunks, float g1, float g2, float g3, float eps, float* __restrict__ logits,
-    int ld_logits, float4* __restrict__ stats, uint16_t* __restrict__ Chi) {
+    const float* __restrict__ Wnorm, const float* __restrict__ Rnorm,
+    const int* __restrict__ lens, int B_img, int B_cap, int n_chunks, float g1, float g2,
+    float g3, float eps, float* __restrict__ logits, int ld_logits,
+    float4* __restrict__ stats, uint16_t* __restrict__ Chi) {
   const int work = xcd_remap(blockIdx.x, n_chunks * B_img);
   const int b = work / n_chunks, chunk = work % n_chunks;
   const int per = (B_cap + n_chunks - 1) / n_chunks;
@@ -658,6 +673,26 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
   int i = c0 + wid;
   if (i >= c1) return;
 
+  // max_r |R_r| of this image (the score bound's image factor)
+  float rmax = INFINITY;
+  if (Rnorm) {
+    const float* rn = Rnorm + (long long)b * RPAD;
+    rmax = fmaxf(fmaxf(rn[lane], rn[lane + 64]), fmaxf(rn[lane + 128], lane < 32 ? rn[lane + 192] : 0.f));
+    rmax = wave_max(rmax);
+  }
+  constexpr float L2E = 1.4426950408889634f;
+  // per-caption bound c (wave-uniform) and GEMM1's initial value; wn = this
+  // lane's |W_t| of the caption
+  auto caption_init = [&](int ii, float wn, float& c) {
+    const int len = lens[ii];
+    c = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(half_max(wn) * rmax)));
+    const float sh = -L2E * c;
+    f32x16 init;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) init[q] = acc_row(q, h) < len ? sh : -1e30f;
+    return init;
+  };
+
   const uint32_t et = FR_OFF_ET + wid * 4096;
   const uint32_t tok = FR_OFF_TOK + wid * 256;
   // per-lane parts of the swizzled R-image addresses (roff); the d >= 128
@@ -680,11 +715,17 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
         f2o[1][bb][dd] = f2o[0][bb][dd] + RPAD * 256;
       }
   }
-  // E^T fragment (B operand of GEMM2), k block s of the wave's buffer etb
-  const uint32_t eo_lane = (8 * h + q4) * 64 + (16 * (g16 & 1) + 4 * p4) * 2;
-  constexpr float L2E = 1.4426950408889634f;
+  // E^T tile [32 regions][32 words] bf16, 64-B rows, 16-B chunk k of row r at
+  // k ^ ((r >> 2) & 3): conflict-free for both the 8-B row-chunk writes and
+  // the transposed reads.  Read bases of the two 4-row blocks of a fragment:
+  const int ec = 2 * (g16 & 1) + (p4 >> 1);
+  const uint32_t eoa = (8 * h + q4) * 64 + ((ec ^ (2 * h)) << 4) + (p4 & 1) * 8;
+  const uint32_t eob = (8 * h + q4 + 4) * 64 + ((ec ^ (2 * h + 1)) << 4) + (p4 & 1) * 8;
+  const uint32_t ew = lr * 64 + h * 8;            // write base; chunk g ^ ewx
+  const int ewx = (lr >> 2) & 3;
   const float kg = g1 * L2E;
   const float rb6 = lr < NREG - 6 * 32 ? 0.f : -1e30f;   // padding regions of tile 6
+  const bf16x8 ones = as_bf8(make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
 
   bf16x8 Wc[16];
   auto load_w = [&](int ii) {
@@ -692,21 +733,14 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     for (int s = 0; s < 16; ++s)
       Wc[s] = as_bf8(*(const uint4*)(Whi + ((long long)ii * TPAD + lr) * D + s * 16 + h * 8));
   };
-  auto token_bias = [&](int ii) {
-    const int len = lens[ii];
-    f32x16 tb;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) tb[q] = acc_row(q, h) < len ? 0.f : -1e30f;
-    return tb;
-  };
   // LDS operand reads, 4-deep ring indexed by slot
   u32x4 rd[4];
   auto issue_read = [&](const FwdSlot sl, u32x4& dst) {
     if (sl.kind == 0) {
       const int s = sl.idx;
       dst = __builtin_bit_cast(u32x4, lds_ld16(f1o[s >> 3][s & 7] + sl.tile * 32 * 256));
-    } else {
-      const int s = sl.idx >> 3, dt = sl.idx & 7;
+    } else if (g2_dt(sl.idx) < 8) {
+      const int s = g2_s(sl.idx), dt = g2_dt(sl.idx);
       const uint32_t kb = (sl.tile * 32 + 16 * s) * 256;
       const s16x4 a = lds_tr4(kb + f2o[dt >> 2][0][dt & 3]);
       const s16x4 c = lds_tr4(kb + f2o[dt >> 2][1][dt & 3]);
@@ -714,31 +748,20 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     }
   };
   auto read_e = [&](uint32_t etb, int s) {
-    const uint32_t eo = etb + eo_lane + s * 16 * 64;
-    return join_tr(lds_tr4(eo), lds_tr4(eo + 4 * 64));
+    return join_tr(lds_tr4(etb + eoa + s * 1024), lds_tr4(etb + eob + s * 1024));
   };
 
-  f32x16 C[8];
-  float zp[16], np[16], p[16];
+  f32x16 C[9];           // C^T tiles (d tiles 0..7) and Z^T (8)
+  float np[16], p[16];
   uint32_t pk[8];
-  float ma[5], mm, kk;
+  float ma[4], kk = 0.f;
   // softmax chunk c (0..31) of the tile in S (region tile j), E^T -> etb
   auto sm_chunk = [&](int c, int j, const f32x16& S, uint32_t etb) {
-    if (c == 0) {
-      ma[0] = max3f(S[0], S[1], S[2]);
-      ma[1] = max3f(S[3], S[4], S[5]);
-    } else if (c == 1) {
-      ma[2] = max3f(S[6], S[7], S[8]);
-      ma[3] = max3f(S[9], S[10], S[11]);
-    } else if (c == 2) {
-      ma[4] = max3f(S[12], S[13], S[14]);
-      ma[0] = max3f(ma[0], ma[1], ma[2]);
-    } else if (c == 3) {
-      mm = -L2E * xhalf_max(max3f(ma[0], max3f(ma[3], ma[4], S[15]), ma[0]));
+    if (c < 4) {
     } else if (c < 12) {
       const int q = 2 * (c - 4);
-      p[q] = __builtin_amdgcn_exp2f(fmaf(S[q], L2E, mm));
-      p[q + 1] = __builtin_amdgcn_exp2f(fmaf(S[q + 1], L2E, mm));
+      p[q] = __builtin_amdgcn_exp2f(S[q]);
+      p[q + 1] = __builtin_amdgcn_exp2f(S[q + 1]);
     } else if (c == 12) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) ma[q] = p[q] + p[q + 8];
@@ -753,25 +776,25 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     } else {
       const int q = c - 16;
       const float e = __builtin_amdgcn_exp2f(j == 6 ? fmaf(p[q], kk, rb6) : p[q] * kk);
-      zp[q] += e;
       np[q] = fmaf(e, S[q], np[q]);
       p[q] = e;
       if (q & 1) pk[q >> 1] = pk_bf16(p[q - 1], p[q]);
       if ((q & 3) == 3) {
         const int g = q >> 2;
-        lds_st8(etb + lr * 64 + (8 * g + 4 * h) * 2, make_uint2(pk[2 * g], pk[2 * g + 1]));
+        lds_st8(etb + ew + ((g ^ ewx) << 4), make_uint2(pk[2 * g], pk[2 * g + 1]));
       }
     }
   };
 
   // ---- prologue: first caption's words, GEMM1 of its tile 0, first reads
+  float c_cur, c_next;
+  f32x16 init = caption_init(i, Wnorm[(long long)i * TPAD + lr], c_cur);
   load_w(i);
-  f32x16 S[7];           // S[j]: GEMM1 result of tile j (only two live at a time)
+  f32x16 S[7];           // S[j]: GEMM1 result of tile j (two live at a time)
   {
-    const f32x16 tb0 = token_bias(i);
     f32x16 acc;
     asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3"
-        : "=&v"(acc) : "v"(Wc[0]), "v"(as_bf8(lds_ld16(f1o[0][0]))), "v"(tb0));
+        : "=&v"(acc) : "v"(Wc[0]), "v"(as_bf8(lds_ld16(f1o[0][0]))), "v"(init));
 #pragma unroll
     for (int s = 1; s < 16; ++s)
       asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
@@ -785,21 +808,19 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
   for (; i < c1; i += 4) {
     const int len = lens[i];
     const int inext = min(i + 4, c1 - 1);   // the last caption recomputes itself
-    const f32x16 tb = token_bias(i);
-    const f32x16 tbn = token_bias(inext);
+    const float wn_next = Wnorm[(long long)inext * TPAD + lr];
+    f32x16 initn;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) zp[q] = np[q] = 0.f;
+    for (int q = 0; q < 16; ++q) np[q] = 0.f;
     bf16x8 eb[2];
 #pragma clang loop unroll(full)
-    for (int n = 0; n < 224; ++n) {
+    for (int n = 0; n < FWD_SLOTS; ++n) {
       const FwdSlot sl = fwd_slot(n);
-      // stage / slot-in-stage
-      const int stage = n < 16 ? 0 : n < 176 ? 1 + (n - 16) / 32 : n < 192 ? 6 : 7;
-      const int m = n < 16 ? n : n < 176 ? (n - 16) % 32 : n < 192 ? n - 176 : n - 192;
+      const int stage = sl.stage, m = sl.m;
       // E^T fragments of the tile GEMM2 consumes in this stage
-      const int g2tile = stage - 1;
-      if (stage >= 1 && m == 0) eb[0] = read_e(et + (g2tile & 1) * 2048, 0);
-      if (stage >= 1 && m == (stage == 6 ? 4 : 10)) eb[1] = read_e(et + (g2tile & 1) * 2048, 1);
+      const uint32_t etg = et + ((stage - 1) & 1) * 2048;
+      if (stage >= 1 && m == 0) eb[0] = read_e(etg, 0);
+      if (stage >= 1 && m == (stage == 6 ? 5 : 14)) eb[1] = read_e(etg, 1);
       // ---- the MFMA of this slot
       const u32x4 opnd = rd[n & 3];
       if (sl.kind == 0) {
@@ -808,43 +829,45 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
         if (s == 0) {
           asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3"
               : "=&v"(S[j]) : "v"(w), "v"(__builtin_bit_cast(bf16x8, opnd)),
-                "v"(j == 0 ? tbn : tb));
+                "v"(j == 0 ? initn : init));
         } else {
           asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
               : "+v"(S[j]) : "v"(w), "v"(__builtin_bit_cast(bf16x8, opnd)));
         }
         if (s == 15 && j == 1) mfma_result_wait(S[1]);   // read in the next slot's stage
       } else {
-        const int s = sl.idx >> 3, dt = sl.idx & 7;
-        const bf16x8 a = __builtin_bit_cast(bf16x8, opnd);
+        const int s = g2_s(sl.idx), dt = g2_dt(sl.idx);
+        const bf16x8 a = dt < 8 ? __builtin_bit_cast(bf16x8, opnd) : ones;
         if (sl.tile == 0 && s == 0)
           C[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, eb[0], (f32x16){}, 0, 0, 0);
         else
           C[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, eb[s], C[dt], 0, 0, 0);
       }
       // ---- reads of the slot three ahead (wrapping into the next caption)
-      issue_read(fwd_slot((n + 3) % 224), rd[(n + 3) & 3]);
+      issue_read(fwd_slot((n + 3) % FWD_SLOTS), rd[(n + 3) & 3]);
       // ---- the softmax VALU of this slot
       if (stage <= 6) {
         const int j = stage;                       // softmax tile
         const uint32_t etb = et + (j & 1) * 2048;
         if (stage == 0 || stage == 6) {
-          sm_chunk(2 * m, j, S[j], etb);
-          sm_chunk(2 * m + 1, j, S[j], etb);
-        } else {
+          if (m < 16) {
+            sm_chunk(2 * m, j, S[j], etb);
+            sm_chunk(2 * m + 1, j, S[j], etb);
+          }
+        } else if (m < 32) {
           sm_chunk(m, j, S[j], etb);
         }
       }
-      // the next caption's words, once GEMM1 of tile 6 is issued
-      if (n == 176) load_w(inext);
+      // the next caption's words, once GEMM1 of tile 6 is issued; its GEMM1
+      // initial value once this caption's is dead
+      if (n == 186) load_w(inext);
+      if (n == 190) initn = caption_init(inext, wn_next, c_next);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // ---- Z and N per token: reduce-scatter over the region lanes -> LDS
+    // ---- N per token: reduce-scatter over the region lanes -> LDS
     {
-      const float zr = rs16(zp, lr), nr = rs16(np, lr);
-      const int t = acc_row(rs16_index(lr), h);
-      lds_stf(tok + t * 4, zr);
-      lds_stf(tok + 128 + t * 4, nr);
+      const float nr = rs16(np, lr);
+      lds_stf(tok + acc_row(rs16_index(lr), h) * 4, nr);
     }
     // ---- per-token epilogue (lane t = lr; both halves hold the same token)
     const int t = lr;
@@ -854,8 +877,9 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
 #pragma unroll
       for (int q = 0; q < 16; ++q) csq = fmaf(C[dt][q], C[dt][q], csq);
     csq = xhalf_sum(csq);
-    const float Z = lds_ldf(tok + t * 4);
-    const float nhat = lds_ldf(tok + 128 + t * 4);
+    const float Z = C[8][0];
+    // np sums E * (S' + init) = log2(e) (N - c Z) over the regions
+    const float nhat = lds_ldf(tok + t * 4) * (1.f / L2E) + c_cur * Z;
     const bool tvalid = t < len;
     const float zinv = __builtin_amdgcn_rcpf(Z);
     const float cn = sqrtf(csq) * zinv;
@@ -868,6 +892,8 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     stats[pair * TPAD + t] =
         tvalid ? make_float4(Z, n_, cn, cosv) : make_float4(0.f, 0.f, 0.f, 0.f);
     store_cq<MODE_BF16>(Chi, nullptr, pair, t, h, C);
+    init = initn;
+    c_cur = c_next;
   }
 }
 
@@ -1207,20 +1233,21 @@ extern "C" {
 
 int tgfr_prep_rows(const float* x, long long s_item, long long s_row, long long s_col,
                    int n_items, int n_rows, int n_cols, int rows_pad, const int* lens,
-                   uint16_t* hi, uint16_t* lo, float* norms, void* stream) {
+                   float scale, uint16_t* hi, uint16_t* lo, float* norms, void* stream) {
   if (n_cols != D || n_rows > rows_pad || n_items <= 0) return 1001;
   const int waves = n_items * rows_pad;
   hipLaunchKernelGGL(prep_rows_kernel, dim3((waves + 3) / 4), dim3(256), 0,
                      (hipStream_t)stream, x, s_item, s_row, s_col, n_items, n_rows, rows_pad,
-                     lens, hi, lo, norms);
+                     lens, scale, hi, lo, norms);
   return (int)hipGetLastError();
 }
 
 int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
-                const uint16_t* Wlo, const float* Wnorm, const int* lens, int B_img, int B_cap,
+                const uint16_t* Wlo, const float* Wnorm, const float* Rnorm, const int* lens,
+                int B_img, int B_cap,
                 int img_offset, float gamma1, float gamma2, float gamma3, float eps,
                 float* logits, int ld_logits, float* stats, uint16_t* Chi, uint16_t* Clo,
-                float* att, int att_T, int mode, void* stream) {
+                float* att, int att_T, int bounded, int mode, void* stream) {
   if (B_img <= 0 || B_cap <= 0 || ld_logits < B_cap) return 1001;
   const int grid = ((B_cap + 3) / 4) * B_img;
   auto* s = (hipStream_t)stream;
@@ -1240,10 +1267,10 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
     // R resident in LDS; caption chunks sized for >= ~256 workgroups
     const int n_chunks = max(1, min((B_cap + 3) / 4, (256 + B_img - 1) / B_img));
     static const bool pipe = !getenv("TGFR_WR_FWD_RES");
-    if (pipe && !att && stats && Chi)
+    if (pipe && bounded && Rnorm && !att && stats && Chi)
       hipLaunchKernelGGL(wr_fwd_pipe_kernel, dim3(n_chunks * B_img), dim3(256), FR_LDS, s,
-                         Rhi, Whi, Wnorm, lens, B_img, B_cap, n_chunks, gamma1, gamma2, gamma3,
-                         eps, logits, ld_logits, (float4*)stats, Chi);
+                         Rhi, Whi, Wnorm, Rnorm, lens, B_img, B_cap, n_chunks, gamma1, gamma2,
+                         gamma3, eps, logits, ld_logits, (float4*)stats, Chi);
     else
       hipLaunchKernelGGL(wr_fwd_res_kernel, dim3(n_chunks * B_img), dim3(256), FR_LDS, s,
                          Rhi, Whi, Wnorm, lens, B_img, B_cap, n_chunks, img_offset, gamma1,
@@ -1306,6 +1333,6 @@ int tgfr_wr_lds_bytes(int which) {
   return which == 0 ? F_LDS : which == 1 ? BwdCfg<MODE_SPLIT>::LDS : FR_LDS;
 }
 
-int tgfr_version(void) { return 100; }
+int tgfr_version(void) { return 101; }
 
 }  // extern "C"

@@ -29,10 +29,15 @@ def _mode(mode):
         raise ValueError(f"precision mode must be one of {sorted(MODES)}") from None
 
 
-def prep_rows(x, n_rows, rows_pad, lens=None, want_norms=False):
-    """fp32 [items, rows, 256] (any strides) -> bf16 hi/lo [items, rows_pad, 256].
+LOG2E = 1.4426950408889634
 
-    Rows >= n_rows (or >= lens[item]) are zero.  Optional fp32 row norms.
+
+def prep_rows(x, n_rows, rows_pad, lens=None, want_norms=False, scale=1.0):
+    """fp32 [items, rows, 256] (any strides) -> bf16 hi/lo of scale * x
+    [items, rows_pad, 256].
+
+    Rows >= n_rows (or >= lens[item]) are zero.  Optional fp32 norms of the
+    unscaled rows.
     """
     assert x.dtype == torch.float32 and x.dim() == 3 and x.shape[2] == D
     n_items = x.shape[0]
@@ -42,7 +47,7 @@ def prep_rows(x, n_rows, rows_pad, lens=None, want_norms=False):
         if want_norms else None
     s0, s1, s2 = x.stride()
     call("tgfr_prep_rows", ptr(x), s0, s1, s2, n_items, n_rows, D, rows_pad,
-         ptr(lens), ptr(hi), ptr(lo), ptr(norms), _hip.stream())
+         ptr(lens), float(scale), ptr(hi), ptr(lo), ptr(norms), _hip.stream())
     return hi, lo, norms
 
 
@@ -77,7 +82,7 @@ class WordRegionLogits(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, img_features, words, lens, gamma1, gamma2, gamma3, mode,
-                img_offset=0, att_T=0, eps=1e-8):
+                img_offset=0, att_T=0, bounded=False, eps=1e-8):
         dev = img_features.device
         regions = regions_view(img_features.float())
         b_img, b_cap = regions.shape[0], words.shape[0]
@@ -85,20 +90,26 @@ class WordRegionLogits(torch.autograd.Function):
         if t_words > TPAD:
             raise ValueError(f"at most {TPAD} words per caption (got {t_words})")
         lens = lens.to(device=dev, dtype=torch.int32).contiguous()
-        r_hi, r_lo, _ = prep_rows(regions, NREG, RPAD)
+        m = _mode(mode)
+        bf16 = m == MODES["bf16"]
+        r_hi, r_lo, r_norm = prep_rows(regions, NREG, RPAD, want_norms=bf16)
         w_hi, w_lo, w_norm = prep_rows(words.float(), t_words, TPAD, lens=lens,
                                        want_norms=True)
+        # the bf16 forward takes log2(e)-scaled words (tgfr.h, tgfr_wr_fwd);
+        # the backward the plain ones
+        w_fwd = prep_rows(words.float(), t_words, TPAD, lens=lens,
+                          scale=LOG2E)[0] if bf16 else w_hi
         logits = torch.empty(b_img, b_cap, dtype=torch.float32, device=dev)
         stats = torch.empty(b_img, b_cap, TPAD, 4, dtype=torch.float32, device=dev)
-        m = _mode(mode)
         # C for the backward: bf16 hi (+lo in fp32 mode), chunk-major [pair][32][32][8]
         c_hi = torch.empty(b_img, b_cap, 32, TPAD, 8, dtype=torch.int16, device=dev)
         c_lo = torch.empty_like(c_hi) if m == MODES["fp32"] else None
         att = torch.zeros(b_img, att_T, NREG, dtype=torch.float32, device=dev) \
             if att_T else None
-        call("tgfr_wr_fwd", ptr(r_hi), ptr(r_lo), ptr(w_hi), ptr(w_lo), ptr(w_norm),
-             ptr(lens), b_img, b_cap, img_offset, gamma1, gamma2, gamma3, eps,
-             ptr(logits), b_cap, ptr(stats), ptr(c_hi), ptr(c_lo), ptr(att), att_T, m,
+        call("tgfr_wr_fwd", ptr(r_hi), ptr(r_lo), ptr(w_fwd), ptr(w_lo), ptr(w_norm),
+             ptr(r_norm), ptr(lens), b_img, b_cap, img_offset, gamma1, gamma2, gamma3, eps,
+             ptr(logits), b_cap, ptr(stats), ptr(c_hi), ptr(c_lo), ptr(att), att_T,
+             int(bool(bounded)), m,
              _hip.stream())
         ctx.save_for_backward(r_hi, r_lo, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo)
         ctx.cfg = (gamma1, gamma2, gamma3, eps, m, img_features.shape)
@@ -126,13 +137,16 @@ class WordRegionLogits(torch.autograd.Function):
              _hip.stream())
         # same logical shape as img_features, channels-last strides
         d_img = d_reg.transpose(1, 2).reshape(shape)
-        return (d_img,) + (None,) * 9
+        return (d_img,) + (None,) * 10
 
 
 def word_region_logits(img_features, words, lens, gamma1, gamma2, gamma3,
-                       mode="fp32", img_offset=0, att_T=0):
+                       mode="fp32", img_offset=0, att_T=0, bounded=False):
+    """bounded: the caller guarantees max|W| max|R| < 43 (L2-normalised rows,
+    the BERT path); the bf16 forward then skips the running max."""
     return WordRegionLogits.apply(img_features, words, lens, float(gamma1),
-                                  float(gamma2), float(gamma3), mode, img_offset, att_T)
+                                  float(gamma2), float(gamma3), mode, img_offset, att_T,
+                                  bool(bounded))
 
 
 # ------------------------------------------------------------ cos logits ---

@@ -101,9 +101,13 @@ def words_loss(img_features, words_emb, labels, cap_lens, class_ids, batch_size,
     row_offset, n_global, group = _dist(args)
     smooth = args.TRAIN.SMOOTH
     want_maps = getattr(args, "return_att_maps", True)
+    # BERT-path features are L2-normalised (TextHeading models/models.py:212,
+    # IMIM :403), so the scores are bounded by 1 and the forward needs no
+    # running max over the words
     out = K.word_region_logits(img_features, words, lens, smooth.GAMMA1, smooth.GAMMA2,
                                smooth.GAMMA3, mode=_precision(args), img_offset=row_offset,
-                               att_T=n_words if want_maps else 0)
+                               att_T=n_words if want_maps else 0,
+                               bounded=args.en_type == "BERT")
     logits, att = (out if want_maps else (out, None))
     att_maps = []
     if att is not None:

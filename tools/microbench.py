@@ -19,7 +19,7 @@ def main(b=64, nw=30, mode="fp32", iters=20):
     labels = torch.arange(b, device=dev)
 
     def step():
-        logits = K.word_region_logits(r, w, lens, 4.0, 5.0, 10.0, mode=mode)
+        logits = K.word_region_logits(r, w, lens, 4.0, 5.0, 10.0, mode=mode, bounded=True)
         loss = F.cross_entropy(logits, labels) + F.cross_entropy(logits.t(), labels)
         loss.backward()
         return loss
@@ -47,7 +47,8 @@ def main(b=64, nw=30, mode="fp32", iters=20):
 
 if __name__ == "__main__":
     if "--bf16-only" in sys.argv:
-        main(mode="bf16", iters=3)
+        rest = [a for a in sys.argv[1:] if not a.startswith("--")]
+        main(b=int(rest[0]) if rest else 64, mode="bf16", iters=3)
         sys.exit(0)
     for mode in ("fp32", "bf16"):
         main(mode=mode)

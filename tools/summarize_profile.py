@@ -10,7 +10,7 @@ import sys
 
 # ABI entry point -> kernel name(s) in the trace
 ABI_KERNELS = {"tgfr_wr_bwd": ("wr_bwd_kernel",),
-               "tgfr_wr_fwd": ("wr_fwd_res_kernel", "wr_fwd_kernel")}
+               "tgfr_wr_fwd": ("wr_fwd_pipe_kernel", "wr_fwd_res_kernel", "wr_fwd_kernel")}
 
 
 def main(src, dst):

@@ -73,14 +73,17 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
  * stats and dlogits into tok_ws (B_img*B_cap*32*8 floats).  tgfr_wr_bwd: the
  * fused recompute + both softmax backwards + dR GEMM; writes n_chunks partial
  * slabs [n_chunks][B_img][224][256] (one per caption chunk).  The text side
- * is detached in the reference (utils/dataset_utils.py:42). */
+ * is detached in the reference (utils/dataset_utils.py:42).  bounded = 1
+ * (mode 0 only, after a bounded forward): both calls must pass it, Whi is the
+ * forward's log2(e)-scaled words, and the pipelined kernel runs (no running
+ * max in the softmax recompute). */
 int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const int* lens, int B_img,
-                    int B_cap, float gamma2, float gamma3, float eps, const float* dlogits,
-                    int ld, float* tok_ws, void* stream);
+                    int B_cap, float gamma1, float gamma2, float gamma3, float eps,
+                    const float* dlogits, int ld, int bounded, float* tok_ws, void* stream);
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, int B_img, int B_cap, int n_chunks, float gamma1,
                 const float* tok_ws, const uint16_t* Chi, const uint16_t* Clo, float* slab,
-                int mode, void* stream);
+                int bounded, int mode, void* stream);
 
 /* dR[b][r][d] (caller strides; r < 196) = (+)= sum over chunks of the slabs. */
 int tgfr_wr_reduce(const float* slab, int n_chunks, int B_img, float* out, long long s_b,

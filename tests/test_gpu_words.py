@@ -3,8 +3,11 @@ against the reference fixtures and the CPU oracle.
 
 Tolerances: fp32 mode (split-bf16 MFMA) must meet the north-star bar of
 1e-3 absolute on logits and losses with identical row/column argmax; the
-bf16 mode is the perf mode and is held to 5e-2 on logits (documented in
-DESIGN.md).  Region gradients are compared relative to their max magnitude.
+bf16 mode is the perf mode: its operands carry 2^-9 relative rounding, which
+the logit gamma3 * log sum exp(gamma2 cos) amplifies by ~gamma2 * gamma3 = 50,
+so it is held to 5e-2 on the reference fixtures and 1e-1 on random unit
+vectors (documented in DESIGN.md).  Region gradients are compared relative
+to their max magnitude.
 """
 import numpy as np
 import pytest
@@ -22,7 +25,7 @@ def _kernels():
     return kernels
 
 
-def _run(g, dev, mode):
+def _run(g, dev, mode, bounded=False):
     K = _kernels()
     r = t(g["img_features"]).to(dev).requires_grad_()
     w = t(g["words_emb"]).to(dev)
@@ -34,8 +37,13 @@ def _run(g, dev, mode):
         nw = int(g["bert_words_num"]) - 2
         lens = torch.full((b,), nw, dtype=torch.int32)
         words = K.words_view(w, nw)
-    logits, att = K.word_region_logits(r, words, lens, 4.0, 5.0, 10.0, mode=mode,
-                                       att_T=words.shape[1])
+    if bounded:     # the pipelined kernels (no attention maps)
+        logits = K.word_region_logits(r, words, lens, 4.0, 5.0, 10.0, mode=mode,
+                                      bounded=True)
+        att = torch.zeros(0)
+    else:
+        logits, att = K.word_region_logits(r, words, lens, 4.0, 5.0, 10.0, mode=mode,
+                                           att_T=words.shape[1])
     labels = torch.arange(b, device=dev)
     l0 = F.cross_entropy(logits, labels)
     l1 = F.cross_entropy(logits.t(), labels)
@@ -73,8 +81,47 @@ def test_words_bf16_vs_golden(gpu, tag):
     assert err < 3e-2, err
 
 
+@pytest.mark.parametrize("tag", ["bert_b4_t30", "bert_b6_t22"])
+def test_words_bf16_bounded_vs_golden(gpu, tag):
+    """The pipelined bf16 kernels (bounded scores: the BERT path's unit-norm
+    features) against the reference fixtures."""
+    g = load_golden(f"words_loss_{tag}")
+    logits, l0, l1, _, dr = _run(g, gpu, "bf16", bounded=True)
+    np.testing.assert_allclose(logits.numpy(), g["logits"], atol=5e-2, rtol=0)
+    assert abs(l0 - float(g["loss0"])) < 5e-2 and abs(l1 - float(g["loss1"])) < 5e-2
+    scale = np.abs(g["d_img"]).max()
+    err = np.abs(dr.numpy() - g["d_img"]).max() / scale
+    assert err < 3e-2, err
+
+
 def _unit(x):
     return x / x.norm(dim=-1, keepdim=True)
+
+
+@pytest.mark.parametrize("b_img,b_cap,nw", [(9, 13, 30), (16, 16, 22), (3, 40, 7),
+                                            (64, 100, 30)])
+def test_words_bf16_bounded_vs_oracle_shapes(gpu, b_img, b_cap, nw):
+    """Pipelined bf16 kernels on ragged grids (caption chunks of 1..many per
+    wave, pipeline fill/drain stages) against the fp32 oracle."""
+    K = _kernels()
+    torch.manual_seed(11 + b_img)
+    r = _unit(torch.randn(b_img, 14, 14, 256)).permute(0, 3, 1, 2)
+    w = _unit(torch.randn(b_cap, nw, 256)).transpose(1, 2)
+    ro = r.clone().requires_grad_()
+    _, _, _, ref = O.words_loss(ro, w, None, None, nw, 4.0, 5.0, 10.0, batch_size=b_cap)
+    probe = torch.randn(b_img, b_cap)
+    (ref * probe).sum().backward()
+    rg = r.to(gpu).requires_grad_()
+    logits = K.word_region_logits(rg, K.words_view(w.to(gpu), nw),
+                                  torch.full((b_cap,), nw, dtype=torch.int32),
+                                  4.0, 5.0, 10.0, mode="bf16", bounded=True)
+    (logits * probe.to(gpu)).sum().backward()
+    got = logits.detach().cpu()
+    assert torch.isfinite(got).all() and torch.isfinite(rg.grad).all()
+    np.testing.assert_allclose(got.numpy(), ref.detach().numpy(), atol=1e-1, rtol=0)
+    scale = ro.grad.abs().max().item()
+    err = (rg.grad.cpu() - ro.grad).abs().max().item() / scale
+    assert err < 3e-2, err
 
 
 @pytest.mark.parametrize("b_img,b_cap,nw", [(9, 13, 30), (16, 16, 22), (3, 40, 7)])

@@ -575,8 +575,8 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
 //   stage 1..5  GEMM1(tile j+1) and GEMM2(tile j-1)    | softmax(tile j)
 //   stage 6     GEMM2(tile 5)                          | softmax(tile 6)
 //   stage 7     GEMM2(tile 6) and the NEXT caption's GEMM1(tile 0)
-// GEMM1 = S'^T = init + W' R^T (16 MFMAs per tile, inline asm, VGPR results
-// read by the softmax); GEMM2 = C^T += R^T E^T (16 per tile) plus Z^T +=
+// GEMM1 = S'^T = init + W' R^T (16 MFMAs per tile, results read by the
+// softmax); GEMM2 = C^T += R^T E^T (16 per tile) plus Z^T +=
 // 1^T E^T (2 per tile: the softmax-2 denominators come out of the matrix
 // core, no per-element adds or cross-lane sums), accumulators in AGPRs.
 // Every slot issues the LDS reads of the slot three ahead (R rows / R^T
@@ -792,14 +792,11 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
   load_w(i);
   f32x16 S[7];           // S[j]: GEMM1 result of tile j (two live at a time)
   {
-    f32x16 acc;
-    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3"
-        : "=&v"(acc) : "v"(Wc[0]), "v"(as_bf8(lds_ld16(f1o[0][0]))), "v"(init));
+    f32x16 acc = init;
 #pragma unroll
-    for (int s = 1; s < 16; ++s)
-      asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
-          : "+v"(acc) : "v"(Wc[s]), "v"(as_bf8(lds_ld16(f1o[s >> 3][s & 7]))));
-    mfma_result_wait(acc);
+    for (int s = 0; s < 16; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Wc[s], as_bf8(lds_ld16(f1o[s >> 3][s & 7])),
+                                                    acc, 0, 0, 0);
     S[0] = acc;
   }
 #pragma unroll
@@ -824,17 +821,12 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
       // ---- the MFMA of this slot
       const u32x4 opnd = rd[n & 3];
       if (sl.kind == 0) {
+        // builtins (not inline asm): the compiler's hazard recognizer then
+        // places the VALU-write -> MFMA-read and MFMA -> VALU-read waits
         const int s = sl.idx, j = sl.tile;
-        const bf16x8 w = Wc[s];
-        if (s == 0) {
-          asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3"
-              : "=&v"(S[j]) : "v"(w), "v"(__builtin_bit_cast(bf16x8, opnd)),
-                "v"(j == 0 ? initn : init));
-        } else {
-          asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
-              : "+v"(S[j]) : "v"(w), "v"(__builtin_bit_cast(bf16x8, opnd)));
-        }
-        if (s == 15 && j == 1) mfma_result_wait(S[1]);   // read in the next slot's stage
+        S[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            Wc[s], __builtin_bit_cast(bf16x8, opnd), s == 0 ? (j == 0 ? initn : init) : S[j],
+            0, 0, 0);
       } else {
         const int s = g2_s(sl.idx), dt = g2_dt(sl.idx);
         const bf16x8 a = dt < 8 ? __builtin_bit_cast(bf16x8, opnd) : ones;
@@ -844,7 +836,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
           C[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, eb[s], C[dt], 0, 0, 0);
       }
       // ---- reads of the slot three ahead (wrapping into the next caption)
-      issue_read(fwd_slot((n + 3) % FWD_SLOTS), rd[(n + 3) & 3]);
+      issue_read(fwd_slot((n + 3) % FWD_SLOTS), rd[((n + 3) % FWD_SLOTS) & 3]);
       // ---- the softmax VALU of this slot
       if (stage <= 6) {
         const int j = stage;                       // softmax tile
@@ -902,15 +894,18 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
 //   dcos_t = g3 * dlogit * g2 * softmax_t(g2 cos)            (losses.py:107-122)
 //   dC_t   = alpha_t W_t + beta_t C_t                          (d cos / d C_t)
 //   sigma_t = sum_r A2[t,r] dA2[t,r] = dC_t . C_t               (softmax-2 bwd)
-// stored as 8 floats {1/Z, alpha, beta/Z, sigma, valid, 0, 0, 0} (beta/Z: the
-// forward stores C-hat = Z C) so one 1-KiB global_load_lds stages a caption's
-// table.
+// stored (layout 0) as 8 floats {1/Z, alpha, beta/Z, sigma, valid, 0, 0, 0}
+// per token (beta/Z: the forward stores C-hat = Z C), or (layout 1, for
+// wr_bwd_pipe_kernel) as 8 scalar rows of 32 tokens with gamma1, 1/Z and
+// log2(e) folded in (see there); either way one 1-KiB global_load_lds stages
+// a caption's table.
 __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ stats,
                                                      const float* __restrict__ Wnorm,
                                                      const int* __restrict__ lens,
                                                      const float* __restrict__ dlogits, int ld,
-                                                     int B_img, int B_cap, float g2, float g3,
-                                                     float eps, float* __restrict__ tok) {
+                                                     int B_img, int B_cap, float g1, float g2,
+                                                     float g3, float eps, int layout,
+                                                     float* __restrict__ tok) {
   const long long pair = (blockIdx.x * 256LL + threadIdx.x) / WAVE;
   if (pair >= (long long)B_img * B_cap) return;
   const int b = pair / B_cap, i = pair % B_cap;
@@ -934,11 +929,32 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
       alpha = dcos / eps;
       beta = 0.f;
     }
-    o[0] = 1.f / st.x;
-    o[1] = alpha;
-    o[2] = beta * o[0];     // applied to C-hat = Z C (store_cq)
-    o[3] = alpha * n + beta * cn * cn;
-    o[4] = 1.f;
+    const float sigma = alpha * n + beta * cn * cn;
+    const float iz = 1.f / st.x;
+    if (layout == 0) {
+      o[0] = iz;
+      o[1] = alpha;
+      o[2] = beta * iz;       // applied to C-hat = Z C (store_cq)
+      o[3] = sigma;
+      o[4] = 1.f;
+    } else {
+      // wr_bwd_pipe_kernel: scores S' = log2(e) S, rows W' = log2(e) W, C-hat
+      constexpr float L2E = 1.4426950408889634f;
+      o[0] = g1 * iz / L2E;             // E -> g1 A2 / log2e
+      o[1] = alpha / L2E;               // coefficient of S' in dA2
+      o[2] = beta * iz;                 // coefficient of Q-hat in dA2
+      o[3] = sigma;
+      o[4] = alpha / g1;                // M_w = dS / log2e + o4 * (g1 A2 / log2e)
+      o[5] = beta * iz * L2E / g1;      // M_c = o5 * (g1 A2 / log2e)
+    }
+  }
+  if (layout != 0) {
+    o[6] = valid ? 0.f : -1e30f;        // G1's initial value row (word bias)
+    if ((threadIdx.x % WAVE) < 32) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) tok[pair * 256 + k * 32 + t] = o[k];
+    }
+    return;
   }
   if ((threadIdx.x % WAVE) < 32) {
     float4* dst = (float4*)(tok + (pair * TPAD + t) * 8);
@@ -1204,6 +1220,260 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
     for (int q = 0; q < 16; ++q) dst[acc_row(q, h) * D + dt * 32 + lr] = dR[dt][q];
 }
 
+// -------------------------------------------- bwd, bf16, bounded, pipelined ---
+// Backward of wr_fwd_pipe_kernel (bf16 mode, bounded scores, log2(e)-scaled
+// words W').  Same work split and slab output as wr_bwd_kernel: workgroup =
+// (image, 4 region tiles, caption chunk), one wave per 32-region tile; the
+// wave's R tile is held as MFMA B fragments in registers.  Per caption:
+//   G1  [S'^T ; Q-hat^T] = [W' ; C-hat] R_tile^T        32 MFMAs (asm, VGPRs)
+//   SM  softmax-1 recompute (p = exp2(S'); no max: the scores are bounded)
+//       and both softmax backwards, per lane (tokens in registers, the
+//       region on the lane); the per-token scalars of wr_tok_kernel's
+//       bounded layout fold gamma1, 1/Z and log2(e), so an element costs
+//       2 exp2 + 13 VALU
+//   G3  dR_tile += [M_w | M_c] [W' ; C-hat]             32 MFMAs (AGPRs)
+// Captions run as a software pipeline: stage t issues G1 of caption t+1 and
+// G3 of caption t-1 alternately (64 MFMA slots, order fixed in the source,
+// LDS reads three slots ahead) while SM of caption t runs in their issue
+// gaps.  X images ([W'; C-hat] + token table) stream through a 4-deep LDS
+// ring by LDS DMA issued two captions ahead; one barrier per stage.
+// Captions past the chunk read a zero token table: their M fragments are
+// zero, so the fill / drain stages need no branches.
+constexpr int BP_NB = 4;                       // ring depth
+constexpr int BP_TOK = 1024;                   // token table bytes
+constexpr int BP_BUF = B_XIMG + BP_TOK;        // one caption: X image + table
+constexpr int BP_ZERO = BP_NB * BP_BUF;        // a zero token table
+constexpr int BP_LDS = BP_ZERO + BP_TOK;
+
+__global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
+    const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi, int B_img, int B_cap,
+    int n_chunks, float g1, const float* __restrict__ tok, const uint16_t* __restrict__ Chi,
+    float* __restrict__ slab) {
+  const int total = n_chunks * 2 * B_img;
+  const int work = xcd_remap(blockIdx.x, total);
+  const int b = work / (2 * n_chunks);
+  const int rem = work % (2 * n_chunks);
+  const int tg = rem / n_chunks, chunk = rem % n_chunks;
+  const int per = (B_cap + n_chunks - 1) / n_chunks;
+  const int c0 = chunk * per, c1 = min(B_cap, c0 + per);
+  const int K = max(0, c1 - c0);
+  const int tid = threadIdx.x, lane = tid % WAVE;
+  const int wid = __builtin_amdgcn_readfirstlane(tid / WAVE);
+  const int lr = lane & 31, h = lane >> 5;
+  const int rt = tg * 4 + wid;                 // region tile (7: padding only)
+  const int g16 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const float gL = g1 * 1.4426950408889634f;
+
+  // zero the ring (the first G3 reads an empty buffer) and the zero table
+  for (int o = tid * 16; o < BP_LDS; o += 256 * 16) lds_st16(o, make_uint4(0, 0, 0, 0));
+  // R tile as B fragments: lane (r, h), k-step s -> d = 16 s + 8 h .. + 7
+  bf16x8 Rf[16];
+  {
+    const long long roff = ((long long)b * RPAD + min(rt, NRT - 1) * 32 + lr) * D;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) Rf[s] = as_bf8(*(const uint4*)(Rhi + roff + s * 16 + h * 8));
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  auto stage_dma = [&](int k) {     // caption c0 + k -> ring slot k % 4
+    if (k < K)
+      bwd_stage<MODE_BF16>((k % BP_NB) * BP_BUF, Whi, nullptr, Chi, nullptr, tok,
+                           (long long)b * B_cap + c0 + k, c0 + k, wid, lane);
+  };
+  stage_dma(0);
+  stage_dma(1);
+
+  // per-lane parts of the swizzled X-image addresses (xoff), as wr_bwd_kernel
+  uint32_t g1o[8], g2o[2][4];
+  {
+    const int sw1 = ((lr & 3) << 2) | ((lr >> 2) & 3);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g1o[k] = lr * 256 + (((2 * k + h) ^ sw1) << 4);
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd)
+        g2o[bb][dd] = (4 * h + q4 + 8 * bb) * 256 + ((dd ^ q4) << 6) +
+                      (((2 * (g16 & 1) + (p4 >> 1)) ^ ((h + 2 * bb) & 3)) << 4) + (p4 & 1) * 8;
+  }
+
+  f32x16 dR[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dR[j][q] = 0.f;
+
+  // G1 operand read u (0..15 W' rows, 16..31 C-hat rows) of the image at xb
+  auto g1_read = [&](int u, uint32_t xb) {
+    const int s = u & 15;
+    return __builtin_bit_cast(
+        u32x4, lds_ld16(xb + g1o[s & 7] + (s >> 3) * (64 * 256) + (u >= 16 ? 32 * 256 : 0)));
+  };
+  // G3 operand read u: d tile dt = u >> 2, k block ks = u & 3
+  auto g3_read = [&](int u, uint32_t xb) {
+    const int dt = u >> 2, ks = u & 3;
+    const uint32_t kb = xb + (dt >> 2) * (64 * 256) + ((ks >> 1) * 32 + (ks & 1) * 16) * 256;
+    return __builtin_bit_cast(u32x4, join_tr(lds_tr4(kb + g2o[0][dt & 3]),
+                                             lds_tr4(kb + g2o[1][dt & 3])));
+  };
+  // (builtins, not inline asm: the operands are produced by VALU ops -- AGPR
+  // reads, register moves -- right before, and only the compiler's hazard
+  // recognizer inserts the VALU-write -> MFMA-read wait states)
+  auto g1_mfma = [&](int u, const u32x4& op, f32x16& A0, f32x16& A1, const f32x16& init) {
+    const bf16x8 x = __builtin_bit_cast(bf16x8, op);
+    const int s = u & 15;
+    if (u < 16)
+      A0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, Rf[s], s == 0 ? init : A0, 0, 0, 0);
+    else
+      A1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, Rf[s], s == 0 ? (f32x16){} : A1, 0, 0,
+                                                   0);
+  };
+  // token scalar k for the lane's tokens 8g + 4h + 0..3 (q = 4g .. 4g+3)
+  auto scal = [&](uint32_t tb, int k, int g) {
+    return __builtin_bit_cast(u32x4, lds_ld16(tb + k * 128 + g * 32 + h * 16));
+  };
+  auto init_of = [&](uint32_t tb) {   // the token-bias row (scalar 6) as G1's init
+    f32x16 r;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const u32x4 x = scal(tb, 6, g);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[4 * g + k] = __uint_as_float(x[k]);
+    }
+    return r;
+  };
+
+  // softmax state of the caption in SM
+  float p[16], a1[16], ax[16], v[16];
+  float s8[8], inv = 0.f, kq = 0.f, rho = 0.f;
+  u32x4 fb[2][4], fc[2][2];     // scalars f0..f3 (phase B) / f4, f5 (phase C), by group parity
+  uint32_t mw2[8], mc2[8];
+  auto fl = [](const u32x4& x, int q) { return __uint_as_float(x[q & 3]); };
+  // SM chunk c (0..63) of the caption with token table tb and G1 results A0, A1;
+  // its M fragments go to Mo
+  auto sm_chunk = [&](int c, uint32_t tb, const f32x16& A0, const f32x16& A1, bf16x8* Mo) {
+    // scalar prefetch: f0..f3 of group g four chunks before its phase-B span
+    // (13 + 8g), f4, f5 three chunks before its phase-C span (46 + 4g)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (c == 9 + 8 * g)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) fb[g & 1][k] = scal(tb, k, g);
+      if (c == 43 + 4 * g) {
+        fc[g & 1][0] = scal(tb, 4, g);
+        fc[g & 1][1] = scal(tb, 5, g);
+      }
+    }
+    if (c < 8) {                  // phase A: p = exp2(S') (bias rows: 0)
+      p[2 * c] = __builtin_amdgcn_exp2f(A0[2 * c]);
+      p[2 * c + 1] = __builtin_amdgcn_exp2f(A0[2 * c + 1]);
+    } else if (c == 8) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s8[k] = p[k] + p[k + 8];
+    } else if (c == 9) {
+#pragma unroll
+      for (int k = 4; k < 8; ++k) s8[k] = p[k] + p[k + 8];
+    } else if (c == 10) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s8[k] += s8[k + 4];
+    } else if (c == 11) {
+      inv = xhalf_sum((s8[0] + s8[1]) + (s8[2] + s8[3]));
+    } else if (c == 12) {
+      inv = __builtin_amdgcn_rcpf(inv);
+      kq = gL * inv;
+      rho = 0.f;
+    } else if (c < 45) {          // phase B, two chunks per token q
+      const int q = (c - 13) >> 1, g = q >> 2;
+      const u32x4* f = fb[g & 1];
+      if (((c - 13) & 1) == 0) {
+        a1[q] = p[q] * inv;                                   // A1
+        ax[q] = __builtin_amdgcn_exp2f(p[q] * kq) * fl(f[0], q);   // g1 A2 / log2e
+      } else {
+        // (dA2 - sigma) = (alpha / log2e) S' + (beta / Z) Q-hat - sigma
+        const float du = fmaf(fl(f[1], q), A0[q], fmaf(fl(f[2], q), A1[q], -fl(f[3], q)));
+        v[q] = a1[q] * (ax[q] * du);                         // A1 dA1 / log2e
+        rho += v[q];
+      }
+    } else if (c == 45) {
+      rho = xhalf_sum(rho);
+    } else if (c < 62) {          // phase C, one chunk per token q
+      const int q = c - 46, g = q >> 2;
+      const u32x4* f = fc[g & 1];
+      const float dsx = fmaf(-a1[q], rho, v[q]);              // dS / log2e
+      p[q] = fmaf(fl(f[0], q), ax[q], dsx);                   // M_w (scaled for W')
+      s8[q & 7] = fl(f[1], q) * ax[q];                        // M_c (for C-hat)
+      if (q & 1) {
+        mw2[q >> 1] = pk_bf16(p[q - 1], p[q]);
+        mc2[q >> 1] = pk_bf16(s8[(q - 1) & 7], s8[q & 7]);
+      }
+      if (q == 15) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          Mo[k] = __builtin_bit_cast(bf16x8, make_uint4(mw2[4 * k], mw2[4 * k + 1],
+                                                          mw2[4 * k + 2], mw2[4 * k + 3]));
+          Mo[2 + k] = __builtin_bit_cast(bf16x8, make_uint4(mc2[4 * k], mc2[4 * k + 1],
+                                                              mc2[4 * k + 2], mc2[4 * k + 3]));
+        }
+      }
+    }
+  };
+
+  // one pipeline stage t: G1(t+1) -> (A0n, A1n), SM(t) on (A0, A1) -> Mo,
+  // G3(t-1) with Mi
+  auto stage = [&](int t, f32x16& A0, f32x16& A1, f32x16& A0n, f32x16& A1n,
+                   const bf16x8* Mi, bf16x8* Mo) {
+    ring_barrier<0>();                 // X(t+1) landed everywhere; X(t-2) retired
+    stage_dma(t + 2);
+    const uint32_t x1 = ((t + 1) % BP_NB) * BP_BUF;          // G1 image
+    const uint32_t x3 = ((t + 3) % BP_NB) * BP_BUF;          // G3 image (t-1)
+    const uint32_t tbs = t < K ? (t % BP_NB) * BP_BUF + B_XIMG : BP_ZERO;
+    const uint32_t tb1 = x1 + B_XIMG;
+    const f32x16 init = init_of(tb1);
+    u32x4 rd[4];
+    // slot n: even -> G1 MFMA n/2, odd -> G3 MFMA n/2
+    auto read = [&](int n) { return (n & 1) ? g3_read(n >> 1, x3) : g1_read(n >> 1, x1); };
+#pragma unroll
+    for (int n = 0; n < 3; ++n) rd[n] = read(n);
+#pragma clang loop unroll(full)
+    for (int n = 0; n < 64; ++n) {
+      const u32x4 op = rd[n & 3];
+      if (n & 1) {
+        const int u = n >> 1, ks = u & 3;
+        dR[u >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            Mi[ks], __builtin_bit_cast(bf16x8, op), dR[u >> 2], 0, 0, 0);
+      } else {
+        g1_mfma(n >> 1, op, A0n, A1n, init);
+      }
+      if (n + 3 < 64) rd[(n + 3) & 3] = read(n + 3);
+      sm_chunk(n, tbs, A0, A1, Mo);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // ---- prologue: G1 of caption 0
+  f32x16 Aa0, Aa1, Ab0, Ab1;
+  bf16x8 Ma[4], Mb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) Ma[k] = Mb[k] = as_bf8(make_uint4(0, 0, 0, 0));
+  {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const f32x16 init = init_of(B_XIMG);
+#pragma unroll
+    for (int u = 0; u < 32; ++u) g1_mfma(u, g1_read(u, 0), Aa0, Aa1, init);
+  }
+  const int T2 = (K + 2) & ~1;         // stages 0..K, padded to even
+  for (int t = 0; t < T2; t += 2) {
+    stage(t, Aa0, Aa1, Ab0, Ab1, Ma, Mb);
+    stage(t + 1, Ab0, Ab1, Aa0, Aa1, Mb, Ma);
+  }
+  if (rt >= NRT) return;
+  float* dst = slab + (((long long)chunk * B_img + b) * RPAD + rt * 32) * D;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dst[acc_row(q, h) * D + dt * 32 + lr] = dR[dt][q];
+}
+
 __global__ __launch_bounds__(256) void wr_reduce_kernel(const float* __restrict__ slab,
                                                         int n_chunks, int B_img,
                                                         float* __restrict__ out, long long s_b,
@@ -1283,21 +1553,33 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
 }
 
 int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const int* lens, int B_img,
-                    int B_cap, float gamma2, float gamma3, float eps, const float* dlogits,
-                    int ld, float* tok_ws, void* stream) {
+                    int B_cap, float gamma1, float gamma2, float gamma3, float eps,
+                    const float* dlogits, int ld, int bounded, float* tok_ws, void* stream) {
   if (B_img <= 0 || B_cap <= 0 || ld < B_cap) return 1001;
   const long long pairs = (long long)B_img * B_cap;
   hipLaunchKernelGGL(wr_tok_kernel, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
                      (hipStream_t)stream, (const float4*)stats, Wnorm, lens, dlogits, ld, B_img,
-                     B_cap, gamma2, gamma3, eps, tok_ws);
+                     B_cap, gamma1, gamma2, gamma3, eps, bounded ? 1 : 0, tok_ws);
   return (int)hipGetLastError();
 }
 
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, int B_img, int B_cap, int n_chunks, float gamma1,
                 const float* tok_ws, const uint16_t* Chi, const uint16_t* Clo, float* slab,
-                int mode, void* stream) {
+                int bounded, int mode, void* stream) {
   if (B_img <= 0 || B_cap <= 0 || n_chunks <= 0 || n_chunks > B_cap) return 1001;
+  if (bounded) {
+    if (mode != MODE_BF16) return 1002;
+    static bool once_p = [] {
+      allow_lds(wr_bwd_pipe_kernel, BP_LDS);
+      return true;
+    }();
+    (void)once_p;
+    hipLaunchKernelGGL(wr_bwd_pipe_kernel, dim3(n_chunks * 2 * B_img), dim3(256), BP_LDS,
+                       (hipStream_t)stream, Rhi, Whi, B_img, B_cap, n_chunks, gamma1, tok_ws,
+                       Chi, slab);
+    return (int)hipGetLastError();
+  }
   if (mode == MODE_SPLIT && (!Rlo || !Wlo || !Clo)) return 1001;
   auto* s = (hipStream_t)stream;
   static bool once = [] {

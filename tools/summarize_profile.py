@@ -9,7 +9,7 @@ import os
 import sys
 
 # ABI entry point -> kernel name(s) in the trace
-ABI_KERNELS = {"tgfr_wr_bwd": ("wr_bwd_kernel",),
+ABI_KERNELS = {"tgfr_wr_bwd": ("wr_bwd_pipe_kernel", "wr_bwd_kernel"),
                "tgfr_wr_fwd": ("wr_fwd_pipe_kernel", "wr_fwd_res_kernel", "wr_fwd_kernel")}
 
 
@@ -32,8 +32,8 @@ def main(src, dst):
         rows = csv.DictReader(open(os.path.join(src, name, "bench_counter_collection.csv")))
         acc = collections.defaultdict(list)
         for r in rows:
-            for tag in ("wr_fwd_res_kernel", "wr_fwd_kernel", "wr_bwd_kernel", "wr_reduce_kernel",
-                        "prep_rows_kernel"):
+            for tag in ("wr_fwd_pipe_kernel", "wr_bwd_pipe_kernel", "wr_fwd_res_kernel",
+                        "wr_fwd_kernel", "wr_bwd_kernel", "wr_reduce_kernel", "prep_rows_kernel"):
                 if tag in r["Kernel_Name"]:
                     acc[tag].append(float(r["Counter_Value"]))
         for k, v in acc.items():

@@ -22,7 +22,9 @@
  *   - bf16 buffers are uint16_t bit patterns.
  *   - Feature dim D is 256 (aux_feat_dim_per_granularity, cfg/train_bert.yml:28);
  *     regions R = 196 (14x14, padded to 224 in the split images); words per
- *     caption T <= 32.
+ *     caption T <= t_pad, t_pad = 32 or 64 (64-token captions, T = 62): the
+ *     token stride of every words / stats / C / token-table buffer.  t_pad =
+ *     64 runs the general (running-max) kernels, bounded must be 0.
  */
 #ifndef TGFR_H
 #define TGFR_H
@@ -66,7 +68,7 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 int B_img, int B_cap,
                 int img_offset, float gamma1, float gamma2, float gamma3, float eps,
                 float* logits, int ld_logits, float* stats, uint16_t* Chi, uint16_t* Clo,
-                float* att, int att_T, int bounded, int mode, void* stream);
+                float* att, int att_T, int bounded, int t_pad, int mode, void* stream);
 
 /* Backward of tgfr_wr_fwd w.r.t. the image regions given dL/dlogits, in two
  * launches.  tgfr_wr_bwd_tok: per-(pair, token) scalars from the forward
@@ -79,11 +81,12 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
  * max in the softmax recompute). */
 int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const int* lens, int B_img,
                     int B_cap, float gamma1, float gamma2, float gamma3, float eps,
-                    const float* dlogits, int ld, int bounded, float* tok_ws, void* stream);
+                    const float* dlogits, int ld, int bounded, int t_pad, float* tok_ws,
+                    void* stream);
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, int B_img, int B_cap, int n_chunks, float gamma1,
                 const float* tok_ws, const uint16_t* Chi, const uint16_t* Clo, float* slab,
-                int bounded, int mode, void* stream);
+                int bounded, int t_pad, int mode, void* stream);
 
 /* dR[b][r][d] (caller strides; r < 196) = (+)= sum over chunks of the slabs. */
 int tgfr_wr_reduce(const float* slab, int n_chunks, int B_img, float* out, long long s_b,

@@ -147,3 +147,49 @@ def test_words_fp32_vs_oracle_shapes(gpu, b_img, b_cap, nw):
     scale = ro.grad.abs().max().item()
     err = (rg.grad.cpu() - ro.grad).abs().max().item() / scale
     assert err < 2e-3, err
+
+
+@pytest.mark.parametrize("mode,b_img,b_cap,nw", [("fp32", 3, 5, 62), ("fp32", 8, 11, 50),
+                                                 ("bf16", 3, 5, 62), ("bf16", 9, 21, 62)])
+def test_words_64_token_captions_vs_oracle(gpu, mode, b_img, b_cap, nw):
+    """64-token captions (BASELINE configs[4], bert_words_num = 64 -> T = 62):
+    the two-tile kernels (t_pad = 64) against the fp32 oracle."""
+    K = _kernels()
+    torch.manual_seed(5 + nw)
+    r = _unit(torch.randn(b_img, 14, 14, 256)).permute(0, 3, 1, 2)
+    w = _unit(torch.randn(b_cap, nw, 256)).transpose(1, 2)
+    ro = r.clone().requires_grad_()
+    _, _, _, ref = O.words_loss(ro, w, None, None, nw, 4.0, 5.0, 10.0, batch_size=b_cap)
+    probe = torch.randn(b_img, b_cap)
+    (ref * probe).sum().backward()
+    rg = r.to(gpu).requires_grad_()
+    logits = K.word_region_logits(rg, K.words_view(w.to(gpu), nw),
+                                  torch.full((b_cap,), nw, dtype=torch.int32),
+                                  4.0, 5.0, 10.0, mode=mode, bounded=True)
+    (logits * probe.to(gpu)).sum().backward()
+    got = logits.detach().cpu()
+    assert torch.isfinite(got).all() and torch.isfinite(rg.grad).all()
+    tol, gtol = (1e-3, 2e-3) if mode == "fp32" else (1e-1, 3e-2)
+    np.testing.assert_allclose(got.numpy(), ref.detach().numpy(), atol=tol, rtol=0)
+    if mode == "fp32":
+        assert (got.argmax(1) == ref.argmax(1)).all() and (got.argmax(0) == ref.argmax(0)).all()
+    err = (rg.grad.cpu() - ro.grad).abs().max().item() / ro.grad.abs().max().item()
+    assert err < gtol, err
+
+
+def test_words_loss_64_token_captions_attention_maps(gpu):
+    """words_loss through the drop-in API with bert_words_num = 64: losses and
+    the matching-pair attention maps against the oracle (fp32 mode)."""
+    from text_guided_face_recognition_amd.config import make_args
+    from text_guided_face_recognition_amd.models import losses as L
+    torch.manual_seed(2)
+    b, nw = 4, 62
+    r = _unit(torch.randn(b, 14, 14, 256)).permute(0, 3, 1, 2)
+    w = _unit(torch.randn(b, nw + 2, 256)).transpose(1, 2)
+    args = make_args(bert_words_num=64, precision="fp32")
+    labels = torch.arange(b)
+    l0, l1, maps, _ = O.words_loss(r.clone(), w, labels, None, nw, 4.0, 5.0, 10.0)
+    g0, g1, gmaps = L.words_loss(r.to(gpu), w.to(gpu), labels.to(gpu), None, None, b, args)
+    assert abs(g0.item() - l0.item()) < 1e-3 and abs(g1.item() - l1.item()) < 1e-3
+    for gm, om in zip(gmaps, maps):
+        np.testing.assert_allclose(gm.cpu().numpy(), om.detach().numpy(), atol=1e-4)

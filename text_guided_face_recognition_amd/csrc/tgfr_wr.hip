@@ -82,6 +82,8 @@ constexpr int F_ET = 2 * 32 * 64;                   // per-wave E^T tile hi+lo
 constexpr int F_OFF_ET = 2 * F_STAGE;
 constexpr int F_OFF_TOK = F_OFF_ET + 4 * F_ET;      // per-wave Z[32], N[32]
 constexpr int F_LDS = F_OFF_TOK + 4 * 64 * 4;
+constexpr int F_OFF_XS = F_LDS;                     // TT = 2 exchange: [wave][7][32]
+constexpr int F_LDS2 = F_OFF_XS + 4 * NRT * 32 * 4;
 constexpr int F_NCHUNK = 8 + NRT;                   // 8 d-chunks + 7 region chunks
 constexpr int F_PIECES = 8;                         // 16-B pieces per thread per chunk
 
@@ -142,7 +144,7 @@ __device__ __forceinline__ void fwd_store_chunk(const StageRegs& s, int c, int b
 // 1/Z into its per-token scalars (wr_tok_kernel), so no per-element scaling
 // here.  Rows of padding tokens are whatever the kernel's E gives them
 // (finite); the backward multiplies them by zero scalars.
-template <int MODE>
+template <int MODE, int TPS = TPAD>
 __device__ __forceinline__ void store_cq(uint16_t* Chi, uint16_t* Clo, long long pair, int t,
                                          int h, const f32x16* C) {
 #pragma unroll
@@ -155,14 +157,20 @@ __device__ __forceinline__ void store_cq(uint16_t* Chi, uint16_t* Clo, long long
         if constexpr (MODE == MODE_SPLIT) split2(C[dt][4 * g + k], hh[k], ll[k]);
         else hh[k] = bf_bits(C[dt][4 * g + k]);
       }
-      const long long o = ((pair * 32 + (4 * dt + g)) * 32 + t) * 8 + 4 * h;
+      const long long o = ((pair * 32 + (4 * dt + g)) * TPS + t) * 8 + 4 * h;
       *(uint2*)(Chi + o) = make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3]));
       if (MODE == MODE_SPLIT)
         *(uint2*)(Clo + o) = make_uint2(pack2(ll[0], ll[1]), pack2(ll[2], ll[3]));
     }
 }
 
-template <int MODE>
+// TT = token tiles per caption: 1 (T <= 32) or 2 (T <= 64, BASELINE configs[4]
+// with 64-token captions): then the workgroup holds 2 captions, one wave per
+// (caption, 32-token tile), and the two waves of a caption exchange the
+// per-region max and sum of the softmax over words and the per-token
+// log-sum-exp partials through LDS.  Buffers then have a token stride of
+// 32 * TT.  MODE_BF16 takes log2(e)-scaled words (tgfr_wr_fwd mode 0).
+template <int MODE, int TT>
 __global__ __launch_bounds__(256, 1) void wr_fwd_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Rlo,
     const uint16_t* __restrict__ Whi, const uint16_t* __restrict__ Wlo,
@@ -170,18 +178,24 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_kernel(
     int img_offset, float g1, float g2, float g3, float eps, float* __restrict__ logits,
     int ld_logits, float4* __restrict__ stats, uint16_t* __restrict__ Chi,
     uint16_t* __restrict__ Clo, float* __restrict__ att, int att_T) {
-  const int groups = (B_cap + 3) / 4;
+  constexpr int CPW = 4 / TT;              // captions per workgroup
+  constexpr int TP = 32 * TT;              // token stride of W, stats, C
+  constexpr bool SCALED = MODE == MODE_BF16;
+  constexpr float L2E = 1.4426950408889634f;
+  const int groups = (B_cap + CPW - 1) / CPW;
   const int work = xcd_remap(blockIdx.x, groups * B_img);
   const int b = work / groups;
   const int grp = work % groups;
   const int tid = threadIdx.x, wid = tid / WAVE, lane = tid % WAVE;
   const int lr = lane & 31, h = lane >> 5;
-  const int i = grp * 4 + wid;
+  const int tt = wid % TT;                 // this wave's token tile
+  const int i = grp * CPW + wid / TT;
   const bool active = i < B_cap;
   const int ic = active ? i : B_cap - 1;  // clamp for address math
   const int len = lens[ic];
+  const int tl = len - 32 * tt;            // valid words of this wave's tile
   const long long img_off = (long long)b * RPAD * D;
-  const long long cap_off = (long long)ic * TPAD * D;
+  const long long cap_off = ((long long)ic * TP + 32 * tt) * D;
 
   f32x16 S[NRT];
 #pragma unroll
@@ -234,31 +248,61 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_kernel(
   }
 
   // ---- softmax over words per region (registers), E = exp(gamma1 A1),
-  //      per-token Z = sum_r E and N = sum_r E S (reduce-scatter over lanes)
-  if (active) {
+  //      per-token Z = sum_r E and N = sum_r E S (reduce-scatter over lanes).
+  //      Inactive waves compute on zeros (their results are never stored) so
+  //      that every wave reaches the TT = 2 exchange barriers.
+  {
     float zp[16], np[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) zp[q] = np[q] = 0.f;
+    float mj[NRT], sj[NRT];
 #pragma unroll
     for (int j = 0; j < NRT; ++j) {
-      const bool rvalid = j * 32 + lr < NREG;
       float m = -INFINITY;
 #pragma unroll
       for (int q = 0; q < 16; ++q)
-        if (acc_row(q, h) < len) m = fmaxf(m, S[j][q]);
-      m = fmaxf(m, __shfl_xor(m, 32));
-      float p[16], sum = 0.f;
+        if (acc_row(q, h) < tl) m = fmaxf(m, S[j][q]);
+      mj[j] = fmaxf(m, __shfl_xor(m, 32));
+    }
+    if constexpr (TT == 2) {           // max over both token tiles of the caption
+      if (h == 0)
+#pragma unroll
+        for (int j = 0; j < NRT; ++j) lds_stf(F_OFF_XS + (wid * NRT + j) * 128 + lr * 4, mj[j]);
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < NRT; ++j)
+        mj[j] = fmaxf(mj[j], lds_ldf(F_OFF_XS + ((wid ^ 1) * NRT + j) * 128 + lr * 4));
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < NRT; ++j) {
+      float sum = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        p[q] = acc_row(q, h) < len ? __expf(S[j][q] - m) : 0.f;
-        sum += p[q];
+        const float x = S[j][q] - mj[j];
+        E[j][q] = acc_row(q, h) < tl ? (SCALED ? __builtin_amdgcn_exp2f(x) : __expf(x)) : 0.f;
+        sum += E[j][q];
       }
-      sum += __shfl_xor(sum, 32);
-      const float inv = 1.f / sum;
+      sj[j] = sum + __shfl_xor(sum, 32);
+    }
+    if constexpr (TT == 2) {           // sum over both token tiles
+      if (h == 0)
+#pragma unroll
+        for (int j = 0; j < NRT; ++j) lds_stf(F_OFF_XS + (wid * NRT + j) * 128 + lr * 4, sj[j]);
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < NRT; ++j)
+        sj[j] += lds_ldf(F_OFF_XS + ((wid ^ 1) * NRT + j) * 128 + lr * 4);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < NRT; ++j) {
+      const bool rvalid = j * 32 + lr < NREG;
+      const float inv = 1.f / sj[j];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const bool ok = rvalid && acc_row(q, h) < len;
-        const float e = ok ? __expf(g1 * (p[q] * inv)) : 0.f;
+        const bool ok = rvalid && acc_row(q, h) < tl;
+        const float e = ok ? __expf(g1 * (E[j][q] * inv)) : 0.f;
         E[j][q] = e;
         zp[q] += e;
         np[q] += e * S[j][q];
@@ -319,9 +363,8 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_kernel(
     __syncthreads();
   }
 
-  if (!active) return;
   // ---- per-token epilogue: lane (t = lr, h) holds C^T[d][t] for d rows of half h
-  const int t = lr;
+  const int t = lr, tg = 32 * tt + lr;     // local and caption token index
   float csq = 0.f;
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt)
@@ -329,20 +372,28 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_kernel(
     for (int q = 0; q < 16; ++q) csq += C[dt][q] * C[dt][q];
   csq += __shfl_xor(csq, 32);
   const float Z = lds_ldf(tok + t * 4);
-  const float nhat = lds_ldf(tok + 128 + t * 4);
-  const bool tvalid = t < len;
+  // scaled scores (bf16 mode): N accumulated E * log2(e) S
+  const float nhat = lds_ldf(tok + 128 + t * 4) * (SCALED ? 1.f / L2E : 1.f);
+  const bool tvalid = t < tl;
   const float zinv = 1.f / Z;
   const float cn = sqrtf(csq) * zinv;
   const float n = nhat * zinv;
-  const float u = Wnorm[(long long)ic * TPAD + t];
+  const float u = Wnorm[(long long)ic * TP + tg];
   const float cosv = n / fmaxf(u * cn, eps);
   float ex = tvalid ? __expf(g2 * cosv) : 0.f;
   ex = half_sum(ex);
+  if constexpr (TT == 2) {               // log-sum-exp over both token tiles
+    if (lane == 0) lds_stf(F_OFF_XS + wid * 4, ex);
+    __syncthreads();
+    ex += lds_ldf(F_OFF_XS + (wid ^ 1) * 4);
+  }
+  if (!active) return;
   const long long pair = (long long)b * B_cap + i;
-  if (lane == 0) logits[(long long)b * ld_logits + i] = g3 * __logf(ex);
+  if (lane == 0 && tt == 0) logits[(long long)b * ld_logits + i] = g3 * __logf(ex);
   if (stats && h == 0)
-    stats[pair * TPAD + t] = tvalid ? make_float4(Z, n, cn, cosv) : make_float4(0.f, 0.f, 0.f, 0.f);
-  if (Chi) store_cq<MODE>(Chi, Clo, pair, t, h, C);
+    stats[pair * TP + tg] =
+        tvalid ? make_float4(Z, n, cn, cosv) : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (Chi) store_cq<MODE, TP>(Chi, Clo, pair, tg, h, C);
   if (att && b + img_offset == i) {
     // attention map of the matching pair: A2[t][r] = E[t][r] / Z_t
     float* dst = att + (long long)b * att_T * NREG;
@@ -350,9 +401,9 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_kernel(
     for (int j = 0; j < NRT; ++j)
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int tt = acc_row(q, h), r = j * 32 + lr;
-        if (tt < len && tt < att_T && r < NREG)
-          dst[tt * NREG + r] = E[j][q] / lds_ldf(tok + tt * 4);
+        const int tq = acc_row(q, h), r = j * 32 + lr;
+        if (tq < tl && 32 * tt + tq < att_T && r < NREG)
+          dst[(32 * tt + tq) * NREG + r] = E[j][q] / lds_ldf(tok + tq * 4);
       }
   }
 }
@@ -899,6 +950,9 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
 // wr_bwd_pipe_kernel) as 8 scalar rows of 32 tokens with gamma1, 1/Z and
 // log2(e) folded in (see there); either way one 1-KiB global_load_lds stages
 // a caption's table.
+// TP = token stride (32, or 64 for the two-tile kernels: then every lane of
+// the wave is a token and the softmax over words sums the whole wave).
+template <int TP>
 __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ stats,
                                                      const float* __restrict__ Wnorm,
                                                      const int* __restrict__ lens,
@@ -909,17 +963,17 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
   const long long pair = (blockIdx.x * 256LL + threadIdx.x) / WAVE;
   if (pair >= (long long)B_img * B_cap) return;
   const int b = pair / B_cap, i = pair % B_cap;
-  const int t = threadIdx.x % 32;
+  const int t = threadIdx.x % TP;
   const int len = lens[i];
   const bool valid = t < len;
-  const float4 st = valid ? stats[pair * TPAD + t] : make_float4(1.f, 0.f, 0.f, 0.f);
+  const float4 st = valid ? stats[pair * TP + t] : make_float4(1.f, 0.f, 0.f, 0.f);
   const float ex = valid ? __expf(g2 * st.w) : 0.f;
-  const float tot = half_sum(ex);
+  const float tot = TP == 64 ? wave_sum(ex) : half_sum(ex);
   float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (valid) {
     const float G = dlogits[(long long)b * ld + i] * g3;
     const float dcos = G * g2 * ex / tot;
-    const float u = Wnorm[(long long)i * TPAD + t];
+    const float u = Wnorm[(long long)i * TP + t];
     const float cn = st.z, n = st.y, cosv = st.w;
     float alpha, beta;
     if (u * cn >= eps) {
@@ -956,8 +1010,8 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
     }
     return;
   }
-  if ((threadIdx.x % WAVE) < 32) {
-    float4* dst = (float4*)(tok + (pair * TPAD + t) * 8);
+  if ((threadIdx.x % WAVE) < TP) {
+    float4* dst = (float4*)(tok + (pair * TP + t) * 8);
     dst[0] = make_float4(o[0], o[1], o[2], o[3]);
     dst[1] = make_float4(o[4], o[5], o[6], o[7]);
   }
@@ -1213,6 +1267,214 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
   }
   if (!active) return;
   mfma_drain();
+  float* dst = slab + (((long long)chunk * B_img + b) * RPAD + rt * 32) * D;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dst[acc_row(q, h) * D + dt * 32 + lr] = dR[dt][q];
+}
+
+// ------------------------------------------------ bwd, 64-token captions ---
+// wr_bwd_kernel for T <= 64 (BASELINE configs[4]: 64-token captions, T = 62),
+// both modes: X = [W (64 rows); C-hat (64 rows)] per caption, so the S / Q
+// accumulators, the softmax over words (two 32-token tiles per lane) and the
+// dR GEMM's K (128) double.  R tile fragments live in registers; the
+// caption ring is 2 deep in bf16 mode (64 KB images) and 1 deep in split mode
+// (hi + lo = 128 KB).  The softmax backward runs in two passes so only two
+// values per element stay live (A1 and A1 dA1) across the rho reduction.
+constexpr int W_XIMG = 128 * 256 * 2;      // one bf16 image, 128 rows
+constexpr int W_TOK = 64 * 32;             // token table, 8 floats per token
+
+template <int MODE>
+struct BwdWCfg {
+  static constexpr int NIMG = MODE == MODE_SPLIT ? 2 : 1;
+  static constexpr int BUF = NIMG * W_XIMG + W_TOK;
+  static constexpr int NB = MODE == MODE_SPLIT ? 1 : 2;
+  static constexpr int LDS = NB * BUF;
+};
+
+template <int MODE>
+__device__ __forceinline__ void bwd_stage_wide(uint32_t base, const uint16_t* Whi,
+                                               const uint16_t* Wlo, const uint16_t* Chi,
+                                               const uint16_t* Clo, const float* tok,
+                                               long long pair, int i, int wid, int lane) {
+  constexpr int NIMG = BwdWCfg<MODE>::NIMG;
+  // 64 one-KiB pieces per image: piece p covers rows 4*(p%32)..+3 of half p/32
+#pragma unroll
+  for (int k = wid; k < 64 * NIMG; k += 4) {
+    const int img = k / 64, p = k % 64;
+    const int half = p / 32;
+    const int row = 4 * (p % 32) + lane / 16, pc = lane % 16;
+    const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
+    const int c = half * 16 + (pc ^ sw);
+    const uint16_t* src;
+    if (row < 64)
+      src = (img ? Wlo : Whi) + ((long long)i * 64 + row) * D + c * 8;
+    else
+      src = (img ? Clo : Chi) + ((pair * 32 + c) * 64 + (row - 64)) * 8;
+    glds16(src, base + img * W_XIMG + half * (128 * 256) + 4 * (p % 32) * 256);
+  }
+  // token table (2 KiB): every wave writes both pieces (identical bytes)
+  glds16(tok + pair * 64 * 8 + lane * 4, base + NIMG * W_XIMG);
+  glds16(tok + pair * 64 * 8 + 256 + lane * 4, base + NIMG * W_XIMG + 1024);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256, 1) void wr_bwd_wide_kernel(
+    const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Rlo,
+    const uint16_t* __restrict__ Whi, const uint16_t* __restrict__ Wlo, int B_img, int B_cap,
+    int n_chunks, float g1, const float* __restrict__ tok, const uint16_t* __restrict__ Chi,
+    const uint16_t* __restrict__ Clo, float* __restrict__ slab) {
+  constexpr int NIMG = BwdWCfg<MODE>::NIMG;
+  constexpr int BUF = BwdWCfg<MODE>::BUF;
+  constexpr int NB = BwdWCfg<MODE>::NB;
+  const int total = n_chunks * 2 * B_img;
+  const int work = xcd_remap(blockIdx.x, total);
+  const int b = work / (2 * n_chunks);
+  const int rem = work % (2 * n_chunks);
+  const int tg = rem / n_chunks, chunk = rem % n_chunks;
+  const int per = (B_cap + n_chunks - 1) / n_chunks;
+  const int c0 = chunk * per, c1 = min(B_cap, c0 + per);
+  const int tid = threadIdx.x, lane = tid % WAVE;
+  const int wid = __builtin_amdgcn_readfirstlane(tid / WAVE);
+  const int lr = lane & 31, h = lane >> 5;
+  const int rt = tg * 4 + wid;
+  const bool active = rt < NRT;
+  const int g16 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+
+  bf16x8 Rh[16], Rl[16];
+  {
+    const long long roff = ((long long)b * RPAD + min(rt, NRT - 1) * 32 + lr) * D;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      Rh[s] = as_bf8(*(const uint4*)(Rhi + roff + s * 16 + h * 8));
+      Rl[s] = MODE == MODE_SPLIT ? as_bf8(*(const uint4*)(Rlo + roff + s * 16 + h * 8)) : Rh[s];
+    }
+  }
+  f32x16 dR[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dR[j][q] = 0.f;
+  uint32_t g1o[8], g2o[2][4];
+  {
+    const int sw1 = ((lr & 3) << 2) | ((lr >> 2) & 3);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g1o[k] = lr * 256 + (((2 * k + h) ^ sw1) << 4);
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd)
+        g2o[bb][dd] = (4 * h + q4 + 8 * bb) * 256 + ((dd ^ q4) << 6) +
+                      (((2 * (g16 & 1) + (p4 >> 1)) ^ ((h + 2 * bb) & 3)) << 4) + (p4 & 1) * 8;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (NB == 2 && c0 < c1)
+    bwd_stage_wide<MODE>(0, Whi, Wlo, Chi, Clo, tok, (long long)b * B_cap + c0, c0, wid, lane);
+
+  for (int i = c0; i < c1; ++i) {
+    const int it = i - c0;
+    uint32_t base;
+    if constexpr (NB == 2) {
+      ring_barrier<0>();     // caption i landed; caption i-1's buffer retired
+      if (i + 1 < c1)
+        bwd_stage_wide<MODE>(((it + 1) & 1) * BUF, Whi, Wlo, Chi, Clo, tok,
+                             (long long)b * B_cap + i + 1, i + 1, wid, lane);
+      base = (it & 1) * BUF;
+    } else {
+      // previous caption's LDS reads retired in every wave
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      bwd_stage_wide<MODE>(0, Whi, Wlo, Chi, Clo, tok, (long long)b * B_cap + i, i, wid, lane);
+      ring_barrier<0>();
+      base = 0;
+    }
+    const uint32_t tk = base + NIMG * W_XIMG;
+    // ---- [S^T ; Q^T] of both token tiles = X R_tile^T
+    f32x16 A0[2], A1[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) A0[u][q] = A1[u][q] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t ow = base + g1o[s & 7] + (s >> 3) * (128 * 256) + u * 32 * 256;
+        const bf16x8 w_hi = as_bf8(lds_ld16(ow)), c_hi = as_bf8(lds_ld16(ow + 64 * 256));
+        bf16x8 w_lo = w_hi, c_lo = c_hi;
+        if (MODE == MODE_SPLIT) {
+          w_lo = as_bf8(lds_ld16(ow + W_XIMG));
+          c_lo = as_bf8(lds_ld16(ow + W_XIMG + 64 * 256));
+        }
+        mma<MODE>(A0[u], w_hi, w_lo, Rh[s], Rl[s]);
+        mma<MODE>(A1[u], c_hi, c_lo, Rh[s], Rl[s]);
+      }
+    }
+    // ---- softmax over the 64 words (two tiles per lane) and its backward
+    auto tokv = [&](int u, int q) { return lds_ld16(tk + (32 * u + acc_row(q, h)) * 32); };
+    float m = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (__uint_as_float(tokv(u, q).x) != 0.f) m = fmaxf(m, A0[u][q]);
+    m = fmaxf(m, __shfl_xor(m, 32));
+    float a1[2][16], v[2][16], sum = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        a1[u][q] = __uint_as_float(tokv(u, q).x) != 0.f ? __expf(A0[u][q] - m) : 0.f;
+        sum += a1[u][q];
+      }
+    sum += __shfl_xor(sum, 32);
+    const float inv = 1.f / sum;
+    float rho = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const uint4 tv = tokv(u, q);             // {1/Z, alpha, beta/Z, sigma}
+        a1[u][q] *= inv;
+        const float a2 = __expf(g1 * a1[u][q]) * __uint_as_float(tv.x);
+        const float da2 = __uint_as_float(tv.y) * A0[u][q] + __uint_as_float(tv.z) * A1[u][q];
+        v[u][q] = a1[u][q] * (g1 * a2 * (da2 - __uint_as_float(tv.w)));
+        rho += v[u][q];
+      }
+    rho += __shfl_xor(rho, 32);
+    // ---- per token tile: M = [dS + alpha A2 | beta A2] fragments, dR GEMM
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float mw[16], mc[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const uint4 tv = tokv(u, q);
+        const float a2 = __expf(g1 * a1[u][q]) * __uint_as_float(tv.x);
+        mw[q] = v[u][q] - a1[u][q] * rho + __uint_as_float(tv.y) * a2;
+        mc[q] = __uint_as_float(tv.z) * a2;
+      }
+      bf16x8 Mh[4], Ml[4];
+      frag8<MODE>(mw, Mh[0], Ml[0]);
+      frag8<MODE>(mw + 8, Mh[1], Ml[1]);
+      frag8<MODE>(mc, Mh[2], Ml[2]);
+      frag8<MODE>(mc + 8, Mh[3], Ml[3]);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          // k block: W rows (k < 2) or C-hat rows of this tile, 16 tokens each
+          const int ks = (k < 2 ? 0 : 4) + 2 * u + (k & 1);
+          const uint32_t kb = base + (dt >> 2) * (128 * 256) + ks * 16 * 256;
+          const uint32_t o0 = kb + g2o[0][dt & 3], o1 = kb + g2o[1][dt & 3];
+          const bf16x8 xh = join_tr(lds_tr4(o0), lds_tr4(o1));
+          const bf16x8 xl =
+              MODE == MODE_SPLIT ? join_tr(lds_tr4(o0 + W_XIMG), lds_tr4(o1 + W_XIMG)) : xh;
+          mma<MODE>(dR[dt], Mh[k], Ml[k], xh, xl);
+        }
+      }
+    }
+  }
+  if (!active) return;
   float* dst = slab + (((long long)chunk * B_img + b) * RPAD + rt * 32) * D;
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt)
@@ -1517,20 +1779,39 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 int B_img, int B_cap,
                 int img_offset, float gamma1, float gamma2, float gamma3, float eps,
                 float* logits, int ld_logits, float* stats, uint16_t* Chi, uint16_t* Clo,
-                float* att, int att_T, int bounded, int mode, void* stream) {
+                float* att, int att_T, int bounded, int t_pad, int mode, void* stream) {
   if (B_img <= 0 || B_cap <= 0 || ld_logits < B_cap) return 1001;
+  if (t_pad != 32 && t_pad != 64) return 1001;
   const int grid = ((B_cap + 3) / 4) * B_img;
   auto* s = (hipStream_t)stream;
   static bool once = [] {
-    allow_lds(wr_fwd_kernel<MODE_SPLIT>, F_LDS);
-    allow_lds(wr_fwd_kernel<MODE_BF16>, F_LDS);
+    allow_lds(wr_fwd_kernel<MODE_SPLIT, 1>, F_LDS);
+    allow_lds(wr_fwd_kernel<MODE_SPLIT, 2>, F_LDS2);
+    allow_lds(wr_fwd_kernel<MODE_BF16, 2>, F_LDS2);
     allow_lds(wr_fwd_res_kernel, FR_LDS);
     allow_lds(wr_fwd_pipe_kernel, FR_LDS);
     return true;
   }();
   (void)once;
+  if (t_pad == 64) {
+    // 64-token captions: two waves per caption, two captions per workgroup
+    const int grid2 = ((B_cap + 1) / 2) * B_img;
+    if (mode == MODE_SPLIT)
+      hipLaunchKernelGGL((wr_fwd_kernel<MODE_SPLIT, 2>), dim3(grid2), dim3(256), F_LDS2, s,
+                         Rhi, Rlo, Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1,
+                         gamma2, gamma3, eps, logits, ld_logits, (float4*)stats, Chi, Clo, att,
+                         att_T);
+    else if (mode == MODE_BF16)
+      hipLaunchKernelGGL((wr_fwd_kernel<MODE_BF16, 2>), dim3(grid2), dim3(256), F_LDS2, s,
+                         Rhi, Rlo, Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1,
+                         gamma2, gamma3, eps, logits, ld_logits, (float4*)stats, Chi, Clo, att,
+                         att_T);
+    else
+      return 1002;
+    return (int)hipGetLastError();
+  }
   if (mode == MODE_SPLIT)
-    hipLaunchKernelGGL(wr_fwd_kernel<MODE_SPLIT>, dim3(grid), dim3(256), F_LDS, s, Rhi, Rlo,
+    hipLaunchKernelGGL((wr_fwd_kernel<MODE_SPLIT, 1>), dim3(grid), dim3(256), F_LDS, s, Rhi, Rlo,
                        Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1, gamma2, gamma3,
                        eps, logits, ld_logits, (float4*)stats, Chi, Clo, att, att_T);
   else if (mode == MODE_BF16) {
@@ -1554,20 +1835,51 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
 
 int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const int* lens, int B_img,
                     int B_cap, float gamma1, float gamma2, float gamma3, float eps,
-                    const float* dlogits, int ld, int bounded, float* tok_ws, void* stream) {
+                    const float* dlogits, int ld, int bounded, int t_pad, float* tok_ws,
+                    void* stream) {
   if (B_img <= 0 || B_cap <= 0 || ld < B_cap) return 1001;
   const long long pairs = (long long)B_img * B_cap;
-  hipLaunchKernelGGL(wr_tok_kernel, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
-                     (hipStream_t)stream, (const float4*)stats, Wnorm, lens, dlogits, ld, B_img,
-                     B_cap, gamma1, gamma2, gamma3, eps, bounded ? 1 : 0, tok_ws);
+  if (t_pad == 64 && !bounded)
+    hipLaunchKernelGGL(wr_tok_kernel<64>, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, (const float4*)stats, Wnorm, lens, dlogits, ld,
+                       B_img, B_cap, gamma1, gamma2, gamma3, eps, 0, tok_ws);
+  else if (t_pad == 32)
+    hipLaunchKernelGGL(wr_tok_kernel<32>, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, (const float4*)stats, Wnorm, lens, dlogits, ld,
+                       B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 1 : 0, tok_ws);
+  else
+    return 1001;
   return (int)hipGetLastError();
 }
 
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, int B_img, int B_cap, int n_chunks, float gamma1,
                 const float* tok_ws, const uint16_t* Chi, const uint16_t* Clo, float* slab,
-                int bounded, int mode, void* stream) {
+                int bounded, int t_pad, int mode, void* stream) {
   if (B_img <= 0 || B_cap <= 0 || n_chunks <= 0 || n_chunks > B_cap) return 1001;
+  if (t_pad == 64) {
+    if (bounded) return 1001;
+    if (mode == MODE_SPLIT && (!Rlo || !Wlo || !Clo)) return 1001;
+    static bool once_w = [] {
+      allow_lds(wr_bwd_wide_kernel<MODE_SPLIT>, BwdWCfg<MODE_SPLIT>::LDS);
+      allow_lds(wr_bwd_wide_kernel<MODE_BF16>, BwdWCfg<MODE_BF16>::LDS);
+      return true;
+    }();
+    (void)once_w;
+    const int grid = n_chunks * 2 * B_img;
+    if (mode == MODE_SPLIT)
+      hipLaunchKernelGGL(wr_bwd_wide_kernel<MODE_SPLIT>, dim3(grid), dim3(256),
+                         BwdWCfg<MODE_SPLIT>::LDS, (hipStream_t)stream, Rhi, Rlo, Whi, Wlo,
+                         B_img, B_cap, n_chunks, gamma1, tok_ws, Chi, Clo, slab);
+    else if (mode == MODE_BF16)
+      hipLaunchKernelGGL(wr_bwd_wide_kernel<MODE_BF16>, dim3(grid), dim3(256),
+                         BwdWCfg<MODE_BF16>::LDS, (hipStream_t)stream, Rhi, Rlo, Whi, Wlo,
+                         B_img, B_cap, n_chunks, gamma1, tok_ws, Chi, Clo, slab);
+    else
+      return 1002;
+    return (int)hipGetLastError();
+  }
+  if (t_pad != 32) return 1001;
   if (bounded) {
     if (mode != MODE_BF16) return 1002;
     static bool once_p = [] {
@@ -1615,6 +1927,6 @@ int tgfr_wr_lds_bytes(int which) {
   return which == 0 ? F_LDS : which == 1 ? BwdCfg<MODE_SPLIT>::LDS : FR_LDS;
 }
 
-int tgfr_version(void) { return 101; }
+int tgfr_version(void) { return 102; }
 
 }  // extern "C"

@@ -87,58 +87,62 @@ class WordRegionLogits(torch.autograd.Function):
         regions = regions_view(img_features.float())
         b_img, b_cap = regions.shape[0], words.shape[0]
         t_words = words.shape[1]
-        if t_words > TPAD:
-            raise ValueError(f"at most {TPAD} words per caption (got {t_words})")
+        if t_words > 2 * TPAD:
+            raise ValueError(f"at most {2 * TPAD} words per caption (got {t_words})")
+        # token stride: 32, or 64 for 64-token captions (general kernels only)
+        t_pad = TPAD if t_words <= TPAD else 2 * TPAD
         lens = lens.to(device=dev, dtype=torch.int32).contiguous()
         m = _mode(mode)
         bf16 = m == MODES["bf16"]
         # the bounded bf16 path runs the pipelined kernels both ways
-        fast = bf16 and bool(bounded) and not att_T
+        fast = bf16 and bool(bounded) and not att_T and t_pad == TPAD
         r_hi, r_lo, r_norm = prep_rows(regions, NREG, RPAD, want_norms=bf16)
         if bf16:
             # the bf16 forward takes log2(e)-scaled words (tgfr.h, tgfr_wr_fwd),
             # and so does the pipelined backward; the other backward the plain ones
-            w_fwd, _, w_norm = prep_rows(words.float(), t_words, TPAD, lens=lens,
+            w_fwd, _, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,
                                          want_norms=True, scale=LOG2E)
-            w_hi = w_fwd if fast else prep_rows(words.float(), t_words, TPAD, lens=lens)[0]
+            w_hi = w_fwd if fast else prep_rows(words.float(), t_words, t_pad, lens=lens)[0]
             w_lo = None
         else:
-            w_hi, w_lo, w_norm = prep_rows(words.float(), t_words, TPAD, lens=lens,
+            w_hi, w_lo, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,
                                            want_norms=True)
             w_fwd = w_hi
         logits = torch.empty(b_img, b_cap, dtype=torch.float32, device=dev)
-        stats = torch.empty(b_img, b_cap, TPAD, 4, dtype=torch.float32, device=dev)
-        # C for the backward: bf16 hi (+lo in fp32 mode), chunk-major [pair][32][32][8]
-        c_hi = torch.empty(b_img, b_cap, 32, TPAD, 8, dtype=torch.int16, device=dev)
+        stats = torch.empty(b_img, b_cap, t_pad, 4, dtype=torch.float32, device=dev)
+        # C for the backward: bf16 hi (+lo in fp32 mode), chunk-major [pair][32][t_pad][8]
+        c_hi = torch.empty(b_img, b_cap, 32, t_pad, 8, dtype=torch.int16, device=dev)
         c_lo = torch.empty_like(c_hi) if m == MODES["fp32"] else None
         att = torch.zeros(b_img, att_T, NREG, dtype=torch.float32, device=dev) \
             if att_T else None
         call("tgfr_wr_fwd", ptr(r_hi), ptr(r_lo), ptr(w_fwd), ptr(w_lo), ptr(w_norm),
              ptr(r_norm), ptr(lens), b_img, b_cap, img_offset, gamma1, gamma2, gamma3, eps,
              ptr(logits), b_cap, ptr(stats), ptr(c_hi), ptr(c_lo), ptr(att), att_T,
-             int(bool(bounded)), m,
+             int(bool(bounded) and t_pad == TPAD), t_pad, m,
              _hip.stream())
         ctx.save_for_backward(r_hi, r_lo, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo)
-        ctx.cfg = (gamma1, gamma2, gamma3, eps, m, img_features.shape, fast)
+        ctx.cfg = (gamma1, gamma2, gamma3, eps, m, img_features.shape, fast, t_pad)
         ctx.mark_non_differentiable(*([att] if att is not None else []))
         return (logits, att) if att is not None else logits
 
     @staticmethod
     def backward(ctx, dlogits, *unused):
         r_hi, r_lo, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo = ctx.saved_tensors
-        gamma1, gamma2, gamma3, eps, m, shape, fast = ctx.cfg
+        gamma1, gamma2, gamma3, eps, m, shape, fast, t_pad = ctx.cfg
         b_img, b_cap = stats.shape[0], stats.shape[1]
         dlogits = dlogits.float().contiguous()
         chunks = bwd_chunks(b_img, b_cap)
         slab = torch.empty(chunks, b_img, RPAD, D, dtype=torch.float32,
                            device=dlogits.device)
-        tok = torch.empty(b_img, b_cap, TPAD, 8, dtype=torch.float32, device=dlogits.device)
+        tok = torch.empty(b_img, b_cap, t_pad, 8, dtype=torch.float32, device=dlogits.device)
         split = m == MODES["fp32"]
         call("tgfr_wr_bwd_tok", ptr(stats), ptr(w_norm), ptr(lens), b_img, b_cap, gamma1,
-             gamma2, gamma3, eps, ptr(dlogits), b_cap, int(fast), ptr(tok), _hip.stream())
+             gamma2, gamma3, eps, ptr(dlogits), b_cap, int(fast), t_pad, ptr(tok),
+             _hip.stream())
         call("tgfr_wr_bwd", ptr(r_hi), ptr(r_lo) if split else None, ptr(w_hi),
              ptr(w_lo) if split else None, b_img, b_cap, chunks, gamma1, ptr(tok),
-             ptr(c_hi), ptr(c_lo) if split else None, ptr(slab), int(fast), m, _hip.stream())
+             ptr(c_hi), ptr(c_lo) if split else None, ptr(slab), int(fast), t_pad, m,
+             _hip.stream())
         d_reg = torch.empty(b_img, NREG, D, dtype=torch.float32, device=dlogits.device)
         call("tgfr_wr_reduce", ptr(slab), chunks, b_img, ptr(d_reg), NREG * D, D, 1, 0,
              _hip.stream())

@@ -13,7 +13,10 @@ import os
 
 import torch  # noqa: F401  (must be imported before the library is mapped)
 
-from .build import LIB
+from .build import LIB as _BUILT
+
+# TGFR_LIB: an alternative build of the same library (kernel experiments)
+LIB = os.environ.get("TGFR_LIB", _BUILT)
 
 _lib = None
 

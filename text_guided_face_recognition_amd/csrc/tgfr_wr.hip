@@ -676,6 +676,16 @@ struct FwdSlot {
   int m;      // slot within the stage
 };
 constexpr int FWD_SLOTS = 16 + 5 * 34 + 18 + 34;
+// LDS operand prefetch distance in MFMA slots (ring of 8; see the wrap
+// argument at the issue site: no live slot is overwritten for 3 <= PF <= 6)
+#ifndef TGFR_PF_FWD
+#define TGFR_PF_FWD 3
+#endif
+#ifndef TGFR_PF_BWD
+#define TGFR_PF_BWD 3
+#endif
+constexpr int PF_FWD = TGFR_PF_FWD;
+constexpr int PF_BWD = TGFR_PF_BWD;
 // the caption's slots in issue order
 __device__ __forceinline__ constexpr FwdSlot fwd_slot(int n) {
   if (n < 16) return {0, 1, n, 0, n};
@@ -784,8 +794,8 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     for (int s = 0; s < 16; ++s)
       Wc[s] = as_bf8(*(const uint4*)(Whi + ((long long)ii * TPAD + lr) * D + s * 16 + h * 8));
   };
-  // LDS operand reads, 4-deep ring indexed by slot
-  u32x4 rd[4];
+  // LDS operand reads, ring indexed by slot, issued PF_FWD slots ahead
+  u32x4 rd[8];
   auto issue_read = [&](const FwdSlot sl, u32x4& dst) {
     if (sl.kind == 0) {
       const int s = sl.idx;
@@ -851,7 +861,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     S[0] = acc;
   }
 #pragma unroll
-  for (int n = 0; n < 3; ++n) issue_read(fwd_slot(n), rd[n]);
+  for (int n = 0; n < PF_FWD; ++n) issue_read(fwd_slot(n), rd[n]);
 
   for (; i < c1; i += 4) {
     const int len = lens[i];
@@ -870,7 +880,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
       if (stage >= 1 && m == 0) eb[0] = read_e(etg, 0);
       if (stage >= 1 && m == (stage == 6 ? 5 : 14)) eb[1] = read_e(etg, 1);
       // ---- the MFMA of this slot
-      const u32x4 opnd = rd[n & 3];
+      const u32x4 opnd = rd[n & 7];
       if (sl.kind == 0) {
         // builtins (not inline asm): the compiler's hazard recognizer then
         // places the VALU-write -> MFMA-read and MFMA -> VALU-read waits
@@ -887,7 +897,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
           C[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, eb[s], C[dt], 0, 0, 0);
       }
       // ---- reads of the slot three ahead (wrapping into the next caption)
-      issue_read(fwd_slot((n + 3) % FWD_SLOTS), rd[((n + 3) % FWD_SLOTS) & 3]);
+      issue_read(fwd_slot((n + PF_FWD) % FWD_SLOTS), rd[((n + PF_FWD) % FWD_SLOTS) & 7]);
       // ---- the softmax VALU of this slot
       if (stage <= 6) {
         const int j = stage;                       // softmax tile
@@ -1691,14 +1701,14 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
     const uint32_t tbs = t < K ? (t % BP_NB) * BP_BUF + B_XIMG : BP_ZERO;
     const uint32_t tb1 = x1 + B_XIMG;
     const f32x16 init = init_of(tb1);
-    u32x4 rd[4];
+    u32x4 rd[8];
     // slot n: even -> G1 MFMA n/2, odd -> G3 MFMA n/2
     auto read = [&](int n) { return (n & 1) ? g3_read(n >> 1, x3) : g1_read(n >> 1, x1); };
 #pragma unroll
-    for (int n = 0; n < 3; ++n) rd[n] = read(n);
+    for (int n = 0; n < PF_BWD; ++n) rd[n] = read(n);
 #pragma clang loop unroll(full)
     for (int n = 0; n < 64; ++n) {
-      const u32x4 op = rd[n & 3];
+      const u32x4 op = rd[n & 7];
       if (n & 1) {
         const int u = n >> 1, ks = u & 3;
         dR[u >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
@@ -1706,7 +1716,7 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
       } else {
         g1_mfma(n >> 1, op, A0n, A1n, init);
       }
-      if (n + 3 < 64) rd[(n + 3) & 3] = read(n + 3);
+      if (n + PF_BWD < 64) rd[(n + PF_BWD) & 7] = read(n + PF_BWD);
       sm_chunk(n, tbs, A0, A1, Mo);
       __builtin_amdgcn_sched_barrier(0);
     }

@@ -241,6 +241,37 @@ int tgfr_bn_unfold(const float* G, const float* s, const float* W, int O, int C,
                    const float* gamma, const float* beta, float* dW, float* dgamma, float* dbeta,
                    float* ws, unsigned* counters, void* stream);
 
+/* ---- optimiser step ------------------------------------------------------
+ * Every trainable tensor of a trainer in one launch (replaces the two torch
+ * optimiser steps of src/train_encoders_bert.py:212-222 / :323-330 and
+ * src/fusion_bert.py:119-139).  Per group:
+ *   Adam (torch.optim.Adam, amsgrad off):  g += wd p;  m = b1 m + (1-b1) g;
+ *     v = b2 v + (1-b2) g^2;  p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
+ *   SGD (torch.optim.SGD, nesterov off):  g += wd p;  buf = g at t = 1, else
+ *     momentum buf + (1-dampening) g;  p -= lr buf  (no buf when momentum = 0)
+ * state0 = m / buf, state1 = v (Adam only).  counters: 2 ints, [0] = steps
+ * taken so far (t - 1; the launch increments it), [1] = 0 (left 0).  The
+ * segment table travels in the kernel arguments, so a captured launch
+ * replays with the pointers it was captured with.  n_segs <= 48,
+ * n_groups <= 4. */
+#define TGFR_OPTIM_ADAM 0
+#define TGFR_OPTIM_SGD 1
+typedef struct {
+  int kind;
+  float lr, beta1, beta2, eps, weight_decay, momentum, dampening;
+} tgfr_optim_group;
+typedef struct {
+  float* param;
+  const float* grad;
+  float* state0;
+  float* state1;
+  long long n;
+  int group;
+  int reserved;
+} tgfr_optim_seg;
+int tgfr_optim_step(const tgfr_optim_seg* segs, int n_segs, const tgfr_optim_group* groups,
+                    int n_groups, int* counters, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,6 +57,7 @@ SIGNATURES = {
     "tgfr_bias_grad": [P, L, I, I, P, L, P, L, P, P, P, P],
     "tgfr_ln_fwd": [P, I, L, P, P, F, I, P, P, P],
     "tgfr_ln_bwd": [P, P, I, L, P, I, P, P, P, P, P],
+    "tgfr_optim_step": [P, I, P, I, P, P],
 }
 
 

@@ -477,14 +477,16 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
   int TM = 64, TN = 64;
   dim3 grid;
   if (dma) {
-    // largest tile that still gives >= 2 blocks per CU (TGFR_GEMM_CFG forces
-    // one, for tuning)
+    // largest tile that still gives >= 2 blocks per CU; the 128x128 tile
+    // (cfg 3) is never picked: at K <= 768 it loses to 128x64 / 64x128 on
+    // every head shape (tools/gemm_bench.py; TGFR_GEMM_CFG forces one, for
+    // tuning)
     static const int forced = getenv("TGFR_GEMM_CFG") ? atoi(getenv("TGFR_GEMM_CFG")) : -1;
     int cfg = 0;
     if (forced >= 0 && forced < 4) {
       cfg = forced;
     } else {
-      for (int c = 3; c >= 1; --c) {
+      for (int c = 2; c >= 1; --c) {
         const long long blocks = (long long)((M + 64 * CFG_WM[c] - 1) / (64 * CFG_WM[c])) *
                                  ((N + 64 * CFG_WN[c] - 1) / (64 * CFG_WN[c])) * batch * ksplit;
         if (blocks >= 512) { cfg = c; break; }

@@ -30,6 +30,7 @@ from .models.fusion_nets import Working, set_precision
 from .models.losses import FocalLoss, global_loss, sent_loss, words_loss
 from .models.metrics import ArcMarginProduct
 from .models.models import ImageHeading
+from .optim import FusedOptimizer, adam_group, sgd_group
 
 
 def _unit(x, dim=-1):
@@ -68,14 +69,11 @@ class Train:
         self.ctx.broadcast_params(self.params)
         self.ident_loss = FocalLoss(gamma=2)
         # :212 (text_head params would join here; the text side is frozen input)
-        self.optimizer_head = torch.optim.Adam(self.image_head.parameters(),
-                                               lr=args.lr_head, betas=(0.5, 0.999),
-                                               capturable=device.type == "cuda",
-                                               fused=device.type == "cuda")
-        # :219-222
-        self.optimizer_cls = torch.optim.SGD(
-            list(self.image_cls.parameters()) + list(self.text_cls.parameters()),
-            lr=0.1, momentum=0.9, weight_decay=5e-5, fused=device.type == "cuda")
+        # :212 Adam for the head, :219-222 SGD for both classifiers: one launch
+        self.optimizer = FusedOptimizer([
+            adam_group(self.image_head.parameters(), lr=args.lr_head, betas=(0.5, 0.999)),
+            sgd_group(list(self.image_cls.parameters()) + list(self.text_cls.parameters()),
+                      lr=0.1, momentum=0.9, weight_decay=5e-5)])
 
     def step(self, batch):
         args, ctx = self.args, self.ctx
@@ -89,8 +87,7 @@ class Train:
         labels = self._labels(ctx.n_global, g.device)
 
         img_features, words_features = self.image_head(g, local)   # :265
-        self.optimizer_head.zero_grad(set_to_none=True)
-        self.optimizer_cls.zero_grad(set_to_none=True)
+        self.optimizer.zero_grad(set_to_none=True)
 
         w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
         s0, s1 = sent_loss(img_features, sent_g, labels, cls_g, b, args)
@@ -110,8 +107,7 @@ class Train:
              (0, 0, 0, 0, 0, wi, wi)])                            # ident
         total.backward()                                           # :323
         ctx.reduce_grads(self.params)
-        self.optimizer_head.step()
-        self.optimizer_cls.step()
+        self.optimizer.step()
         return {"damsm": report[0], "clip": report[1], "ident": report[2]}
 
     def _labels(self, n, device):
@@ -136,13 +132,11 @@ class Fusion:
                        for p in m.parameters()]
         self.ctx.broadcast_params(self.params)
         self.criterion = FocalLoss(gamma=2)                        # :92-96
-        self.optimizer_cls = torch.optim.SGD(self.metric_fc.parameters(), lr=0.1,
-                                             weight_decay=5e-4,
-                                             fused=device.type == "cuda")   # :119-130
-        self.optimizer_head = torch.optim.Adam(
-            list(self.image_head.parameters()) + list(self.fusion_net.parameters()),
-            weight_decay=5e-5, lr=args.lr_head,
-            capturable=device.type == "cuda", fused=device.type == "cuda")   # :137-139
+        # :119-130 SGD for the classifier, :137-139 Adam for head + fusion net
+        self.optimizer = FusedOptimizer([
+            sgd_group(self.metric_fc.parameters(), lr=0.1, weight_decay=5e-4),
+            adam_group(list(self.image_head.parameters()) + list(self.fusion_net.parameters()),
+                       lr=args.lr_head, weight_decay=5e-5)])
 
     def step(self, batch):
         g, local, words, sent, class_ids = batch
@@ -151,14 +145,12 @@ class Fusion:
         img_feats, local_feats = self.image_head(g, local)         # :220
         output = self.fusion_net(local_feats, words, img_feats, sent)   # :153
         output = self.metric_fc(output, class_ids)                 # :224
-        self.optimizer_cls.zero_grad(set_to_none=True)
-        self.optimizer_head.zero_grad(set_to_none=True)
+        self.optimizer.zero_grad(set_to_none=True)
         loss = self.criterion(output, class_ids)                   # :232
         # replicas only: per-rank mean losses, summed gradients -> scale 1/world
         (loss if self.ctx.world == 1 else loss / self.ctx.world).backward()
         self.ctx.reduce_grads(self.params)
-        self.optimizer_cls.step()
-        self.optimizer_head.step()
+        self.optimizer.step()
         return {"loss": loss.detach()}
 
 

@@ -207,7 +207,7 @@ int tgfr_ln_bwd(const float* dy, const float* x, int rows, long long E, const fl
 
 /* Bias gradient of a row-wise linear map: db[c] = sum_r dy[r][c].  With y
  * (the ReLU output) the ReLU mask is applied first and the masked gradient is
- * written to dym (both set or both NULL).  ws: ceil(rows / 256) * cols floats;
+ * written to dym (both set or both NULL).  ws: ceil(rows / 128) * cols floats;
  * counters: ceil(cols / 64) zeroed words (left zeroed). */
 int tgfr_bias_grad(const float* dy, long long lddy, int rows, int cols, const float* y,
                    long long ldy, float* dym, long long lddm, float* db, float* ws,

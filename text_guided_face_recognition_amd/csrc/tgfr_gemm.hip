@@ -64,6 +64,9 @@ __device__ __forceinline__ void store_acc(const f32x16& acc, float* Cb, long lon
       float* o = Cb + m * sCm + n * sCn;
       float v = alpha * acc[q] + bn;
       if (accumulate) v += *o;
+#ifdef TGFR_GEMM_EXP_NOSTORE
+      if (v == 12345.f)
+#endif
       *o = relu ? fmaxf(v, 0.f) : v;
     }
   }
@@ -190,12 +193,14 @@ __global__ __launch_bounds__(256) void bgemm_glds_kernel(
   constexpr int TM = 64 * WM, TN = 64 * WN;
   constexpr int SA = Img<LA, TM>::BYTES, SB = Img<LB, TN>::BYTES, STG = SA + SB;
   constexpr int PER = (Img<LA, TM>::PIECES + Img<LB, TN>::PIECES) / 4;   // DMA ops / wave / stage
-  // XCD-aware tile order: consecutive work ids (same A row block) share an L2
+  // XCD-aware tile order over the whole (batch x slice, row, col) grid:
+  // consecutive work ids -- the tiles of one A row block, all tiles of one
+  // batch item, the K slices of one tile -- run on one XCD and share its L2
   const int gx = gridDim.x, gy = gridDim.y;
-  const int w = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
-  const int tn = w % gx, tm = w / gx;
+  const int w = xcd_remap((blockIdx.z * gy + blockIdx.y) * gx + blockIdx.x, gx * gy * gridDim.z);
+  const int tn = w % gx, tm = (w / gx) % gy, z = w / (gx * gy);
   const int n0 = tn * TN, m0 = tm * TM;
-  const int bt = blockIdx.z / ksplit, kz = blockIdx.z % ksplit;
+  const int bt = z / ksplit, kz = z % ksplit;
   const int kc = ((Kfull + ksplit - 1) / ksplit + BK - 1) / BK * BK;
   const int kb = kz * kc;
   const int K = max(0, min(Kfull - kb, kc));
@@ -213,6 +218,9 @@ __global__ __launch_bounds__(256) void bgemm_glds_kernel(
 
   const int nk = (K + BK - 1) / BK;
   auto issue = [&](int kt) {
+#ifdef TGFR_GEMM_EXP_NOLOAD
+    if (kt > 0) return;
+#endif
     const uint32_t o = (kt % NS) * STG;
     const int k0 = kt * BK;
     issue_tile<LA, TM>(Ab + (long long)k0 * sAk, sAm, sAk, M - m0, K - k0, o, wid, lane);
@@ -245,7 +253,13 @@ __global__ __launch_bounds__(256) void bgemm_glds_kernel(
         read_frag<LA, TM>(f, o, wm * 32 * WM + 32 * i, s, lane);
         frag8<MODE>(f.v, ah, al);
 #pragma unroll
-        for (int j = 0; j < WN; ++j) mma<MODE>(acc[i][j], ah, al, bh[j], bl[j]);
+        for (int j = 0; j < WN; ++j) {
+#ifdef TGFR_GEMM_EXP_NOMFMA
+          acc[i][j][0] += (float)ah[0] * (float)bh[j][0];
+#else
+          mma<MODE>(acc[i][j], ah, al, bh[j], bl[j]);
+#endif
+        }
       }
     }
   }
@@ -477,7 +491,7 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
   int TM = 64, TN = 64;
   dim3 grid;
   if (dma) {
-    // largest tile that still gives >= 2 blocks per CU; the 128x128 tile
+    // largest tile that still gives >= 1 block per CU (two fit); the 128x128 tile
     // (cfg 3) is never picked: at K <= 768 it loses to 128x64 / 64x128 on
     // every head shape (tools/gemm_bench.py; TGFR_GEMM_CFG forces one, for
     // tuning)
@@ -489,7 +503,7 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
       for (int c = 2; c >= 1; --c) {
         const long long blocks = (long long)((M + 64 * CFG_WM[c] - 1) / (64 * CFG_WM[c])) *
                                  ((N + 64 * CFG_WN[c] - 1) / (64 * CFG_WN[c])) * batch * ksplit;
-        if (blocks >= 512) { cfg = c; break; }
+        if (blocks >= 256) { cfg = c; break; }
       }
     }
     TM = 64 * CFG_WM[cfg];

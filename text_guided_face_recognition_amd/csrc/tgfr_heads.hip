@@ -207,6 +207,105 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(
   if (ry == 0 && c < cols) db[c] = red[tx] + red[64 + tx] + red[128 + tx] + red[192 + tx];
 }
 
+// Vector form (cols, strides % 4 == 0, 16-B aligned rows): grid
+// (ceil(cols / 256), ceil(rows / BG4_ROWS)), 16 waves; lane = 4 columns (one
+// float4), wave w = rows w, w + 16, ... of the block's BG4_ROWS.  Every load
+// is unconditional (clamped row / column, value masked afterwards) so all of
+// a lane's loads are in flight before the first add.  Block partials are
+// stored write-through (agent-scope relaxed stores), so the arrival needs no
+// release fence; the last block of a column group sums the group's partials
+// in block order with agent-scope loads.
+constexpr int BG4_WAVES = 16, BG4_ROWS = 128, BG4_PER_WAVE = BG4_ROWS / BG4_WAVES;
+
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void add4(float4& a, const float4& b) {
+  a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+}
+
+template <bool RELU>
+__global__ __launch_bounds__(64 * BG4_WAVES) void bias_grad4_kernel(
+    const float* __restrict__ dy, long long lddy, int rows, int cols, const float* __restrict__ y,
+    long long ldy, float* __restrict__ dym, long long lddm, float* __restrict__ part,
+    unsigned* __restrict__ counters, float* __restrict__ db) {
+  __shared__ float4 red[BG4_WAVES * 64];
+  __shared__ int last;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + 4 * lane;
+  const bool on = c < cols;
+  const int cc = on ? c : 0;
+  const int r0 = blockIdx.y * BG4_ROWS + w;
+  float4 v[BG4_PER_WAVE], m[BG4_PER_WAVE];
+  // 32-bit element offsets (the host checks they fit): SGPR base + VGPR
+  // offset addressing, two VGPRs fewer per load
+#pragma unroll
+  for (int i = 0; i < BG4_PER_WAVE; ++i) {
+    const unsigned r = (unsigned)min(r0 + BG4_WAVES * i, rows - 1);
+    v[i] = *(const float4*)(dy + (r * (unsigned)lddy + (unsigned)cc));
+    if constexpr (RELU) m[i] = *(const float4*)(y + (r * (unsigned)ldy + (unsigned)cc));
+  }
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < BG4_PER_WAVE; ++i) {
+    const int r = r0 + BG4_WAVES * i;
+    const bool ok = on && r < rows;
+    if constexpr (RELU) {
+      v[i].x = m[i].x > 0.f ? v[i].x : 0.f;
+      v[i].y = m[i].y > 0.f ? v[i].y : 0.f;
+      v[i].z = m[i].z > 0.f ? v[i].z : 0.f;
+      v[i].w = m[i].w > 0.f ? v[i].w : 0.f;
+      if (ok) *(float4*)(dym + (long long)r * lddm + c) = v[i];
+    }
+    if (ok) add4(a, v[i]);
+  }
+  red[w * 64 + lane] = a;
+  __syncthreads();
+  if (w == 0 && on) {
+    float4 t = red[lane];
+#pragma unroll
+    for (int k = 1; k < BG4_WAVES; ++k) add4(t, red[k * 64 + lane]);
+    float* o = part + (long long)blockIdx.y * cols + c;
+    st_agent(o, t.x); st_agent(o + 1, t.y); st_agent(o + 2, t.z); st_agent(o + 3, t.w);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned n = __hip_atomic_fetch_add(counters + blockIdx.x, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    last = n == gridDim.y - 1;
+    if (last)
+      __hip_atomic_store(counters + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  // the column group's partials: wave w sums blocks w, w + 16, ... (in order)
+  const int nb = gridDim.y;
+  float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k0 = w; k0 < nb; k0 += BG4_WAVES * 8) {
+    float4 t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float* q = part + (long long)min(k0 + BG4_WAVES * j, nb - 1) * cols + cc;
+      t[j] = make_float4(ld_agent(q), ld_agent(q + 1), ld_agent(q + 2), ld_agent(q + 3));
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (k0 + BG4_WAVES * j < nb) add4(s4, t[j]);
+  }
+  red[w * 64 + lane] = s4;
+  __syncthreads();
+  if (w == 0 && on) {
+    float4 t = red[lane];
+#pragma unroll
+    for (int k = 1; k < BG4_WAVES; ++k) add4(t, red[k * 64 + lane]);
+    *(float4*)(db + c) = t;
+  }
+}
+
 constexpr int MIX_N = 16, MIX_M = 4;
 struct MixArgs {
   const float* loss[MIX_N];
@@ -287,14 +386,28 @@ int tgfr_focal_ce_bwd(const float* L, int rows, int cols, const long long* label
   return (int)hipGetLastError();
 }
 
-// ws: ceil(rows / 256) * cols floats; counters: ceil(cols / 64) zeroed words.
+// ws: ceil(rows / 128) * cols floats; counters: ceil(cols / 64) zeroed words.
 // y (ReLU output) and dym are both set or both NULL.
 int tgfr_bias_grad(const float* dy, long long lddy, int rows, int cols, const float* y,
                    long long ldy, float* dym, long long lddm, float* db, float* ws,
                    unsigned* counters, void* stream) {
   if (rows <= 0 || cols <= 0 || (!y) != (!dym) || !counters) return 1001;
-  const dim3 grid((cols + 63) / 64, (rows + BG_ROWS - 1) / BG_ROWS);
   auto* st = (hipStream_t)stream;
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  const long long span = (long long)rows * (lddy > ldy ? lddy : ldy);
+  const bool vec = cols % 4 == 0 && lddy % 4 == 0 && a16(dy) && a16(db) && span < (1LL << 31) &&
+                   (!y || (ldy % 4 == 0 && lddm % 4 == 0 && a16(y) && a16(dym)));
+  if (vec) {
+    const dim3 g4((cols + 255) / 256, (rows + BG4_ROWS - 1) / BG4_ROWS);
+    if (y)
+      hipLaunchKernelGGL(bias_grad4_kernel<true>, g4, dim3(64 * BG4_WAVES), 0, st, dy, lddy, rows, cols, y,
+                         ldy, dym, lddm, ws, counters, db);
+    else
+      hipLaunchKernelGGL(bias_grad4_kernel<false>, g4, dim3(64 * BG4_WAVES), 0, st, dy, lddy, rows, cols,
+                         y, ldy, dym, lddm, ws, counters, db);
+    return (int)hipGetLastError();
+  }
+  const dim3 grid((cols + 63) / 64, (rows + BG_ROWS - 1) / BG_ROWS);
   if (y)
     hipLaunchKernelGGL(bias_grad_kernel<true>, grid, dim3(256), 0, st, dy, lddy, rows, cols, y,
                        ldy, dym, lddm, ws, counters, db);

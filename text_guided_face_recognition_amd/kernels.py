@@ -338,7 +338,7 @@ class LinearRows(torch.autograd.Function):
         want_db = has_bias and ctx.needs_input_grad[2]
         if relu or want_db:
             rows, cols = dy.shape
-            ws = torch.empty(-(-rows // 256) * cols, dtype=torch.float32, device=dy.device)
+            ws = torch.empty(-(-rows // 128) * cols, dtype=torch.float32, device=dy.device)
             db = torch.empty(cols, dtype=torch.float32, device=dy.device)
             dym = torch.empty_like(dy) if relu else None
             call("tgfr_bias_grad", ptr(dy), dy.stride(0), rows, cols, ptr(y),
@@ -472,7 +472,7 @@ class BNLinear(torch.autograd.Function):
             dp = dp.contiguous()
         dev = dp.device
         s = torch.empty(o, dtype=torch.float32, device=dev)
-        ws = torch.empty(-(-rows // 256) * o, dtype=torch.float32, device=dev)
+        ws = torch.empty(-(-rows // 128) * o, dtype=torch.float32, device=dev)
         call("tgfr_bias_grad", ptr(dp), o, rows, o, None, 0, None, 0, ptr(s), ptr(ws),
              ptr(_hip.counters(dev)), _hip.stream())
         mb = -(-o // 64) * -(-c // 64)

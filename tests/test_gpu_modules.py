@@ -247,12 +247,12 @@ def test_bn_linear_fold(gpu, training):
     assert int(bn_g.num_batches_tracked) == int(bn.num_batches_tracked)
 
 
-def test_layer_norm_rows_channel_major_affine(gpu):
+@pytest.mark.parametrize("n,c,h,w", [(4, 24, 5, 6), (64, 256, 14, 14), (13, 32, 3, 3)])
+def test_layer_norm_rows_channel_major_affine(gpu, n, c, h, w):
     """IMIM layout: channels-last rows [HW, C] with the reference's [C, H, W]
-    affine maps read in place (ch = C)."""
+    affine maps (ch = C; transposed once into the workspace)."""
     from text_guided_face_recognition_amd import kernels as K
     gen = torch.Generator().manual_seed(7)
-    n, c, h, w = 4, 24, 5, 6
     x = torch.randn(n, c, h, w, generator=gen) * 2 - 1
     wt = torch.randn(c, h, w, generator=gen)
     bs = torch.randn(c, h, w, generator=gen)

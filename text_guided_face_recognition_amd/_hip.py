@@ -48,7 +48,7 @@ SIGNATURES = {
     "tgfr_focal_ce": [P, I, I, P, F, P, P, P, P],
     "tgfr_focal_ce_bwd": [P, I, I, P, F, P, P, P, P],
     "tgfr_attn_softmax_bwd": [P, P, P, L, I, L, F, P],
-    "tgfr_ln_ws_floats": [I, L, I, P],
+    "tgfr_ln_ws_floats": [I, L, I, I, P],
     "tgfr_loss_mix": [I, P, I, P, P, P],
     "tgfr_bn_fwd_cl": [P, I, I, I, F, F, I, P, P, P, P, P, P, P],
     "tgfr_bn_fold": [P, P, I, I, P, P, P, P, P],

@@ -5,9 +5,14 @@
 // PyTorch launches one block per sample (64 blocks on a 256-CU part, ~100 us
 // for the backward).  Here every sample is cut into S slices so the launch has
 // >= ~1024 blocks:
+//   ln_aff_t    (ch > 0 only) w, b [ch][E / ch] -> channels-last copies in
+//               the workspace, so every later access to them is a coalesced
+//               float4 (the backward reuses the copies)
 //   ln_part     per (sample, slice): count-free (mean_i, M2_i) of the slice
-//   ln_apply    combine the S slice moments (Chan, fixed order) -> mean, rstd;
-//               y = (x - mean) rstd w + b; block (b, 0) stores mean/rstd
+//   ln_apply    per (element block, group of samples): combine the S slice
+//               moments (Chan, fixed order) -> mean, rstd of the group's
+//               samples; y = (x - mean) rstd w + b with w, b loaded once per
+//               thread; block (0, g) stores the group's mean/rstd
 //   ln_bwd_part per (sample, slice): sums of g = dy w and g xhat
 //   ln_bwd_dx   dx = rstd (g - mean(g) - xhat mean(g xhat)); per element e the
 //               block also sums dy xhat and dy over its group of samples
@@ -30,18 +35,37 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return red[0] + red[1] + red[2] + red[3];
 }
 
-// The affine map w, b is indexed like x's rows ([E]) or, with ch > 0, stored
+// dw, db scatter back to the reference layout: the affine map is stored
 // channel-major [ch][E / ch] while x's rows are [E / ch][ch] (IMIM's
-// LayerNorm([C, H, W]) on channels-last rows: no permuted copies of w, b).
+// LayerNorm([C, H, W]) on channels-last rows).
 __device__ __forceinline__ long long aidx(long long e, int ch, long long E) {
   return ch ? (e % ch) * (E / ch) + e / ch : e;
 }
-// 4 consecutive elements 4 i4 .. +3 (ch % 4 == 0 keeps them in one position)
-__device__ __forceinline__ float4 aff4(const float* __restrict__ a, long long i4, int ch,
-                                       long long E) {
-  if (!ch) return ((const float4*)a)[i4];
-  const long long e = i4 * 4, n = E / ch, c = e % ch, p = e / ch;
-  return make_float4(a[c * n + p], a[(c + 1) * n + p], a[(c + 2) * n + p], a[(c + 3) * n + p]);
+
+// wt[p * ch + c] = w[c * n + p] (n = E / ch), same for b: 32 x 32 LDS tiles.
+__global__ __launch_bounds__(NT) void ln_aff_t_kernel(const float* __restrict__ w,
+                                                      const float* __restrict__ b, int ch, int n,
+                                                      float* __restrict__ wt,
+                                                      float* __restrict__ bt) {
+  __shared__ float tile[2][32][33];
+  const int c0 = blockIdx.y * 32, p0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 8 rows per pass
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int c = c0 + ty + k, p = p0 + tx;
+    const bool ok = c < ch && p < n;
+    tile[0][ty + k][tx] = ok ? w[(long long)c * n + p] : 0.f;
+    tile[1][ty + k][tx] = ok ? b[(long long)c * n + p] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int p = p0 + ty + k, c = c0 + tx;
+    if (p < n && c < ch) {
+      wt[(long long)p * ch + c] = tile[0][tx][ty + k];
+      bt[(long long)p * ch + c] = tile[1][tx][ty + k];
+    }
+  }
 }
 
 struct Slice {
@@ -59,15 +83,21 @@ __global__ __launch_bounds__(NT) void ln_part_kernel(const float* __restrict__ x
   __shared__ float red[4];
   const int b = blockIdx.y, s = blockIdx.x;
   const Slice sl = slice_of(E, S, s);
-  const float* xr = x + (long long)b * E;
+  // slices are whole float4s (slice_of rounds the length to 4, E % 4 == 0)
+  const float4* xr = (const float4*)(x + (long long)b * E);
+  const long long lo = sl.lo / 4, hi = sl.hi / 4;
   float sum = 0.f;
-  for (long long e = sl.lo + threadIdx.x; e < sl.hi; e += NT) sum += xr[e];
+  for (long long i = lo + threadIdx.x; i < hi; i += NT) {
+    const float4 v = xr[i];
+    sum += (v.x + v.y) + (v.z + v.w);
+  }
   const float n = (float)(sl.hi - sl.lo);
   const float mean = n > 0.f ? block_sum(sum, red) / n : 0.f;
   float m2 = 0.f;
-  for (long long e = sl.lo + threadIdx.x; e < sl.hi; e += NT) {
-    const float d = xr[e] - mean;
-    m2 += d * d;
+  for (long long i = lo + threadIdx.x; i < hi; i += NT) {
+    const float4 v = xr[i];
+    const float a = v.x - mean, c = v.y - mean, d = v.z - mean, e = v.w - mean;
+    m2 += (a * a + c * c) + (d * d + e * e);
   }
   m2 = block_sum(m2, red);
   if (threadIdx.x == 0) {
@@ -94,26 +124,43 @@ __device__ __forceinline__ void ln_stats(const float* part, long long E, int S, 
   rstd = rsqrtf(m2 / n + eps);   // biased variance, as nn.LayerNorm
 }
 
+constexpr int LN_GROUP = 8;   // samples per ln_apply / ln_bwd_dx block
+
+// grid (ceil(E/4 / NT), ceil(rows / LN_GROUP)); w, b row-indexed ([E]).
 __global__ __launch_bounds__(NT) void ln_apply_kernel(const float* __restrict__ x, long long E,
                                                       int S, const float* __restrict__ w,
                                                       const float* __restrict__ bias, float eps,
                                                       const float* __restrict__ part,
                                                       float* __restrict__ stats, int rows,
-                                                      int ch, float* __restrict__ y) {
-  const int b = blockIdx.y;
-  float mean, rstd;
-  ln_stats(part, E, S, b, eps, mean, rstd);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    stats[b] = mean;
-    stats[rows + b] = rstd;
+                                                      float* __restrict__ y) {
+  __shared__ float ms[2][LN_GROUP];
+  const int g0 = blockIdx.y * LN_GROUP, g1 = min(rows, g0 + LN_GROUP);
+  if (threadIdx.x < g1 - g0) {
+    const int b = g0 + threadIdx.x;
+    float mean, rstd;
+    ln_stats(part, E, S, b, eps, mean, rstd);
+    ms[0][threadIdx.x] = mean;
+    ms[1][threadIdx.x] = rstd;
+    if (blockIdx.x == 0) {
+      stats[b] = mean;
+      stats[rows + b] = rstd;
+    }
   }
-  const long long n4 = E / 4;
-  const float4* x4 = (const float4*)(x + (long long)b * E);
-  float4* y4 = (float4*)(y + (long long)b * E);
-  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n4; i += gridDim.x * (long long)NT) {
-    const float4 v = x4[i], ww = aff4(w, i, ch, E), bb = aff4(bias, i, ch, E);
-    y4[i] = make_float4((v.x - mean) * rstd * ww.x + bb.x, (v.y - mean) * rstd * ww.y + bb.y,
-                        (v.z - mean) * rstd * ww.z + bb.z, (v.w - mean) * rstd * ww.w + bb.w);
+  __syncthreads();
+  const long long i = blockIdx.x * (long long)NT + threadIdx.x;
+  if (i >= E / 4) return;
+  const float4 ww = ((const float4*)w)[i], bb = ((const float4*)bias)[i];
+  float4 v[LN_GROUP];
+#pragma unroll
+  for (int k = 0; k < LN_GROUP; ++k)
+    if (g0 + k < g1) v[k] = ((const float4*)(x + (long long)(g0 + k) * E))[i];
+#pragma unroll
+  for (int k = 0; k < LN_GROUP; ++k) {
+    if (g0 + k >= g1) break;
+    const float mean = ms[0][k], rstd = ms[1][k];
+    ((float4*)(y + (long long)(g0 + k) * E))[i] =
+        make_float4((v[k].x - mean) * rstd * ww.x + bb.x, (v[k].y - mean) * rstd * ww.y + bb.y,
+                    (v[k].z - mean) * rstd * ww.z + bb.z, (v[k].w - mean) * rstd * ww.w + bb.w);
   }
 }
 
@@ -122,19 +169,22 @@ __global__ __launch_bounds__(NT) void ln_bwd_part_kernel(const float* __restrict
                                                          const float* __restrict__ x, long long E,
                                                          int S, const float* __restrict__ w,
                                                          const float* __restrict__ stats, int rows,
-                                                         int ch, float* __restrict__ part) {
+                                                         float* __restrict__ part) {
   __shared__ float red[4];
   const int b = blockIdx.y, s = blockIdx.x;
   const Slice sl = slice_of(E, S, s);
   const float mean = stats[b], rstd = stats[rows + b];
-  const float* xr = x + (long long)b * E;
-  const float* gr = dy + (long long)b * E;
+  const float4* xr = (const float4*)(x + (long long)b * E);
+  const float4* gr = (const float4*)(dy + (long long)b * E);
+  const float4* w4 = (const float4*)w;
   float sg = 0.f, sgx = 0.f;
-  for (long long e = sl.lo + threadIdx.x; e < sl.hi; e += NT) {
-    const float g = gr[e] * w[aidx(e, ch, E)];
-    sg += g;
-    sgx += g * (xr[e] - mean) * rstd;
+  for (long long i = sl.lo / 4 + threadIdx.x; i < sl.hi / 4; i += NT) {
+    const float4 d = gr[i], ww = w4[i], v = xr[i];
+    const float ga = d.x * ww.x, gb = d.y * ww.y, gc = d.z * ww.z, gd = d.w * ww.w;
+    sg += (ga + gb) + (gc + gd);
+    sgx += (ga * (v.x - mean) + gb * (v.y - mean)) + (gc * (v.z - mean) + gd * (v.w - mean));
   }
+  sgx *= rstd;
   sg = block_sum(sg, red);
   sgx = block_sum(sgx, red);
   if (threadIdx.x == 0) {
@@ -148,7 +198,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_part_kernel(const float* __restrict
 __global__ __launch_bounds__(NT) void ln_bwd_dx_kernel(
     const float* __restrict__ dy, const float* __restrict__ x, long long E, int S,
     const float* __restrict__ w, const float* __restrict__ stats, int rows,
-    const float* __restrict__ part, int per_group, int ch, float* __restrict__ dx,
+    const float* __restrict__ part, int per_group, float* __restrict__ dx,
     float* __restrict__ dwp, float* __restrict__ dbp) {
   __shared__ float coef[3][64];
   const int g0 = blockIdx.y * per_group, g1 = min(rows, g0 + per_group);
@@ -166,7 +216,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_dx_kernel(
   __syncthreads();
   const long long i = blockIdx.x * (long long)NT + threadIdx.x;
   if (i >= E / 4) return;
-  const float4 ww = aff4(w, i, ch, E);
+  const float4 ww = ((const float4*)w)[i];
   float4 dw = make_float4(0.f, 0.f, 0.f, 0.f), db = dw;
   for (int b = g0; b < g1; ++b) {
     const float mean = stats[b], rstd = coef[0][b - g0];
@@ -207,53 +257,84 @@ int slices_for(int rows, long long E) {
   return (int)std::max<long long>(1, s);
 }
 
+// Workspace floats: part [rows][S][2] | mean [rows] | rstd [rows] | (ch > 0)
+// channels-last w, b [2][E] -- all written by the forward and read by the
+// backward -- then (backward) dw, db group partials [2][G][E], G =
+// ceil(rows / LN_GROUP).
+struct LnWs {
+  long long stats, aff, bwd, total_fwd, total_bwd;
+};
+LnWs ln_ws(int rows, long long E, int ch) {
+  const long long S = slices_for(rows, E);
+  LnWs o;
+  o.stats = rows * S * 2;
+  o.aff = o.stats + 2LL * rows;
+  o.bwd = o.aff + (ch ? 2 * E : 0);
+  o.total_fwd = o.bwd;
+  o.total_bwd = o.bwd + 2LL * ((rows + LN_GROUP - 1) / LN_GROUP) * E;
+  return o;
+}
+
+bool ln_args_ok(int rows, long long E, int ch) {
+  return rows > 0 && E > 0 && !(E & 3) && rows <= 65535 && ch >= 0 &&
+         !(ch && (ch & 3 || E % ch));
+}
+
 }  // namespace
 
 extern "C" {
 
-// *out = workspace floats: rows * S * 2 + 2 * rows for the forward (mean and
-// rstd at the end, read by the backward); the backward additionally needs
-// 2 * G * E (G = ceil(rows / 8) sample groups).
-int tgfr_ln_ws_floats(int rows, long long E, int backward, long long* out) {
-  if (rows <= 0 || E <= 0 || !out) return 1001;
-  const long long S = slices_for(rows, E);
-  long long n = rows * S * 2 + 2LL * rows;
-  if (backward) n += 2LL * ((rows + 7) / 8) * E;
-  *out = n;
+int tgfr_ln_ws_floats(int rows, long long E, int ch, int backward, long long* out) {
+  if (!ln_args_ok(rows, E, ch) || !out) return 1001;
+  const LnWs o = ln_ws(rows, E, ch);
+  *out = backward ? o.total_bwd : o.total_fwd;
   return 0;
 }
 
 int tgfr_ln_fwd(const float* x, int rows, long long E, const float* w, const float* b, float eps,
                 int ch, float* y, float* ws, void* stream) {
-  if (rows <= 0 || E <= 0 || (E & 3) || rows > 65535 || ch < 0 || (ch && (ch & 3 || E % ch)))
-    return 1001;
+  if (!ln_args_ok(rows, E, ch)) return 1001;
   const int S = slices_for(rows, E);
+  const LnWs o = ln_ws(rows, E, ch);
   float* part = ws;
-  float* stats = ws + (long long)rows * S * 2;
+  float* stats = ws + o.stats;
   auto* st = (hipStream_t)stream;
+  const float* wr = w;
+  const float* br = b;
+  if (ch) {
+    float* wt = ws + o.aff;
+    const int n = (int)(E / ch);
+    hipLaunchKernelGGL(ln_aff_t_kernel, dim3((n + 31) / 32, (ch + 31) / 32), dim3(NT), 0, st, w,
+                       b, ch, n, wt, wt + E);
+    wr = wt;
+    br = wt + E;
+  }
   hipLaunchKernelGGL(ln_part_kernel, dim3(S, rows), dim3(NT), 0, st, x, E, S, part);
-  const long long blocks = std::min<long long>((E / 4 + NT - 1) / NT, 64);
-  hipLaunchKernelGGL(ln_apply_kernel, dim3((unsigned)blocks, rows), dim3(NT), 0, st, x, E, S, w,
-                     b, eps, part, stats, rows, ch, y);
+  hipLaunchKernelGGL(ln_apply_kernel,
+                     dim3((unsigned)((E / 4 + NT - 1) / NT), (rows + LN_GROUP - 1) / LN_GROUP),
+                     dim3(NT), 0, st, x, E, S, wr, br, eps, part, stats, rows, y);
   return (int)hipGetLastError();
 }
 
+// ws: the forward's workspace (its stats and, for ch > 0, its channels-last w
+// copy), sized for the backward.
 int tgfr_ln_bwd(const float* dy, const float* x, int rows, long long E, const float* w, int ch,
                 float* ws, float* dx, float* dw, float* db, void* stream) {
-  if (rows <= 0 || E <= 0 || (E & 3) || rows > 65535 || ch < 0 || (ch && (ch & 3 || E % ch)))
-    return 1001;
+  if (!ln_args_ok(rows, E, ch)) return 1001;
   const int S = slices_for(rows, E);
-  const int per = 8, groups = (rows + per - 1) / per;
+  const LnWs o = ln_ws(rows, E, ch);
+  const int groups = (rows + LN_GROUP - 1) / LN_GROUP;
   float* part = ws;
-  const float* stats = ws + (long long)rows * S * 2;
-  float* dwp = ws + (long long)rows * S * 2 + 2LL * rows;
+  const float* stats = ws + o.stats;
+  const float* wr = ch ? ws + o.aff : w;
+  float* dwp = ws + o.bwd;
   float* dbp = dwp + (long long)groups * E;
   auto* st = (hipStream_t)stream;
   // the forward's slice moments are no longer needed: reuse their slots
-  hipLaunchKernelGGL(ln_bwd_part_kernel, dim3(S, rows), dim3(NT), 0, st, dy, x, E, S, w, stats,
-                     rows, ch, part);
+  hipLaunchKernelGGL(ln_bwd_part_kernel, dim3(S, rows), dim3(NT), 0, st, dy, x, E, S, wr, stats,
+                     rows, part);
   hipLaunchKernelGGL(ln_bwd_dx_kernel, dim3((unsigned)((E / 4 + NT - 1) / NT), groups),
-                     dim3(NT), 0, st, dy, x, E, S, w, stats, rows, part, per, ch, dx, dwp, dbp);
+                     dim3(NT), 0, st, dy, x, E, S, wr, stats, rows, part, LN_GROUP, dx, dwp, dbp);
   hipLaunchKernelGGL(ln_bwd_dw_kernel, dim3((unsigned)((E + NT - 1) / NT)), dim3(NT), 0, st,
                      dwp, dbp, E, groups, ch, dw, db);
   return (int)hipGetLastError();

@@ -509,9 +509,10 @@ def _aligned(t):
     return t if t.data_ptr() % 16 == 0 else t.clone()
 
 
-def ln_ws_floats(rows, e, backward=True):
+def ln_ws_floats(rows, e, ch=0, backward=True):
     out = (ctypes.c_longlong * 1)()
-    rc = _hip.lib().tgfr_ln_ws_floats(int(rows), int(e), int(backward), ctypes.addressof(out))
+    rc = _hip.lib().tgfr_ln_ws_floats(int(rows), int(e), int(ch), int(backward),
+                                      ctypes.addressof(out))
     if rc != 0:
         raise RuntimeError(f"tgfr_ln_ws_floats failed with code {rc}")
     return int(out[0])
@@ -521,7 +522,8 @@ class LayerNormRows(torch.autograd.Function):
     """Per-sample LayerNorm over all trailing elements with an elementwise
     affine of the same size (nn.LayerNorm([C, H, W]), models.py:388/:401).
     ch > 0: x rows are channels-last [HW, ch] while weight/bias keep the
-    reference's [ch, H, W] layout (read in place, no permuted copies)."""
+    reference's [ch, H, W] layout (the forward makes channels-last copies in
+    its workspace, which the backward reuses)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, eps, ch):
@@ -530,7 +532,7 @@ class LayerNormRows(torch.autograd.Function):
         e = x2.shape[1]
         assert weight.numel() == e and bias.numel() == e
         w, b = _aligned(weight.reshape(-1)), _aligned(bias.reshape(-1))
-        ws = torch.empty(ln_ws_floats(rows, e), dtype=torch.float32, device=x.device)
+        ws = torch.empty(ln_ws_floats(rows, e, ch), dtype=torch.float32, device=x.device)
         y = torch.empty_like(x2)
         call("tgfr_ln_fwd", ptr(x2), rows, e, ptr(w), ptr(b), float(eps), int(ch), ptr(y),
              ptr(ws), _hip.stream())

@@ -91,3 +91,29 @@ def test_dma_path_configs(gpu, mode, shape, la, lb):
     ref = a.double() @ b.double()
     err = (c.double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < (2e-5 if mode == "fp32" else 1e-2), err
+
+
+@pytest.mark.parametrize("m,n,k", [(12544, 768, 256), (12544, 128, 256), (12544, 256, 128),
+                                   (4100, 200, 256), (2050, 64, 128), (3000, 130, 256)])
+@pytest.mark.parametrize("lb", ["row", "col"])
+@pytest.mark.parametrize("epi", ["plain", "bias_relu", "accumulate"])
+def test_weight_resident_path(gpu, m, n, k, lb, epi):
+    """bf16 products with a tall k-contiguous A and K = 128 / 256 take the
+    weight-resident row-stream kernel: ragged M and N, both B layouts (W[n][k]
+    forward / W[k][n] dX), the epilogues, a row stride > K on A."""
+    from text_guided_face_recognition_amd import kernels as K
+    gen = torch.Generator().manual_seed(m + n + k)
+    a = torch.randn(m, k + 4, generator=gen).to(gpu)[:, :k]          # sAm = k + 4
+    b = _operand(k, n, lb, gpu, gen)
+    bias = torch.randn(n, generator=gen).to(gpu) if epi == "bias_relu" else None
+    ref = 0.75 * (a.double() @ b.double())
+    if epi == "bias_relu":
+        ref = torch.relu(ref + bias.double())
+    out = None
+    if epi == "accumulate":
+        out = torch.randn(1, m, n, generator=gen).to(gpu)
+        ref = ref + out[0].double()
+    c = K.bgemm(a.unsqueeze(0), b.unsqueeze(0), out=out, alpha=0.75, mode="bf16", bias=bias,
+                relu=epi == "bias_relu", accumulate=epi == "accumulate")[0]
+    err = (c.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err

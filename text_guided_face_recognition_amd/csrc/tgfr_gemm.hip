@@ -34,6 +34,8 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 using namespace tgfr;
 
 namespace {
@@ -141,13 +143,13 @@ __device__ __forceinline__ int kswz(int row, int q) { return q ^ ((row >> 1) & 7
 
 // Issue this wave's share of the DMA pieces of one operand tile.
 // base: element (mn = 0, k = 0) of the tile; mn_lim / k_lim: valid extents.
-template <int LAY, int R>
+template <int LAY, int R, int NW = 4>
 __device__ __forceinline__ void issue_tile(const float* base, long long s_mn, long long s_k,
                                            int mn_lim, int k_lim, uint32_t lds_off, int wid,
                                            int lane) {
   constexpr int P = Img<LAY, R>::PIECES;
 #pragma unroll
-  for (int p = wid; p < P; p += 4) {
+  for (int p = wid; p < P; p += NW) {
     const float* src;
     if constexpr (LAY == LAY_K) {
       const int row = p * 8 + (lane >> 3);
@@ -427,6 +429,169 @@ __global__ __launch_bounds__(256) void bgemm_regs_kernel(
             bias, relu, lane);
 }
 
+// ------------------------------------------ weight-resident row stream ---
+// C = epi(alpha A B + bias) for a tall A [M][K] (k-contiguous rows) and a
+// small B [K][N] with K = 128 or 256 (a Linear / 1x1 conv weight): every
+// forward Linear of the head and the backward dX products (A = dY).
+// bgemm_glds re-reads a B tile for every 64-row block of A, which on these
+// shapes moves more bytes than A itself.  Here a persistent block owns a
+// 128-column slice of B, converts it to bf16 ONCE into an LDS image, and
+// streams its share of A's 64-row tiles through an NS-deep DMA ring that runs
+// continuously across tiles (the epilogue of tile i overlaps the DMA of tile
+// i+1).  Blocks of one A tile's slices are consecutive after the XCD remap,
+// so they read A through one L2.  8 waves (2 x 4 of 32 x 32) per block: two
+// per SIMD hide each other's LDS / convert latency.  The epilogue reads no
+// global memory (bias preloaded, no accumulate): a plain load in the loop
+// would make hipcc drain the DMA ring (vmcnt(0)) at every use.  bf16 mode
+// only (the split image would not fit beside the ring).  On the step's
+// shapes 20-25 % faster than bgemm_glds (tools/gemm_wres_ab.py).
+constexpr int WR_TM = 64, WR_TN = 128, WR_NS = 6, WR_NW = 8;
+constexpr int WR_STG = WR_TM * BK * 4;                 // one fp32 A stage
+constexpr int WR_PER = WR_STG / 1024 / WR_NW;          // DMA ops per wave per stage
+
+// B image [128 n][K] bf16, 16-B chunks XOR-swizzled by n.
+__device__ __forceinline__ uint32_t wres_off(int n, int c, int K) {
+  return (uint32_t)(n * K * 2 + ((c ^ (n & (K / 8 - 1))) << 4));
+}
+
+// Item = (n, 8-k chunk c) of the B slice: consecutive threads take
+// consecutive c for k-contiguous B (W[n][k], the forward: two float4 per
+// item) and consecutive n for n-contiguous B (W[k][n], the dX products: eight
+// coalesced dwords).  Separate instantiations: a runtime layout branch per
+// item made hipcc merge both into eight scalar loads.
+template <int K, bool KC>
+__device__ __forceinline__ void wres_load_b(const float* __restrict__ B, long long sBk,
+                                            long long sBn, int n0, int N, int tid) {
+  constexpr int ITEMS = WR_TN * (K / 8) / (64 * WR_NW), PASS = ITEMS < 8 ? ITEMS : 8;
+#pragma unroll
+  for (int p0 = 0; p0 < ITEMS; p0 += PASS) {
+    float v[PASS][8];
+#pragma unroll
+    for (int i = 0; i < PASS; ++i) {
+      const int idx = tid + 64 * WR_NW * (p0 + i);
+      const int nl = KC ? idx / (K / 8) : idx % WR_TN;
+      const int c = KC ? idx % (K / 8) : idx / WR_TN;
+      const int n = min(n0 + nl, N - 1);
+      if constexpr (KC) {
+        const float* src = B + (long long)n * sBn + 8 * c;
+        const float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
+        v[i][0] = a.x; v[i][1] = a.y; v[i][2] = a.z; v[i][3] = a.w;
+        v[i][4] = b.x; v[i][5] = b.y; v[i][6] = b.z; v[i][7] = b.w;
+      } else {
+        const float* src = B + (long long)n * sBn + (long long)(8 * c) * sBk;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[i][e] = src[e * sBk];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PASS; ++i) {
+      const int idx = tid + 64 * WR_NW * (p0 + i);
+      const int nl = KC ? idx / (K / 8) : idx % WR_TN;
+      const int c = KC ? idx % (K / 8) : idx / WR_TN;
+      if (n0 + nl >= N) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+      }
+      bf16x8 hi, lo;
+      frag8<MODE_BF16>(v[i], hi, lo);
+      lds_st16(wres_off(nl, c, K), __builtin_bit_cast(uint4, hi));
+    }
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(64 * WR_NW) void bgemm_wres_kernel(
+    const float* __restrict__ A, long long sAm, const float* __restrict__ B, long long sBk,
+    long long sBn, float* __restrict__ Cm, long long sCm, long long sCn, int M, int N,
+    float alpha, const float* __restrict__ bias, int relu, int n_slices, int per_slice) {
+  constexpr int WB = WR_TN * K * 2;                     // B image bytes
+  constexpr int NK = K / BK;
+  const int tid = threadIdx.x, wid = tid / WAVE, lane = tid % WAVE;
+  const int wm = wid >> 2, wn = wid & 3;              // 2 x 4 waves of 32 x 32
+  // block -> (slice, g): consecutive remapped ids = the slices of one A tile
+  const int total = gridDim.x;
+  const int w = xcd_remap(blockIdx.x, total);
+  const int slice = w % n_slices, g = w / n_slices;
+  const int n0 = slice * WR_TN;
+  const int m_tiles = (M + WR_TM - 1) / WR_TM;
+  // this block's A tiles: g, g + per_slice, ...
+  const int my_tiles = g < m_tiles ? (m_tiles - 1 - g) / per_slice + 1 : 0;
+  const int T = my_tiles * NK;                          // k-steps in the stream
+
+  auto issue = [&](int t) {
+    const int j = t / NK, kt = t % NK;
+    const int m0 = (g + j * per_slice) * WR_TM;
+    issue_tile<LAY_K, WR_TM, WR_NW>(A + (long long)m0 * sAm + kt * BK, sAm, 1, M - m0,
+                                    K - kt * BK,
+                             WB + (t % WR_NS) * WR_STG, wid, lane);
+  };
+#pragma unroll
+  for (int t = 0; t < WR_NS - 1; ++t)
+    if (t < T) issue(t);
+
+  // B slice -> bf16 image (plain loads, all of a pass in flight at once;
+  // overlaps the ring's first stages).
+  if (sBk == 1)
+    wres_load_b<K, true>(B, sBk, sBn, n0, N, tid);
+  else
+    wres_load_b<K, false>(B, sBk, sBn, n0, N, tid);
+
+  constexpr int NJ = WR_TN / 32 / (WR_NW / 2);          // 32-col tiles per wave
+  f32x16 acc[NJ];
+  // the epilogue's bias values, loaded once: no plain global load may sit in
+  // the loop beside the DMA ring (hipcc would drain the ring with vmcnt(0)
+  // before every use of it)
+  float bcol[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int n = n0 + wn * 32 * NJ + 32 * j + (lane & 31);
+    bcol[j] = bias && n < N ? bias[n] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
+  }
+
+  for (int t = 0; t < T; ++t) {
+    // stage t has landed once at most NS-2 younger stages (and the stores of
+    // an epilogue) are outstanding; the barrier also publishes the B image
+    if (t + WR_NS - 2 < T) ring_barrier<(WR_NS - 2) * WR_PER>();
+    else ring_barrier<0>();
+    if (t + WR_NS - 1 < T) issue(t + WR_NS - 1);
+    const uint32_t o = WB + (t % WR_NS) * WR_STG;
+    const int kt = t % NK;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      Frag8 f;
+      bf16x8 ah, al;
+      read_frag<LAY_K, WR_TM>(f, o, wm * 32, s, lane);
+      frag8<MODE_BF16>(f.v, ah, al);
+      const int c = (kt * BK + 16 * s) / 8 + (lane >> 5);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int nl = wn * 32 * NJ + 32 * j + (lane & 31);
+        const bf16x8 bh = as_bf8(lds_ld16(wres_off(nl, c, K)));
+        mma<MODE_BF16>(acc[j], ah, al, bh, bh);
+      }
+    }
+    if (kt == NK - 1) {
+      const int m0 = (g + (t / NK) * per_slice) * WR_TM;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wn * 32 * NJ + 32 * j + (lane & 31);
+        if (n < N) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int m = m0 + wm * 32 + acc_row(q, lane >> 5);
+            const float v = alpha * acc[j][q] + bcol[j];
+            if (m < M) Cm[m * sCm + n * sCn] = relu ? fmaxf(v, 0.f) : v;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
+      }
+    }
+  }
+}
+
 using GemmFn = void (*)(const float*, long long, long long, long long, const float*, long long,
                         long long, long long, float*, long long, long long, long long, int, int,
                         int, float, int, const float*, int, int, float*, unsigned*);
@@ -486,6 +651,28 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
   auto* s = (hipStream_t)stream;
   const int la = sAk == 1 ? LAY_K : sAm == 1 ? LAY_MN : LAY_ANY;
   const int lb = sBk == 1 ? LAY_K : sBn == 1 ? LAY_MN : LAY_ANY;
+  // weight-resident row stream (TGFR_GEMM_WRES=0 turns it off; read per call)
+  const char* wres_env = getenv("TGFR_GEMM_WRES");
+  const bool wres_on = !wres_env || atoi(wres_env) != 0;
+  if (wres_on && mode == MODE_BF16 && batch == 1 && ksplit == 1 && !accumulate && la == LAY_K &&
+      (K == 128 || K == 256) && M >= 2048 && dma_ok(A, LAY_K, 0, sAm, 1, M, K, 1) &&
+      (sBk != 1 || (al16(B) && (sBn & 3) == 0))) {
+    const int n_slices = (N + WR_TN - 1) / WR_TN;
+    const int m_tiles = (M + WR_TM - 1) / WR_TM;
+    // ~one block per CU: per_slice blocks stream each B slice's A tiles
+    const int per_slice = std::max(1, std::min(m_tiles, 256 / n_slices));
+    const int lds = WR_TN * K * 2 + WR_NS * WR_STG;
+    auto fn = K == 256 ? &bgemm_wres_kernel<256> : &bgemm_wres_kernel<128>;
+    static bool set[2];
+    if (!set[K == 256]) {
+      hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      set[K == 256] = true;
+    }
+    hipLaunchKernelGGL(fn, dim3(n_slices * per_slice), dim3(64 * WR_NW), lds, s, A, sAm, B, sBk,
+                       sBn, C,
+                       sCm, sCn, M, N, alpha, bias, relu, n_slices, per_slice);
+    return (int)hipGetLastError();
+  }
   const bool dma = dma_ok(A, la, sAb, sAm, sAk, M, K, batch) &&
                    dma_ok(B, lb, sBb, sBn, sBk, N, K, batch);
   int TM = 64, TN = 64;

@@ -243,6 +243,25 @@ int tgfr_bn_unfold(const float* G, const float* s, const float* W, int O, int C,
                    const float* gamma, const float* beta, float* dW, float* dgamma, float* dbeta,
                    float* ws, unsigned* counters, void* stream);
 
+/* ---- ArcMarginProduct (models/metrics.py:17-60), fused --------------------
+ * tgfr_arc_fwd: logits[b][c] = s * margin(cos[b][c]) with cos = normalize(x_b)
+ * . normalize(W_c) (F.normalize eps), the additive angular margin on column
+ * label[b] (easy_margin or the th / mm fallback, :45-57); also writes cos
+ * [B][C], xn = normalize(x) [B][D] and the inverse norms inv_nx [B], inv_nw
+ * [C] for the backward.  fp32 FMA.  D % 4 == 0, D <= 1024, 16-B aligned rows.
+ * tgfr_arc_bwd: from dlogits, dW = the gradient w.r.t. W (margin backward and
+ * the l2-norm backward fused) and, when dcs is non-NULL, dcs[b][c] = dcos[b][c]
+ * * inv_nw[c], so that d normalize(x) = dcs W (a GEMM) feeds
+ * tgfr_l2norm_rows_bwd for dx.  B <= 1024. */
+int tgfr_arc_fwd(const float* x, long long ldx, int B, int D, const float* W, long long ldw,
+                 int C, const long long* label, float s, float m, int easy, float eps,
+                 float* logits, float* cosv, float* xn, float* inv_nx, float* inv_nw,
+                 void* stream);
+int tgfr_arc_bwd(const float* dlogits, const float* cosv, const long long* label,
+                 const float* xn, const float* W, long long ldw, const float* inv_nw, int B,
+                 int D, int C, float s, float m, int easy, float eps, float* dW, long long lddw,
+                 float* dcs, void* stream);
+
 /* ---- optimiser step ------------------------------------------------------
  * Every trainable tensor of a trainer in one launch (replaces the two torch
  * optimiser steps of src/train_encoders_bert.py:212-222 / :323-330 and

@@ -168,6 +168,51 @@ def test_arc_margin_and_focal(gpu):
     assert _relerr(lg.grad, g["d_logits"]) < 1e-4
 
 
+@pytest.mark.parametrize("b,d,c,easy,precision", [
+    (64, 256, 4500, False, "bf16"), (64, 640, 1000, False, "fp32"), (13, 256, 300, True, "fp32"),
+    (70, 128, 37, False, "bf16")])
+def test_arc_head_fused(gpu, b, d, c, easy, precision):
+    """The fused ArcMarginProduct launches (tgfr_arc_fwd / tgfr_arc_bwd) vs torch
+    fp32 autograd of F.linear(F.normalize(x), F.normalize(W)) + the margin:
+    logits, dx (through the GEMM + l2-norm backward) and dW; ragged batch and
+    class counts, D = 640 (the stage-2 head), easy margin; plus a frozen input
+    (no dx path).  Tolerances: fp32 logits 1e-5, dW 1e-4, dx 1e-4 (fp32 mode)
+    / 1e-2 (the bf16 dx GEMM)."""
+    import math
+    from text_guided_face_recognition_amd.models.metrics import ArcMarginProduct
+    gen = torch.Generator().manual_seed(b + d + c)
+    x = torch.randn(b, d, generator=gen)
+    lab = torch.randint(0, c, (b,), generator=gen)
+    probe = torch.randn(b, c, generator=gen)
+    head = ArcMarginProduct(d, c, s=30, m=0.5, easy_margin=easy).to(gpu)
+    head.precision = precision
+    w = head.weight.detach().cpu().clone()
+    xo, wo = x.clone().requires_grad_(), w.clone().requires_grad_()
+    cos = torch.nn.functional.linear(torch.nn.functional.normalize(xo),
+                                     torch.nn.functional.normalize(wo))
+    sine = torch.sqrt((1.0 - cos * cos).clamp(0, 1))
+    phi = cos * math.cos(0.5) - sine * math.sin(0.5)
+    if easy:
+        phi = torch.where(cos > 0, phi, cos)
+    else:
+        phi = torch.where(cos > math.cos(math.pi - 0.5), phi,
+                          cos - math.sin(math.pi - 0.5) * 0.5)
+    one_hot = torch.zeros_like(cos).scatter_(1, lab.view(-1, 1), 1)
+    ref = (one_hot * phi + (1 - one_hot) * cos) * 30
+    (ref * probe).sum().backward()
+    xg = x.to(gpu).requires_grad_()
+    out = head(xg, lab.to(gpu))
+    (out * probe.to(gpu)).sum().backward()
+    assert _relerr(out, ref.detach().numpy()) < 1e-5
+    assert _relerr(head.weight.grad, wo.grad.numpy()) < 1e-4
+    assert _relerr(xg.grad, xo.grad.numpy()) < (1e-4 if precision == "fp32" else 1e-2)
+    # frozen input (the text classifier's sentence features): W grad only
+    head.weight.grad = None
+    out2 = head(x.to(gpu), lab.to(gpu))
+    (out2 * probe.to(gpu)).sum().backward()
+    assert _relerr(head.weight.grad, wo.grad.numpy()) < 1e-4
+
+
 def test_l2norm_rows(gpu):
     from text_guided_face_recognition_amd import kernels as K
     torch.manual_seed(4)

@@ -58,6 +58,8 @@ SIGNATURES = {
     "tgfr_ln_fwd": [P, I, L, P, P, F, I, P, P, P],
     "tgfr_ln_bwd": [P, P, I, L, P, I, P, P, P, P, P],
     "tgfr_optim_step": [P, I, P, I, P, P],
+    "tgfr_arc_fwd": [P, L, I, I, P, L, I, P, F, F, I, F, P, P, P, P, P, P],
+    "tgfr_arc_bwd": [P, P, P, P, P, L, P, I, I, I, F, F, I, F, P, L, P, P],
 }
 
 

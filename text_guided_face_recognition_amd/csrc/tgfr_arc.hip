@@ -1,0 +1,360 @@
+// ArcMarginProduct (models/metrics.py:17-60) as two fused launches:
+//
+//   arc_fwd   logits[b][c] = s * margin(cos), cos = normalize(x_b) .
+//             normalize(W_c) (F.linear of the two F.normalize, :43-44) with the
+//             additive angular margin on the label column (:45-57) -- one
+//             launch instead of two row normalisations, a GEMM and the margin
+//   arc_bwd   dcos from dlogits through the margin; dW_c = d normalize(W_c)
+//             applied to dWn_c = sum_b dcos[b][c] xn_b (the l2-norm backward
+//             fused in); dcs[b][c] = dcos[b][c] / |W_c| for the input side
+//             (dxn = dcs W, a plain GEMM, then the x l2-norm backward)
+//
+// fp32 FMA throughout (the products are 64 x 4500 x 256: far from MFMA-bound
+// and the fp32 sums match the reference more closely than bf16).  Block = 16
+// classes (32 in the forward); the class tile of W and a chunk of x rows sit in LDS (rows padded
+// by 4 floats so the 16 classes of a 16-lane group read distinct banks).
+#include "tgfr_common.h"
+
+#include <math.h>
+
+#include <algorithm>
+
+using namespace tgfr;
+
+namespace {
+
+constexpr int CB = 16;          // classes per block
+constexpr int NT = 256;
+
+__device__ __forceinline__ float group16_sum(float v) {
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *(const float4*)p; }
+__device__ __forceinline__ float4 lds4(uint32_t off) {
+  return __builtin_bit_cast(float4, lds_ld16(off));
+}
+
+// Rows [r0, r0 + n) of a [rows][D] matrix -> LDS rows of stride (D + 4)
+// floats, zero rows past `rows`.  Eight loads per thread are issued before
+// the first LDS store (a load-store loop would pay one L2 round trip per
+// float4).
+__device__ __forceinline__ void stage_rows(const float* __restrict__ src, long long ld, int r0,
+                                           int n, int rows, int D, uint32_t off) {
+  constexpr int U = 8;
+  const int q = D / 4, total = n * q;
+  for (int base = threadIdx.x; base < total; base += NT * U) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(base + u * NT, total - 1);
+      const int r = i / q, k = i % q;
+      const int row = min(r0 + r, rows - 1);
+      v[u] = ld4(src + (long long)row * ld + 4 * k);
+      if (r0 + r >= rows) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * NT;
+      if (i < total) {
+        const int r = i / q, k = i % q;
+        lds_st16(off + (uint32_t)((r * (D + 4) + 4 * k) * 4), __builtin_bit_cast(uint4, v[u]));
+      }
+    }
+  }
+}
+
+// 1 / max(|row|, eps) of n LDS rows (16 lanes per row) -> out[r]
+__device__ __forceinline__ void row_inv_norms(uint32_t off, int n, int D, float eps, float* out) {
+  const int g = threadIdx.x & 15;
+  for (int r = threadIdx.x >> 4; r < n; r += NT / 16) {
+    float ss = 0.f;
+    for (int k = g; k < D / 4; k += 16) {
+      const float4 v = lds4(off + (uint32_t)((r * (D + 4) + 4 * k) * 4));
+      ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    ss = group16_sum(ss);
+    if (g == 0) out[r] = 1.f / fmaxf(sqrtf(ss), eps);
+  }
+}
+
+struct Margin {
+  float s, cos_m, sin_m, th, mm;
+  int easy;
+};
+
+__device__ __forceinline__ float margin_fwd(float cv, bool target, const Margin& M) {
+  float v = cv;
+  if (target) {
+    const float sine = sqrtf(fminf(fmaxf(1.f - cv * cv, 0.f), 1.f));
+    const float phi = cv * M.cos_m - sine * M.sin_m;
+    v = M.easy ? (cv > 0.f ? phi : cv) : (cv > M.th ? phi : cv - M.mm);
+  }
+  return v * M.s;
+}
+
+__device__ __forceinline__ float margin_bwd(float g, float cv, bool target, const Margin& M) {
+  g *= M.s;
+  if (target && (M.easy ? cv > 0.f : cv > M.th)) {
+    const float one_m = 1.f - cv * cv;
+    const float sine = sqrtf(fminf(fmaxf(one_m, 0.f), 1.f));
+    const float dsine = (one_m >= 0.f && one_m <= 1.f) ? -cv / sine : 0.f;
+    g *= M.cos_m - M.sin_m * dsine;
+  }
+  return g;
+}
+
+// LDS: W tile [CBF][D+4] | x chunk [RB][D+4] | inv_nw [CBF] | inv_nx [RB] |
+// labels [B] (int).  Thread: classes c, c + 16 (c = tid % 16), rows
+// tid / 16 + 16 j (j < 4) of the chunk: 8 outputs from 2 W + 4 x reads per
+// float4 step.
+constexpr int CBF = 32;         // classes per forward block
+
+__global__ __launch_bounds__(NT) void arc_fwd_kernel(
+    const float* __restrict__ x, long long ldx, int B, int D, const float* __restrict__ W,
+    long long ldw, int C, const long long* __restrict__ label, Margin M, float eps, int RB,
+    float* __restrict__ logits, float* __restrict__ cosv, float* __restrict__ xn,
+    float* __restrict__ inv_nx, float* __restrict__ inv_nw) {
+  float* lds_f = (float*)g_smem;
+  const uint32_t w_off = 0, x_off = CBF * (D + 4) * 4;
+  // the x chunk region also carries the k-half exchange (2048 floats)
+  float* nw = lds_f + CBF * (D + 4) + max(RB * (D + 4), 2048);
+  float* nx = nw + CBF;
+  int* lab = (int*)(nx + RB);
+  const int c0 = blockIdx.x * CBF, tid = threadIdx.x, c = tid & 15;
+  for (int b = tid; b < B; b += NT) {
+    const long long l = label[b];
+    lab[b] = l >= c0 && l < c0 + CBF ? (int)(l - c0) : -1;    // column within the block
+  }
+  stage_rows(W, ldw, c0, CBF, C, D, w_off);
+  __syncthreads();
+  row_inv_norms(w_off, CBF, D, eps, nw);
+  for (int b0 = 0; b0 < B; b0 += RB) {
+    const int nb = min(RB, B - b0);
+    __syncthreads();                       // previous chunk's readers are done
+    stage_rows(x, ldx, b0, nb, B, D, x_off);
+    __syncthreads();
+    row_inv_norms(x_off, nb, D, eps, nx);
+    __syncthreads();
+    if (blockIdx.x == 0) {                 // the normalised rows, for the backward
+      const int q = D / 4;
+      for (int i = tid; i < nb * q; i += NT) {
+        const int r = i / q, k = i % q;
+        float4 v = lds4(x_off + (uint32_t)((r * (D + 4) + 4 * k) * 4));
+        const float s = nx[r];
+        v.x *= s; v.y *= s; v.z *= s; v.w *= s;
+        *(float4*)(xn + (long long)(b0 + r) * D + 4 * k) = v;
+      }
+      for (int r = tid; r < nb; r += NT) inv_nx[b0 + r] = nx[r];
+    }
+    // cos on v_mfma_f32_32x32x2_f32 (fp32 operands, fp32 sums): wave w owns
+    // row tile rt = w & 1 (32 rows; rows past the chunk re-read its last row,
+    // masked at the store) and k half kh = w >> 1 of D; one float4 LDS read
+    // per operand feeds two MFMAs (lane half h uses elements h and h + 2).
+    {                                      // nb <= 64: one pass
+      const int w = tid >> 6, lane = tid & 63, rt = w & 1, kh = w >> 1, h = lane >> 5;
+      const int row = min(32 * rt + (lane & 31), nb - 1);
+      const uint32_t xa = x_off + (uint32_t)(row * (D + 4) * 4);
+      const uint32_t wa = w_off + (uint32_t)((lane & 31) * (D + 4) * 4);
+      f32x16 acc;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+      const int k_lo = kh * (D / 2), k_hi = k_lo + D / 2;
+#pragma unroll 4
+      for (int k = k_lo; k < k_hi; k += 4) {
+        const float4 av = lds4(xa + 4 * k), bv = lds4(wa + 4 * k);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? av.y : av.x, h ? bv.y : bv.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? av.w : av.z, h ? bv.w : bv.z, acc, 0, 0, 0);
+      }
+      // k halves: waves 2, 3 hand their sums to waves 0, 1 through LDS (the
+      // x chunk's space is free once every wave has passed the barrier)
+      __syncthreads();
+      float* xs = (float*)(g_smem + x_off);
+      if (kh == 1) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) xs[(rt * 16 + q) * 64 + lane] = acc[q];
+      }
+      __syncthreads();
+      if (kh == 0) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int r = 32 * rt + acc_row(q, h), cc = lane & 31;
+          const float v = acc[q] + xs[(rt * 16 + q) * 64 + lane];
+          if (r < nb && c0 + cc < C) {
+            const int b = b0 + r;
+            const float cv = v * nx[r] * nw[cc];
+            const long long e = (long long)b * C + c0 + cc;
+            cosv[e] = cv;
+            logits[e] = margin_fwd(cv, lab[b] == cc, M);
+          }
+        }
+      }
+    }
+  }
+  if (tid < CBF && c0 + tid < C) inv_nw[c0 + tid] = nw[tid];
+}
+
+// LDS: dcos [B][CB] | xn chunk [RB][D+4]
+// thread: class c = tid / 16, d-group g = tid % 16 owns dims 4 g + 64 j
+template <int NJ>   // float4 columns per thread: D = 64 NJ (NJ = 0: any D <= 1024)
+__global__ __launch_bounds__(NT) void arc_bwd_kernel(
+    const float* __restrict__ dlogits, const float* __restrict__ cosv,
+    const long long* __restrict__ label, const float* __restrict__ xn,
+    const float* __restrict__ W, long long ldw, const float* __restrict__ inv_nw, int B, int D,
+    int C, Margin M, float eps, int RB, float* __restrict__ dW, long long lddw,
+    float* __restrict__ dcs) {
+  float* dc = (float*)g_smem;
+  const uint32_t x_off = (uint32_t)(B * CB * 4);
+  const int c0 = blockIdx.x * CB, tid = threadIdx.x;
+  const int c = tid >> 4, g = tid & 15, col = c0 + c;
+  constexpr int MAXJ = NJ ? NJ : 16;       // D <= 1024
+  const int nj = NJ ? NJ : D / 64 + ((D % 64) > 4 * g ? 1 : 0);
+  // this thread's W row slice, needed only at the end: loaded first so its
+  // latency hides under the rest
+  float4 wv[MAXJ];
+  {
+    const float* wr = W + (long long)min(col, C - 1) * ldw + 4 * g;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j)
+      wv[j] = j < nj ? ld4(wr + 64 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // dcos of the block's columns (all loads of a thread issued together)
+  for (int base = tid; base < B * CB; base += NT * 4) {
+    float gl[4], cv[4], iw[4];
+    bool tg[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = min(base + u * NT, B * CB - 1);
+      const int b = i / CB, col = min(c0 + i % CB, C - 1);
+      const long long e = (long long)b * C + col;
+      gl[u] = dlogits[e];
+      cv[u] = cosv[e];
+      iw[u] = inv_nw[col];
+      tg[u] = label[b] == col;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = base + u * NT;
+      if (i < B * CB) {
+        const int b = i / CB, col = c0 + i % CB;
+        float d = 0.f;
+        if (col < C) {
+          d = margin_bwd(gl[u], cv[u], tg[u], M);
+          if (dcs) dcs[(long long)b * C + col] = d * iw[u];
+        }
+        dc[i] = d;
+      }
+    }
+  }
+  float4 acc[MAXJ];
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b0 = 0; b0 < B; b0 += RB) {
+    const int nb = min(RB, B - b0);
+    __syncthreads();
+    stage_rows(xn, D, b0, nb, B, D, x_off);
+    __syncthreads();
+    for (int r = 0; r < nb; ++r) {
+      const float a = dc[(b0 + r) * CB + c];
+#pragma unroll
+      for (int j = 0; j < MAXJ; ++j) {
+        if (j < nj) {
+          const float4 v = lds4(x_off + (uint32_t)((r * (D + 4) + 4 * g + 64 * j) * 4));
+          acc[j].x = fmaf(a, v.x, acc[j].x);
+          acc[j].y = fmaf(a, v.y, acc[j].y);
+          acc[j].z = fmaf(a, v.z, acc[j].z);
+          acc[j].w = fmaf(a, v.w, acc[j].w);
+        }
+      }
+    }
+  }
+  if (col >= C) return;                    // whole 16-lane groups leave together
+  const float inv = inv_nw[col];
+  const bool clamped = inv >= 1.f / eps;   // |W_c| <= eps: y = W / eps, no projection
+  float4 wn[MAXJ];
+  float dot = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    if (j < nj) {
+      const float4 w = wv[j];
+      wn[j] = make_float4(w.x * inv, w.y * inv, w.z * inv, w.w * inv);
+      dot += wn[j].x * acc[j].x + wn[j].y * acc[j].y + wn[j].z * acc[j].z + wn[j].w * acc[j].w;
+    }
+  }
+  dot = clamped ? 0.f : group16_sum(dot);
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    if (j < nj) {
+      const float4 o = make_float4((acc[j].x - wn[j].x * dot) * inv, (acc[j].y - wn[j].y * dot) * inv,
+                                   (acc[j].z - wn[j].z * dot) * inv, (acc[j].w - wn[j].w * dot) * inv);
+      *(float4*)(dW + (long long)col * lddw + 4 * g + 64 * j) = o;
+    }
+  }
+}
+
+Margin make_margin(float s, float m, int easy) {
+  const float PI = 3.14159265358979323846f;
+  return Margin{s, cosf(m), sinf(m), cosf(PI - m), sinf(PI - m) * m, easy};
+}
+
+bool a16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// rows per x chunk so that the LDS stays under 128 KiB
+int chunk_rows(int B, int D, int fixed_floats) {
+  const int budget = 32768 - fixed_floats;
+  return std::max(1, std::min(B, budget / (D + 4)));
+}
+
+}  // namespace
+
+extern "C" {
+
+int tgfr_arc_fwd(const float* x, long long ldx, int B, int D, const float* W, long long ldw,
+                 int C, const long long* label, float s, float m, int easy, float eps,
+                 float* logits, float* cosv, float* xn, float* inv_nx, float* inv_nw,
+                 void* stream) {
+  if (B <= 0 || B > 4096 || C <= 0 || D <= 0 || D % 8 || D > 1024 || ldx % 4 || ldw % 4 ||
+      !a16(x) || !a16(W) || !a16(xn))
+    return 1001;
+  // <= 64 rows per chunk: one pass of the two 32-row MFMA tiles per chunk
+  const int RB = std::min(64, chunk_rows(B, D, CBF * (D + 4) + CBF + B + 64));
+  const int lds = (CBF * (D + 4) + std::max(RB * (D + 4), 2048) + CBF + RB + B) * 4;
+  static bool set = false;
+  if (!set) {
+    hipFuncSetAttribute((const void*)arc_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    set = true;
+  }
+  hipLaunchKernelGGL(arc_fwd_kernel, dim3((C + CBF - 1) / CBF), dim3(NT), lds, (hipStream_t)stream,
+                     x, ldx, B, D, W, ldw, C, label, make_margin(s, m, easy), eps, RB, logits,
+                     cosv, xn, inv_nx, inv_nw);
+  return (int)hipGetLastError();
+}
+
+int tgfr_arc_bwd(const float* dlogits, const float* cosv, const long long* label,
+                 const float* xn, const float* W, long long ldw, const float* inv_nw, int B,
+                 int D, int C, float s, float m, int easy, float eps, float* dW, long long lddw,
+                 float* dcs, void* stream) {
+  if (B <= 0 || C <= 0 || D <= 0 || D % 4 || D > 1024 || ldw % 4 || lddw % 4 || !a16(W) ||
+      !a16(dW) || !a16(xn) || B * CB > 16384)
+    return 1001;
+  const int RB = chunk_rows(B, D, B * CB);
+  const int lds = (B * CB + RB * (D + 4)) * 4;
+  using Fn = decltype(&arc_bwd_kernel<0>);
+  Fn fn = D == 128 ? &arc_bwd_kernel<2> : D == 256 ? &arc_bwd_kernel<4>
+        : D == 512 ? &arc_bwd_kernel<8> : D == 640 ? &arc_bwd_kernel<10> : &arc_bwd_kernel<0>;
+  static bool set[5];
+  const int which = D == 128 ? 0 : D == 256 ? 1 : D == 512 ? 2 : D == 640 ? 3 : 4;
+  if (!set[which]) {
+    hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    set[which] = true;
+  }
+  hipLaunchKernelGGL(fn, dim3((C + CB - 1) / CB), dim3(NT), lds, (hipStream_t)stream, dlogits,
+                     cosv, label, xn, W, ldw, inv_nw, B, D, C, make_margin(s, m, easy), eps, RB,
+                     dW, lddw, dcs);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

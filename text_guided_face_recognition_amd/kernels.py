@@ -622,6 +622,59 @@ def arc_margin(cosine, label, s, m, easy_margin=False):
     return ArcMargin.apply(cosine, label, s, m, easy_margin)
 
 
+class ArcHead(torch.autograd.Function):
+    """ArcMarginProduct.forward (metrics.py:43-57) in one launch each way:
+    normalise x and W, cosine, margin (tgfr_arc_fwd); margin backward, dW with
+    the l2-norm backward fused (tgfr_arc_bwd); dx = l2-norm backward of
+    (dcos / |W|) W (one GEMM + one row kernel, only when x needs a gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, label, s, m, easy, eps, mode):
+        x2 = _aligned(x)
+        w = _aligned(weight)
+        label = label.to(torch.int64).contiguous()
+        b, d = x2.shape
+        c = w.shape[0]
+        dev = x2.device
+        logits = torch.empty(b, c, dtype=torch.float32, device=dev)
+        cosv = torch.empty_like(logits)
+        xn = torch.empty_like(x2)
+        inv_nx = torch.empty(b, dtype=torch.float32, device=dev)
+        inv_nw = torch.empty(c, dtype=torch.float32, device=dev)
+        call("tgfr_arc_fwd", ptr(x2), d, b, d, ptr(w), d, c, ptr(label), float(s), float(m),
+             int(easy), float(eps), ptr(logits), ptr(cosv), ptr(xn), ptr(inv_nx), ptr(inv_nw),
+             _hip.stream())
+        ctx.save_for_backward(w, label, cosv, xn, inv_nx, inv_nw)
+        ctx.cfg = (float(s), float(m), int(easy), float(eps), mode)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        w, label, cosv, xn, inv_nx, inv_nw = ctx.saved_tensors
+        s, m, easy, eps, mode = ctx.cfg
+        b, d = xn.shape
+        c = w.shape[0]
+        dl = dlogits.float().contiguous()
+        dw = torch.empty_like(w)
+        want_dx = ctx.needs_input_grad[0]
+        dcs = torch.empty(b, c, dtype=torch.float32, device=w.device) if want_dx else None
+        call("tgfr_arc_bwd", ptr(dl), ptr(cosv), ptr(label), ptr(xn), ptr(w), d, ptr(inv_nw),
+             b, d, c, s, m, easy, eps, ptr(dw), d, ptr(dcs), _hip.stream())
+        dx = None
+        if want_dx:
+            mb = -(-b // 64) * -(-d // 64)
+            dxn = bgemm(dcs.unsqueeze(0), w.unsqueeze(0), mode=mode,
+                        ksplit=_ksplit(c, mb))[0]
+            dx = torch.empty_like(xn)
+            call("tgfr_l2norm_rows_bwd", ptr(dxn), d, ptr(xn), d, ptr(inv_nx), b, d, eps,
+                 ptr(dx), d, _hip.stream())
+        return dx, dw, None, None, None, None, None, None
+
+
+def arc_head(x, weight, label, s, m, easy_margin=False, eps=1e-12, mode="fp32"):
+    return ArcHead.apply(x, weight, label, s, m, easy_margin, eps, mode)
+
+
 class FocalCE(torch.autograd.Function):
     """FocalLoss(gamma)(logits, target) (losses.py:313-325)."""
 

@@ -1,7 +1,7 @@
 """ArcMarginProduct (models/metrics.py:17-60): the identity head that runs
 after the hot path every step.  Row normalisation,
-the cosine GEMM (split-bf16 MFMA) and the margin (with the one-hot that is
-CUDA-only in the reference, :53) each run as one gfx950 kernel."""
+the cosine product and the margin (with the one-hot that is CUDA-only in the
+reference, :53) run as one gfx950 launch each way (csrc/tgfr_arc.hip)."""
 from __future__ import annotations
 
 import math
@@ -33,8 +33,8 @@ class ArcMarginProduct(nn.Module):
         self.precision = "fp32"
 
     def forward(self, input, label):
-        # cos = normalize(x) normalize(W)^T on the split-bf16 MFMA GEMM, then the
-        # fused margin kernel (the reference's 15 elementwise ops, :45-57)
-        cosine = K.linear_rows(K.l2norm_rows(input), K.l2norm_rows(self.weight),
-                               mode=self.precision)
-        return K.arc_margin(cosine, label, self.s, self.m, self.easy_margin)
+        # normalize(x) normalize(W)^T and the margin (the reference's two
+        # F.normalize, F.linear and 15 elementwise ops, :43-57) in one fp32
+        # launch each way (kernels.ArcHead)
+        return K.arc_head(input, self.weight, label, self.s, self.m, self.easy_margin,
+                          mode=self.precision)

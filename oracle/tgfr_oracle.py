@@ -26,6 +26,7 @@ Reference anchors (paths relative to the reference checkout):
   IMIM                models/models.py:380-405
   ImageHeading        models/models.py:328-338
   ArcMarginProduct    models/metrics.py:17-60
+  TextHeading         models/models.py:170-232 (Bert_Word_Mapping + TextHeading)
 """
 from __future__ import annotations
 
@@ -38,7 +39,7 @@ import torch.nn.functional as F
 __all__ = [
     "cosine_similarity", "func_attention", "words_loss", "sent_loss",
     "global_loss", "clip_loss", "focal_loss", "self_attention", "working",
-    "projection_head", "imim", "image_heading", "arc_margin",
+    "projection_head", "imim", "image_heading", "arc_margin", "text_heading",
 ]
 
 
@@ -231,3 +232,29 @@ def arc_margin(x, weight, label, s=30.0, m=0.5, easy_margin=False):
     one_hot = torch.zeros_like(cosine)
     one_hot.scatter_(1, label.view(-1, 1).long(), 1)
     return (one_hot * phi + (1.0 - one_hot) * cosine) * s
+
+
+def text_heading(words_emb, conv_w, conv_b, bert_words_num=None):
+    """models.py:170-232 (forward of TextHeading; run under no_grad in the
+    reference, utils/dataset_utils.py:42).
+
+    words_emb [B, L-1, 768] (BERT last hidden state without [CLS],
+    models.py:166); conv_w[k] [256, 1, K, 768], conv_b[k] [256] for K = 2, 3, 4.
+    Returns (words [B, 256, L-2] -- a transposed view of [B, L-2, 256] storage,
+    as :231 -- and sent [B, 256]).
+    """
+    x = words_emb.unsqueeze(1)                                            # :182
+    x = [F.relu(F.conv2d(x, w, b)).squeeze(3) for w, b in zip(conv_w, conv_b)]  # :183
+    L = words_emb.shape[1] + 1 if bert_words_num is None else bert_words_num
+    a, b_, c = (t.transpose(2, 1) for t in x)                             # :199-201
+    code = []
+    seq = L - 1 - 3                                                       # :204
+    for i in range(a.shape[0]):
+        t = [torch.amax(torch.stack((a[i, j], b_[i, j], c[i, j])), dim=0) for j in range(seq)]
+        t += [torch.amax(torch.stack((a[i, seq], b_[i, seq])), dim=0)]   # :206
+        t += [a[i, seq + 1].float()]                                      # :207
+        code.append(torch.stack(t))
+    words = F.normalize(torch.stack(code), p=2, dim=2)                    # :211-212
+    pooled = [F.max_pool1d(t, t.size(2)).squeeze(2) for t in x]          # :217
+    sent = F.normalize(torch.stack(pooled).mean(dim=0), p=2, dim=1)       # :218-219
+    return words.transpose(1, 2), sent

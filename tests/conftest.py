@@ -32,3 +32,15 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     return torch.device("cuda:0")
+
+
+def text_heading_golden(name):
+    """A TextHeading fixture with its conv weights regenerated from the stored
+    seed (tests/golden/make_golden.py:text_heading_inputs)."""
+    from tests.golden.make_golden import text_heading_inputs
+    g = load_golden(name)
+    b, L = g["words_emb"].shape[0], int(g["bert_words_num"])
+    words, ws, bs = text_heading_inputs(int(g["seed"]), b, L)
+    assert np.array_equal(words, g["words_emb"])
+    g["conv_w"], g["conv_b"] = ws, bs
+    return g

@@ -239,6 +239,39 @@ def gen_image_heading(ref_models):
           **_params(net), **grads)
 
 
+def text_heading_inputs(seed, b, L):
+    """Deterministic TextHeading inputs (numpy PCG64, stable across versions):
+    BERT last hidden state without [CLS] [b, L-1, 768] and the three conv
+    weights [256, 1, K, 768] / biases [256] for K = 2, 3, 4.  The test side
+    regenerates the 7 MB of weights from the seed instead of storing them."""
+    rng = np.random.default_rng(seed)
+    words = rng.standard_normal((b, L - 1, 768), dtype=np.float32)
+    ws, bs = [], []
+    for k in (2, 3, 4):
+        bound = 1.0 / np.sqrt(k * 768.0)
+        ws.append((rng.uniform(-bound, bound, (256, 1, k, 768))).astype(np.float32))
+        bs.append((rng.uniform(-bound, bound, (256,))).astype(np.float32))
+    return words, ws, bs
+
+
+def gen_text_heading(ref_models):
+    """models/models.py:170-232, run as the trainer does (no_grad,
+    utils/dataset_utils.py:42); torch.cuda.FloatTensor (:207) is the one
+    CUDA-only call and is patched to a CPU float copy."""
+    torch.cuda.FloatTensor = lambda t: t.float()
+    for seed, b, L in ((700, 3, 32), (701, 2, 24)):
+        args = _Args(bert_words_num=L)
+        net = ref_models.TextHeading(args).eval()
+        words, ws, bs = text_heading_inputs(seed, b, L)
+        with torch.no_grad():
+            for conv, w, bb in zip(net.bwm.convs1, ws, bs):
+                conv.weight.copy_(torch.from_numpy(w))
+                conv.bias.copy_(torch.from_numpy(bb))
+            w_out, s_out = net(torch.from_numpy(words), torch.zeros(b, 768))
+        _save(f"text_heading_b{b}_l{L}", seed=seed, bert_words_num=L,
+              words_emb=words, words_out=w_out.contiguous(), sent_out=s_out)
+
+
 def main():
     root = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
     torch.set_num_threads(8)
@@ -249,6 +282,7 @@ def main():
     gen_self_attention(ref_fus)
     gen_working(ref_fus)
     gen_image_heading(ref_models)
+    gen_text_heading(ref_models)
 
 
 if __name__ == "__main__":

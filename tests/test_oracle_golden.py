@@ -148,3 +148,13 @@ def test_image_heading():
     ((gp * t(g["probe_g"])).sum() + (r * t(g["probe_r"])).sum()).backward()
     close(gi.grad, g["d_global"], atol=1e-5)
     close(li.grad, g["d_local"], atol=1e-4, rtol=1e-3)
+
+
+@pytest.mark.parametrize("tag", ["b3_l32", "b2_l24"])
+def test_text_heading(tag):
+    from conftest import text_heading_golden
+    g = text_heading_golden(f"text_heading_{tag}")
+    words, sent = O.text_heading(t(g["words_emb"]), [t(w) for w in g["conv_w"]],
+                                 [t(b) for b in g["conv_b"]], int(g["bert_words_num"]))
+    close(words, g["words_out"])
+    close(sent, g["sent_out"])

@@ -293,6 +293,31 @@ typedef struct {
 int tgfr_optim_step(const tgfr_optim_seg* segs, int n_segs, const tgfr_optim_group* groups,
                     int n_groups, int* counters, void* stream);
 
+/* TextHeading / Bert_Word_Mapping forward (models/models.py:170-232; run under
+ * no_grad by utils/dataset_utils.py:42-45).
+ *   tgfr_text_pack: conv_w, a host array of 3 device pointers to the
+ *     Conv2d(1, 256, (K, 768)) weights [256][K*768] for K = 2, 3, 4 -> taps,
+ *     tgfr_text_pack_bytes(mode) bytes of bf16 planes [9 taps][256][768] in
+ *     the kernel's staging order (opaque to the caller)
+ *     (hi, plus lo in mode 1).  Run once per weight update (the module
+ *     caches it; the reference never updates these weights, no gradient
+ *     reaches them).
+ *   tgfr_text_heading: X [B][L1][768] fp32 BERT hidden states without [CLS]
+ *     (L1 = bert_words_num - 1 >= 4), conv_b host array of 3 device pointers
+ *     to the biases [256].  Writes words [B][L1-1][256] (row stride s_wt,
+ *     caption stride s_wb; unit rows, the storage behind the reference's
+ *     transposed [B, 256, L-2] view, :231) and sent [B][256] (row stride s_sb;
+ *     unit rows, :215-220).  ws: tgfr_text_heading_ws floats (the three relu'd
+ *     conv maps).  X, taps and the weights 16-byte aligned.
+ * Replaces the conv stack and the per-token Python loop of
+ * get_each_word_feature / get_word_feature. */
+int tgfr_text_pack_bytes(int mode, long long* bytes);
+int tgfr_text_pack(const float* const* conv_w, uint16_t* taps, int mode, void* stream);
+int tgfr_text_heading_ws(int B, int L1, long long* floats);
+int tgfr_text_heading(const float* X, int B, int L1, const uint16_t* taps,
+                      const float* const* conv_b, float* ws, float* words, long long s_wb,
+                      long long s_wt, float* sent, long long s_sb, int mode, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -742,3 +742,57 @@ def loss_mix(losses, weights):
     """weights: m rows of len(losses) floats; returns (total [], report [m-1])."""
     return LossMix.apply(tuple(tuple(r) for r in weights), *losses)
 
+
+
+# ---------------------------------------------------------------------------
+# TextHeading (models/models.py:170-232)
+
+def text_heading_ws_floats(b, l1):
+    out = (ctypes.c_longlong * 1)()
+    rc = _hip.lib().tgfr_text_heading_ws(int(b), int(l1), ctypes.addressof(out))
+    if rc != 0:
+        raise RuntimeError(f"tgfr_text_heading_ws failed with code {rc}")
+    return int(out[0])
+
+
+def text_pack(conv_w, mode="fp32"):
+    """conv_w[k] [256, 1, k+2, 768] fp32 -> tap-major bf16 planes (uint16) for
+    tgfr_text_heading (hi, plus lo in the fp32 mode)."""
+    ws_ = [w.contiguous() for w in conv_w]
+    for k, w in enumerate(ws_):
+        assert tuple(w.shape) == (D, 1, k + 2, 768) and w.dtype == torch.float32
+    out = (ctypes.c_longlong * 1)()
+    rc = _hip.lib().tgfr_text_pack_bytes(_mode(mode), ctypes.addressof(out))
+    if rc != 0:
+        raise RuntimeError(f"tgfr_text_pack_bytes failed with code {rc}")
+    taps = torch.empty(int(out[0]) // 2, dtype=torch.int16, device=ws_[0].device)
+    wp = (ctypes.c_void_p * 3)(*[ptr(w) for w in ws_])
+    call("tgfr_text_pack", ctypes.addressof(wp), ptr(taps), _mode(mode), _hip.stream())
+    return taps
+
+
+def text_heading(words_emb, taps, conv_b, mode="fp32", words=None, sent=None):
+    """Bert_Word_Mapping + TextHeading forward: words_emb [B, L1, 768] fp32 (BERT
+    last hidden state without [CLS]), taps = text_pack(conv weights, mode),
+    conv_b[k] [256] -> (words [B, L1-1, 256] unit rows, sent [B, 256] unit
+    rows).  One launch for the three convs + one pooling launch (tgfr_text.hip)."""
+    assert words_emb.dim() == 3 and words_emb.shape[2] == 768
+    assert words_emb.dtype == torch.float32
+    b, l1, _ = words_emb.shape
+    if l1 < 4:
+        raise ValueError("TextHeading needs bert_words_num >= 5 (three conv widths up to 4)")
+    x = words_emb.contiguous()
+    bs_ = [v.contiguous() for v in conv_b]
+    for v in bs_:
+        assert tuple(v.shape) == (D,) and v.dtype == torch.float32
+    dev = x.device
+    if words is None:
+        words = torch.empty(b, l1 - 1, D, dtype=torch.float32, device=dev)
+    if sent is None:
+        sent = torch.empty(b, D, dtype=torch.float32, device=dev)
+    ws = torch.empty(text_heading_ws_floats(b, l1), dtype=torch.float32, device=dev)
+    bp = (ctypes.c_void_p * 3)(*[ptr(v) for v in bs_])
+    call("tgfr_text_heading", ptr(x), b, l1, ptr(taps), ctypes.addressof(bp),
+         ptr(ws), ptr(words), words.stride(0), words.stride(1),
+         ptr(sent), sent.stride(0), _mode(mode), _hip.stream())
+    return words, sent

@@ -1,5 +1,5 @@
 """Drop-in for the reference's image head (models/models.py:98-120, 328-338,
-380-405).  Parameter names match the reference for checkpoint interop.
+380-405) and text head (models/models.py:170-232).  Parameter names match the reference for checkpoint interop.
 
 IMIM runs channels-last from the attention onwards: the SelfAttention core
 is the gfx950 kernel, LayerNorm([256,14,14]) normalises each sample over all
@@ -18,7 +18,7 @@ import torch.nn.functional as F
 from .. import kernels as K
 from .fusion_nets import SelfAttention, _cl, set_precision
 
-__all__ = ["ProjectionHead", "IMIM", "ImageHeading"]
+__all__ = ["ProjectionHead", "IMIM", "ImageHeading", "Bert_Word_Mapping", "TextHeading"]
 
 
 class ProjectionHead(nn.Module):
@@ -86,3 +86,55 @@ class ImageHeading(nn.Module):
         local_image = self.imim(local_image)
         global_image = self.project_global(global_image)
         return global_image, local_image
+
+
+class Bert_Word_Mapping(nn.Module):  # noqa: N801  (reference class name)
+    """models.py:170-184: Conv2d(1, feat_dim, (K, 768)) for K = 2, 3, 4 (+ an
+    unused Dropout).  The forward is fused into TextHeading's kernels."""
+
+    def __init__(self, feat_dim):
+        super().__init__()
+        self.convs1 = nn.ModuleList([nn.Conv2d(1, feat_dim, (k, 768)) for k in (2, 3, 4)])
+        self.dropout = nn.Dropout(0.1)
+
+
+class TextHeading(nn.Module):
+    """models.py:187-232 -> (words [B, 256, L-2] -- a transposed view of
+    [B, L-2, 256] unit rows, as :231 -- and sent [B, 256] unit rows).
+
+    Forward only: the reference runs it under no_grad
+    (utils/dataset_utils.py:42-45), so no gradient reaches it; asking for one
+    raises instead of returning a silently detached result."""
+
+    def __init__(self, args):
+        super().__init__()
+        self.feat_dim = args.aux_feat_dim_per_granularity
+        if self.feat_dim != K.D:
+            raise ValueError(f"TextHeading kernels are built for feat_dim {K.D}")
+        self.bwm = Bert_Word_Mapping(self.feat_dim)
+        self.args = args
+        self.precision = getattr(args, "precision", "fp32")
+        self._taps = None          # (key, packed tap planes)
+
+    def packed_taps(self):
+        """The conv weights as tap-major bf16 planes, re-packed only when a
+        weight tensor is replaced or modified in place (its version moves)."""
+        ws = [c.weight for c in self.bwm.convs1]
+        key = (self.precision,) + tuple((w.data_ptr(), w._version) for w in ws)
+        if self._taps is None or self._taps[0] != key:
+            self._taps = (key, K.text_pack(ws, mode=self.precision))
+        return self._taps[1]
+
+    def forward(self, words_emb, sent_emb=None):
+        # seq = bert_words_num - 1 - 3 (:204) fixes the token count
+        if words_emb.shape[1] != self.args.bert_words_num - 1:
+            raise ValueError(f"words_emb has {words_emb.shape[1]} tokens, expected "
+                             f"bert_words_num - 1 = {self.args.bert_words_num - 1}")
+        if torch.is_grad_enabled() and (words_emb.requires_grad or any(
+                p.requires_grad for p in self.parameters())):
+            raise RuntimeError("TextHeading is forward-only (the reference calls it under "
+                               "torch.no_grad(), utils/dataset_utils.py:42); wrap the call "
+                               "in torch.no_grad()")
+        words, sent = K.text_heading(words_emb, self.packed_taps(),
+                                     [c.bias for c in self.bwm.convs1], mode=self.precision)
+        return words.transpose(1, 2), sent

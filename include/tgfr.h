@@ -252,7 +252,10 @@ int tgfr_bn_unfold(const float* G, const float* s, const float* W, int O, int C,
  * tgfr_arc_bwd: from dlogits, dW = the gradient w.r.t. W (margin backward and
  * the l2-norm backward fused) and, when dcs is non-NULL, dcs[b][c] = dcos[b][c]
  * * inv_nw[c], so that d normalize(x) = dcs W (a GEMM) feeds
- * tgfr_l2norm_rows_bwd for dx.  B <= 1024. */
+ * tgfr_l2norm_rows_bwd for dx.  B <= 1024.  ws: tgfr_arc_bwd_ws floats (0 for
+ * B <= 64; NULL is accepted and runs the single-block-row path): for B > 64
+ * the batch is split over block rows of <= 64 rows whose partial dW sums are
+ * added in fixed order by a second launch. */
 int tgfr_arc_fwd(const float* x, long long ldx, int B, int D, const float* W, long long ldw,
                  int C, const long long* label, float s, float m, int easy, float eps,
                  float* logits, float* cosv, float* xn, float* inv_nx, float* inv_nw,
@@ -260,7 +263,8 @@ int tgfr_arc_fwd(const float* x, long long ldx, int B, int D, const float* W, lo
 int tgfr_arc_bwd(const float* dlogits, const float* cosv, const long long* label,
                  const float* xn, const float* W, long long ldw, const float* inv_nw, int B,
                  int D, int C, float s, float m, int easy, float eps, float* dW, long long lddw,
-                 float* dcs, void* stream);
+                 float* dcs, float* ws, void* stream);
+int tgfr_arc_bwd_ws(int B, int D, int C, long long* floats);
 
 /* ---- optimiser step ------------------------------------------------------
  * Every trainable tensor of a trainer in one launch (replaces the two torch

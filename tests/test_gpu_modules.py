@@ -170,7 +170,7 @@ def test_arc_margin_and_focal(gpu):
 
 @pytest.mark.parametrize("b,d,c,easy,precision", [
     (64, 256, 4500, False, "bf16"), (64, 640, 1000, False, "fp32"), (13, 256, 300, True, "fp32"),
-    (70, 128, 37, False, "bf16")])
+    (70, 128, 37, False, "bf16"), (256, 640, 4500, False, "bf16"), (200, 256, 300, True, "fp32")])
 def test_arc_head_fused(gpu, b, d, c, easy, precision):
     """The fused ArcMarginProduct launches (tgfr_arc_fwd / tgfr_arc_bwd) vs torch
     fp32 autograd of F.linear(F.normalize(x), F.normalize(W)) + the margin:

@@ -59,7 +59,8 @@ SIGNATURES = {
     "tgfr_ln_bwd": [P, P, I, L, P, I, P, P, P, P, P],
     "tgfr_optim_step": [P, I, P, I, P, P],
     "tgfr_arc_fwd": [P, L, I, I, P, L, I, P, F, F, I, F, P, P, P, P, P, P],
-    "tgfr_arc_bwd": [P, P, P, P, P, L, P, I, I, I, F, F, I, F, P, L, P, P],
+    "tgfr_arc_bwd": [P, P, P, P, P, L, P, I, I, I, F, F, I, F, P, L, P, P, P],
+    "tgfr_arc_bwd_ws": [I, I, I, P],
     "tgfr_text_pack_bytes": [I, P],
     "tgfr_text_pack": [P, P, I, P],
     "tgfr_text_heading_ws": [I, I, P],

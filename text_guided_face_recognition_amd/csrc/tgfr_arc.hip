@@ -131,7 +131,9 @@ __global__ __launch_bounds__(NT) void arc_fwd_kernel(
   stage_rows(W, ldw, c0, CBF, C, D, w_off);
   __syncthreads();
   row_inv_norms(w_off, CBF, D, eps, nw);
-  for (int b0 = 0; b0 < B; b0 += RB) {
+  // row chunks are spread over gridDim.y (one chunk per block when the grid
+  // covers B; the loop keeps any grid height correct)
+  for (int b0 = blockIdx.y * RB; b0 < B; b0 += RB * gridDim.y) {
     const int nb = min(RB, B - b0);
     __syncthreads();                       // previous chunk's readers are done
     stage_rows(x, ldx, b0, nb, B, D, x_off);
@@ -193,85 +195,15 @@ __global__ __launch_bounds__(NT) void arc_fwd_kernel(
       }
     }
   }
-  if (tid < CBF && c0 + tid < C) inv_nw[c0 + tid] = nw[tid];
+  if (blockIdx.y == 0 && tid < CBF && c0 + tid < C) inv_nw[c0 + tid] = nw[tid];
 }
 
-// LDS: dcos [B][CB] | xn chunk [RB][D+4]
-// thread: class c = tid / 16, d-group g = tid % 16 owns dims 4 g + 64 j
-template <int NJ>   // float4 columns per thread: D = 64 NJ (NJ = 0: any D <= 1024)
-__global__ __launch_bounds__(NT) void arc_bwd_kernel(
-    const float* __restrict__ dlogits, const float* __restrict__ cosv,
-    const long long* __restrict__ label, const float* __restrict__ xn,
-    const float* __restrict__ W, long long ldw, const float* __restrict__ inv_nw, int B, int D,
-    int C, Margin M, float eps, int RB, float* __restrict__ dW, long long lddw,
-    float* __restrict__ dcs) {
-  float* dc = (float*)g_smem;
-  const uint32_t x_off = (uint32_t)(B * CB * 4);
-  const int c0 = blockIdx.x * CB, tid = threadIdx.x;
-  const int c = tid >> 4, g = tid & 15, col = c0 + c;
-  constexpr int MAXJ = NJ ? NJ : 16;       // D <= 1024
-  const int nj = NJ ? NJ : D / 64 + ((D % 64) > 4 * g ? 1 : 0);
-  // this thread's W row slice, needed only at the end: loaded first so its
-  // latency hides under the rest
-  float4 wv[MAXJ];
-  {
-    const float* wr = W + (long long)min(col, C - 1) * ldw + 4 * g;
-#pragma unroll
-    for (int j = 0; j < MAXJ; ++j)
-      wv[j] = j < nj ? ld4(wr + 64 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  // dcos of the block's columns (all loads of a thread issued together)
-  for (int base = tid; base < B * CB; base += NT * 4) {
-    float gl[4], cv[4], iw[4];
-    bool tg[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = min(base + u * NT, B * CB - 1);
-      const int b = i / CB, col = min(c0 + i % CB, C - 1);
-      const long long e = (long long)b * C + col;
-      gl[u] = dlogits[e];
-      cv[u] = cosv[e];
-      iw[u] = inv_nw[col];
-      tg[u] = label[b] == col;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = base + u * NT;
-      if (i < B * CB) {
-        const int b = i / CB, col = c0 + i % CB;
-        float d = 0.f;
-        if (col < C) {
-          d = margin_bwd(gl[u], cv[u], tg[u], M);
-          if (dcs) dcs[(long long)b * C + col] = d * iw[u];
-        }
-        dc[i] = d;
-      }
-    }
-  }
-  float4 acc[MAXJ];
-#pragma unroll
-  for (int j = 0; j < MAXJ; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int b0 = 0; b0 < B; b0 += RB) {
-    const int nb = min(RB, B - b0);
-    __syncthreads();
-    stage_rows(xn, D, b0, nb, B, D, x_off);
-    __syncthreads();
-    for (int r = 0; r < nb; ++r) {
-      const float a = dc[(b0 + r) * CB + c];
-#pragma unroll
-      for (int j = 0; j < MAXJ; ++j) {
-        if (j < nj) {
-          const float4 v = lds4(x_off + (uint32_t)((r * (D + 4) + 4 * g + 64 * j) * 4));
-          acc[j].x = fmaf(a, v.x, acc[j].x);
-          acc[j].y = fmaf(a, v.y, acc[j].y);
-          acc[j].z = fmaf(a, v.z, acc[j].z);
-          acc[j].w = fmaf(a, v.w, acc[j].w);
-        }
-      }
-    }
-  }
-  if (col >= C) return;                    // whole 16-lane groups leave together
-  const float inv = inv_nw[col];
+// dW_c = (dWn - wn (wn . dWn)) / |W_c| for one class row held by a 16-lane
+// group (lane g owns dims 4 g + 64 j); acc = dWn, wv = the raw W row slice.
+template <int MAXJ>
+__device__ __forceinline__ void arc_dw_epilogue(const float4 (&acc)[MAXJ],
+                                                const float4 (&wv)[MAXJ], int nj, float inv,
+                                                float eps, int g, float* __restrict__ dWrow) {
   const bool clamped = inv >= 1.f / eps;   // |W_c| <= eps: y = W / eps, no projection
   float4 wn[MAXJ];
   float dot = 0.f;
@@ -289,9 +221,128 @@ __global__ __launch_bounds__(NT) void arc_bwd_kernel(
     if (j < nj) {
       const float4 o = make_float4((acc[j].x - wn[j].x * dot) * inv, (acc[j].y - wn[j].y * dot) * inv,
                                    (acc[j].z - wn[j].z * dot) * inv, (acc[j].w - wn[j].w * dot) * inv);
-      *(float4*)(dW + (long long)col * lddw + 4 * g + 64 * j) = o;
+      *(float4*)(dWrow + 4 * g + 64 * j) = o;
     }
   }
+}
+
+// LDS: dcos [rows_per][CB] | xn chunk [RB][D+4]
+// thread: class c = tid / 16, d-group g = tid % 16 owns dims 4 g + 64 j
+template <int NJ>   // float4 columns per thread: D = 64 NJ (NJ = 0: any D <= 1024)
+__global__ __launch_bounds__(NT) void arc_bwd_kernel(
+    const float* __restrict__ dlogits, const float* __restrict__ cosv,
+    const long long* __restrict__ label, const float* __restrict__ xn,
+    const float* __restrict__ W, long long ldw, const float* __restrict__ inv_nw, int B, int D,
+    int C, Margin M, float eps, int RB, float* __restrict__ dW, long long lddw,
+    float* __restrict__ dcs, int rows_per, float* __restrict__ part) {
+  // block row y owns rows [rb0, rb1); with gridDim.y > 1 the raw sums go to
+  // part[y][C][D] and arc_bwd_finish_kernel applies the l2-norm backward
+  const int rb0 = blockIdx.y * rows_per, rb1 = min(B, rb0 + rows_per), nbs = rb1 - rb0;
+  float* dc = (float*)g_smem;
+  const uint32_t x_off = (uint32_t)(rows_per * CB * 4);
+  const int c0 = blockIdx.x * CB, tid = threadIdx.x;
+  const int c = tid >> 4, g = tid & 15, col = c0 + c;
+  constexpr int MAXJ = NJ ? NJ : 16;       // D <= 1024
+  const int nj = NJ ? NJ : D / 64 + ((D % 64) > 4 * g ? 1 : 0);
+  // this thread's W row slice, needed only at the end: loaded first so its
+  // latency hides under the rest
+  float4 wv[MAXJ];
+  {
+    const float* wr = W + (long long)min(col, C - 1) * ldw + 4 * g;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j)
+      wv[j] = j < nj ? ld4(wr + 64 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // dcos of the block's columns (all loads of a thread issued together)
+  for (int base = tid; base < nbs * CB; base += NT * 4) {
+    float gl[4], cv[4], iw[4];
+    bool tg[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = min(base + u * NT, nbs * CB - 1);
+      const int b = rb0 + i / CB, col = min(c0 + i % CB, C - 1);
+      const long long e = (long long)b * C + col;
+      gl[u] = dlogits[e];
+      cv[u] = cosv[e];
+      iw[u] = inv_nw[col];
+      tg[u] = label[b] == col;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = base + u * NT;
+      if (i < nbs * CB) {
+        const int b = rb0 + i / CB, col = c0 + i % CB;
+        float d = 0.f;
+        if (col < C) {
+          d = margin_bwd(gl[u], cv[u], tg[u], M);
+          if (dcs) dcs[(long long)b * C + col] = d * iw[u];
+        }
+        dc[i] = d;
+      }
+    }
+  }
+  float4 acc[MAXJ];
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b0 = rb0; b0 < rb1; b0 += RB) {
+    const int nb = min(RB, rb1 - b0);
+    __syncthreads();
+    stage_rows(xn, D, b0, nb, B, D, x_off);
+    __syncthreads();
+    for (int r = 0; r < nb; ++r) {
+      const float a = dc[(b0 - rb0 + r) * CB + c];
+#pragma unroll
+      for (int j = 0; j < MAXJ; ++j) {
+        if (j < nj) {
+          const float4 v = lds4(x_off + (uint32_t)((r * (D + 4) + 4 * g + 64 * j) * 4));
+          acc[j].x = fmaf(a, v.x, acc[j].x);
+          acc[j].y = fmaf(a, v.y, acc[j].y);
+          acc[j].z = fmaf(a, v.z, acc[j].z);
+          acc[j].w = fmaf(a, v.w, acc[j].w);
+        }
+      }
+    }
+  }
+  if (col >= C) return;                    // whole 16-lane groups leave together
+  if (gridDim.y > 1) {
+    float* pr = part + ((long long)blockIdx.y * C + col) * D + 4 * g;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j)
+      if (j < nj) *(float4*)(pr + 64 * j) = acc[j];
+    return;
+  }
+  arc_dw_epilogue<MAXJ>(acc, wv, nj, inv_nw[col], eps, g, dW + (long long)col * lddw);
+}
+
+// Sums the block rows' partial dWn in fixed order and applies the l2-norm
+// backward; the thread layout of arc_bwd_kernel (16 classes x 16 lanes).
+template <int NJ>
+__global__ __launch_bounds__(NT) void arc_bwd_finish_kernel(
+    const float* __restrict__ part, int S, const float* __restrict__ W, long long ldw,
+    const float* __restrict__ inv_nw, int D, int C, float eps, float* __restrict__ dW,
+    long long lddw) {
+  const int tid = threadIdx.x, g = tid & 15, col = blockIdx.x * CB + (tid >> 4);
+  if (col >= C) return;                    // whole 16-lane groups leave together
+  constexpr int MAXJ = NJ ? NJ : 16;
+  const int nj = NJ ? NJ : D / 64 + ((D % 64) > 4 * g ? 1 : 0);
+  float4 wv[MAXJ], acc[MAXJ];
+  const float* wr = W + (long long)col * ldw + 4 * g;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    wv[j] = j < nj ? ld4(wr + 64 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+    acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int y = 0; y < S; ++y) {
+    const float* pr = part + ((long long)y * C + col) * D + 4 * g;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      if (j < nj) {
+        const float4 v = ld4(pr + 64 * j);
+        acc[j].x += v.x; acc[j].y += v.y; acc[j].z += v.z; acc[j].w += v.w;
+      }
+    }
+  }
+  arc_dw_epilogue<MAXJ>(acc, wv, nj, inv_nw[col], eps, g, dW + (long long)col * lddw);
 }
 
 Margin make_margin(float s, float m, int easy) {
@@ -300,6 +351,9 @@ Margin make_margin(float s, float m, int easy) {
 }
 
 bool a16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// block rows of the dW backward: one up to 64 batch rows, then <= 64 rows each
+int arc_bwd_slices(int B) { return B <= 64 ? 1 : (B + 63) / 64; }
 
 // rows per x chunk so that the LDS stays under 128 KiB
 int chunk_rows(int B, int D, int fixed_floats) {
@@ -327,7 +381,10 @@ int tgfr_arc_fwd(const float* x, long long ldx, int B, int D, const float* W, lo
                         160 * 1024);
     set = true;
   }
-  hipLaunchKernelGGL(arc_fwd_kernel, dim3((C + CBF - 1) / CBF), dim3(NT), lds, (hipStream_t)stream,
+  // one row chunk per block row: at D = 640 a chunk is 18 rows, and a single
+  // block row would walk B / 18 chunks serially on C / 32 blocks
+  hipLaunchKernelGGL(arc_fwd_kernel, dim3((C + CBF - 1) / CBF, (B + RB - 1) / RB), dim3(NT), lds,
+                     (hipStream_t)stream,
                      x, ldx, B, D, W, ldw, C, label, make_margin(s, m, easy), eps, RB, logits,
                      cosv, xn, inv_nx, inv_nw);
   return (int)hipGetLastError();
@@ -336,12 +393,17 @@ int tgfr_arc_fwd(const float* x, long long ldx, int B, int D, const float* W, lo
 int tgfr_arc_bwd(const float* dlogits, const float* cosv, const long long* label,
                  const float* xn, const float* W, long long ldw, const float* inv_nw, int B,
                  int D, int C, float s, float m, int easy, float eps, float* dW, long long lddw,
-                 float* dcs, void* stream) {
+                 float* dcs, float* ws, void* stream) {
   if (B <= 0 || C <= 0 || D <= 0 || D % 4 || D > 1024 || ldw % 4 || lddw % 4 || !a16(W) ||
-      !a16(dW) || !a16(xn) || B * CB > 16384)
+      !a16(dW) || !a16(xn) || B * CB > 16384 || (ws && !a16(ws)))
     return 1001;
-  const int RB = chunk_rows(B, D, B * CB);
-  const int lds = (B * CB + RB * (D + 4)) * 4;
+  // B > 64 with a workspace: block rows of <= 64 batch rows each (partial
+  // dWn to ws, summed by the finish launch) and small x chunks, so several
+  // blocks share a CU instead of one block walking all B rows
+  const int S = ws ? arc_bwd_slices(B) : 1;
+  const int rows_per = (B + S - 1) / S;
+  const int RB = S > 1 ? std::min(16, rows_per) : chunk_rows(B, D, B * CB);
+  const int lds = (rows_per * CB + RB * (D + 4)) * 4;
   using Fn = decltype(&arc_bwd_kernel<0>);
   Fn fn = D == 128 ? &arc_bwd_kernel<2> : D == 256 ? &arc_bwd_kernel<4>
         : D == 512 ? &arc_bwd_kernel<8> : D == 640 ? &arc_bwd_kernel<10> : &arc_bwd_kernel<0>;
@@ -351,10 +413,25 @@ int tgfr_arc_bwd(const float* dlogits, const float* cosv, const long long* label
     hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     set[which] = true;
   }
-  hipLaunchKernelGGL(fn, dim3((C + CB - 1) / CB), dim3(NT), lds, (hipStream_t)stream, dlogits,
+  hipLaunchKernelGGL(fn, dim3((C + CB - 1) / CB, S), dim3(NT), lds, (hipStream_t)stream, dlogits,
                      cosv, label, xn, W, ldw, inv_nw, B, D, C, make_margin(s, m, easy), eps, RB,
-                     dW, lddw, dcs);
+                     dW, lddw, dcs, rows_per, ws);
+  if (S > 1) {
+    using Gn = decltype(&arc_bwd_finish_kernel<0>);
+    Gn gn = D == 128 ? &arc_bwd_finish_kernel<2> : D == 256 ? &arc_bwd_finish_kernel<4>
+          : D == 512 ? &arc_bwd_finish_kernel<8> : D == 640 ? &arc_bwd_finish_kernel<10>
+          : &arc_bwd_finish_kernel<0>;
+    hipLaunchKernelGGL(gn, dim3((C + CB - 1) / CB), dim3(NT), 0, (hipStream_t)stream, ws, S, W,
+                       ldw, inv_nw, D, C, eps, dW, lddw);
+  }
   return (int)hipGetLastError();
+}
+
+int tgfr_arc_bwd_ws(int B, int D, int C, long long* floats) {
+  if (B <= 0 || C <= 0 || D <= 0 || !floats) return 1001;
+  const int S = arc_bwd_slices(B);
+  *floats = S > 1 ? (long long)S * C * D : 0;
+  return 0;
 }
 
 }  // extern "C"

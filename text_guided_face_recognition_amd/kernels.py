@@ -658,8 +658,10 @@ class ArcHead(torch.autograd.Function):
         dw = torch.empty_like(w)
         want_dx = ctx.needs_input_grad[0]
         dcs = torch.empty(b, c, dtype=torch.float32, device=w.device) if want_dx else None
+        nws = arc_bwd_ws_floats(b, d, c)
+        ws = torch.empty(nws, dtype=torch.float32, device=w.device) if nws else None
         call("tgfr_arc_bwd", ptr(dl), ptr(cosv), ptr(label), ptr(xn), ptr(w), d, ptr(inv_nw),
-             b, d, c, s, m, easy, eps, ptr(dw), d, ptr(dcs), _hip.stream())
+             b, d, c, s, m, easy, eps, ptr(dw), d, ptr(dcs), ptr(ws), _hip.stream())
         dx = None
         if want_dx:
             mb = -(-b // 64) * -(-d // 64)
@@ -669,6 +671,14 @@ class ArcHead(torch.autograd.Function):
             call("tgfr_l2norm_rows_bwd", ptr(dxn), d, ptr(xn), d, ptr(inv_nx), b, d, eps,
                  ptr(dx), d, _hip.stream())
         return dx, dw, None, None, None, None, None, None
+
+
+def arc_bwd_ws_floats(b, d, c):
+    out = (ctypes.c_longlong * 1)()
+    rc = _hip.lib().tgfr_arc_bwd_ws(int(b), int(d), int(c), ctypes.addressof(out))
+    if rc != 0:
+        raise RuntimeError(f"tgfr_arc_bwd_ws failed with code {rc}")
+    return int(out[0])
 
 
 def arc_head(x, weight, label, s, m, easy_margin=False, eps=1e-12, mode="fp32"):

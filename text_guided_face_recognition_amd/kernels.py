@@ -310,6 +310,85 @@ def _ksplit(k, mn_blocks):
     return int(max(1, min(k // chunk, -(-512 // mn_blocks))))
 
 
+class Conv3x3Rows(torch.autograd.Function):
+    """relu(Conv2d(Cin, Cout, 3, padding=0)(x)) of the FCFM image branch
+    (fusion_nets.py:236, 14x14 -> 12x12) as implicit GEMMs on tgfr_bgemm over the
+    channels-last rows of x, with no im2col copy.
+
+    With X the [B*H*W, Cin] rows and q = b*H*W + y*W + x, the output row q is
+    sum over (dy, dx) of X[q + W*dy + dx] . W_{dy,dx}.  For one dy the (dx, e)
+    pairs of the window are 3*Cin CONTIGUOUS floats of X starting at row
+    q + W*dy, so each dy is one GEMM whose A operand is an overlapping-row
+    stride view of X (row stride Cin, K = 3*Cin): three accumulating launches,
+    bias + ReLU in the last one's epilogue.  Rows whose window leaves the image
+    (x >= W-2, y >= H-2) are computed and discarded.
+
+    Backward: the masked output gradient G is scattered into a zero row buffer
+    with 2W+2 leading pad rows; then per dy
+      dX[r] += sum_{dx', c} Gp[r - W*dy - 2 + dx', c] W[c, :, dy, 2 - dx']
+    (again a contiguous 3*Cout window per row: K = 3*Cout), and
+      dW_dy = X_dy^T G (K = the row count, split-K)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, mode):
+        b, cin, h, w = x.shape
+        cout = weight.shape[0]
+        xr = x.permute(0, 2, 3, 1).contiguous().float()          # [B, H, W, Cin] rows
+        rows = b * h * w
+        m = rows - (2 * w + 2)                                    # last row with an in-buffer window
+        wt = weight.float().permute(2, 3, 1, 0).reshape(3, 3 * cin, cout).contiguous()
+        out = torch.empty(rows, cout, dtype=torch.float32, device=x.device)
+        mb = -(-m // 64) * -(-cout // 64)
+        for dy in range(3):
+            a = xr.as_strided((1, m, 3 * cin), (0, cin, 1), xr.storage_offset() + dy * w * cin)
+            last = dy == 2
+            bgemm(a, wt[dy].unsqueeze(0), out=out[:m].unsqueeze(0), accumulate=dy > 0,
+                  mode=mode, bias=bias.float().contiguous() if last else None, relu=last,
+                  ksplit=_ksplit(3 * cin, mb))
+        y = out.view(b, h, w, cout)[:, :h - 2, :w - 2].permute(0, 3, 1, 2)
+        ctx.save_for_backward(xr, weight, y)
+        ctx.cfg = (b, cin, h, w, cout, mode)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xr, weight, y = ctx.saved_tensors
+        b, cin, h, w, cout, mode = ctx.cfg
+        rows, pad = b * h * w, 2 * w + 2
+        g = gy.float() * (y > 0)                                  # ReLU backward
+        gp = torch.zeros(pad + rows, cout, dtype=torch.float32, device=gy.device)
+        gp[pad:].view(b, h, w, cout)[:, :h - 2, :w - 2] = g.permute(0, 2, 3, 1)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            # B'_dy[(2 - dx) * Cout + c, e] = W[c, e, dy, dx]
+            wb = weight.float().flip(3).permute(2, 3, 0, 1).reshape(3, 3 * cout, cin).contiguous()
+            dxr = torch.empty(rows, cin, dtype=torch.float32, device=gy.device)
+            mb = -(-rows // 64) * -(-cin // 64)
+            for dy in range(3):
+                a = gp.as_strided((1, rows, 3 * cout), (0, cout, 1),
+                                  gp.storage_offset() + (pad - w * dy - 2) * cout)
+                bgemm(a, wb[dy].unsqueeze(0), out=dxr.unsqueeze(0), accumulate=dy > 0,
+                      mode=mode, ksplit=_ksplit(3 * cout, mb))
+            dx = dxr.view(b, h, w, cin).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            m = rows - pad
+            gm = gp[pad:pad + m].unsqueeze(0)
+            dwt = torch.empty(3, 3 * cin, cout, dtype=torch.float32, device=gy.device)
+            mb = -(-(3 * cin) // 64) * -(-cout // 64)
+            for dy in range(3):
+                at = xr.as_strided((1, 3 * cin, m), (0, 1, cin),
+                                   xr.storage_offset() + dy * w * cin)
+                bgemm(at, gm, out=dwt[dy].unsqueeze(0), mode=mode, ksplit=_ksplit(m, mb))
+            dw = dwt.view(3, 3, cin, cout).permute(3, 2, 0, 1).to(weight.dtype)
+        if ctx.needs_input_grad[2]:
+            db = g.sum(dim=(0, 2, 3))
+        return dx, dw, db, None
+
+
+def conv3x3_relu(x, weight, bias, mode="fp32"):
+    return Conv3x3Rows.apply(x, weight, bias, mode)
+
+
 class LinearRows(torch.autograd.Function):
     """y = x W^T + b (optionally ReLU) over the rows of x [..., K]: every
     nn.Linear / 1x1 conv of the head, on the split-bf16 MFMA GEMM."""

@@ -106,94 +106,110 @@ __device__ __forceinline__ float margin_bwd(float g, float cv, bool target, cons
   return g;
 }
 
-// LDS: W tile [CBF][D+4] | x chunk [RB][D+4] | inv_nw [CBF] | inv_nx [RB] |
-// labels [B] (int).  Thread: classes c, c + 16 (c = tid % 16), rows
-// tid / 16 + 16 j (j < 4) of the chunk: 8 outputs from 2 W + 4 x reads per
-// float4 step.
+// Block = (32-class tile, 64-row x chunk).  D is walked in FK-wide k chunks:
+// LDS holds only W [CBF][FK+4] and x [64][FK+4] (~51 KB, several blocks per
+// CU), the row sums of squares accumulate in registers across chunks.
+// LDS: W chunk | x chunk (also the k-half exchange) | inv_nw [CBF] |
+// inv_nx [64] | labels [64] (column within the block or -1).
 constexpr int CBF = 32;         // classes per forward block
+constexpr int FRB = 64;         // x rows per forward block
+constexpr int FK = 128;         // k chunk
 
 __global__ __launch_bounds__(NT) void arc_fwd_kernel(
     const float* __restrict__ x, long long ldx, int B, int D, const float* __restrict__ W,
-    long long ldw, int C, const long long* __restrict__ label, Margin M, float eps, int RB,
+    long long ldw, int C, const long long* __restrict__ label, Margin M, float eps,
     float* __restrict__ logits, float* __restrict__ cosv, float* __restrict__ xn,
     float* __restrict__ inv_nx, float* __restrict__ inv_nw) {
   float* lds_f = (float*)g_smem;
-  const uint32_t w_off = 0, x_off = CBF * (D + 4) * 4;
-  // the x chunk region also carries the k-half exchange (2048 floats)
-  float* nw = lds_f + CBF * (D + 4) + max(RB * (D + 4), 2048);
+  const uint32_t w_off = 0, x_off = CBF * (FK + 4) * 4;
+  float* nw = lds_f + (CBF + FRB) * (FK + 4);
   float* nx = nw + CBF;
-  int* lab = (int*)(nx + RB);
-  const int c0 = blockIdx.x * CBF, tid = threadIdx.x, c = tid & 15;
-  for (int b = tid; b < B; b += NT) {
-    const long long l = label[b];
-    lab[b] = l >= c0 && l < c0 + CBF ? (int)(l - c0) : -1;    // column within the block
+  int* lab = (int*)(nx + FRB);
+  const int c0 = blockIdx.x * CBF, b0 = blockIdx.y * FRB, nb = min(FRB, B - b0);
+  const int tid = threadIdx.x, g = tid & 15;
+  if (tid < nb) {
+    const long long l = label[b0 + tid];
+    lab[tid] = l >= c0 && l < c0 + CBF ? (int)(l - c0) : -1;
   }
-  stage_rows(W, ldw, c0, CBF, C, D, w_off);
-  __syncthreads();
-  row_inv_norms(w_off, CBF, D, eps, nw);
-  // row chunks are spread over gridDim.y (one chunk per block when the grid
-  // covers B; the loop keeps any grid height correct)
-  for (int b0 = blockIdx.y * RB; b0 < B; b0 += RB * gridDim.y) {
-    const int nb = min(RB, B - b0);
-    __syncthreads();                       // previous chunk's readers are done
-    stage_rows(x, ldx, b0, nb, B, D, x_off);
+  // cos on v_mfma_f32_32x32x2_f32 (fp32 operands, fp32 sums): wave w owns
+  // row tile rt = w & 1 (32 rows; rows past B are staged as zeros) and k half
+  // kh = w >> 1 of each chunk; one float4 LDS read per operand feeds two MFMAs
+  // (lane half h uses elements h and h + 2).
+  const int w = tid >> 6, lane = tid & 63, rt = w & 1, kh = w >> 1, h = lane >> 5;
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  float sw[2] = {0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < D; k0 += FK) {
+    const int kc = min(FK, D - k0);      // multiple of 8 (D % 8 == 0)
+    __syncthreads();                     // previous chunk's readers are done
+    stage_rows(W + k0, ldw, c0, CBF, C, kc, w_off);
+    stage_rows(x + k0, ldx, b0, FRB, B, kc, x_off);
     __syncthreads();
-    row_inv_norms(x_off, nb, D, eps, nx);
-    __syncthreads();
-    if (blockIdx.x == 0) {                 // the normalised rows, for the backward
-      const int q = D / 4;
-      for (int i = tid; i < nb * q; i += NT) {
-        const int r = i / q, k = i % q;
-        float4 v = lds4(x_off + (uint32_t)((r * (D + 4) + 4 * k) * 4));
-        const float s = nx[r];
-        v.x *= s; v.y *= s; v.z *= s; v.w *= s;
-        *(float4*)(xn + (long long)(b0 + r) * D + 4 * k) = v;
-      }
-      for (int r = tid; r < nb; r += NT) inv_nx[b0 + r] = nx[r];
-    }
-    // cos on v_mfma_f32_32x32x2_f32 (fp32 operands, fp32 sums): wave w owns
-    // row tile rt = w & 1 (32 rows; rows past the chunk re-read its last row,
-    // masked at the store) and k half kh = w >> 1 of D; one float4 LDS read
-    // per operand feeds two MFMAs (lane half h uses elements h and h + 2).
-    {                                      // nb <= 64: one pass
-      const int w = tid >> 6, lane = tid & 63, rt = w & 1, kh = w >> 1, h = lane >> 5;
-      const int row = min(32 * rt + (lane & 31), nb - 1);
-      const uint32_t xa = x_off + (uint32_t)(row * (D + 4) * 4);
-      const uint32_t wa = w_off + (uint32_t)((lane & 31) * (D + 4) * 4);
-      f32x16 acc;
+    // running sums of squares: 16 lanes per row, rows tid / 16 + 16 i
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-      const int k_lo = kh * (D / 2), k_hi = k_lo + D / 2;
-#pragma unroll 4
-      for (int k = k_lo; k < k_hi; k += 4) {
-        const float4 av = lds4(xa + 4 * k), bv = lds4(wa + 4 * k);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? av.y : av.x, h ? bv.y : bv.x, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? av.w : av.z, h ? bv.w : bv.z, acc, 0, 0, 0);
-      }
-      // k halves: waves 2, 3 hand their sums to waves 0, 1 through LDS (the
-      // x chunk's space is free once every wave has passed the barrier)
-      __syncthreads();
-      float* xs = (float*)(g_smem + x_off);
-      if (kh == 1) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) xs[(rt * 16 + q) * 64 + lane] = acc[q];
-      }
-      __syncthreads();
-      if (kh == 0) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int r = 32 * rt + acc_row(q, h), cc = lane & 31;
-          const float v = acc[q] + xs[(rt * 16 + q) * 64 + lane];
-          if (r < nb && c0 + cc < C) {
-            const int b = b0 + r;
-            const float cv = v * nx[r] * nw[cc];
-            const long long e = (long long)b * C + c0 + cc;
-            cosv[e] = cv;
-            logits[e] = margin_fwd(cv, lab[b] == cc, M);
-          }
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 4) + 16 * i;
+      for (int k = g; k < kc / 4; k += 16) {
+        const float4 v = lds4(x_off + (uint32_t)((r * (kc + 4) + 4 * k) * 4));
+        sx[i] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        if (i < 2) {
+          const float4 u = lds4(w_off + (uint32_t)((r * (kc + 4) + 4 * k) * 4));
+          sw[i] += u.x * u.x + u.y * u.y + u.z * u.z + u.w * u.w;
         }
       }
     }
+    const uint32_t xa = x_off + (uint32_t)((32 * rt + (lane & 31)) * (kc + 4) * 4);
+    const uint32_t wa = w_off + (uint32_t)((lane & 31) * (kc + 4) * 4);
+    const int k_lo = kh * (kc / 2), k_hi = k_lo + kc / 2;
+#pragma unroll 4
+    for (int k = k_lo; k < k_hi; k += 4) {
+      const float4 av = lds4(xa + 4 * k), bv = lds4(wa + 4 * k);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? av.y : av.x, h ? bv.y : bv.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? av.w : av.z, h ? bv.w : bv.z, acc, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float ssx = group16_sum(sx[i]);
+    if (g == 0) nx[(tid >> 4) + 16 * i] = 1.f / fmaxf(sqrtf(ssx), eps);
+    if (i < 2) {
+      const float ssw = group16_sum(sw[i]);
+      if (g == 0) nw[(tid >> 4) + 16 * i] = 1.f / fmaxf(sqrtf(ssw), eps);
+    }
+  }
+  // k halves: waves 2, 3 hand their sums to waves 0, 1 through LDS (the x
+  // chunk's space is free once every wave has passed the barrier)
+  __syncthreads();
+  float* xs = (float*)(g_smem + x_off);
+  if (kh == 1) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) xs[(rt * 16 + q) * 64 + lane] = acc[q];
+  }
+  __syncthreads();
+  if (kh == 0) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r = 32 * rt + acc_row(q, h), cc = lane & 31;
+      const float v = acc[q] + xs[(rt * 16 + q) * 64 + lane];
+      if (r < nb && c0 + cc < C) {
+        const float cv = v * nx[r] * nw[cc];
+        const long long e = (long long)(b0 + r) * C + c0 + cc;
+        cosv[e] = cv;
+        logits[e] = margin_fwd(cv, lab[r] == cc, M);
+      }
+    }
+  }
+  if (blockIdx.x == 0) {                 // the normalised rows, for the backward
+    const int q = D / 4;
+    for (int i = tid; i < nb * q; i += NT) {
+      const int r = i / q, k = i % q;
+      float4 v = ld4(x + (long long)(b0 + r) * ldx + 4 * k);
+      const float sc = nx[r];
+      v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
+      *(float4*)(xn + (long long)(b0 + r) * D + 4 * k) = v;
+    }
+    for (int r = tid; r < nb; r += NT) inv_nx[b0 + r] = nx[r];
   }
   if (blockIdx.y == 0 && tid < CBF && c0 + tid < C) inv_nw[c0 + tid] = nw[tid];
 }
@@ -372,21 +388,10 @@ int tgfr_arc_fwd(const float* x, long long ldx, int B, int D, const float* W, lo
   if (B <= 0 || B > 4096 || C <= 0 || D <= 0 || D % 8 || D > 1024 || ldx % 4 || ldw % 4 ||
       !a16(x) || !a16(W) || !a16(xn))
     return 1001;
-  // <= 64 rows per chunk: one pass of the two 32-row MFMA tiles per chunk
-  const int RB = std::min(64, chunk_rows(B, D, CBF * (D + 4) + CBF + B + 64));
-  const int lds = (CBF * (D + 4) + std::max(RB * (D + 4), 2048) + CBF + RB + B) * 4;
-  static bool set = false;
-  if (!set) {
-    hipFuncSetAttribute((const void*)arc_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    set = true;
-  }
-  // one row chunk per block row: at D = 640 a chunk is 18 rows, and a single
-  // block row would walk B / 18 chunks serially on C / 32 blocks
-  hipLaunchKernelGGL(arc_fwd_kernel, dim3((C + CBF - 1) / CBF, (B + RB - 1) / RB), dim3(NT), lds,
-                     (hipStream_t)stream,
-                     x, ldx, B, D, W, ldw, C, label, make_margin(s, m, easy), eps, RB, logits,
-                     cosv, xn, inv_nx, inv_nw);
+  const int lds = ((CBF + FRB) * (FK + 4) + CBF + 2 * FRB) * 4;
+  hipLaunchKernelGGL(arc_fwd_kernel, dim3((C + CBF - 1) / CBF, (B + FRB - 1) / FRB), dim3(NT),
+                     lds, (hipStream_t)stream, x, ldx, B, D, W, ldw, C, label,
+                     make_margin(s, m, easy), eps, logits, cosv, xn, inv_nx, inv_nw);
   return (int)hipGetLastError();
 }
 

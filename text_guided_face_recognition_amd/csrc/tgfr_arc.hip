@@ -107,14 +107,15 @@ __device__ __forceinline__ float margin_bwd(float g, float cv, bool target, cons
 }
 
 // Block = (32-class tile, 64-row x chunk).  D is walked in FK-wide k chunks:
-// LDS holds only W [CBF][FK+4] and x [64][FK+4] (~51 KB, several blocks per
-// CU), the row sums of squares accumulate in registers across chunks.
+// LDS holds only W [CBF][FK+4] and x [64][FK+4] (~51 KB at FK = 128, several
+// blocks per CU), the row sums of squares accumulate in registers across chunks.
 // LDS: W chunk | x chunk (also the k-half exchange) | inv_nw [CBF] |
 // inv_nx [64] | labels [64] (column within the block or -1).
 constexpr int CBF = 32;         // classes per forward block
 constexpr int FRB = 64;         // x rows per forward block
-constexpr int FK = 128;         // k chunk
-
+// FK: k chunk (256 when D <= 256 and B <= 64: one chunk, no re-staging barriers;
+// 128 else, so that several blocks share a CU)
+template <int FK>
 __global__ __launch_bounds__(NT) void arc_fwd_kernel(
     const float* __restrict__ x, long long ldx, int B, int D, const float* __restrict__ W,
     long long ldw, int C, const long long* __restrict__ label, Margin M, float eps,
@@ -388,8 +389,16 @@ int tgfr_arc_fwd(const float* x, long long ldx, int B, int D, const float* W, lo
   if (B <= 0 || B > 4096 || C <= 0 || D <= 0 || D % 8 || D > 1024 || ldx % 4 || ldw % 4 ||
       !a16(x) || !a16(W) || !a16(xn))
     return 1001;
-  const int lds = ((CBF + FRB) * (FK + 4) + CBF + 2 * FRB) * 4;
-  hipLaunchKernelGGL(arc_fwd_kernel, dim3((C + CBF - 1) / CBF, (B + FRB - 1) / FRB), dim3(NT),
+  const int fk = D <= 256 && B <= FRB ? 256 : 128;   // one row block: LDS per block is free
+  const int lds = ((CBF + FRB) * (fk + 4) + CBF + 2 * FRB) * 4;
+  auto fn = fk == 256 ? &arc_fwd_kernel<256> : &arc_fwd_kernel<128>;
+  static bool set = false;
+  if (!set) {
+    hipFuncSetAttribute((const void*)&arc_fwd_kernel<256>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    set = true;
+  }
+  hipLaunchKernelGGL(fn, dim3((C + CBF - 1) / CBF, (B + FRB - 1) / FRB), dim3(NT),
                      lds, (hipStream_t)stream, x, ldx, B, D, W, ldw, C, label,
                      make_margin(s, m, easy), eps, logits, cosv, xn, inv_nx, inv_nw);
   return (int)hipGetLastError();

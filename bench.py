@@ -96,25 +96,50 @@ def kernel_profile(trainer, batch, steps):
     return kt.summary(), kt
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC passes of the
-    latest round (profiles/rNN/pmc.json, written by tools/summarize_profile.py
-    from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench
-    config; FETCH_SIZE doubled per MI355X_MICROARCH.md 'HBM').  None if absent."""
+def config_key(args, world):
+    """The bench configuration a PMC measurement belongs to."""
+    return f"b{args.batch}_w{args.words}_{args.precision}_n{world}"
+
+
+def pmc_traffic(kernel, key):
+    """HBM bytes per launch of `kernel` measured for THIS configuration `key`
+    (config_key) by the newest round's committed PMC passes
+    (profiles/rNN/pmc.json, tools/summarize_profile.py: separate FETCH_SIZE /
+    WRITE_SIZE rocprofv3 passes, FETCH_SIZE doubled per MI355X_MICROARCH.md
+    'HBM').  None when no round measured this configuration: a number from
+    another configuration is never attached."""
     import glob
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                           "profiles", "r*", "pmc.json")))
-    if not files:
-        return None
-    data = json.load(open(files[-1]))
-    entry = data.get("kernels", {}).get(kernel)
-    return None if entry is None else entry.get("hbm_bytes_per_launch")
+    for f in reversed(files):
+        data = json.load(open(f))
+        entry = data.get("configs", {}).get(key, {}).get("kernels", {}).get(kernel)
+        if entry is not None:
+            return entry.get("hbm_bytes_per_launch")
+    return None
+
+
+def host_cores():
+    """(cores this process may run on, the machine's CPU count): the CPU
+    affinity mask, capped by a cgroup CPU quota when one is set."""
+    total = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = total
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            avail = max(1, min(avail, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return avail, total
 
 
 def cpu_baseline(args, n_words):
     """The CPU oracle restatement of the same step on the host cores."""
     from oracle import tgfr_oracle as O
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
+    threads, machine = host_cores()
     torch.set_num_threads(threads)
     b = args.batch
     gen = torch.Generator().manual_seed(100)
@@ -179,19 +204,39 @@ def cpu_baseline(args, n_words):
     times.sort()
     med = times[len(times) // 2]
     return {"value": round(b / med, 3), "unit": "pairs/s", "cores": threads,
-            "kind": "port",
+            "machine_cpus": machine, "kind": "port",
             "sample": f"{args.cpu_steps} steps (+1 warm-up) of the same bs={b}, T={n_words} "
-                      f"stage-1 step through the fp32 oracle; median step "
-                      f"{med * 1000:.0f} ms"}
+                      f"stage-1 step through the fp32 oracle on {threads} torch threads "
+                      f"(every core this process may use; the machine has {machine}); "
+                      f"median step {med * 1000:.0f} ms"}
+
+
+def spawn_ranks(args):
+    """`bench.py --gpus N` run directly (no WORLD_SIZE): start N ranks with
+    torch.distributed.run as a CHILD process (nothing here has touched the
+    GPU) and exit with its status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     from text_guided_face_recognition_amd.config import make_args
     from text_guided_face_recognition_amd.dist import DistContext, ReplicaGroup, init_from_env
     from text_guided_face_recognition_amd.train import GraphedStep, Train, synthetic_batch
 
     ctx = init_from_env()
+    if args.gpus != ctx.world and args.simulate_world <= 1:
+        raise SystemExit(f"--gpus {args.gpus} but {ctx.world} rank(s) were launched")
     if args.simulate_world > 1 and not ctx.active:
         ctx = DistContext(ReplicaGroup(args.simulate_world))
         args.no_cpu = True
@@ -257,7 +302,7 @@ def main():
     roofline = {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 2),
                 "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                "traffic": pmc_traffic(dominant),
+                "traffic": pmc_traffic(dominant, config_key(args, n)),
                 "avg_launch_ms": round(dom_ms, 4),
                 "flop_per_launch": flops[dominant]}
 

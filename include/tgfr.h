@@ -274,7 +274,10 @@ int tgfr_arc_bwd_ws(int B, int D, int C, long long* floats);
  *     v = b2 v + (1-b2) g^2;  p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
  *   SGD (torch.optim.SGD, nesterov off):  g += wd p;  buf = g at t = 1, else
  *     momentum buf + (1-dampening) g;  p -= lr buf  (no buf when momentum = 0)
- * state0 = m / buf, state1 = v (Adam only).  counters: 2 ints, [0] = steps
+ * state0 = m / buf, state1 = v (Adam only).  lr_scale (device, nullable):
+ * one float per group multiplying that group's lr, read at launch time, so
+ * an lr schedule applies to a captured step without re-capture.
+ * counters: 2 ints, [0] = steps
  * taken so far (t - 1; the launch increments it), [1] = 0 (left 0).  The
  * segment table travels in the kernel arguments, so a captured launch
  * replays with the pointers it was captured with.  n_segs <= 48,
@@ -295,7 +298,7 @@ typedef struct {
   int reserved;
 } tgfr_optim_seg;
 int tgfr_optim_step(const tgfr_optim_seg* segs, int n_segs, const tgfr_optim_group* groups,
-                    int n_groups, int* counters, void* stream);
+                    int n_groups, const float* lr_scale, int* counters, void* stream);
 
 /* TextHeading / Bert_Word_Mapping forward (models/models.py:170-232; run under
  * no_grad by utils/dataset_utils.py:42-45).

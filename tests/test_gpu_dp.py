@@ -39,6 +39,9 @@ def test_dp_world2_matches_global(gpu, tmp_path):
     for rank in range(2):
         r = json.load(open(f"{out}.{rank}"))
         assert r["err_loss"] < 1e-4 and r["err_r"] < 1e-4 and r["err_i"] < 1e-4, r
+        assert r["oracle_err_loss"] < 1e-3 and r["oracle_err_r"] < 2e-3 and \
+            r["oracle_err_i"] < 2e-3, r
+        assert r["focal_err"] < 1e-5 and r["focal_grad_err"] < 1e-5, r
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
@@ -50,6 +53,7 @@ def test_dp_graphed_train_step(gpu, tmp_path, precision):
     _run("dp_train_worker.py", out, TGFR_DP_PRECISION=precision)
     for rank in range(2):
         r = json.load(open(f"{out}.{rank}"))
-        # text gather, 3 column exchanges, gradient all-reduce -> 6 graphs
-        assert r["segments"] == 6, r
+        # text gather, 3 column exchanges, the focal NLL-sum all-reduce, the
+        # gradient all-reduce -> 7 graphs
+        assert r["segments"] == 7, r
         assert r["err_out"] < 1e-4 and r["err_par"] < 1e-5 and r["err_rank"] == 0.0, r

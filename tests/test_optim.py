@@ -114,3 +114,48 @@ def test_limits():
         FusedOptimizer([adam_group(ps)])
     with pytest.raises(ValueError):
         FusedOptimizer([adam_group([torch.zeros(4, dtype=torch.float64)])])
+
+
+@pytest.mark.gpu
+def test_lr_schedule_between_graph_replays(gpu):
+    """The reference's schedules (ExponentialLR(0.98) on the head every epoch,
+    the classifier SGD lr cut 10x at epochs 3 and 8,
+    src/train_encoders_bert.py:225, :406-410) applied between replays of ONE
+    captured step match torch.optim + torch.optim.lr_scheduler."""
+    mine, ref, grads = _setup(gpu, "stage1", seed=2)
+    opt = FusedOptimizer(_groups(mine, True, "stage1"))
+    adam, sgd = _groups(ref, False, "stage1")
+    sched = torch.optim.lr_scheduler.ExponentialLR(adam, gamma=0.98)
+    static = [torch.zeros(s, device=gpu) for s in SHAPES]
+    for p, g in zip(mine, static):
+        p.grad = g
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph):
+            opt.step()
+    torch.cuda.current_stream().wait_stream(side)
+    for epoch, gs in enumerate(grads * 3):
+        for g, h in zip(static, gs):
+            g.copy_(h)
+        graph.replay()
+        for o in (adam, sgd):
+            o.zero_grad()
+        for q, g in zip(ref, gs):
+            q.grad = g.to(gpu)
+        adam.step()
+        sgd.step()
+        # end of "epoch": schedules advance on both sides
+        sched.step()
+        opt.scale_lr(0, 0.98)
+        if epoch in (3, 8):
+            for pg in sgd.param_groups:
+                pg["lr"] *= 0.1
+            opt.scale_lr(1, 0.1)
+        assert abs(opt.get_lr(0) - adam.param_groups[0]["lr"]) < 1e-12
+        assert abs(opt.get_lr(1) - sgd.param_groups[0]["lr"]) < 1e-12
+    torch.cuda.synchronize()
+    for p, q in zip(mine, ref):
+        err = ((p - q).abs().max() / q.abs().max()).item()
+        assert err < 1e-5, err

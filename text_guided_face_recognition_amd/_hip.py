@@ -3,8 +3,10 @@
 The library is loaded after torch so that its NEEDED libamdhip64.so.7 resolves
 to the HIP runtime torch already mapped (same SONAME): one runtime per
 process, so torch's streams and device pointers are valid in the kernels.
-There is no fallback: if the library is missing or a call fails, this module
-raises.
+There is no fallback: if the library cannot be built or a call fails, this
+module raises.  A library whose source stamp does not match the tree (or a
+missing one) is rebuilt from csrc/ before it is mapped (build.stale), so the
+kernels that run are always the ones in the tree.
 """
 from __future__ import annotations
 
@@ -13,10 +15,9 @@ import os
 
 import torch  # noqa: F401  (must be imported before the library is mapped)
 
-from .build import LIB as _BUILT
+from . import build as _build
 
-# TGFR_LIB: an alternative build of the same library (kernel experiments)
-LIB = os.environ.get("TGFR_LIB", _BUILT)
+LIB = _build.LIB
 
 _lib = None
 
@@ -57,7 +58,7 @@ SIGNATURES = {
     "tgfr_bias_grad": [P, L, I, I, P, L, P, L, P, P, P, P],
     "tgfr_ln_fwd": [P, I, L, P, P, F, I, P, P, P],
     "tgfr_ln_bwd": [P, P, I, L, P, I, P, P, P, P, P],
-    "tgfr_optim_step": [P, I, P, I, P, P],
+    "tgfr_optim_step": [P, I, P, I, P, P, P],
     "tgfr_arc_fwd": [P, L, I, I, P, L, I, P, F, F, I, F, P, P, P, P, P, P],
     "tgfr_arc_bwd": [P, P, P, P, P, L, P, I, I, I, F, F, I, F, P, L, P, P, P],
     "tgfr_arc_bwd_ws": [I, I, I, P],
@@ -72,10 +73,14 @@ def lib():
     """The loaded kernel library (raises if it has not been built)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB):
-            raise RuntimeError(
-                f"{LIB} is missing: build it with "
-                "`python -m text_guided_face_recognition_amd.build` (no CPU fallback)")
+        if _build.stale():
+            import sys
+            sys.stderr.write(f"[tgfr] {LIB} is missing or stale: building it from csrc/\n")
+            try:
+                _build.build()
+            except Exception as e:  # noqa: BLE001
+                raise RuntimeError(f"{LIB} could not be built ({e}); there is no CPU "
+                                   "fallback") from e
         handle = C.CDLL(LIB, mode=C.RTLD_GLOBAL)
         for name, argtypes in SIGNATURES.items():
             fn = getattr(handle, name, None)

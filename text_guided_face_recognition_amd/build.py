@@ -4,10 +4,16 @@
 
 Each csrc/*.hip compiles to its own object (in parallel, with per-file
 flags), then hipcc links the shared library.  Nothing here depends on torch.
+
+The library is stamped with a hash of everything it is built from (sources,
+headers, this file's flags): ``stale()`` compares the stamp with the tree, and
+the loader (_hip.lib) rebuilds a stale or missing library before mapping it,
+so a run never uses a binary built from other sources.
 """
 from __future__ import annotations
 
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -18,8 +24,10 @@ CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 OBJ_DIR = os.path.join(LIB_DIR, "obj")
 LIB = os.path.join(LIB_DIR, "libtgfr_hip.so")
-HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-ARCH = os.environ.get("TGFR_ARCH", "gfx950")
+STAMP = LIB + ".sha256"
+INCLUDE = os.path.join(os.path.dirname(PKG), "include")
+HIPCC = "/opt/rocm/bin/hipcc"
+ARCH = "gfx950"
 
 # Per-file flags.  The word<->region kernels interleave f32 VALU with MFMAs by
 # hand: SLP vectorisation would pack adjacent f32 adds/multiplies into
@@ -34,12 +42,27 @@ def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
 
-def _stale():
-    if not os.path.exists(LIB):
+def deps():
+    """Every file the library is built from."""
+    return sorted(sources() + glob.glob(os.path.join(CSRC, "*.h")) +
+                  glob.glob(os.path.join(INCLUDE, "*.h")) + [os.path.abspath(__file__)])
+
+
+def source_hash():
+    h = hashlib.sha256()
+    for p in deps():
+        h.update(os.path.relpath(p, os.path.dirname(PKG)).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def stale():
+    """True when the library is missing or was built from other sources."""
+    if not (os.path.exists(LIB) and os.path.exists(STAMP)):
         return True
-    t = os.path.getmtime(LIB)
-    deps = sources() + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.abspath(__file__)]
-    return any(os.path.getmtime(p) > t for p in deps)
+    with open(STAMP) as f:
+        return f.read().strip() != source_hash()
 
 
 def _run(cmd, verbose):
@@ -54,9 +77,21 @@ def _run(cmd, verbose):
 
 
 def build(force=False, verbose=False, extra=()):
-    """Compile every csrc/*.hip and link one shared library; returns its path."""
-    if not force and not _stale():
+    """Compile every csrc/*.hip and link one shared library; returns its path.
+    Concurrent callers (test workers, ranks) serialise on a lock file."""
+    if not force and not stale():
         return LIB
+    import fcntl
+    os.makedirs(LIB_DIR, exist_ok=True)
+    with open(os.path.join(LIB_DIR, ".build.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        if not force and not stale():
+            return LIB
+        return _build_locked(verbose, extra)
+
+
+def _build_locked(verbose, extra):
+    digest = source_hash()
     os.makedirs(OBJ_DIR, exist_ok=True)
     common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
               "-fno-gpu-rdc", "-Wno-unused-result", "-Wno-unused-value", "-I", CSRC, *extra]
@@ -74,6 +109,8 @@ def build(force=False, verbose=False, extra=()):
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-fno-gpu-rdc", "-o", tmp,
           *[o for _, o in jobs]], verbose)
     os.replace(tmp, LIB)
+    with open(STAMP, "w") as f:
+        f.write(digest + "\n")
     return LIB
 
 

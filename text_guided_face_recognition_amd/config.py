@@ -39,6 +39,15 @@ DEFAULTS = {
 }
 
 
+# cfg/train_lstm.yml (stage 1 with the BiLSTM text encoder, BASELINE configs[0])
+LSTM_DEFAULTS = {
+    "en_type": "LSTM", "lambda_clip": 1.0, "lambda_id": 100, "lr_head": 0.002,
+    "weight_decay": 0.0001, "clip_max_norm": 0.5, "batch_size": 128, "init_lr_lstm": 0.001,
+    "min_lr_lstm": 0.00009, "lstm_words_num": 18, "embedding_dim": 256,
+    "captions_per_image": 4, "num_classes": 4500,
+}
+
+
 def _coerce(v):
     # cfg/train_bert.yml:35 ships "min_lr_bert: 0.00002)" which YAML reads as a
     # string; the reference then fails in Adam(lr=str).  Coerce numeric strings.
@@ -50,8 +59,12 @@ def _coerce(v):
     return v
 
 
-def make_args(yaml_path=None, **overrides):
+def make_args(yaml_path=None, lstm=False, **overrides):
+    """cfg/train_bert.yml defaults (cfg/train_lstm.yml with lstm=True), then a
+    YAML file's keys, then keyword overrides."""
     cfg = dict(DEFAULTS)
+    if lstm:
+        cfg.update(LSTM_DEFAULTS)
     if yaml_path:
         with open(yaml_path) as f:
             loaded = yaml.safe_load(f) or {}

@@ -392,12 +392,7 @@ int tgfr_arc_fwd(const float* x, long long ldx, int B, int D, const float* W, lo
   const int fk = D <= 256 && B <= FRB ? 256 : 128;   // one row block: LDS per block is free
   const int lds = ((CBF + FRB) * (fk + 4) + CBF + 2 * FRB) * 4;
   auto fn = fk == 256 ? &arc_fwd_kernel<256> : &arc_fwd_kernel<128>;
-  static bool set = false;
-  if (!set) {
-    hipFuncSetAttribute((const void*)&arc_fwd_kernel<256>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    set = true;
-  }
+  if (const int e = set_max_lds((const void*)fn, lds)) return e;
   hipLaunchKernelGGL(fn, dim3((C + CBF - 1) / CBF, (B + FRB - 1) / FRB), dim3(NT),
                      lds, (hipStream_t)stream, x, ldx, B, D, W, ldw, C, label,
                      make_margin(s, m, easy), eps, logits, cosv, xn, inv_nx, inv_nw);
@@ -409,7 +404,7 @@ int tgfr_arc_bwd(const float* dlogits, const float* cosv, const long long* label
                  int D, int C, float s, float m, int easy, float eps, float* dW, long long lddw,
                  float* dcs, float* ws, void* stream) {
   if (B <= 0 || C <= 0 || D <= 0 || D % 4 || D > 1024 || ldw % 4 || lddw % 4 || !a16(W) ||
-      !a16(dW) || !a16(xn) || B * CB > 16384 || (ws && !a16(ws)))
+      !a16(dW) || !a16(xn) || B > 4096 || (!ws && B * CB > 16384) || (ws && !a16(ws)))
     return 1001;
   // B > 64 with a workspace: block rows of <= 64 batch rows each (partial
   // dWn to ws, summed by the finish launch) and small x chunks, so several
@@ -421,12 +416,7 @@ int tgfr_arc_bwd(const float* dlogits, const float* cosv, const long long* label
   using Fn = decltype(&arc_bwd_kernel<0>);
   Fn fn = D == 128 ? &arc_bwd_kernel<2> : D == 256 ? &arc_bwd_kernel<4>
         : D == 512 ? &arc_bwd_kernel<8> : D == 640 ? &arc_bwd_kernel<10> : &arc_bwd_kernel<0>;
-  static bool set[5];
-  const int which = D == 128 ? 0 : D == 256 ? 1 : D == 512 ? 2 : D == 640 ? 3 : 4;
-  if (!set[which]) {
-    hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    set[which] = true;
-  }
+  if (const int e = set_max_lds((const void*)fn, lds)) return e;
   hipLaunchKernelGGL(fn, dim3((C + CB - 1) / CB, S), dim3(NT), lds, (hipStream_t)stream, dlogits,
                      cosv, label, xn, W, ldw, inv_nw, B, D, C, make_margin(s, m, easy), eps, RB,
                      dW, lddw, dcs, rows_per, ws);

@@ -175,8 +175,7 @@ int tgfr_bn_fwd_cl(const float* x, int N, int C, int HW, float eps, float moment
                      training, running_mean, running_var, nbt, mean, rstd);
   const int lds = 64 * (HW + 1) * 4;
   if (lds > 64 * 1024)
-    hipFuncSetAttribute((const void*)bn_norm_cl_kernel,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (const int e = set_max_lds((const void*)bn_norm_cl_kernel, lds)) return e;
   hipLaunchKernelGGL(bn_norm_cl_kernel, dim3((C + 63) / 64, N), dim3(256), lds, st, x, C, HW,
                      mean, rstd, xhat);
   return (int)hipGetLastError();

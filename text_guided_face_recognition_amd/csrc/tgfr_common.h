@@ -9,6 +9,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #define LDS_AS __attribute__((address_space(3)))
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -266,6 +270,25 @@ __device__ __forceinline__ bool last_arrival(unsigned* cnt, unsigned expected, i
 // Row index inside a 32x32 MFMA accumulator tile for register q of wave half h.
 __device__ __forceinline__ constexpr int acc_row(int q, int h) {
   return (q & 3) + 8 * (q >> 2) + 4 * h;
+}
+
+// Host: allow `bytes` of dynamic LDS for kernel `fn` on the current device,
+// once per (kernel, device) and thread-safe; returns the hipError_t of the
+// attribute call (0 when already set).  Every entry point that launches with
+// more than 64 KB of dynamic LDS calls this before its launch.
+inline int set_max_lds(const void* fn, int bytes) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> done;
+  int dev = 0;
+  const hipError_t e0 = hipGetDevice(&dev);
+  if (e0 != hipSuccess) return (int)e0;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = done.find({fn, dev});
+  if (it != done.end() && it->second >= bytes) return 0;
+  const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e != hipSuccess) return (int)e;
+  done[{fn, dev}] = bytes;
+  return 0;
 }
 
 }  // namespace tgfr

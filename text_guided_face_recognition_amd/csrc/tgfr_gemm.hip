@@ -66,9 +66,6 @@ __device__ __forceinline__ void store_acc(const f32x16& acc, float* Cb, long lon
       float* o = Cb + m * sCm + n * sCn;
       float v = alpha * acc[q] + bn;
       if (accumulate) v += *o;
-#ifdef TGFR_GEMM_EXP_NOSTORE
-      if (v == 12345.f)
-#endif
       *o = relu ? fmaxf(v, 0.f) : v;
     }
   }
@@ -220,9 +217,6 @@ __global__ __launch_bounds__(256) void bgemm_glds_kernel(
 
   const int nk = (K + BK - 1) / BK;
   auto issue = [&](int kt) {
-#ifdef TGFR_GEMM_EXP_NOLOAD
-    if (kt > 0) return;
-#endif
     const uint32_t o = (kt % NS) * STG;
     const int k0 = kt * BK;
     issue_tile<LA, TM>(Ab + (long long)k0 * sAk, sAm, sAk, M - m0, K - k0, o, wid, lane);
@@ -256,11 +250,7 @@ __global__ __launch_bounds__(256) void bgemm_glds_kernel(
         frag8<MODE>(f.v, ah, al);
 #pragma unroll
         for (int j = 0; j < WN; ++j) {
-#ifdef TGFR_GEMM_EXP_NOMFMA
-          acc[i][j][0] += (float)ah[0] * (float)bh[j][0];
-#else
           mma<MODE>(acc[i][j], ah, al, bh[j], bl[j]);
-#endif
         }
       }
     }
@@ -651,10 +641,8 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
   auto* s = (hipStream_t)stream;
   const int la = sAk == 1 ? LAY_K : sAm == 1 ? LAY_MN : LAY_ANY;
   const int lb = sBk == 1 ? LAY_K : sBn == 1 ? LAY_MN : LAY_ANY;
-  // weight-resident row stream (TGFR_GEMM_WRES=0 turns it off; read per call)
-  const char* wres_env = getenv("TGFR_GEMM_WRES");
-  const bool wres_on = !wres_env || atoi(wres_env) != 0;
-  if (wres_on && mode == MODE_BF16 && batch == 1 && ksplit == 1 && !accumulate && la == LAY_K &&
+  // weight-resident row stream
+  if (mode == MODE_BF16 && batch == 1 && ksplit == 1 && !accumulate && la == LAY_K &&
       (K == 128 || K == 256) && M >= 2048 && dma_ok(A, LAY_K, 0, sAm, 1, M, K, 1) &&
       (sBk != 1 || (al16(B) && (sBn & 3) == 0))) {
     const int n_slices = (N + WR_TN - 1) / WR_TN;
@@ -663,11 +651,7 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
     const int per_slice = std::max(1, std::min(m_tiles, 256 / n_slices));
     const int lds = WR_TN * K * 2 + WR_NS * WR_STG;
     auto fn = K == 256 ? &bgemm_wres_kernel<256> : &bgemm_wres_kernel<128>;
-    static bool set[2];
-    if (!set[K == 256]) {
-      hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      set[K == 256] = true;
-    }
+    if (const int e = set_max_lds((const void*)fn, lds)) return e;
     hipLaunchKernelGGL(fn, dim3(n_slices * per_slice), dim3(64 * WR_NW), lds, s, A, sAm, B, sBk,
                        sBn, C,
                        sCm, sCn, M, N, alpha, bias, relu, n_slices, per_slice);
@@ -680,18 +664,12 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
   if (dma) {
     // largest tile that still gives >= 1 block per CU (two fit); the 128x128 tile
     // (cfg 3) is never picked: at K <= 768 it loses to 128x64 / 64x128 on
-    // every head shape (tools/gemm_bench.py; TGFR_GEMM_CFG forces one, for
-    // tuning)
-    static const int forced = getenv("TGFR_GEMM_CFG") ? atoi(getenv("TGFR_GEMM_CFG")) : -1;
+    // every head shape (measured in round 1)
     int cfg = 0;
-    if (forced >= 0 && forced < 4) {
-      cfg = forced;
-    } else {
-      for (int c = 2; c >= 1; --c) {
-        const long long blocks = (long long)((M + 64 * CFG_WM[c] - 1) / (64 * CFG_WM[c])) *
-                                 ((N + 64 * CFG_WN[c] - 1) / (64 * CFG_WN[c])) * batch * ksplit;
-        if (blocks >= 256) { cfg = c; break; }
-      }
+    for (int c = 2; c >= 1; --c) {
+      const long long blocks = (long long)((M + 64 * CFG_WM[c] - 1) / (64 * CFG_WM[c])) *
+                               ((N + 64 * CFG_WN[c] - 1) / (64 * CFG_WN[c])) * batch * ksplit;
+      if (blocks >= 256) { cfg = c; break; }
     }
     TM = 64 * CFG_WM[cfg];
     TN = 64 * CFG_WN[cfg];
@@ -700,12 +678,7 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
     const int lds = CFG_NS[cfg] * stg + 16;
     GemmFn fn = mode == MODE_SPLIT ? pick_glds<MODE_SPLIT>(la, lb, cfg)
                                    : pick_glds<MODE_BF16>(la, lb, cfg);
-    static bool lds_set[2][2][2][4];
-    bool& done = lds_set[mode][la][lb][cfg];
-    if (!done) {
-      hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      done = true;
-    }
+    if (const int e = set_max_lds((const void*)fn, lds)) return e;
     hipLaunchKernelGGL(fn, grid, dim3(256), lds, s, A, sAb, sAm, sAk, B, sBb, sBk, sBn, C, sCb,
                        sCm, sCn, M, N, K, alpha, accumulate, bias, relu, ksplit, slab, counters);
   } else {

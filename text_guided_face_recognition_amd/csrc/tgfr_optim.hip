@@ -10,7 +10,11 @@
 // (segment starts are padded to whole blocks), so the segment lookup is a
 // scalar loop.  The step count lives on the device (counters[0]) and is
 // bumped by the last block to finish, so a captured graph replays the step
-// with the right bias corrections.
+// with the right bias corrections.  Learning rates are the group's lr times a
+// per-group factor read from device memory (lr_scale), so a schedule
+// (ExponentialLR on the head, the 10x classifier cuts of
+// src/train_encoders_bert.py:406-410) changes a captured step's lr between
+// replays without re-capturing.
 //
 // HBM-bound: Adam moves 28 B per element (p, g, m, v in; p, m, v out), SGD
 // 20 B (p, g, buf in; p, buf out).
@@ -44,12 +48,14 @@ struct Args {
 };
 
 struct Consts {
+  float lr;                    // effective learning rate (G.lr * lr_scale[group])
   float step_size, bc2_sqrt;   // Adam: lr / (1 - b1^t), sqrt(1 - b2^t)
   int first;                   // SGD: momentum buffer starts as d_p at t = 1
 };
 
 __device__ __forceinline__ void update(float& p, float g, float& s0, float& s1,
                                        const tgfr_optim_group& G, const Consts& c) {
+  // c.lr: G.lr times the group's device-side scale
   if (G.weight_decay != 0.f) g = fmaf(G.weight_decay, p, g);
   if (G.kind == TGFR_OPTIM_ADAM) {
     s0 = G.beta1 * s0 + (1.f - G.beta1) * g;
@@ -61,7 +67,7 @@ __device__ __forceinline__ void update(float& p, float g, float& s0, float& s1,
       s0 = c.first ? g : G.momentum * s0 + (1.f - G.dampening) * g;
       g = s0;
     }
-    p -= G.lr * g;
+    p -= c.lr * g;
   }
 }
 
@@ -90,7 +96,8 @@ __device__ __forceinline__ void update_vec(const Seg& sg, long long e0, bool ada
   }
 }
 
-__global__ __launch_bounds__(THREADS) void optim_step_kernel(Args a, int* counters) {
+__global__ __launch_bounds__(THREADS) void optim_step_kernel(Args a, const float* lr_scale,
+                                                             int* counters) {
   const int b = blockIdx.x;
   int s = 0;
   while (s + 1 < a.nseg && a.bstart[s + 1] <= b) ++s;
@@ -99,7 +106,8 @@ __global__ __launch_bounds__(THREADS) void optim_step_kernel(Args a, int* counte
   const int t = counters[0] + 1;
   Consts c;
   c.first = t == 1;
-  c.step_size = (float)((double)G.lr / (1.0 - pow((double)G.beta1, (double)t)));
+  c.lr = lr_scale ? G.lr * lr_scale[sg.grp] : G.lr;
+  c.step_size = (float)((double)c.lr / (1.0 - pow((double)G.beta1, (double)t)));
   c.bc2_sqrt = (float)sqrt(1.0 - pow((double)G.beta2, (double)t));
   const bool adam = G.kind == TGFR_OPTIM_ADAM;
   const bool has_s0 = adam || G.momentum != 0.f;
@@ -126,8 +134,8 @@ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 }  // namespace
 
 extern "C" int tgfr_optim_step(const tgfr_optim_seg* segs, int n_segs,
-                               const tgfr_optim_group* groups, int n_groups, int* counters,
-                               void* stream) {
+                               const tgfr_optim_group* groups, int n_groups,
+                               const float* lr_scale, int* counters, void* stream) {
   if (n_segs <= 0 || n_segs > MAX_SEG || n_groups <= 0 || n_groups > MAX_GRP || !counters)
     return 1001;
   Args a;
@@ -160,6 +168,6 @@ extern "C" int tgfr_optim_step(const tgfr_optim_seg* segs, int n_segs,
   }
   a.bstart[n_segs] = (int)blocks;
   hipLaunchKernelGGL(optim_step_kernel, dim3((unsigned)blocks), dim3(THREADS), 0,
-                     (hipStream_t)stream, a, counters);
+                     (hipStream_t)stream, a, lr_scale, counters);
   return (int)hipGetLastError();
 }

@@ -175,15 +175,15 @@ template <int MODE>
 __global__ __launch_bounds__(TC_NT) void text_conv_kernel(
     const float* __restrict__ X, int rows, const uint16_t* __restrict__ taps,
     const float* __restrict__ b2, const float* __restrict__ b3, const float* __restrict__ b4,
-    float* __restrict__ Y, long long map_stride, int tn_major) {
+    float* __restrict__ Y, long long map_stride) {
   using G = TcCfg<MODE>;
   constexpr int NS = G::NS, STG = G::STG, PER = G::PER, XP = G::X_PIECES;
   const int mt_n = gridDim.y;
   const int wid_ = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * mt_n);
   // an XCD takes consecutive row tiles x all 8 channel tiles: its X rows are
   // read from HBM once, the 3.5 MB of bf16 taps stay in its L2
-  const int tn = tn_major ? wid_ / mt_n : wid_ % (TH_D / TC_TN);
-  const int tm = tn_major ? wid_ % mt_n : wid_ / (TH_D / TC_TN);
+  const int tn = wid_ % (TH_D / TC_TN);
+  const int tm = wid_ / (TH_D / TC_TN);
   const int m0 = tm * TC_TM, n0 = tn * TC_TN;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
   const int wm = wid & 1, ks = (wid >> 1) & 1, tg = wid >> 2;
@@ -348,23 +348,22 @@ int tgfr_text_heading(const float* X, int B, int L1, const uint16_t* taps,
   const long long map = rows * TH_D;
   auto* s = (hipStream_t)stream;
   const dim3 grid(TH_D / TC_TN, (unsigned)((rows + TC_TM - 1) / TC_TM));
-  static const int tn_major = getenv("TGFR_TEXT_TN_MAJOR") ? atoi(getenv("TGFR_TEXT_TN_MAJOR")) : 0;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)&text_conv_kernel<MODE_SPLIT>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, TcCfg<MODE_SPLIT>::LDS);
-    hipFuncSetAttribute((const void*)&text_conv_kernel<MODE_BF16>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, TcCfg<MODE_BF16>::LDS);
-    attr_set = true;
+  if (mode == MODE_SPLIT) {
+    if (const int e = set_max_lds((const void*)&text_conv_kernel<MODE_SPLIT>,
+                                  TcCfg<MODE_SPLIT>::LDS))
+      return e;
+  } else if (const int e = set_max_lds((const void*)&text_conv_kernel<MODE_BF16>,
+                                       TcCfg<MODE_BF16>::LDS)) {
+    return e;
   }
   if (mode == MODE_SPLIT) {
     hipLaunchKernelGGL(text_conv_kernel<MODE_SPLIT>, grid, dim3(TC_NT),
                        TcCfg<MODE_SPLIT>::LDS, s, X, (int)rows, taps, conv_b[0], conv_b[1],
-                       conv_b[2], ws, map, tn_major);
+                       conv_b[2], ws, map);
   } else {
     hipLaunchKernelGGL(text_conv_kernel<MODE_BF16>, grid, dim3(TC_NT),
                        TcCfg<MODE_BF16>::LDS, s, X, (int)rows, taps, conv_b[0], conv_b[1],
-                       conv_b[2], ws, map, tn_major);
+                       conv_b[2], ws, map);
   }
   hipLaunchKernelGGL(text_pool_kernel, dim3(B), dim3(64 * TH_NW), 0, s, ws, map, L1, words,
                      s_wb, s_wt, sent, s_sb);

@@ -27,8 +27,6 @@
 //               [S^T; dA2^T] = X R_tile^T, the two softmax backwards in
 //               registers, and dR_tile += [dS | A2] X.  Writes partial slabs.
 //   wr_reduce   sums the caption-chunk slabs into dR (caller's strides).
-#include <stdlib.h>
-
 #include "tgfr_common.h"
 
 using namespace tgfr;
@@ -678,14 +676,8 @@ struct FwdSlot {
 constexpr int FWD_SLOTS = 16 + 5 * 34 + 18 + 34;
 // LDS operand prefetch distance in MFMA slots (ring of 8; see the wrap
 // argument at the issue site: no live slot is overwritten for 3 <= PF <= 6)
-#ifndef TGFR_PF_FWD
-#define TGFR_PF_FWD 3
-#endif
-#ifndef TGFR_PF_BWD
-#define TGFR_PF_BWD 3
-#endif
-constexpr int PF_FWD = TGFR_PF_FWD;
-constexpr int PF_BWD = TGFR_PF_BWD;
+constexpr int PF_FWD = 3;
+constexpr int PF_BWD = 3;
 // the caption's slots in issue order
 __device__ __forceinline__ constexpr FwdSlot fwd_slot(int n) {
   if (n < 16) return {0, 1, n, 0, n};
@@ -1766,8 +1758,8 @@ __global__ __launch_bounds__(256) void wr_reduce_kernel(const float* __restrict_
 }  // namespace
 
 template <typename K>
-static void allow_lds(K kernel, int bytes) {
-  hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+static int allow_lds(K kernel, int bytes) {
+  return set_max_lds((const void*)kernel, bytes);
 }
 
 // ============================================================== C ABI ===
@@ -1794,15 +1786,11 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   if (t_pad != 32 && t_pad != 64) return 1001;
   const int grid = ((B_cap + 3) / 4) * B_img;
   auto* s = (hipStream_t)stream;
-  static bool once = [] {
-    allow_lds(wr_fwd_kernel<MODE_SPLIT, 1>, F_LDS);
-    allow_lds(wr_fwd_kernel<MODE_SPLIT, 2>, F_LDS2);
-    allow_lds(wr_fwd_kernel<MODE_BF16, 2>, F_LDS2);
-    allow_lds(wr_fwd_res_kernel, FR_LDS);
-    allow_lds(wr_fwd_pipe_kernel, FR_LDS);
-    return true;
-  }();
-  (void)once;
+  if (const int e = allow_lds(wr_fwd_kernel<MODE_SPLIT, 1>, F_LDS)) return e;
+  if (const int e = allow_lds(wr_fwd_kernel<MODE_SPLIT, 2>, F_LDS2)) return e;
+  if (const int e = allow_lds(wr_fwd_kernel<MODE_BF16, 2>, F_LDS2)) return e;
+  if (const int e = allow_lds(wr_fwd_res_kernel, FR_LDS)) return e;
+  if (const int e = allow_lds(wr_fwd_pipe_kernel, FR_LDS)) return e;
   if (t_pad == 64) {
     // 64-token captions: two waves per caption, two captions per workgroup
     const int grid2 = ((B_cap + 1) / 2) * B_img;
@@ -1827,8 +1815,7 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   else if (mode == MODE_BF16) {
     // R resident in LDS; caption chunks sized for >= ~256 workgroups
     const int n_chunks = max(1, min((B_cap + 3) / 4, (256 + B_img - 1) / B_img));
-    static const bool pipe = !getenv("TGFR_WR_FWD_RES");
-    if (pipe && bounded && Rnorm && !att && stats && Chi)
+    if (bounded && Rnorm && !att && stats && Chi)
       hipLaunchKernelGGL(wr_fwd_pipe_kernel, dim3(n_chunks * B_img), dim3(256), FR_LDS, s,
                          Rhi, Whi, Wnorm, Rnorm, lens, B_img, B_cap, n_chunks, gamma1, gamma2,
                          gamma3, eps, logits, ld_logits, (float4*)stats, Chi);
@@ -1870,12 +1857,8 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   if (t_pad == 64) {
     if (bounded) return 1001;
     if (mode == MODE_SPLIT && (!Rlo || !Wlo || !Clo)) return 1001;
-    static bool once_w = [] {
-      allow_lds(wr_bwd_wide_kernel<MODE_SPLIT>, BwdWCfg<MODE_SPLIT>::LDS);
-      allow_lds(wr_bwd_wide_kernel<MODE_BF16>, BwdWCfg<MODE_BF16>::LDS);
-      return true;
-    }();
-    (void)once_w;
+    if (const int e = allow_lds(wr_bwd_wide_kernel<MODE_SPLIT>, BwdWCfg<MODE_SPLIT>::LDS)) return e;
+    if (const int e = allow_lds(wr_bwd_wide_kernel<MODE_BF16>, BwdWCfg<MODE_BF16>::LDS)) return e;
     const int grid = n_chunks * 2 * B_img;
     if (mode == MODE_SPLIT)
       hipLaunchKernelGGL(wr_bwd_wide_kernel<MODE_SPLIT>, dim3(grid), dim3(256),
@@ -1892,11 +1875,7 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   if (t_pad != 32) return 1001;
   if (bounded) {
     if (mode != MODE_BF16) return 1002;
-    static bool once_p = [] {
-      allow_lds(wr_bwd_pipe_kernel, BP_LDS);
-      return true;
-    }();
-    (void)once_p;
+    if (const int e = allow_lds(wr_bwd_pipe_kernel, BP_LDS)) return e;
     hipLaunchKernelGGL(wr_bwd_pipe_kernel, dim3(n_chunks * 2 * B_img), dim3(256), BP_LDS,
                        (hipStream_t)stream, Rhi, Whi, B_img, B_cap, n_chunks, gamma1, tok_ws,
                        Chi, slab);
@@ -1904,12 +1883,8 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   }
   if (mode == MODE_SPLIT && (!Rlo || !Wlo || !Clo)) return 1001;
   auto* s = (hipStream_t)stream;
-  static bool once = [] {
-    allow_lds(wr_bwd_kernel<MODE_SPLIT>, BwdCfg<MODE_SPLIT>::LDS);
-    allow_lds(wr_bwd_kernel<MODE_BF16>, BwdCfg<MODE_BF16>::LDS);
-    return true;
-  }();
-  (void)once;
+  if (const int e = allow_lds(wr_bwd_kernel<MODE_SPLIT>, BwdCfg<MODE_SPLIT>::LDS)) return e;
+  if (const int e = allow_lds(wr_bwd_kernel<MODE_BF16>, BwdCfg<MODE_BF16>::LDS)) return e;
   const int grid = n_chunks * 2 * B_img;
   if (mode == MODE_SPLIT)
     hipLaunchKernelGGL(wr_bwd_kernel<MODE_SPLIT>, dim3(grid), dim3(256),
@@ -1937,6 +1912,6 @@ int tgfr_wr_lds_bytes(int which) {
   return which == 0 ? F_LDS : which == 1 ? BwdCfg<MODE_SPLIT>::LDS : FR_LDS;
 }
 
-int tgfr_version(void) { return 104; }
+int tgfr_version(void) { return 200; }
 
 }  // extern "C"

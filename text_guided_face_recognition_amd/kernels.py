@@ -66,7 +66,7 @@ def words_view(words_emb, n_words):
 def bwd_chunks(b_img, b_cap):
     """Caption chunks for the backward grid: ~one workgroup per CU (the kernel
     runs one 256-thread workgroup per CU), fewer slabs to reduce."""
-    per_cu = int(os.environ.get("TGFR_BWD_BLOCKS", "256"))
+    per_cu = 256
     want = max(1, -(-per_cu // (2 * b_img)))
     return max(1, min(b_cap, want))
 
@@ -199,8 +199,8 @@ class CosLogits(torch.autograd.Function):
         return dx, dy, None, None, None, None, None
 
 
-def cos_logits(x, y, scale, normalize=True, cls=None, row_offset=0):
-    return CosLogits.apply(x, y, scale, normalize, cls, row_offset)
+def cos_logits(x, y, scale, normalize=True, cls=None, row_offset=0, eps=1e-8):
+    return CosLogits.apply(x, y, scale, normalize, cls, row_offset, float(eps))
 
 
 # ---------------------------------------------------------- contrastive CE ---
@@ -765,34 +765,82 @@ def arc_head(x, weight, label, s, m, easy_margin=False, eps=1e-12, mode="fp32"):
 
 
 class FocalCE(torch.autograd.Function):
-    """FocalLoss(gamma)(logits, target) (losses.py:313-325)."""
+    """FocalLoss(gamma)(logits, target) (losses.py:313-325) on one or more
+    (logits, target) pairs.
+
+    The reference applies the focal factor to the mean cross-entropy of the
+    WHOLE batch it sees (DataParallel gathers every replica's logits on GPU 0).
+    With a process group each rank holds its own rows: the per-rank NLL sums
+    of all pairs are summed over ranks by ONE all-reduce, the focal loss is
+    formed from the global mean on every rank, and each rank's logit gradient
+    carries f'(CE_global) / N_global -- so the gradients summed over ranks are
+    the reference's global-batch gradients."""
 
     @staticmethod
-    def forward(ctx, logits, target, gamma):
-        logits = logits.float().contiguous()
-        target = target.to(torch.int64).contiguous()
-        rows, cols = logits.shape
-        ws = torch.empty(2 * rows + 1, dtype=torch.float32, device=logits.device)
-        loss = torch.empty(1, dtype=torch.float32, device=logits.device)
-        call("tgfr_focal_ce", ptr(logits), rows, cols, ptr(target), float(gamma), ptr(ws),
-             ptr(_hip.counters(logits.device)), ptr(loss), _hip.stream())
-        ctx.save_for_backward(logits, target, ws)
-        ctx.gamma = float(gamma)
-        return loss[0]
+    def forward(ctx, gamma, group, n_global, *pairs):
+        n = len(pairs) // 2
+        dev = pairs[0].device
+        outs, saved = [], []
+        for k in range(n):
+            logits = pairs[2 * k].float().contiguous()
+            target = pairs[2 * k + 1].to(torch.int64).contiguous()
+            rows, cols = logits.shape
+            ws = torch.empty(2 * rows + 1, dtype=torch.float32, device=dev)
+            loss = torch.empty(1, dtype=torch.float32, device=dev)
+            call("tgfr_focal_ce", ptr(logits), rows, cols, ptr(target), float(gamma), ptr(ws),
+                 ptr(_hip.counters(dev)), ptr(loss), _hip.stream())
+            outs.append(loss)
+            saved += [logits, target, ws]
+        rows_l = [saved[3 * k].shape[0] for k in range(n)]
+        if group is not None:
+            from .dist import all_reduce_sum_
+            # every pair's local NLL sum in one collective
+            sums = torch.cat([saved[3 * k + 2][rows_l[k]:rows_l[k] + 1] * rows_l[k]
+                              for k in range(n)])
+            all_reduce_sum_(sums, group)
+            for k in range(n):
+                ws = saved[3 * k + 2]
+                logp = sums[k:k + 1] / float(n_global)
+                ws[rows_l[k]:rows_l[k] + 1].copy_(logp)
+                outs[k] = (1.0 - torch.exp(-logp)).pow(float(gamma)) * logp
+        ctx.save_for_backward(*saved)
+        ctx.cfg = (float(gamma), n, rows_l, n_global if group is not None else None)
+        return tuple(o[0] for o in outs)
 
     @staticmethod
-    def backward(ctx, g):
-        logits, target, ws = ctx.saved_tensors
-        rows, cols = logits.shape
-        g = g.float().contiguous()
-        dl = torch.empty_like(logits)
-        call("tgfr_focal_ce_bwd", ptr(logits), rows, cols, ptr(target), ctx.gamma, ptr(ws),
-             ptr(g), ptr(dl), _hip.stream())
-        return dl, None, None
+    def backward(ctx, *gs):
+        gamma, n, rows_l, n_global = ctx.cfg
+        saved = ctx.saved_tensors
+        grads = []
+        for k in range(n):
+            logits, target, ws = saved[3 * k:3 * k + 3]
+            rows, cols = logits.shape
+            g = gs[k]
+            if g is None:
+                grads += [None, None]
+                continue
+            g = g.float().reshape(1)
+            if n_global is not None:
+                # the kernel divides by the local row count; the global mean's
+                # gradient divides by the global one
+                g = g * (rows / float(n_global))
+            g = g.contiguous()
+            dl = torch.empty_like(logits)
+            call("tgfr_focal_ce_bwd", ptr(logits), rows, cols, ptr(target), gamma, ptr(ws),
+                 ptr(g), ptr(dl), _hip.stream())
+            grads += [dl, None]
+        return (None, None, None) + tuple(grads)
 
 
-def focal_ce(logits, target, gamma):
-    return FocalCE.apply(logits, target, gamma)
+def focal_ce(logits, target, gamma, group=None, n_global=None):
+    return FocalCE.apply(gamma, group, n_global, logits, target)[0]
+
+
+def focal_ce_multi(pairs, gamma, group=None, n_global=None):
+    """Focal losses of several (logits, target) pairs; under a process group
+    their global means cost one all-reduce together."""
+    flat = [x for p in pairs for x in p]
+    return FocalCE.apply(gamma, group, n_global, *flat)
 
 
 # ------------------------------------------------------------- loss mix ---

@@ -62,7 +62,7 @@ def sent_loss(cnn_code, rnn_code, labels, class_ids, batch_size, args, eps=1e-8)
     row_offset, n_global, group = _dist(args)
     cls = _class_tensor(class_ids, cnn_code.device)
     logits = K.cos_logits(cnn_code, rnn_code, args.TRAIN.SMOOTH.GAMMA3, True, cls,
-                          row_offset)
+                          row_offset, eps=eps)
     if labels is None:
         return None, None
     return K.contrastive_ce(logits, row_offset, n_global or logits.shape[0], group)
@@ -85,18 +85,26 @@ def words_loss(img_features, words_emb, labels, cap_lens, class_ids, batch_size,
 
     img_features [B, 256, 14, 14] (any strides); words_emb [B_cap, 256, T'].
     BERT: every caption uses bert_words_num - 2 words (:83); LSTM: cap_lens[i]
-    (:82).  att_maps are the matching-pair maps [1, T, 14, 14] (:97), produced
-    by the forward kernel.
+    (:82) -- host data (a list, numpy array or CPU tensor, as the reference
+    passes) or a device int tensor (then T' is taken as the longest caption,
+    which keeps the call free of host synchronisation for graph capture).
+    att_maps are the matching-pair maps [1, T, 14, 14] (:97), produced by the
+    forward kernel.
     """
     b_img = img_features.shape[0]
     b_cap = words_emb.shape[0]
+    lens_host = None
     if args.en_type == "BERT":
         n_words = args.bert_words_num - 2
         lens = _const_lens(b_cap, n_words, img_features.device)
+    elif torch.is_tensor(cap_lens) and cap_lens.is_cuda:
+        n_words = words_emb.shape[2]
+        lens = cap_lens.to(torch.int32)
     else:
-        lens = torch.as_tensor(cap_lens).to(torch.int32)
-        n_words = int(lens.max())
-        lens = lens.to(img_features.device)
+        lens_host = [int(x) for x in np.asarray(cap_lens).reshape(-1)]
+        n_words = max(lens_host)
+        lens = torch.tensor(lens_host, dtype=torch.int32).to(img_features.device,
+                                                               non_blocking=True)
     words = K.words_view(words_emb, n_words)
     row_offset, n_global, group = _dist(args)
     smooth = args.TRAIN.SMOOTH
@@ -111,9 +119,12 @@ def words_loss(img_features, words_emb, labels, cap_lens, class_ids, batch_size,
     logits, att = (out if want_maps else (out, None))
     att_maps = []
     if att is not None:
-        lens_l = lens.tolist()
+        if lens_host is None:
+            # BERT: every caption has n_words; a device cap_lens tensor is read
+            # back once here (the maps' shapes depend on it, as in :97)
+            lens_host = [n_words] * b_cap if args.en_type == "BERT" else lens.tolist()
         for b in range(b_img):
-            t = lens_l[row_offset + b] if row_offset + b < b_cap else n_words
+            t = lens_host[row_offset + b] if row_offset + b < b_cap else n_words
             att_maps.append(att[b, :t].reshape(1, t, 14, 14))
     if labels is None:
         return None, None, att_maps
@@ -124,7 +135,7 @@ def words_loss(img_features, words_emb, labels, cap_lens, class_ids, batch_size,
 def global_loss(cnn_code, rnn_code, eps=1e-8, temp3=10.0, args=None):
     """losses.py:329-351 -> loss0 + loss1 (labels are arange(batch))."""
     row_offset, n_global, group = _dist(args)
-    logits = K.cos_logits(cnn_code, rnn_code, temp3, True, None, row_offset)
+    logits = K.cos_logits(cnn_code, rnn_code, temp3, True, None, row_offset, eps=eps)
     l0, l1 = K.contrastive_ce(logits, row_offset, n_global or logits.shape[0], group)
     return l0 + l1
 

@@ -5,7 +5,11 @@ ArcMargin classifiers (src/train_encoders_bert.py:212-222, :323-330;
 src/fusion_bert.py:119-139, :238-239).  ``FusedOptimizer`` holds both as
 parameter groups and updates every tensor in one launch; the update rules are
 torch's (include/tgfr.h, 'optimiser step').  The step count is kept on the
-device, so a step captured into a HIP graph replays correctly.
+device, so a step captured into a HIP graph replays correctly; so are the
+per-group learning-rate factors, so ``set_lr`` / ``scale_lr`` (the reference's
+ExponentialLR(gamma=0.98) on the head and its 10x classifier cuts,
+src/train_encoders_bert.py:225, :406-410) take effect at the next step, also
+on a captured step that is replayed without re-capture.
 
     opt = FusedOptimizer([adam_group(head.parameters(), lr=2e-4, betas=(0.5, 0.999)),
                           sgd_group(cls.parameters(), lr=0.1, momentum=0.9,
@@ -70,6 +74,9 @@ class FusedOptimizer:
                 self.state[p] = st
         # [steps taken, last-arriver count]
         self.counters = torch.zeros(2, dtype=torch.int32, device=dev)
+        # per-group multipliers of the captured base lr, read by the kernel
+        self.base_lr = [float(g["lr"]) for g in groups]
+        self.lr_scale = torch.ones(len(groups), dtype=torch.float32, device=dev)
         self._groups_c = (_Group * len(groups))()
         for i, g in enumerate(groups):
             c = self._groups_c[i]
@@ -83,6 +90,30 @@ class FusedOptimizer:
                 c.momentum = g["momentum"]
                 c.dampening = g["dampening"]
         self._segs_c = (_Seg * len(self.params))()
+
+    def get_lr(self, group):
+        """The learning rate group `group` uses at the next step (host value)."""
+        return self.groups[group]["lr"]
+
+    def set_lr(self, group, lr):
+        """Set group `group`'s learning rate for the following steps (one tiny
+        device write; no re-capture of a graphed step needed)."""
+        lr = float(lr)
+        self.groups[group]["lr"] = lr
+        base = self.base_lr[group]
+        with torch.no_grad():
+            self.lr_scale[group].fill_(lr / base if base != 0.0 else 0.0)
+        if base == 0.0 and lr != 0.0:
+            raise ValueError("cannot rescale a group created with lr = 0")
+
+    def scale_lr(self, group, gamma):
+        """lr *= gamma for one group (ExponentialLR.step, the 0.1 cuts)."""
+        self.set_lr(group, self.groups[group]["lr"] * gamma)
+
+    @property
+    def param_groups(self):
+        """torch.optim-style view: one dict per group with its current 'lr'."""
+        return self.groups
 
     @property
     def step_count(self):
@@ -119,5 +150,6 @@ class FusedOptimizer:
         if n == 0:
             return
         _hip.call("tgfr_optim_step", C.addressof(segs), n, C.addressof(self._groups_c),
-                  len(self.groups), _hip.ptr(self.counters), _hip.stream())
+                  len(self.groups), _hip.ptr(self.lr_scale), _hip.ptr(self.counters),
+                  _hip.stream())
 

@@ -3,6 +3,10 @@
   Train   src/train_encoders_bert.py:233-331 (stage 1, FCAM): image head (IMIM)
           -> words_loss + sent_loss (DAMSM) + 2 ArcMargin/focal identity
           losses + global_loss (CLIP term) -> backward -> optimiser steps.
+  TrainLSTM  src/train_encoders_lstm.py:236-314 (stage 1, LSTM text encoder,
+          BASELINE configs[0]): words_loss with per-caption lengths (w0 + w1;
+          the reference computes sent_loss and discards it, :263-266) +
+          2 ArcMargin/focal identity losses + lambda_clip * ClipLoss (:288-291).
   Fusion  src/fusion_bert.py:195-243 (stage 2, FCFM): image head -> Working
           -> ArcMargin(640) -> focal loss -> backward -> optimiser steps.
 
@@ -15,11 +19,13 @@ them with the shapes and statistics SURVEY.md 8(d) prescribes.
 One process per GPU: pass a DistContext; text features and class ids are
 all-gathered (one collective) so every contrastive denominator sees the global
 batch.  Gradients are summed over ranks by one flat all-reduce
-(DistContext.reduce_grads, in place of DDP), so the contrastive losses -- this
-rank's contributions to the global-batch losses -- enter with weight 1 and the
-per-rank-mean identity losses with weight 1/world: the summed gradient is the
-reference's global-batch gradient.  Initial parameters are broadcast from
-rank 0.
+(DistContext.reduce_grads, in place of DDP).  The contrastive losses are this
+rank's contributions to the global-batch losses; the focal identity losses are
+formed from the GLOBAL mean cross-entropy (one all-reduce of the per-rank NLL
+sums, kernels.FocalCE), as the reference's DataParallel computes them on the
+gathered batch.  Every term enters with the reference's weight, and the
+summed gradient is the reference's global-batch gradient.  Initial parameters
+are broadcast from rank 0.
 """
 from __future__ import annotations
 
@@ -27,7 +33,7 @@ import torch
 from . import kernels as K
 from .dist import DistContext, StepCapture
 from .models.fusion_nets import Working, set_precision
-from .models.losses import FocalLoss, global_loss, sent_loss, words_loss
+from .models.losses import ClipLoss, FocalLoss, global_loss, sent_loss, words_loss
 from .models.metrics import ArcMarginProduct
 from .models.models import ImageHeading
 from .optim import FusedOptimizer, adam_group, sgd_group
@@ -48,6 +54,23 @@ def synthetic_batch(b, n_words, device, seed, n_ids=10000):
     to = dict(device=device)
     return (g.to(**to), local.to(**to), words.to(**to).transpose(1, 2), sent.to(**to),
             cls.to(**to))
+
+
+def synthetic_batch_lstm(b, max_words, device, seed, n_ids=1000):
+    """Frozen BiLSTM-encoder outputs for one batch:
+    words [B, 256, Lmax] (unnormalised, tanh-range like the LSTM's outputs,
+    models/models.py:311-318; storage [B, Lmax, 256]), sentence codes
+    L2-normalised (:323), caption lengths U[3, Lmax] (device int32)."""
+    gen = torch.Generator(device="cpu").manual_seed(seed)
+    g = torch.randn(b, 512, generator=gen)
+    local = torch.randn(b, 256, 14, 14, generator=gen)
+    words = torch.tanh(torch.randn(b, max_words, 256, generator=gen))
+    sent = _unit(torch.randn(b, 256, generator=gen))
+    cls = torch.randint(0, n_ids, (b,), generator=gen)
+    lens = torch.randint(3, max_words + 1, (b,), generator=gen)
+    to = dict(device=device)
+    return (g.to(**to), local.to(**to), words.to(**to).transpose(1, 2), sent.to(**to),
+            cls.to(**to), lens.to(device=device, dtype=torch.int32))
 
 
 class Train:
@@ -91,17 +114,18 @@ class Train:
 
         w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
         s0, s1 = sent_loss(img_features, sent_g, labels, cls_g, b, args)
-        tid = self.ident_loss(self.text_cls(sent, class_ids), class_ids)      # :293-294
-        iid = self.ident_loss(self.image_cls(img_features, class_ids), class_ids)
+        # :293-306, both focal losses from the global-batch mean CE
+        tid, iid = K.focal_ce_multi(
+            [(self.text_cls(sent, class_ids), class_ids),
+             (self.image_cls(img_features, class_ids), class_ids)],
+            self.ident_loss.gamma, ctx.group if ctx.active else None, ctx.n_global)
         cl = global_loss(img_features, sent_g, args=args)          # :310
-        # total = damsm + lambda_clip * cl + lambda_id / world * (tid + iid)
-        # (:279, :316-323; see the module docstring for the 1/world) and the
-        # logged terms, as one launch each way
+        # total = damsm + lambda_clip * cl + lambda_id * (tid + iid)
+        # (:279, :316-323) and the logged terms, as one launch each way
         wi = float(args.lambda_id)
-        wo = wi / ctx.world
         total, report = K.loss_mix(
             (w0, w1, s0, s1, cl, tid, iid),
-            [(1, 1, 1, 1, args.lambda_clip, wo, wo),              # objective
+            [(1, 1, 1, 1, args.lambda_clip, wi, wi),              # objective
              (1, 1, 1, 1, 0, 0, 0),                               # damsm
              (0, 0, 0, 0, 1, 0, 0),                               # clip
              (0, 0, 0, 0, 0, wi, wi)])                            # ident
@@ -115,6 +139,51 @@ class Train:
         if lab is None or lab.numel() != n or lab.device != device:
             lab = self._lab = torch.arange(n, device=device)
         return lab
+
+
+class TrainLSTM(Train):
+    """Stage-1 LSTM trainer step (src/train_encoders_lstm.py:236-314).
+
+    The reference also steps an Adam on the text encoder (:178-181), but the
+    encoder runs under no_grad (utils/dataset_utils.py:25-33), so that step
+    never changes it; the text side here is frozen input as for BERT."""
+
+    def __init__(self, args, device, ctx=None):
+        args.en_type = "LSTM"
+        super().__init__(args, device, ctx)
+        self.clip_loss = ClipLoss()
+
+    def step(self, batch):
+        args, ctx = self.args, self.ctx
+        g, local, words, sent, class_ids, cap_lens = batch
+        b = g.shape[0]
+        ctx.set_batch(b)
+        args.dist = ctx
+        words_g, sent_g, cls_g, lens_g = ctx.gather_text(words.transpose(1, 2), sent,
+                                                         class_ids, cap_lens)
+        words_g = words_g.transpose(1, 2)
+        labels = self._labels(ctx.n_global, g.device)
+
+        img_features, words_features = self.image_head(g, local)
+        self.optimizer.zero_grad(set_to_none=True)
+        # :260-266: damsm = w0 + w1 (sent_loss is computed there and discarded)
+        w0, w1, _ = words_loss(words_features, words_g, labels, lens_g, cls_g, b, args)
+        tid, iid = K.focal_ce_multi(                               # :272-282
+            [(self.text_cls(sent, class_ids), class_ids),
+             (self.image_cls(img_features, class_ids), class_ids)],
+            self.ident_loss.gamma, ctx.group if ctx.active else None, ctx.n_global)
+        cl = self.clip_loss(sent_g, img_features, args)            # :288-291
+        wi = float(args.lambda_id)
+        total, report = K.loss_mix(
+            (w0, w1, cl, tid, iid),
+            [(1, 1, args.lambda_clip, wi, wi),                     # objective
+             (1, 1, 0, 0, 0),                                      # damsm
+             (0, 0, args.lambda_clip, 0, 0),                       # clip (logged x lambda)
+             (0, 0, 0, wi, wi)])                                   # ident
+        total.backward()
+        ctx.reduce_grads(self.params)
+        self.optimizer.step()
+        return {"damsm": report[0], "clip": report[1], "ident": report[2]}
 
 
 class Fusion:
@@ -140,16 +209,20 @@ class Fusion:
 
     def step(self, batch):
         g, local, words, sent, class_ids = batch
+        ctx = self.ctx
+        ctx.set_batch(g.shape[0])
         words = words.requires_grad_()                             # :211-212
         sent = sent.requires_grad_()
         img_feats, local_feats = self.image_head(g, local)         # :220
         output = self.fusion_net(local_feats, words, img_feats, sent)   # :153
         output = self.metric_fc(output, class_ids)                 # :224
         self.optimizer.zero_grad(set_to_none=True)
-        loss = self.criterion(output, class_ids)                   # :232
-        # replicas only: per-rank mean losses, summed gradients -> scale 1/world
-        (loss if self.ctx.world == 1 else loss / self.ctx.world).backward()
-        self.ctx.reduce_grads(self.params)
+        # :232; under DP the focal factor of the global-batch mean CE (one
+        # all-reduce of the NLL sums), gradients summed over ranks
+        loss, = K.focal_ce_multi([(output, class_ids)], self.criterion.gamma,
+                                 ctx.group if ctx.active else None, ctx.n_global)
+        loss.backward()
+        ctx.reduce_grads(self.params)
         self.optimizer.step()
         return {"loss": loss.detach()}
 

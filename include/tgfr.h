@@ -71,26 +71,26 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 float* att, int att_T, int bounded, int t_pad, int mode, void* stream);
 
 /* Backward of tgfr_wr_fwd w.r.t. the image regions given dL/dlogits, in two
- * launches.  tgfr_wr_bwd_tok: per-(pair, token) scalars from the forward
- * stats and dlogits into tok_ws (B_img*B_cap*32*8 floats).  tgfr_wr_bwd: the
- * fused recompute + both softmax backwards + dR GEMM; writes n_chunks partial
- * slabs [n_chunks][B_img][224][256] (one per caption chunk).  The text side
- * is detached in the reference (utils/dataset_utils.py:42).  bounded = 1
- * (mode 0 only, after a bounded forward): both calls must pass it, Whi is the
- * forward's log2(e)-scaled words, and the pipelined kernel runs (no running
- * max in the softmax recompute). */
+ * calls.  tgfr_wr_bwd_tok: per-(pair, token) scalars from the forward stats
+ * and dlogits into tok_ws (B_img*B_cap*t_pad*8 floats).  tgfr_wr_bwd: the
+ * fused recompute + both softmax backwards + dR GEMM, writing
+ * dR[b][r][d] (r < 196) at dR[b*s_b + r*s_r + d*s_d] -- overwritten, not
+ * accumulated.  ws: tgfr_wr_bwd_ws floats of workspace: caption-chunk partial
+ * slabs, added in chunk order into dR by a reduction launch inside the call;
+ * counters: reserved (may be NULL).  The text side is detached in the
+ * reference (utils/dataset_utils.py:42).  bounded = 1 (mode 0, t_pad 32,
+ * after a bounded forward): both calls must pass it, Whi is the forward's
+ * log2(e)-scaled words, and the software-pipelined kernel runs. */
 int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const int* lens, int B_img,
                     int B_cap, float gamma1, float gamma2, float gamma3, float eps,
                     const float* dlogits, int ld, int bounded, int t_pad, float* tok_ws,
                     void* stream);
+int tgfr_wr_bwd_ws(int B_img, int B_cap, int bounded, int t_pad, int mode, long long* floats);
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
-                const uint16_t* Wlo, int B_img, int B_cap, int n_chunks, float gamma1,
-                const float* tok_ws, const uint16_t* Chi, const uint16_t* Clo, float* slab,
-                int bounded, int t_pad, int mode, void* stream);
-
-/* dR[b][r][d] (caller strides; r < 196) = (+)= sum over chunks of the slabs. */
-int tgfr_wr_reduce(const float* slab, int n_chunks, int B_img, float* out, long long s_b,
-                   long long s_r, long long s_d, int accumulate, void* stream);
+                const uint16_t* Wlo, int B_img, int B_cap, float gamma1, const float* tok_ws,
+                const uint16_t* Chi, const uint16_t* Clo, float* dR, long long s_b,
+                long long s_r, long long s_d, float* ws, unsigned* counters, int bounded,
+                int t_pad, int mode, void* stream);
 
 /* Dynamic LDS bytes of the streaming forward (which = 0), the fp32-mode
  * backward (1) and the resident-R bf16 forward (2). */

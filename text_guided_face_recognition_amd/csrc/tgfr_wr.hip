@@ -29,6 +29,8 @@
 //   wr_reduce   sums the caption-chunk slabs into dR (caller's strides).
 #include "tgfr_common.h"
 
+#include <algorithm>
+
 using namespace tgfr;
 
 namespace {
@@ -634,14 +636,20 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
 // MFMA gap carries ~5 issue slots of other work (MI355X_MICROARCH.md,
 // 'single-issue instructions HIDDEN per MFMA gap').
 //
-// Words come in scaled by log2(e) (W' = log2(e) W, tgfr_prep_rows scale), and
-// GEMM1's accumulator starts at init[t] = bias[t] - log2(e) c with c =
-// max_t |W_t| * max_r |R_r| >= every score of the caption: the softmax over
-// words is then p = exp2(S'^T) directly (no max, no subtraction; exact in
-// real arithmetic, the shift cancels in the normalisation; no term can
-// overflow, and a region's sum cannot underflow while 2c < 87 -- c = 1 for
-// the L2-normalised BERT-path features, models/models.py:212,403).  The host
-// routes other inputs to wr_fwd_res_kernel (exact running max).  Padding
+// Words come in scaled by log2(e) (W' = log2(e) W, tgfr_prep_rows scale).
+// With c = max_t |W_t| * max_r |R_r| >= |every score of the caption|, the
+// softmax over words is p = exp2(S'^T) directly -- no max, no subtraction:
+// exact in real arithmetic (any shift cancels in the normalisation), and no
+// term overflows and no region's sum underflows while c < 40 (c = 1 for the
+// L2-normalised BERT-path features, models/models.py:212,403; <= 16 for the
+// LSTM's tanh outputs against unit regions).  GEMM1's accumulator starts at
+// the word bias (0, or -1e30 for padding words).  For 40 <= c < 43 it also
+// carries the shift -log2(e) c (p <= 1); the shift is added back in the
+// statistics.  The shift is applied only where needed: N = sum_r E S then
+// cancels c Z, which costs ~1e-4 of N when Z is formed from the bf16 E of
+// GEMM2 -- visible as ~0.05 logit error through cos = N / (|W| |C|) with
+// |C| ~ 0.07 for diffuse attention.  The host routes other inputs to
+// wr_fwd_res_kernel (exact running max).  Padding
 // words carry bias -1e30 (p = 0; their E = exp(0) = 1 only feeds their own
 // unused statistics and C-hat rows); padding regions (tile 6) get -1e30
 // inside the second exp2.  Outputs: logits, stats {Z, n, |C|, cos}, C-hat
@@ -739,6 +747,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
   auto caption_init = [&](int ii, float wn, float& c) {
     const int len = lens[ii];
     c = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(half_max(wn) * rmax)));
+    if (c < 40.f) c = 0.f;             // no shift needed (see above)
     const float sh = -L2E * c;
     f32x16 init;
 #pragma unroll
@@ -1503,6 +1512,11 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide_kernel(
 // ring by LDS DMA issued two captions ahead; one barrier per stage.
 // Captions past the chunk read a zero token table: their M fragments are
 // zero, so the fill / drain stages need no branches.
+// Each caption chunk writes its partial dR tiles to its own slab; one
+// reduction launch (wr_reduce_kernel) adds them in chunk order.  (An in-launch
+// last-arriver sum measured slower here: the last arrivers' cross-XCD slab
+// reads run at low memory parallelism, ~15 us against ~10 us for the
+// chip-wide reduction launch.)
 constexpr int BP_NB = 4;                       // ring depth
 constexpr int BP_TOK = 1024;                   // token table bytes
 constexpr int BP_BUF = B_XIMG + BP_TOK;        // one caption: X image + table
@@ -1757,6 +1771,29 @@ __global__ __launch_bounds__(256) void wr_reduce_kernel(const float* __restrict_
 
 }  // namespace
 
+// Number of compute units of the current device (cached per device).
+static int device_cus() {
+  static std::mutex mu;
+  static std::map<int, int> cus;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cus.find(dev);
+  if (it != cus.end()) return it->second;
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    n = 256;
+  cus[dev] = n;
+  return n;
+}
+
+// Caption chunks of the general backward kernels (one 256-thread workgroup
+// per CU): each chunk's partial dR goes to its own slab.
+static int slab_chunks(int B_img, int B_cap) {
+  const int want = std::max(1, (device_cus() + 2 * B_img - 1) / (2 * B_img));
+  return std::max(1, std::min(B_cap, want));
+}
+
 template <typename K>
 static int allow_lds(K kernel, int bytes) {
   return set_max_lds((const void*)kernel, bytes);
@@ -1849,62 +1886,61 @@ int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const int* lens, int
   return (int)hipGetLastError();
 }
 
-int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
-                const uint16_t* Wlo, int B_img, int B_cap, int n_chunks, float gamma1,
-                const float* tok_ws, const uint16_t* Chi, const uint16_t* Clo, float* slab,
-                int bounded, int t_pad, int mode, void* stream) {
-  if (B_img <= 0 || B_cap <= 0 || n_chunks <= 0 || n_chunks > B_cap) return 1001;
-  if (t_pad == 64) {
-    if (bounded) return 1001;
-    if (mode == MODE_SPLIT && (!Rlo || !Wlo || !Clo)) return 1001;
-    if (const int e = allow_lds(wr_bwd_wide_kernel<MODE_SPLIT>, BwdWCfg<MODE_SPLIT>::LDS)) return e;
-    if (const int e = allow_lds(wr_bwd_wide_kernel<MODE_BF16>, BwdWCfg<MODE_BF16>::LDS)) return e;
-    const int grid = n_chunks * 2 * B_img;
-    if (mode == MODE_SPLIT)
-      hipLaunchKernelGGL(wr_bwd_wide_kernel<MODE_SPLIT>, dim3(grid), dim3(256),
-                         BwdWCfg<MODE_SPLIT>::LDS, (hipStream_t)stream, Rhi, Rlo, Whi, Wlo,
-                         B_img, B_cap, n_chunks, gamma1, tok_ws, Chi, Clo, slab);
-    else if (mode == MODE_BF16)
-      hipLaunchKernelGGL(wr_bwd_wide_kernel<MODE_BF16>, dim3(grid), dim3(256),
-                         BwdWCfg<MODE_BF16>::LDS, (hipStream_t)stream, Rhi, Rlo, Whi, Wlo,
-                         B_img, B_cap, n_chunks, gamma1, tok_ws, Chi, Clo, slab);
-    else
-      return 1002;
-    return (int)hipGetLastError();
-  }
-  if (t_pad != 32) return 1001;
-  if (bounded) {
-    if (mode != MODE_BF16) return 1002;
-    if (const int e = allow_lds(wr_bwd_pipe_kernel, BP_LDS)) return e;
-    hipLaunchKernelGGL(wr_bwd_pipe_kernel, dim3(n_chunks * 2 * B_img), dim3(256), BP_LDS,
-                       (hipStream_t)stream, Rhi, Whi, B_img, B_cap, n_chunks, gamma1, tok_ws,
-                       Chi, slab);
-    return (int)hipGetLastError();
-  }
-  if (mode == MODE_SPLIT && (!Rlo || !Wlo || !Clo)) return 1001;
-  auto* s = (hipStream_t)stream;
-  if (const int e = allow_lds(wr_bwd_kernel<MODE_SPLIT>, BwdCfg<MODE_SPLIT>::LDS)) return e;
-  if (const int e = allow_lds(wr_bwd_kernel<MODE_BF16>, BwdCfg<MODE_BF16>::LDS)) return e;
-  const int grid = n_chunks * 2 * B_img;
-  if (mode == MODE_SPLIT)
-    hipLaunchKernelGGL(wr_bwd_kernel<MODE_SPLIT>, dim3(grid), dim3(256),
-                       BwdCfg<MODE_SPLIT>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
-                       gamma1, tok_ws, Chi, Clo, slab);
-  else if (mode == MODE_BF16)
-    hipLaunchKernelGGL(wr_bwd_kernel<MODE_BF16>, dim3(grid), dim3(256),
-                       BwdCfg<MODE_BF16>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
-                       gamma1, tok_ws, Chi, Clo, slab);
-  else
-    return 1002;
-  return (int)hipGetLastError();
+int tgfr_wr_bwd_ws(int B_img, int B_cap, int bounded, int t_pad, int mode, long long* floats) {
+  if (B_img <= 0 || B_cap <= 0 || !floats) return 1001;
+  *floats = (long long)slab_chunks(B_img, B_cap) * B_img * RPAD * D;
+  return 0;
 }
 
-int tgfr_wr_reduce(const float* slab, int n_chunks, int B_img, float* out, long long s_b,
-                   long long s_r, long long s_d, int accumulate, void* stream) {
+int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
+                const uint16_t* Wlo, int B_img, int B_cap, float gamma1, const float* tok_ws,
+                const uint16_t* Chi, const uint16_t* Clo, float* dR, long long s_b,
+                long long s_r, long long s_d, float* ws, unsigned* counters, int bounded,
+                int t_pad, int mode, void* stream) {
+  (void)counters;
+  if (B_img <= 0 || B_cap <= 0 || !dR || !ws) return 1001;
+  if (mode != MODE_SPLIT && mode != MODE_BF16) return 1002;
+  auto* s = (hipStream_t)stream;
+  // caption-chunk partial slabs in ws, summed into dR by wr_reduce_kernel
+  const int n_chunks = slab_chunks(B_img, B_cap);
+  const int grid = n_chunks * 2 * B_img;
+  if (bounded) {
+    if (t_pad != 32) return 1001;
+    if (mode != MODE_BF16) return 1002;
+    if (const int e = allow_lds(wr_bwd_pipe_kernel, BP_LDS)) return e;
+    hipLaunchKernelGGL(wr_bwd_pipe_kernel, dim3(grid), dim3(256), BP_LDS, s, Rhi, Whi, B_img,
+                       B_cap, n_chunks, gamma1, tok_ws, Chi, ws);
+  } else if (mode == MODE_SPLIT && (!Rlo || !Wlo || !Clo)) {
+    return 1001;
+  } else if (t_pad == 64) {
+    if (const int e = allow_lds(wr_bwd_wide_kernel<MODE_SPLIT>, BwdWCfg<MODE_SPLIT>::LDS)) return e;
+    if (const int e = allow_lds(wr_bwd_wide_kernel<MODE_BF16>, BwdWCfg<MODE_BF16>::LDS)) return e;
+    if (mode == MODE_SPLIT)
+      hipLaunchKernelGGL(wr_bwd_wide_kernel<MODE_SPLIT>, dim3(grid), dim3(256),
+                         BwdWCfg<MODE_SPLIT>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
+                         gamma1, tok_ws, Chi, Clo, ws);
+    else
+      hipLaunchKernelGGL(wr_bwd_wide_kernel<MODE_BF16>, dim3(grid), dim3(256),
+                         BwdWCfg<MODE_BF16>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
+                         gamma1, tok_ws, Chi, Clo, ws);
+  } else if (t_pad == 32) {
+    if (const int e = allow_lds(wr_bwd_kernel<MODE_SPLIT>, BwdCfg<MODE_SPLIT>::LDS)) return e;
+    if (const int e = allow_lds(wr_bwd_kernel<MODE_BF16>, BwdCfg<MODE_BF16>::LDS)) return e;
+    if (mode == MODE_SPLIT)
+      hipLaunchKernelGGL(wr_bwd_kernel<MODE_SPLIT>, dim3(grid), dim3(256),
+                         BwdCfg<MODE_SPLIT>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
+                         gamma1, tok_ws, Chi, Clo, ws);
+    else
+      hipLaunchKernelGGL(wr_bwd_kernel<MODE_BF16>, dim3(grid), dim3(256),
+                         BwdCfg<MODE_BF16>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
+                         gamma1, tok_ws, Chi, Clo, ws);
+  } else {
+    return 1001;
+  }
   const long long n = (long long)B_img * NREG * D;
-  const int grid = (int)min((n + 255) / 256, 4096LL);
-  hipLaunchKernelGGL(wr_reduce_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, slab,
-                     n_chunks, B_img, out, s_b, s_r, s_d, accumulate);
+  const int rgrid = (int)min((n + 255) / 256, 4096LL);
+  hipLaunchKernelGGL(wr_reduce_kernel, dim3(rgrid), dim3(256), 0, s, ws, n_chunks, B_img, dR, s_b,
+                     s_r, s_d, 0);
   return (int)hipGetLastError();
 }
 

@@ -7,7 +7,6 @@ in a HIP graph.  There is no CPU fallback: CPU tensors raise.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -63,12 +62,13 @@ def words_view(words_emb, n_words):
     return words_emb[:, :, :n_words].transpose(1, 2)
 
 
-def bwd_chunks(b_img, b_cap):
-    """Caption chunks for the backward grid: ~one workgroup per CU (the kernel
-    runs one 256-thread workgroup per CU), fewer slabs to reduce."""
-    per_cu = 256
-    want = max(1, -(-per_cu // (2 * b_img)))
-    return max(1, min(b_cap, want))
+def wr_bwd_ws_floats(b_img, b_cap, bounded, t_pad, mode):
+    out = (ctypes.c_longlong * 1)()
+    rc = _hip.lib().tgfr_wr_bwd_ws(int(b_img), int(b_cap), int(bounded), int(t_pad), int(mode),
+                                   ctypes.addressof(out))
+    if rc != 0:
+        raise RuntimeError(f"tgfr_wr_bwd_ws failed with code {rc}")
+    return int(out[0])
 
 
 class WordRegionLogits(torch.autograd.Function):
@@ -130,22 +130,21 @@ class WordRegionLogits(torch.autograd.Function):
         r_hi, r_lo, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo = ctx.saved_tensors
         gamma1, gamma2, gamma3, eps, m, shape, fast, t_pad = ctx.cfg
         b_img, b_cap = stats.shape[0], stats.shape[1]
+        dev = dlogits.device
         dlogits = dlogits.float().contiguous()
-        chunks = bwd_chunks(b_img, b_cap)
-        slab = torch.empty(chunks, b_img, RPAD, D, dtype=torch.float32,
-                           device=dlogits.device)
-        tok = torch.empty(b_img, b_cap, t_pad, 8, dtype=torch.float32, device=dlogits.device)
+        ws = torch.empty(wr_bwd_ws_floats(b_img, b_cap, fast, t_pad, m), dtype=torch.float32,
+                         device=dev)
+        tok = torch.empty(b_img, b_cap, t_pad, 8, dtype=torch.float32, device=dev)
         split = m == MODES["fp32"]
         call("tgfr_wr_bwd_tok", ptr(stats), ptr(w_norm), ptr(lens), b_img, b_cap, gamma1,
              gamma2, gamma3, eps, ptr(dlogits), b_cap, int(fast), t_pad, ptr(tok),
              _hip.stream())
+        d_reg = torch.empty(b_img, NREG, D, dtype=torch.float32, device=dev)
+        assert 2 * b_img <= _hip.N_COUNTERS
         call("tgfr_wr_bwd", ptr(r_hi), ptr(r_lo) if split else None, ptr(w_hi),
-             ptr(w_lo) if split else None, b_img, b_cap, chunks, gamma1, ptr(tok),
-             ptr(c_hi), ptr(c_lo) if split else None, ptr(slab), int(fast), t_pad, m,
-             _hip.stream())
-        d_reg = torch.empty(b_img, NREG, D, dtype=torch.float32, device=dlogits.device)
-        call("tgfr_wr_reduce", ptr(slab), chunks, b_img, ptr(d_reg), NREG * D, D, 1, 0,
-             _hip.stream())
+             ptr(w_lo) if split else None, b_img, b_cap, gamma1, ptr(tok),
+             ptr(c_hi), ptr(c_lo) if split else None, ptr(d_reg), NREG * D, D, 1, ptr(ws),
+             ptr(_hip.counters(dev)), int(fast), t_pad, m, _hip.stream())
         # same logical shape as img_features, channels-last strides
         d_img = d_reg.transpose(1, 2).reshape(shape)
         return (d_img,) + (None,) * 10

@@ -7,12 +7,13 @@ weights and batch.
              text side from the reference's own words_loss_lstm_b5 fixture)
   Fusion     src/fusion_bert.py:205-243           (Working -> ArcMargin(640) -> focal)
 
-Checked: every loss term within 1e-3 absolute, and the parameters after the
-optimiser step.  SGD updates are linear in the gradient: relative 1e-4 of the
-tensor's scale.  Adam's first update is lr * g / (|g| + eps), i.e. +-lr for
-every element whose gradient is not ~0, so it is compared where the
-reference gradient is well away from zero (|g| > 1e-3 max|g|, where fp32
-rounding cannot flip its sign) at 1e-4 relative, and everywhere within 2 lr.
+Checked: every loss term within 1e-3 absolute; every head parameter's
+gradient within 5e-3 of its largest reference gradient; the parameters after
+the optimiser step.  SGD updates are linear in the gradient: relative 1e-4 of
+the tensor's scale.  Adam's first update is lr * g / (|g| + eps), i.e. +-lr
+for every element whose gradient is not ~0 -- a sign decision -- so it is
+compared where the reference gradient exceeds 4x the measured gradient error
+(the sign cannot flip) at 1e-4 relative, and everywhere within 2 lr.
 """
 import numpy as np
 import pytest
@@ -52,13 +53,38 @@ def _cpu_params(module, keys):
     return {v: named[k].detach().cpu().clone().requires_grad_() for k, v in keys.items()}
 
 
-def _check_adam(new, old, ref_new, grad, lr):
+def _check_adam(param, old, ref_new, grad, lr, name="", g_all=0.0, wd=0.0):
+    """Gradient and first Adam update of one parameter against the oracle.
+
+    The gradient (p.grad after the step) must be within 5e-3 of the tensor's
+    largest reference gradient (the IMIM q/k projections reach ~4e-3: their
+    gradient runs through the 196-wide attention softmax backward), plus
+    1e-5 of the largest gradient of the whole head (g_all) -- a floor for
+    tensors whose exact gradient is zero, such as the key-role bias, which
+    the attention softmax cancels.  Adam's
+    first update is lr * g / (|g| + 1e-8), i.e. +-lr: a sign decision, so it
+    is compared (1e-4 of the tensor's scale) where |g_ref| exceeds 4x the
+    measured gradient error and Adam's eps (with the weight decay term
+    added: g + wd p), where the sign cannot flip; and
+    everywhere it must stay within 2 lr."""
+    new = param.detach().cpu()
+    g_mine = param.grad.detach().cpu()
+    g_err = (g_mine - grad).abs().max().item()
+    g_scale = grad.abs().max().item()
+    assert g_err <= 5e-3 * g_scale + 1e-5 * g_all + 1e-12, (
+        f"{name}: gradient error {g_err:.3e} = {g_err / g_scale:.3e} of max {g_scale:.3e}")
     d_mine, d_ref = new - old, ref_new - old
-    assert (d_mine - d_ref).abs().max().item() <= 2 * lr + 1e-7
-    sure = grad.abs() > 1e-3 * grad.abs().max()
+    assert (d_mine - d_ref).abs().max().item() <= 2 * lr + 1e-7, name
+    # the update's sign follows g + wd p (Adam's L2 weight decay)
+    sure = (grad + wd * old).abs() > max(4 * g_err, 1e-6)
     scale = old.abs().max().clamp(min=1e-3)
-    err = ((d_mine - d_ref).abs() * sure).max() / scale
-    assert err.item() < 1e-4, err.item()
+    diff = (d_mine - d_ref).abs() * sure
+    err = diff.max() / scale
+    if err.item() >= 1e-4:
+        i = int(diff.argmax())
+        raise AssertionError(f"{name}: update error {err.item():.3e} of scale at element {i}: "
+                             f"ref grad {grad.flatten()[i].item():.3e} (max {g_scale:.3e}), "
+                             f"d_mine {d_mine.flatten()[i]:.3e}, d_ref {d_ref.flatten()[i]:.3e}")
 
 
 def _check_sgd(new, ref_new):
@@ -114,7 +140,8 @@ def test_train_step_matches_oracle(gpu, b, nw, n_ids):
         assert abs(out[k].item() - v) < tol, (k, out[k].item(), v)
     named = dict(tr.image_head.named_parameters())
     for k, v in HEAD_KEYS.items():
-        _check_adam(named[k].detach().cpu(), old[v], hp[v].detach(), grads[v], args.lr_head)
+        _check_adam(named[k], old[v], hp[v].detach(), grads[v], args.lr_head, k,
+                    max(x.abs().max().item() for x in grads.values()))
     _check_sgd(tr.image_cls.weight.detach().cpu(), arc_i.detach())
     _check_sgd(tr.text_cls.weight.detach().cpu(), arc_t.detach())
     assert not torch.equal(tr.image_cls.weight.detach().cpu(), old_i)
@@ -196,7 +223,8 @@ def test_lstm_step_matches_oracle(gpu):
     assert abs(out["ident"].item() - args.lambda_id * (tid + iid).item()) < 2e-1
     named = dict(tr.image_head.named_parameters())
     for k, v in HEAD_KEYS.items():
-        _check_adam(named[k].detach().cpu(), old[v], hp[v].detach(), grads[v], args.lr_head)
+        _check_adam(named[k], old[v], hp[v].detach(), grads[v], args.lr_head, k,
+                    max(x.abs().max().item() for x in grads.values()))
     _check_sgd(tr.image_cls.weight.detach().cpu(), arc_i.detach())
     _check_sgd(tr.text_cls.weight.detach().cpu(), arc_t.detach())
 
@@ -252,11 +280,12 @@ def test_fusion_step_matches_oracle(gpu):
     torch.cuda.synchronize()
     assert abs(got - loss.item()) < 1e-3, (got, loss.item())
     _check_sgd(tr.metric_fc.weight.detach().cpu(), arc.detach())
+    g_all = max(x.abs().max().item() for x in grads.values())
     named_h = dict(tr.image_head.named_parameters())
     for k, v in HEAD_KEYS.items():
-        _check_adam(named_h[k].detach().cpu(), old[("h", v)], hp[v].detach(), grads[("h", v)],
-                    args.lr_head)
+        _check_adam(named_h[k], old[("h", v)], hp[v].detach(), grads[("h", v)], args.lr_head,
+                    k, g_all, wd=5e-5)
     named_w = dict(tr.fusion_net.named_parameters())
     for k, v in WORKING_KEYS.items():
-        _check_adam(named_w[k].detach().cpu(), old[("w", v)], wp[v].detach(), grads[("w", v)],
-                    args.lr_head)
+        _check_adam(named_w[k], old[("w", v)], wp[v].detach(), grads[("w", v)], args.lr_head,
+                    k, g_all, wd=5e-5)

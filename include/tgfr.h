@@ -207,6 +207,38 @@ int tgfr_ln_fwd(const float* x, int rows, long long E, const float* w, const flo
 int tgfr_ln_bwd(const float* dy, const float* x, int rows, long long E, const float* w, int ch,
                 float* ws, float* dx, float* dw, float* db, void* stream);
 
+/* ---- IMIM tail (models/models.py:399-405 + ProjectionHead :98-120), bf16 ----
+ * Replaces, after IMIM's LayerNorm: conv1x1_1 + ReLU (:399-400), conv1x1_2 +
+ * ReLU (:402), project_local (Linear 256->256, :403/:116) and F.normalize
+ * (:117), over channels-last rows Z [rows][256] (rows = B*196), and their
+ * backward.  One fused launch each way; weight gradients in one launch + a
+ * deterministic slice reduce.
+ *   tail_pack: W1 [128][256], W2 [256][128], Wp [256][256] (fp32, as the
+ *     reference's conv/linear weights) -> pk, tgfr_tail_pack_elems() uint16
+ *     (bf16 weights and their transposes); re-pack after every update.
+ *   tail_fwd: R [rows][256] (ld ldr) = normalize(...); saves for the backward
+ *     Zb [rows][256], H1b [rows][128], H2b [rows][256] (bf16) and
+ *     inv [rows] = 1 / max(|P|, eps).
+ *   tail_bwd: dZ [rows][256] (fp32, ld lddz) from dR; writes dPb [rows][256],
+ *     dH2b [rows][256], dH1b [rows][128] (bf16, the ReLU masks applied).
+ *   tail_dw: dWp = dP^T H2, dW2 = dH2^T H1, dW1 = dH1^T Z ([out][in], fp32,
+ *     overwritten) and dbp/db2/db1 = column sums; ws: tgfr_tail_dw_ws floats. */
+int tgfr_tail_pack_elems(void);
+int tgfr_tail_pack(const float* W1, const float* W2, const float* Wp, uint16_t* pk,
+                   void* stream);
+int tgfr_tail_fwd(const float* Z, long long ldz, int rows, const uint16_t* pk, const float* b1,
+                  const float* b2, const float* bp, float eps, float* R, long long ldr,
+                  uint16_t* Zb, uint16_t* H1b, uint16_t* H2b, float* inv, void* stream);
+int tgfr_tail_bwd(const float* dR, long long lddr, const float* R, long long ldr,
+                  const float* inv, int rows, float eps, const uint16_t* pk, const uint16_t* H1b,
+                  const uint16_t* H2b, float* dZ, long long lddz, uint16_t* dPb, uint16_t* dH2b,
+                  uint16_t* dH1b, void* stream);
+int tgfr_tail_dw_ws(int rows, long long* floats);
+int tgfr_tail_dw(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
+                 const uint16_t* H1b, const uint16_t* dH1b, const uint16_t* Zb, int rows,
+                 float* dWp, float* dbp, float* dW2, float* db2, float* dW1, float* db1, float* ws,
+                 void* stream);
+
 /* Bias gradient of a row-wise linear map: db[c] = sum_r dy[r][c].  With y
  * (the ReLU output) the ReLU mask is applied first and the masked gradient is
  * written to dym (both set or both NULL).  ws: ceil(rows / 128) * cols floats;

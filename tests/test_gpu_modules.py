@@ -170,6 +170,38 @@ def test_image_heading(gpu):
     assert _relerr(net.imim.ln.weight.grad, g["d_imim_ln_weight"]) < 1e-3
 
 
+def test_image_heading_bf16(gpu):
+    """ImageHeading in bf16 mode (fused attention core operands in bf16, the
+    fused IMIM tail) against the reference's fp32 outputs on the golden:
+    relative Frobenius error <= 1e-2 on R and 1.2e-1 on the gradients (bf16
+    operands; a ReLU mask flips where a pre-activation is within rounding of
+    0, tests/test_gpu_tail.py)."""
+    from text_guided_face_recognition_amd.models.models import ImageHeading
+    g = load_golden("image_heading_b2")
+    net = _load(ImageHeading(_args(precision="bf16")), g).to(gpu).train()
+    assert net.imim.precision == "bf16"
+    gi = t(g["global_image"]).to(gpu).requires_grad_()
+    li = t(g["local_image"]).to(gpu).requires_grad_()
+    gp, r = net(gi, li)
+
+    def frob(a, ref):
+        ref = torch.as_tensor(ref).to(a.device)
+        return float((a.detach() - ref).norm() / ref.norm())
+
+    assert frob(r, g["r_out"]) < 1e-2
+    assert r.stride() == (196 * 256, 1, 14 * 256, 256)
+    ((gp * t(g["probe_g"]).to(gpu)).sum() + (r * t(g["probe_r"]).to(gpu)).sum()).backward()
+    errs = {"d_local": frob(li.grad, g["d_local"]),
+            "d_v_w": frob(net.imim.sa.value_proj.weight.grad, g["d_imim_sa_value_proj_weight"]),
+            "d_ln_w": frob(net.imim.ln.weight.grad, g["d_imim_ln_weight"]),
+            "d_proj_w": frob(net.imim.project_local.projection.weight.grad,
+                             g["d_imim_project_local_projection_weight"])}
+    # the projection sits above the ReLUs; the rest see the flipped masks of
+    # a 2-sample batch undamped
+    assert errs["d_proj_w"] < 1e-2, errs
+    assert max(errs.values()) < 1.2e-1, errs
+
+
 def test_words_loss_module(gpu):
     """models.losses.words_loss end to end (fused kernel + CE kernel)."""
     from text_guided_face_recognition_amd.models import losses as L

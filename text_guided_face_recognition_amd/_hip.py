@@ -58,6 +58,12 @@ SIGNATURES = {
     "tgfr_bias_grad": [P, L, I, I, P, L, P, L, P, P, P, P],
     "tgfr_ln_fwd": [P, I, L, P, P, F, I, P, P, P],
     "tgfr_ln_bwd": [P, P, I, L, P, I, P, P, P, P, P],
+    "tgfr_tail_pack_elems": [],
+    "tgfr_tail_pack": [P, P, P, P, P],
+    "tgfr_tail_fwd": [P, L, I, P, P, P, P, F, P, L, P, P, P, P, P],
+    "tgfr_tail_bwd": [P, L, P, L, P, I, F, P, P, P, P, L, P, P, P, P],
+    "tgfr_tail_dw_ws": [I, P],
+    "tgfr_tail_dw": [P, P, P, P, P, P, I, P, P, P, P, P, P, P, P],
     "tgfr_optim_step": [P, I, P, I, P, P, P],
     "tgfr_arc_fwd": [P, L, I, I, P, L, I, P, F, F, I, F, P, P, P, P, P, P],
     "tgfr_arc_bwd": [P, P, P, P, P, L, P, I, I, I, F, F, I, F, P, L, P, P, P],

@@ -1,0 +1,737 @@
+// IMIM tail (models/models.py:399-405 + ProjectionHead :98-120) fused for
+// gfx950, bf16 operands with fp32 accumulation:
+//
+//   H1 = relu(Z W1^T + b1)      conv1x1_1, 256 -> 128   (:399-400)
+//   H2 = relu(H1 W2^T + b2)     conv1x1_2, 128 -> 256   (:402)
+//   P  = H2 Wp^T + bp           project_local.projection (:403, :116)
+//   R  = P / max(|P|, eps)      F.normalize               (:117)
+//
+// over the channels-last rows of the LayerNorm output Z [rows = B*196][256].
+// One workgroup owns 64 rows and runs the whole chain: the intermediate
+// activations never leave LDS, only the bf16 copies the backward needs (Z, H1,
+// H2) and R go to HBM.  Layers 1 and 2 are computed transposed
+// (Out^T = W In^T): the MFMA accumulator of a lane then holds 4 consecutive
+// output features of ONE row per register quad, which is one ds_write_b64
+// into the next layer's [row][feature] operand image (no 2-byte scatter).
+// The last layer is computed upright so that its fp32 result is stored as
+// 128-B row segments and its row norms reduce across lanes (rs16).
+//
+// Backward (one workgroup per 64 rows again):
+//   dP  = (dR - R (R.dR)) / max(|P|, eps)        (clamped rows: dR / eps)
+//   dH2 = (dP Wp) * [H2 > 0],  dH1 = (dH2 W2) * [H1 > 0],  dZ = dH1 W1
+// writing dZ in fp32 (the LayerNorm backward's input) and dP, dH2, dH1 in
+// bf16 for the weight gradients, which tail_dw computes as
+//   dWp = dP^T H2, dW2 = dH2^T H1, dW1 = dH1^T Z  (+ the bias column sums)
+// in one launch: row slices per workgroup, operands transposed at LDS read
+// time by ds_read_b64_tr_b16, slice partials summed in slice order by
+// tail_dw_reduce (deterministic).
+#include "tgfr_common.h"
+
+#include <algorithm>
+
+using namespace tgfr;
+
+namespace {
+
+constexpr int TC = 256;   // IMIM channels (LayerNorm / conv1x1_1 input, conv1x1_2 output)
+constexpr int TH = 128;   // conv1x1_1 output
+constexpr int TD = 256;   // projection dim (aux_feat_dim_per_granularity)
+constexpr int TM = 64;    // rows per workgroup
+
+// packed bf16 weights (uint16 element offsets)
+constexpr int OFF_W1 = 0;                     // W1  [TH][TC]
+constexpr int OFF_W2 = OFF_W1 + TH * TC;      // W2  [TC][TH]
+constexpr int OFF_WP = OFF_W2 + TC * TH;      // Wp  [TD][TC]
+constexpr int OFF_W1T = OFF_WP + TD * TC;     // W1^T [TC][TH]
+constexpr int OFF_W2T = OFF_W1T + TC * TH;    // W2^T [TH][TC]
+constexpr int OFF_WPT = OFF_W2T + TH * TC;    // Wp^T [TC][TD]
+constexpr int PACK_ELEMS = OFF_WPT + TC * TD;
+
+// [TM rows][K] bf16 operand image, 16-B chunks XOR-swizzled by row: the 32
+// rows of a fragment read land on 32 distinct chunks (conflict-free
+// ds_read_b128 lane groups).
+template <int K>
+__device__ __forceinline__ uint32_t img(int m, int c) {
+  return (uint32_t)(m * K * 2 + ((c ^ (m & (K / 8 - 1))) << 4));
+}
+// byte offset of feature n (multiple of 4) of row m
+template <int K>
+__device__ __forceinline__ uint32_t img_at(int m, int n) {
+  return img<K>(m, n >> 3) + (n & 7) * 2;
+}
+
+__device__ __forceinline__ bf16x8 gld16(const uint16_t* p) {
+  return as_bf8(*(const uint4*)p);
+}
+
+__device__ __forceinline__ uint2 pk4(float a, float b, float c, float d) {
+  return make_uint2(pk_bf16(a, b), pk_bf16(c, d));
+}
+
+// image -> HBM rows [row0 + m][K] (ld elements), rows < n_rows only
+template <int K>
+__device__ __forceinline__ void copy_out(uint32_t base, uint16_t* dst, long long ld, int row0,
+                                         int n_rows, int tid) {
+  constexpr int CH = K / 8;
+#pragma unroll
+  for (int i = tid; i < TM * CH; i += 256) {
+    const int m = i / CH, c = i % CH;
+    if (row0 + m < n_rows)
+      *(uint4*)(dst + (long long)(row0 + m) * ld + 8 * c) = lds_ld16(base + img<K>(m, c));
+  }
+}
+
+// --------------------------------------------------------------- pack ---
+__global__ __launch_bounds__(256) void tail_pack_kernel(const float* __restrict__ W1,
+                                                        const float* __restrict__ W2,
+                                                        const float* __restrict__ Wp,
+                                                        uint16_t* __restrict__ pk) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e < TH * TC) {
+    const int r = e / TC, c = e % TC;
+    const uint16_t v = bf_bits(W1[e]);
+    pk[OFF_W1 + e] = v;
+    pk[OFF_W1T + c * TH + r] = v;
+  } else if (e < TH * TC + TC * TH) {
+    const int f = e - TH * TC, r = f / TH, c = f % TH;
+    const uint16_t v = bf_bits(W2[f]);
+    pk[OFF_W2 + f] = v;
+    pk[OFF_W2T + c * TC + r] = v;
+  } else if (e < PACK_ELEMS / 2) {
+    const int f = e - 2 * TH * TC, r = f / TC, c = f % TC;
+    const uint16_t v = bf_bits(Wp[f]);
+    pk[OFF_WP + f] = v;
+    pk[OFF_WPT + c * TD + r] = v;
+  }
+}
+
+// ------------------------------------------------------------ forward ---
+// LDS: [0, 32K) Z image (later the H2 image), [32K, 48K) H1 image,
+//      [48K, 49K) row sum-of-squares partials [4 waves][64], [49K, 49.25K) 1/norm
+constexpr int F_Z = 0, F_H2 = 0, F_H1 = 32768, F_SS = 49152, F_INV = F_SS + 4 * TM * 4;
+constexpr int F_LDS = F_INV + TM * 4;
+
+__global__ __launch_bounds__(256) void tail_fwd_kernel(
+    const float* __restrict__ Z, long long ldz, int rows, const uint16_t* __restrict__ pk,
+    const float* __restrict__ b1, const float* __restrict__ b2, const float* __restrict__ bp,
+    float eps, float* __restrict__ R, long long ldr, uint16_t* __restrict__ Zb,
+    uint16_t* __restrict__ H1b, uint16_t* __restrict__ H2b, float* __restrict__ inv_out) {
+  const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE;
+  const int lr = lane & 31, h = lane >> 5;
+  const int row0 = blockIdx.x * TM;
+
+  // Z rows -> bf16 image (and the bf16 copy for dW1); rows past the end are 0
+#pragma unroll
+  for (int i = tid; i < TM * (TC / 8); i += 256) {
+    const int m = i / (TC / 8), c = i % (TC / 8);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row0 + m < rows) {
+      const float* src = Z + (long long)(row0 + m) * ldz + 8 * c;
+      const float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
+      v = make_uint4(pk_bf16(a.x, a.y), pk_bf16(a.z, a.w), pk_bf16(b.x, b.y), pk_bf16(b.z, b.w));
+      *(uint4*)(Zb + (long long)(row0 + m) * TC + 8 * c) = v;
+    }
+    lds_st16(F_Z + img<TC>(m, c), v);
+  }
+  __syncthreads();
+
+  // layer 1, transposed: H1^T[i][m] = sum_c W1[i][c] Z[m][c]; wave w: i in [32w, 32w+32)
+  {
+    f32x16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+    const uint16_t* wa = pk + OFF_W1 + (32 * w + lr) * TC + 8 * h;
+#pragma unroll 4
+    for (int s = 0; s < TC / 16; ++s) {
+      const bf16x8 a = gld16(wa + 16 * s);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const bf16x8 b = as_bf8(lds_ld16(F_Z + img<TC>(32 * mt + lr, 2 * s + h)));
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[mt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int i0 = 32 * w + 8 * g + 4 * h;
+      const float4 bb = *(const float4*)(b1 + i0);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const f32x16& a = acc[mt];
+        lds_st8(F_H1 + img_at<TH>(32 * mt + lr, i0),
+                pk4(fmaxf(a[4 * g] + bb.x, 0.f), fmaxf(a[4 * g + 1] + bb.y, 0.f),
+                    fmaxf(a[4 * g + 2] + bb.z, 0.f), fmaxf(a[4 * g + 3] + bb.w, 0.f)));
+      }
+    }
+  }
+  __syncthreads();
+  copy_out<TH>(F_H1, H1b, TH, row0, rows, tid);
+
+  // layer 2, transposed: H2^T[j][m] = sum_i W2[j][i] H1[m][i]; wave w: j in [64w, 64w+64)
+  {
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
+    const uint16_t* wa = pk + OFF_W2 + (64 * w + lr) * TH + 8 * h;
+#pragma unroll 2
+    for (int s = 0; s < TH / 16; ++s) {
+      bf16x8 a[2], b[2];
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) a[jt] = gld16(wa + 32 * jt * TH + 16 * s);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        b[mt] = as_bf8(lds_ld16(F_H1 + img<TH>(32 * mt + lr, 2 * s + h)));
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          acc[jt][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[jt], b[mt], acc[jt][mt], 0, 0, 0);
+    }
+    // the Z image is dead (every wave passed the barrier after layer 1): H2 reuses it
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int j0 = 64 * w + 32 * jt + 8 * g + 4 * h;
+        const float4 bb = *(const float4*)(b2 + j0);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const f32x16& a = acc[jt][mt];
+          lds_st8(F_H2 + img_at<TC>(32 * mt + lr, j0),
+                  pk4(fmaxf(a[4 * g] + bb.x, 0.f), fmaxf(a[4 * g + 1] + bb.y, 0.f),
+                      fmaxf(a[4 * g + 2] + bb.z, 0.f), fmaxf(a[4 * g + 3] + bb.w, 0.f)));
+        }
+      }
+  }
+  __syncthreads();
+  copy_out<TC>(F_H2, H2b, TC, row0, rows, tid);
+
+  // layer 3, upright: P[m][n] = sum_j H2[m][j] Wp[n][j] + bp[n]; wave w: n in [64w, 64w+64)
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
+  {
+    const uint16_t* wb = pk + OFF_WP + (64 * w + lr) * TC + 8 * h;
+#pragma unroll 4
+    for (int s = 0; s < TC / 16; ++s) {
+      bf16x8 a[2], b[2];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) b[nt] = gld16(wb + 32 * nt * TC + 16 * s);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        a[mt] = as_bf8(lds_ld16(F_H2 + img<TC>(32 * mt + lr, 2 * s + h)));
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+    }
+  }
+  // bias, then the row sums of squares: lane-local over this wave's two
+  // column tiles, then over the 32 columns of each half-wave (rs16)
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const float bb = bp[64 * w + 32 * nt + lr];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[mt][nt][q] += bb;
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    float sq[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      sq[q] = acc[mt][0][q] * acc[mt][0][q] + acc[mt][1][q] * acc[mt][1][q];
+    const float tot = rs16(sq, lr);
+    if (!(lr & 1))
+      lds_stf(F_SS + (w * TM + 32 * mt + acc_row(rs16_index(lr), h)) * 4, tot);
+  }
+  __syncthreads();
+  if (tid < TM) {
+    const float ss = lds_ldf(F_SS + tid * 4) + lds_ldf(F_SS + (TM + tid) * 4) +
+                     lds_ldf(F_SS + (2 * TM + tid) * 4) + lds_ldf(F_SS + (3 * TM + tid) * 4);
+    const float iv = 1.f / fmaxf(sqrtf(ss), eps);
+    lds_stf(F_INV + tid * 4, iv);
+    if (row0 + tid < rows) inv_out[row0 + tid] = iv;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int m = 32 * mt + acc_row(q, h);
+      if (row0 + m < rows) {
+        const float iv = lds_ldf(F_INV + m * 4);
+        float* o = R + (long long)(row0 + m) * ldr + 64 * w + lr;
+        o[0] = acc[mt][0][q] * iv;
+        o[32] = acc[mt][1][q] * iv;
+      }
+    }
+}
+
+// ----------------------------------------------------------- backward ---
+// LDS: [0, 32K) dP image (later the dH1 image), [32K, 64K) dH2 image
+constexpr int B_DP = 0, B_DH1 = 0, B_DH2 = 32768, B_LDS = 65536;
+
+__global__ __launch_bounds__(256) void tail_bwd_kernel(
+    const float* __restrict__ dR, long long lddr, const float* __restrict__ R, long long ldr,
+    const float* __restrict__ inv, int rows, float eps, const uint16_t* __restrict__ pk,
+    const uint16_t* __restrict__ H1b, const uint16_t* __restrict__ H2b, float* __restrict__ dZ,
+    long long lddz, uint16_t* __restrict__ dPb, uint16_t* __restrict__ dH2b,
+    uint16_t* __restrict__ dH1b) {
+  const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE;
+  const int lr = lane & 31, h = lane >> 5;
+  const int row0 = blockIdx.x * TM;
+
+  // F.normalize backward, one row per wave pass (lane: 4 columns)
+#pragma unroll 2
+  for (int r = 0; r < TM / 4; ++r) {
+    const int m = 16 * w + r, row = row0 + m;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f), y = g;
+    float iv = 0.f;
+    if (row < rows) {
+      g = *(const float4*)(dR + (long long)row * lddr + 4 * lane);
+      y = *(const float4*)(R + (long long)row * ldr + 4 * lane);
+      iv = inv[row];
+    }
+    float dot = wave_sum(g.x * y.x + g.y * y.y + g.z * y.z + g.w * y.w);
+    if (iv >= 1.f / eps) dot = 0.f;          // clamped row: y = x / eps
+    const uint2 v = pk4((g.x - y.x * dot) * iv, (g.y - y.y * dot) * iv,
+                        (g.z - y.z * dot) * iv, (g.w - y.w * dot) * iv);
+    lds_st8(B_DP + img_at<TD>(m, 4 * lane), v);
+    if (row < rows) *(uint2*)(dPb + (long long)row * TD + 4 * lane) = v;
+  }
+  __syncthreads();
+
+  // dH2^T[j][m] = sum_n Wp[n][j] dP[m][n] (A = Wp^T rows); wave w: j in [64w, 64w+64)
+  {
+    // relu masks first: H2[m][j0..j0+3] for this lane's accumulator quads
+    uint2 msk[2][2][4];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = row0 + 32 * mt + lr, j0 = 64 * w + 32 * jt + 8 * g + 4 * h;
+          msk[jt][mt][g] = row < rows ? *(const uint2*)(H2b + (long long)row * TC + j0)
+                                      : make_uint2(0, 0);
+        }
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
+    const uint16_t* wa = pk + OFF_WPT + (64 * w + lr) * TD + 8 * h;
+#pragma unroll 4
+    for (int s = 0; s < TD / 16; ++s) {
+      bf16x8 a[2], b[2];
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) a[jt] = gld16(wa + 32 * jt * TD + 16 * s);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        b[mt] = as_bf8(lds_ld16(B_DP + img<TD>(32 * mt + lr, 2 * s + h)));
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          acc[jt][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[jt], b[mt], acc[jt][mt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int j0 = 64 * w + 32 * jt + 8 * g + 4 * h;
+          const uint2 mk = msk[jt][mt][g];
+          const f32x16& a = acc[jt][mt];
+          // bf16 bits > 0 as a signed 16-bit value <=> the activation is positive
+          const float v0 = (short)(mk.x & 0xffff) > 0 ? a[4 * g] : 0.f;
+          const float v1 = (short)(mk.x >> 16) > 0 ? a[4 * g + 1] : 0.f;
+          const float v2 = (short)(mk.y & 0xffff) > 0 ? a[4 * g + 2] : 0.f;
+          const float v3 = (short)(mk.y >> 16) > 0 ? a[4 * g + 3] : 0.f;
+          lds_st8(B_DH2 + img_at<TC>(32 * mt + lr, j0), pk4(v0, v1, v2, v3));
+        }
+  }
+  __syncthreads();
+  copy_out<TC>(B_DH2, dH2b, TC, row0, rows, tid);
+
+  // dH1^T[i][m] = sum_j W2[j][i] dH2[m][j] (A = W2^T rows); wave w: i in [32w, 32w+32)
+  {
+    uint2 msk[2][4];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int row = row0 + 32 * mt + lr, i0 = 32 * w + 8 * g + 4 * h;
+        msk[mt][g] = row < rows ? *(const uint2*)(H1b + (long long)row * TH + i0)
+                                : make_uint2(0, 0);
+      }
+    f32x16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+    const uint16_t* wa = pk + OFF_W2T + (32 * w + lr) * TC + 8 * h;
+#pragma unroll 4
+    for (int s = 0; s < TC / 16; ++s) {
+      const bf16x8 a = gld16(wa + 16 * s);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const bf16x8 b = as_bf8(lds_ld16(B_DH2 + img<TC>(32 * mt + lr, 2 * s + h)));
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[mt], 0, 0, 0);
+      }
+    }
+    // the dP image is dead (every wave passed the barrier before this GEMM)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i0 = 32 * w + 8 * g + 4 * h;
+        const uint2 mk = msk[mt][g];
+        const f32x16& a = acc[mt];
+        const float v0 = (short)(mk.x & 0xffff) > 0 ? a[4 * g] : 0.f;
+        const float v1 = (short)(mk.x >> 16) > 0 ? a[4 * g + 1] : 0.f;
+        const float v2 = (short)(mk.y & 0xffff) > 0 ? a[4 * g + 2] : 0.f;
+        const float v3 = (short)(mk.y >> 16) > 0 ? a[4 * g + 3] : 0.f;
+        lds_st8(B_DH1 + img_at<TH>(32 * mt + lr, i0), pk4(v0, v1, v2, v3));
+      }
+  }
+  __syncthreads();
+  copy_out<TH>(B_DH1, dH1b, TH, row0, rows, tid);
+
+  // dZ[m][c] = sum_i dH1[m][i] W1[i][c] (B = W1^T rows); wave w: c in [64w, 64w+64)
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
+  const uint16_t* wb = pk + OFF_W1T + (64 * w + lr) * TH + 8 * h;
+#pragma unroll 2
+  for (int s = 0; s < TH / 16; ++s) {
+    bf16x8 a[2], b[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) b[ct] = gld16(wb + 32 * ct * TH + 16 * s);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+      a[mt] = as_bf8(lds_ld16(B_DH1 + img<TH>(32 * mt + lr, 2 * s + h)));
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+        acc[mt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mt], b[ct], acc[mt][ct], 0, 0, 0);
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int row = row0 + 32 * mt + acc_row(q, h);
+      if (row < rows) {
+        float* o = dZ + (long long)row * lddz + 64 * w + lr;
+        o[0] = acc[mt][0][q];
+        o[32] = acc[mt][1][q];
+      }
+    }
+}
+
+// ------------------------------------------------- weight gradients ---
+// dW[n][k] = sum_rows X[row][n] Y[row][k] and db[n] = sum_rows X[row][n] for
+// the three products of the tail; X, Y bf16 rows.  Workgroup = (product,
+// 128 x 128 output block, row slice); 4 waves of 64 x 64 (2 x 2 tiles).  Row
+// chunks of 32 are staged in LDS as rows with a 64-B pad per row (row pitch
+// = 64 mod 256 B: the 4 rows x 64 B of one ds_read_b64_tr_b16 lane half hit
+// distinct banks); the MFMA operands (X^T and Y with rows as the reduction
+// axis) come out of the transposing read.
+constexpr int DW_NB = 128, DW_CH = 32;
+constexpr int DW_PITCH = DW_NB * 2 + 64;               // bytes per staged row
+constexpr int DW_IMG = DW_CH * DW_PITCH;               // one operand chunk
+constexpr int DW_LDS = 4 * DW_IMG;                     // X, Y, double-buffered
+
+struct DwProb {
+  const uint16_t* X;
+  const uint16_t* Y;
+  int N, K;          // X row width (= ld), Y row width (= ld)
+  int nb_n, nb_k;    // 128-blocks
+  int first;         // first workgroup of this product
+  long long slab;    // float offset of this product's slabs in the workspace
+};
+struct DwArgs {
+  DwProb p[3];
+  int rows, slices, rows_per;
+};
+
+// operand fragment from a staged chunk: lane (col c = col0 + lane%32, rows
+// 16 s + 8 h .. +7), as the bf16x8 of a 32x32x16 MFMA operand
+__device__ __forceinline__ bf16x8 tr_frag(uint32_t base, int col0, int s, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
+  const int col = col0 + 16 * (g & 1) + 4 * p;
+  const int r = 16 * s + 8 * (g >> 1) + q;
+  const uint32_t a = base + r * DW_PITCH + col * 2;
+  return join_tr(lds_tr4(a), lds_tr4(a + 4 * DW_PITCH));
+}
+
+__global__ __launch_bounds__(256) void tail_dw_kernel(DwArgs A, float* __restrict__ ws) {
+  const int tid = threadIdx.x, wv = tid / WAVE, lane = tid % WAVE;
+  const int total = gridDim.x;
+  // consecutive ids after the remap: the blocks of one (product, slice) on one XCD
+  const int wgi = xcd_remap(blockIdx.x, total);
+  int pi = 0;
+  if (wgi >= A.p[1].first) pi = 1;
+  if (wgi >= A.p[2].first) pi = 2;
+  const DwProb P = A.p[pi];
+  const int local = wgi - P.first;
+  const int nblk = P.nb_n * P.nb_k;
+  const int slice = local / nblk, blk = local % nblk;
+  const int bn = blk / P.nb_k, bk = blk % P.nb_k;
+  const int r_begin = slice * A.rows_per, r_end = min(A.rows, r_begin + A.rows_per);
+  const int n_chunks = max(0, (r_end - r_begin + DW_CH - 1) / DW_CH);
+  const int wn = wv >> 1, wk = wv & 1;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
+  float cs[2] = {0.f, 0.f};
+
+  // staging: thread t loads 16 B of X and 16 B of Y per pass; 2 passes per chunk
+  auto load = [&](int c, uint4 (&vx)[2], uint4 (&vy)[2]) {
+#pragma unroll
+    for (int ps = 0; ps < 2; ++ps) {
+      const int i = tid + 256 * ps, r = i / 16, c16 = i % 16;
+      const int row = r_begin + c * DW_CH + r;
+      vx[ps] = vy[ps] = make_uint4(0, 0, 0, 0);
+      if (row < r_end) {
+        vx[ps] = *(const uint4*)(P.X + (long long)row * P.N + bn * DW_NB + 8 * c16);
+        vy[ps] = *(const uint4*)(P.Y + (long long)row * P.K + bk * DW_NB + 8 * c16);
+      }
+    }
+  };
+  auto store = [&](int buf, const uint4 (&vx)[2], const uint4 (&vy)[2]) {
+#pragma unroll
+    for (int ps = 0; ps < 2; ++ps) {
+      const int i = tid + 256 * ps, r = i / 16, c16 = i % 16;
+      lds_st16(buf * 2 * DW_IMG + r * DW_PITCH + 16 * c16, vx[ps]);
+      lds_st16(buf * 2 * DW_IMG + DW_IMG + r * DW_PITCH + 16 * c16, vy[ps]);
+    }
+  };
+  uint4 vx[2], vy[2];
+  if (n_chunks > 0) {
+    load(0, vx, vy);
+    store(0, vx, vy);
+  }
+  __syncthreads();
+  for (int c = 0; c < n_chunks; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < n_chunks) load(c + 1, vx, vy);
+    const uint32_t bx = buf * 2 * DW_IMG, by = bx + DW_IMG;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 a[2], b[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) a[t] = tr_frag(bx, 64 * wn + 32 * t, s, lane);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) b[u] = tr_frag(by, 64 * wk + 32 * u, s, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], b[u], acc[t][u], 0, 0, 0);
+      if (wk == 0 && bk == 0) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) cs[t] += (float)a[t][j];
+      }
+    }
+    if (c + 1 < n_chunks) store(buf ^ 1, vx, vy);
+    __syncthreads();
+  }
+
+  // slab [slice][N][K] (+ [slice][N] column sums after all products' dW slabs)
+  float* slab = ws + P.slab + (long long)slice * P.N * P.K;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int n = bn * DW_NB + 64 * wn + 32 * t + acc_row(q, lane >> 5);
+        const int k = bk * DW_NB + 64 * wk + 32 * u + (lane & 31);
+        slab[(long long)n * P.K + k] = acc[t][u][q];
+      }
+  if (wk == 0 && bk == 0) {
+    float* cslab = ws + P.slab + (long long)A.slices * P.N * P.K + (long long)slice * P.N;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const float v = xhalf_sum(cs[t]);
+      if (lane < 32) cslab[bn * DW_NB + 64 * wn + 32 * t + lane] = v;
+    }
+  }
+}
+
+struct DwOut {
+  float* dW[3];
+  float* db[3];
+};
+
+// out = sum over slices, in slice order; thread = 4 consecutive outputs
+__global__ __launch_bounds__(256) void tail_dw_reduce_kernel(DwArgs A, DwOut O,
+                                                             const float* __restrict__ ws,
+                                                             long long e_total) {
+  const long long e4 = (blockIdx.x * 256LL + threadIdx.x) * 4;
+  if (e4 >= e_total) return;
+  // which product / region: products laid out as [dW N*K][db N] each
+  long long off = e4;
+  int pi = 0;
+  for (; pi < 3; ++pi) {
+    const long long sz = (long long)A.p[pi].N * A.p[pi].K + A.p[pi].N;
+    if (off < sz) break;
+    off -= sz;
+  }
+  const DwProb P = A.p[pi];
+  const long long nk = (long long)P.N * P.K;
+  const float* src;
+  long long stride;
+  float* dst;
+  if (off < nk) {
+    src = ws + P.slab + off;
+    stride = nk;
+    dst = O.dW[pi] + off;
+  } else {
+    src = ws + P.slab + A.slices * nk + (off - nk);
+    stride = P.N;
+    dst = O.db[pi] + (off - nk);
+  }
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int z = 0; z < A.slices; ++z) {
+    const float4 v = *(const float4*)(src + z * stride);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  *(float4*)dst = s;
+}
+
+void dw_plan(int rows, DwArgs& A, long long& ws_floats, int& n_wg) {
+  const int NS[3] = {TD, TC, TH}, KS[3] = {TC, TH, TC};   // dWp, dW2, dW1
+  int blocks = 0;
+  for (int i = 0; i < 3; ++i) blocks += (NS[i] / DW_NB) * (KS[i] / DW_NB);
+  // slices: enough workgroups to cover the chip, but the slabs (slices x
+  // 0.53 MB, written here and read back by the reduce) stay well under the
+  // 32 MB of operands at the step's 12544 rows; at least 4 chunks per slice
+  const int want = std::max(1, 128 / blocks);
+  const int max_slices = std::max(1, rows / (4 * DW_CH));
+  A.slices = std::min(want, max_slices);
+  A.rows_per = ((rows + A.slices - 1) / A.slices + DW_CH - 1) / DW_CH * DW_CH;
+  A.rows = rows;
+  long long slab = 0;
+  int first = 0;
+  for (int i = 0; i < 3; ++i) {
+    DwProb& p = A.p[i];
+    p.N = NS[i];
+    p.K = KS[i];
+    p.nb_n = NS[i] / DW_NB;
+    p.nb_k = KS[i] / DW_NB;
+    p.first = first;
+    p.slab = slab;
+    first += p.nb_n * p.nb_k * A.slices;
+    slab += (long long)A.slices * (p.N * (long long)p.K + p.N);
+  }
+  ws_floats = slab;
+  n_wg = first;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tgfr_tail_pack_elems(void) { return PACK_ELEMS; }
+
+int tgfr_tail_pack(const float* W1, const float* W2, const float* Wp, uint16_t* pk,
+                   void* stream) {
+  if (!W1 || !W2 || !Wp || !pk) return 1001;
+  hipLaunchKernelGGL(tail_pack_kernel, dim3((PACK_ELEMS / 2 + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, W1, W2, Wp, pk);
+  return (int)hipGetLastError();
+}
+
+int tgfr_tail_fwd(const float* Z, long long ldz, int rows, const uint16_t* pk, const float* b1,
+                  const float* b2, const float* bp, float eps, float* R, long long ldr,
+                  uint16_t* Zb, uint16_t* H1b, uint16_t* H2b, float* inv, void* stream) {
+  if (rows <= 0 || ldz < TC || ldr < TD || (ldz & 3) || (ldr & 3)) return 1001;
+  if (((uintptr_t)Z & 15) || !pk || !b1 || !b2 || !bp || !R || !Zb || !H1b || !H2b || !inv)
+    return 1001;
+  hipLaunchKernelGGL(tail_fwd_kernel, dim3((rows + TM - 1) / TM), dim3(256), F_LDS,
+                     (hipStream_t)stream, Z, ldz, rows, pk, b1, b2, bp, eps, R, ldr, Zb, H1b, H2b,
+                     inv);
+  return (int)hipGetLastError();
+}
+
+int tgfr_tail_bwd(const float* dR, long long lddr, const float* R, long long ldr,
+                  const float* inv, int rows, float eps, const uint16_t* pk, const uint16_t* H1b,
+                  const uint16_t* H2b, float* dZ, long long lddz, uint16_t* dPb, uint16_t* dH2b,
+                  uint16_t* dH1b, void* stream) {
+  if (rows <= 0 || lddr < TD || ldr < TD || lddz < TC || (lddr & 3) || (ldr & 3)) return 1001;
+  if (((uintptr_t)dR & 15) || ((uintptr_t)R & 15) || !inv || !pk || !H1b || !H2b || !dZ ||
+      !dPb || !dH2b || !dH1b)
+    return 1001;
+  hipLaunchKernelGGL(tail_bwd_kernel, dim3((rows + TM - 1) / TM), dim3(256), B_LDS,
+                     (hipStream_t)stream, dR, lddr, R, ldr, inv, rows, eps, pk, H1b, H2b, dZ,
+                     lddz, dPb, dH2b, dH1b);
+  return (int)hipGetLastError();
+}
+
+int tgfr_tail_dw_ws(int rows, long long* floats) {
+  if (rows <= 0 || !floats) return 1001;
+  DwArgs A;
+  int n_wg;
+  dw_plan(rows, A, *floats, n_wg);
+  return 0;
+}
+
+// dWp = dP^T H2, dW2 = dH2^T H1, dW1 = dH1^T Z and the bias sums; outputs
+// overwritten, row-major [out][in] like the reference weights.
+int tgfr_tail_dw(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
+                 const uint16_t* H1b, const uint16_t* dH1b, const uint16_t* Zb, int rows,
+                 float* dWp, float* dbp, float* dW2, float* db2, float* dW1, float* db1, float* ws,
+                 void* stream) {
+  if (rows <= 0 || !dPb || !H2b || !dH2b || !H1b || !dH1b || !Zb || !dWp || !dbp || !dW2 ||
+      !db2 || !dW1 || !db1 || !ws)
+    return 1001;
+  DwArgs A;
+  long long wsf;
+  int n_wg;
+  dw_plan(rows, A, wsf, n_wg);
+  A.p[0].X = dPb;  A.p[0].Y = H2b;
+  A.p[1].X = dH2b; A.p[1].Y = H1b;
+  A.p[2].X = dH1b; A.p[2].Y = Zb;
+  if (const int e = set_max_lds((const void*)tail_dw_kernel, DW_LDS)) return e;
+  hipLaunchKernelGGL(tail_dw_kernel, dim3(n_wg), dim3(256), DW_LDS, (hipStream_t)stream, A, ws);
+  DwOut O;
+  O.dW[0] = dWp; O.db[0] = dbp;
+  O.dW[1] = dW2; O.db[1] = db2;
+  O.dW[2] = dW1; O.db[2] = db1;
+  long long e_total = 0;
+  for (int i = 0; i < 3; ++i) e_total += (long long)A.p[i].N * A.p[i].K + A.p[i].N;
+  hipLaunchKernelGGL(tail_dw_reduce_kernel, dim3((unsigned)((e_total / 4 + 255) / 256)),
+                     dim3(256), 0, (hipStream_t)stream, A, O, ws, e_total);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -636,6 +636,80 @@ def layer_norm_rows(x, weight, bias, eps=1e-5, ch=0):
     return LayerNormRows.apply(x, weight, bias, eps, ch)
 
 
+# ------------------------------------------------------------- IMIM tail ---
+_TAIL_C, _TAIL_H, _TAIL_D = 256, 128, 256
+
+
+def tail_dw_ws_floats(rows):
+    out = (ctypes.c_longlong * 1)()
+    rc = _hip.lib().tgfr_tail_dw_ws(int(rows), ctypes.addressof(out))
+    if rc != 0:
+        raise RuntimeError(f"tgfr_tail_dw_ws failed with code {rc}")
+    return int(out[0])
+
+
+class ImimTail(torch.autograd.Function):
+    """IMIM after its LayerNorm (models/models.py:399-405 with ProjectionHead
+    :98-120): relu(conv1x1_1) -> relu(conv1x1_2) -> project_local -> L2 norm,
+    over channels-last rows, as ONE fused bf16 kernel each way (tgfr_tail.hip)
+    plus one weight-gradient launch.  Activations saved for the backward are
+    bf16 (Z, H1, H2), the operands the bf16 GEMMs consume anyway."""
+
+    @staticmethod
+    def forward(ctx, z, w1, b1, w2, b2, wp, bp, eps):
+        shape = z.shape
+        assert shape[-1] == _TAIL_C and tuple(w1.shape[:2]) == (_TAIL_H, _TAIL_C)
+        assert tuple(w2.shape[:2]) == (_TAIL_C, _TAIL_H) and tuple(wp.shape) == (_TAIL_D, _TAIL_C)
+        z2 = _aligned(z.reshape(-1, _TAIL_C))
+        rows, dev = z2.shape[0], z2.device
+        pk = torch.empty(_hip.lib().tgfr_tail_pack_elems(), dtype=torch.int16, device=dev)
+        call("tgfr_tail_pack", ptr(_aligned(w1.reshape(_TAIL_H, _TAIL_C))),
+             ptr(_aligned(w2.reshape(_TAIL_C, _TAIL_H))), ptr(_aligned(wp)), ptr(pk),
+             _hip.stream())
+        r = torch.empty(rows, _TAIL_D, dtype=torch.float32, device=dev)
+        zb = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)
+        h1 = torch.empty(rows, _TAIL_H, dtype=torch.int16, device=dev)
+        h2 = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)
+        inv = torch.empty(rows, dtype=torch.float32, device=dev)
+        call("tgfr_tail_fwd", ptr(z2), _TAIL_C, rows, ptr(pk), ptr(_aligned(b1)),
+             ptr(_aligned(b2)), ptr(_aligned(bp)), float(eps), ptr(r), _TAIL_D, ptr(zb), ptr(h1),
+             ptr(h2), ptr(inv), _hip.stream())
+        ctx.save_for_backward(r, inv, pk, zb, h1, h2)
+        ctx.cfg = (float(eps), shape, w1.shape, w2.shape)
+        return r.reshape(*shape[:-1], _TAIL_D)
+
+    @staticmethod
+    def backward(ctx, dr):
+        r, inv, pk, zb, h1, h2 = ctx.saved_tensors
+        eps, shape, w1shape, w2shape = ctx.cfg
+        rows, dev = r.shape[0], r.device
+        dr2 = _aligned(dr.reshape(rows, _TAIL_D))
+        dz = torch.empty(rows, _TAIL_C, dtype=torch.float32, device=dev)
+        dp = torch.empty(rows, _TAIL_D, dtype=torch.int16, device=dev)
+        dh2 = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)
+        dh1 = torch.empty(rows, _TAIL_H, dtype=torch.int16, device=dev)
+        call("tgfr_tail_bwd", ptr(dr2), _TAIL_D, ptr(r), _TAIL_D, ptr(inv), rows, eps, ptr(pk),
+             ptr(h1), ptr(h2), ptr(dz), _TAIL_C, ptr(dp), ptr(dh2), ptr(dh1), _hip.stream())
+        ws = torch.empty(tail_dw_ws_floats(rows), dtype=torch.float32, device=dev)
+        dwp = torch.empty(_TAIL_D, _TAIL_C, dtype=torch.float32, device=dev)
+        dbp = torch.empty(_TAIL_D, dtype=torch.float32, device=dev)
+        dw2 = torch.empty(_TAIL_C, _TAIL_H, dtype=torch.float32, device=dev)
+        db2 = torch.empty(_TAIL_C, dtype=torch.float32, device=dev)
+        dw1 = torch.empty(_TAIL_H, _TAIL_C, dtype=torch.float32, device=dev)
+        db1 = torch.empty(_TAIL_H, dtype=torch.float32, device=dev)
+        call("tgfr_tail_dw", ptr(dp), ptr(h2), ptr(dh2), ptr(h1), ptr(dh1), ptr(zb), rows,
+             ptr(dwp), ptr(dbp), ptr(dw2), ptr(db2), ptr(dw1), ptr(db1), ptr(ws), _hip.stream())
+        return (dz.reshape(shape), dw1.reshape(w1shape), db1, dw2.reshape(w2shape), db2, dwp,
+                dbp, None)
+
+
+def imim_tail(z, conv1, conv2, proj, eps=1e-12):
+    """R = normalize(proj(relu(conv2(relu(conv1(z)))))) on channels-last rows
+    z [..., 256] (bf16 operands, fp32 accumulation)."""
+    return ImimTail.apply(z, conv1.weight, conv1.bias, conv2.weight, conv2.bias, proj.weight,
+                          proj.bias, eps)
+
+
 # ---------------------------------------------------------------- heads ---
 class L2NormRows(torch.autograd.Function):
     """F.normalize(x, p=2, dim=-1, eps) in one kernel each way."""

@@ -64,6 +64,10 @@ class IMIM(nn.Module):
         # LayerNorm over (C, H, W) of each sample == over the channels-last
         # [HW, C] rows; the [C, H, W] affine maps are read channel-major in place
         z = K.layer_norm_rows(z, self.ln.weight, self.ln.bias, self.ln.eps, ch=c)
+        if self.precision == "bf16":
+            # conv1x1_1 -> ReLU -> conv1x1_2 -> ReLU -> project_local, fused
+            z = K.imim_tail(z, self.conv1x1_1, self.conv1x1_2, self.project_local.projection)
+            return z.reshape(n, h, w, -1).permute(0, 3, 1, 2)
         z = K.linear_rows(z, self.conv1x1_1.weight, self.conv1x1_1.bias, relu=True,
                           mode=self.precision)
         z = K.linear_rows(z, self.conv1x1_2.weight, self.conv1x1_2.bias, relu=True,

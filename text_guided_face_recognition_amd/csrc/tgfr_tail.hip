@@ -28,6 +28,7 @@
 #include "tgfr_common.h"
 
 #include <algorithm>
+#include <type_traits>
 
 using namespace tgfr;
 
@@ -82,27 +83,36 @@ __device__ __forceinline__ void copy_out(uint32_t base, uint16_t* dst, long long
 }
 
 // --------------------------------------------------------------- pack ---
+// Each packed matrix M [rows][K] is stored in MFMA fragment order: the 64
+// lanes' 16-B operand pieces of one (32-row tile rt, 16-k step s) are one
+// contiguous KiB, lane l holding M[32 rt + l%32][16 s + 8 (l/32) .. +7].  A
+// wave's fragment load is then one coalesced KiB instead of 64 scattered
+// 16-B pieces (one cache line each), which made the weight reads of the
+// first version cost a third of the kernel.
+__device__ __forceinline__ const uint16_t* frag_ptr(const uint16_t* pk, int off, int K, int rt,
+                                                    int s, int lane) {
+  return pk + off + ((rt * (K / 16) + s) * 64 + lane) * 8;
+}
+
 __global__ __launch_bounds__(256) void tail_pack_kernel(const float* __restrict__ W1,
                                                         const float* __restrict__ W2,
                                                         const float* __restrict__ Wp,
                                                         uint16_t* __restrict__ pk) {
   const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e < TH * TC) {
-    const int r = e / TC, c = e % TC;
-    const uint16_t v = bf_bits(W1[e]);
-    pk[OFF_W1 + e] = v;
-    pk[OFF_W1T + c * TH + r] = v;
-  } else if (e < TH * TC + TC * TH) {
-    const int f = e - TH * TC, r = f / TH, c = f % TH;
-    const uint16_t v = bf_bits(W2[f]);
-    pk[OFF_W2 + f] = v;
-    pk[OFF_W2T + c * TC + r] = v;
-  } else if (e < PACK_ELEMS / 2) {
-    const int f = e - 2 * TH * TC, r = f / TC, c = f % TC;
-    const uint16_t v = bf_bits(Wp[f]);
-    pk[OFF_WP + f] = v;
-    pk[OFF_WPT + c * TD + r] = v;
-  }
+  if (e >= PACK_ELEMS) return;
+  // segment: (source, source row length, transposed?, K of M, offset)
+  const float* W;
+  int off, K, ld, tr;
+  if (e < OFF_W2) { W = W1; off = OFF_W1; K = TC; ld = TC; tr = 0; }
+  else if (e < OFF_WP) { W = W2; off = OFF_W2; K = TH; ld = TH; tr = 0; }
+  else if (e < OFF_W1T) { W = Wp; off = OFF_WP; K = TC; ld = TC; tr = 0; }
+  else if (e < OFF_W2T) { W = W1; off = OFF_W1T; K = TH; ld = TC; tr = 1; }
+  else if (e < OFF_WPT) { W = W2; off = OFF_W2T; K = TC; ld = TH; tr = 1; }
+  else { W = Wp; off = OFF_WPT; K = TD; ld = TC; tr = 1; }
+  const int f = e - off, j = f & 7, lane = (f >> 3) & 63, piece = f >> 9;
+  const int s = piece % (K / 16), rt = piece / (K / 16);
+  const int r = 32 * rt + (lane & 31), k = 16 * s + 8 * (lane >> 5) + j;   // M[r][k]
+  pk[e] = bf_bits(tr ? W[k * ld + r] : W[r * ld + k]);
 }
 
 // ------------------------------------------------------------ forward ---
@@ -119,6 +129,18 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
   const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE;
   const int lr = lane & 31, h = lane >> 5;
   const int row0 = blockIdx.x * TM;
+
+  // every weight fragment of layers 1 and 2 is issued up front (they do not
+  // depend on the activations): one memory latency per kernel instead of one
+  // per k-step -- with one 4-wave workgroup per CU nothing else would hide it
+  bf16x8 w1f[TC / 16], w2f[TH / 16][2];
+#pragma unroll
+  for (int s = 0; s < TC / 16; ++s) w1f[s] = gld16(frag_ptr(pk, OFF_W1, TC, w, s, lane));
+#pragma unroll
+  for (int s = 0; s < TH / 16; ++s)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+      w2f[s][jt] = gld16(frag_ptr(pk, OFF_W2, TH, 2 * w + jt, s, lane));
 
   // Z rows -> bf16 image (and the bf16 copy for dW1); rows past the end are 0
 #pragma unroll
@@ -142,14 +164,12 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
-    const uint16_t* wa = pk + OFF_W1 + (32 * w + lr) * TC + 8 * h;
-#pragma unroll 4
+#pragma unroll
     for (int s = 0; s < TC / 16; ++s) {
-      const bf16x8 a = gld16(wa + 16 * s);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         const bf16x8 b = as_bf8(lds_ld16(F_Z + img<TC>(32 * mt + lr, 2 * s + h)));
-        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[s], b, acc[mt], 0, 0, 0);
       }
     }
 #pragma unroll
@@ -165,6 +185,13 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
       }
     }
   }
+  // layer 3's weight fragments, issued while layer 2 runs
+  bf16x8 wpf[TC / 16][2];
+#pragma unroll
+  for (int s = 0; s < TC / 16; ++s)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      wpf[s][nt] = gld16(frag_ptr(pk, OFF_WP, TC, 2 * w + nt, s, lane));
   __syncthreads();
   copy_out<TH>(F_H1, H1b, TH, row0, rows, tid);
 
@@ -177,12 +204,9 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
-    const uint16_t* wa = pk + OFF_W2 + (64 * w + lr) * TH + 8 * h;
-#pragma unroll 2
-    for (int s = 0; s < TH / 16; ++s) {
-      bf16x8 a[2], b[2];
 #pragma unroll
-      for (int jt = 0; jt < 2; ++jt) a[jt] = gld16(wa + 32 * jt * TH + 16 * s);
+    for (int s = 0; s < TH / 16; ++s) {
+      bf16x8 b[2];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
         b[mt] = as_bf8(lds_ld16(F_H1 + img<TH>(32 * mt + lr, 2 * s + h)));
@@ -190,7 +214,8 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
       for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
-          acc[jt][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[jt], b[mt], acc[jt][mt], 0, 0, 0);
+          acc[jt][mt] =
+              __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2f[s][jt], b[mt], acc[jt][mt], 0, 0, 0);
     }
     // the Z image is dead (every wave passed the barrier after layer 1): H2 reuses it
 #pragma unroll
@@ -219,22 +244,17 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
-  {
-    const uint16_t* wb = pk + OFF_WP + (64 * w + lr) * TC + 8 * h;
-#pragma unroll 4
-    for (int s = 0; s < TC / 16; ++s) {
-      bf16x8 a[2], b[2];
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) b[nt] = gld16(wb + 32 * nt * TC + 16 * s);
+  for (int s = 0; s < TC / 16; ++s) {
+    bf16x8 a[2];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-        a[mt] = as_bf8(lds_ld16(F_H2 + img<TC>(32 * mt + lr, 2 * s + h)));
+    for (int mt = 0; mt < 2; ++mt)
+      a[mt] = as_bf8(lds_ld16(F_H2 + img<TC>(32 * mt + lr, 2 * s + h)));
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
-    }
+      for (int nt = 0; nt < 2; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mt], wpf[s][nt], acc[mt][nt], 0, 0, 0);
   }
   // bias, then the row sums of squares: lane-local over this wave's two
   // column tiles, then over the 32 columns of each half-wave (rs16)
@@ -293,6 +313,17 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
   const int lr = lane & 31, h = lane >> 5;
   const int row0 = blockIdx.x * TM;
 
+  // the first two GEMMs' weight fragments, issued before anything else
+  bf16x8 wptf[TD / 16][2], w2tf[TC / 16];
+#pragma unroll
+  for (int s = 0; s < TD / 16; ++s)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+      wptf[s][jt] = gld16(frag_ptr(pk, OFF_WPT, TD, 2 * w + jt, s, lane));
+#pragma unroll
+  for (int s = 0; s < TC / 16; ++s)
+    w2tf[s] = gld16(frag_ptr(pk, OFF_W2T, TC, w, s, lane));
+
   // F.normalize backward, one row per wave pass (lane: 4 columns)
 #pragma unroll 2
   for (int r = 0; r < TM / 4; ++r) {
@@ -334,12 +365,9 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
-    const uint16_t* wa = pk + OFF_WPT + (64 * w + lr) * TD + 8 * h;
-#pragma unroll 4
-    for (int s = 0; s < TD / 16; ++s) {
-      bf16x8 a[2], b[2];
 #pragma unroll
-      for (int jt = 0; jt < 2; ++jt) a[jt] = gld16(wa + 32 * jt * TD + 16 * s);
+    for (int s = 0; s < TD / 16; ++s) {
+      bf16x8 b[2];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
         b[mt] = as_bf8(lds_ld16(B_DP + img<TD>(32 * mt + lr, 2 * s + h)));
@@ -347,7 +375,8 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
       for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
-          acc[jt][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[jt], b[mt], acc[jt][mt], 0, 0, 0);
+          acc[jt][mt] =
+              __builtin_amdgcn_mfma_f32_32x32x16_bf16(wptf[s][jt], b[mt], acc[jt][mt], 0, 0, 0);
     }
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
@@ -366,6 +395,13 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
           lds_st8(B_DH2 + img_at<TC>(32 * mt + lr, j0), pk4(v0, v1, v2, v3));
         }
   }
+  // the last GEMM's weight fragments, issued while dH1 is computed
+  bf16x8 w1tf[TH / 16][2];
+#pragma unroll
+  for (int s = 0; s < TH / 16; ++s)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+      w1tf[s][ct] = gld16(frag_ptr(pk, OFF_W1T, TH, 2 * w + ct, s, lane));
   __syncthreads();
   copy_out<TC>(B_DH2, dH2b, TC, row0, rows, tid);
 
@@ -385,14 +421,12 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
-    const uint16_t* wa = pk + OFF_W2T + (32 * w + lr) * TC + 8 * h;
-#pragma unroll 4
+#pragma unroll
     for (int s = 0; s < TC / 16; ++s) {
-      const bf16x8 a = gld16(wa + 16 * s);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         const bf16x8 b = as_bf8(lds_ld16(B_DH2 + img<TC>(32 * mt + lr, 2 * s + h)));
-        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2tf[s], b, acc[mt], 0, 0, 0);
       }
     }
     // the dP image is dead (every wave passed the barrier before this GEMM)
@@ -421,12 +455,9 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
-  const uint16_t* wb = pk + OFF_W1T + (64 * w + lr) * TH + 8 * h;
-#pragma unroll 2
-  for (int s = 0; s < TH / 16; ++s) {
-    bf16x8 a[2], b[2];
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct) b[ct] = gld16(wb + 32 * ct * TH + 16 * s);
+  for (int s = 0; s < TH / 16; ++s) {
+    bf16x8 a[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
       a[mt] = as_bf8(lds_ld16(B_DH1 + img<TH>(32 * mt + lr, 2 * s + h)));
@@ -434,7 +465,7 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
-        acc[mt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mt], b[ct], acc[mt][ct], 0, 0, 0);
+        acc[mt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mt], w1tf[s][ct], acc[mt][ct], 0, 0, 0);
   }
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -460,7 +491,7 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
 constexpr int DW_NB = 128, DW_CH = 32;
 constexpr int DW_PITCH = DW_NB * 2 + 64;               // bytes per staged row
 constexpr int DW_IMG = DW_CH * DW_PITCH;               // one operand chunk
-constexpr int DW_LDS = 4 * DW_IMG;                     // X, Y, double-buffered
+constexpr int DW_LDS = 6 * DW_IMG;                     // X, Y, three buffers
 
 struct DwProb {
   const uint16_t* X;
@@ -532,15 +563,7 @@ __global__ __launch_bounds__(256) void tail_dw_kernel(DwArgs A, float* __restric
       lds_st16(buf * 2 * DW_IMG + DW_IMG + r * DW_PITCH + 16 * c16, vy[ps]);
     }
   };
-  uint4 vx[2], vy[2];
-  if (n_chunks > 0) {
-    load(0, vx, vy);
-    store(0, vx, vy);
-  }
-  __syncthreads();
-  for (int c = 0; c < n_chunks; ++c) {
-    const int buf = c & 1;
-    if (c + 1 < n_chunks) load(c + 1, vx, vy);
+  auto compute = [&](int buf) {
     const uint32_t bx = buf * 2 * DW_IMG, by = bx + DW_IMG;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -561,8 +584,27 @@ __global__ __launch_bounds__(256) void tail_dw_kernel(DwArgs A, float* __restric
           for (int j = 0; j < 8; ++j) cs[t] += (float)a[t][j];
       }
     }
-    if (c + 1 < n_chunks) store(buf ^ 1, vx, vy);
+  };
+  // three chunks in flight: chunk c sits in register slot c % 3 from its load
+  // (issued three steps ahead) until it is stored to LDS buffer c % 3 one
+  // step before it is used
+  uint4 rx[3][2], ry[3][2];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    if (j < n_chunks) load(j, rx[j], ry[j]);
+  if (n_chunks > 0) store(0, rx[0], ry[0]);
+  __syncthreads();
+  auto step = [&](auto J, int c) {
+    constexpr int j = decltype(J)::value, j1 = (j + 1) % 3;
+    if (c + 1 < n_chunks) store(j1, rx[j1], ry[j1]);
+    if (c + 3 < n_chunks) load(c + 3, rx[j], ry[j]);
+    compute(j);
     __syncthreads();
+  };
+  for (int c = 0; c < n_chunks; c += 3) {
+    step(std::integral_constant<int, 0>{}, c);
+    if (c + 1 < n_chunks) step(std::integral_constant<int, 1>{}, c + 1);
+    if (c + 2 < n_chunks) step(std::integral_constant<int, 2>{}, c + 2);
   }
 
   // slab [slice][N][K] (+ [slice][N] column sums after all products' dW slabs)
@@ -632,10 +674,10 @@ void dw_plan(int rows, DwArgs& A, long long& ws_floats, int& n_wg) {
   const int NS[3] = {TD, TC, TH}, KS[3] = {TC, TH, TC};   // dWp, dW2, dW1
   int blocks = 0;
   for (int i = 0; i < 3; ++i) blocks += (NS[i] / DW_NB) * (KS[i] / DW_NB);
-  // slices: enough workgroups to cover the chip, but the slabs (slices x
-  // 0.53 MB, written here and read back by the reduce) stay well under the
-  // 32 MB of operands at the step's 12544 rows; at least 4 chunks per slice
-  const int want = std::max(1, 128 / blocks);
+  // slices: one workgroup per CU (the slabs, slices x 0.53 MB written here
+  // and read back by the reduce, are then ~half the 32 MB of operands at the
+  // step's 12544 rows); at least 4 chunks per slice
+  const int want = std::max(1, 256 / blocks);
   const int max_slices = std::max(1, rows / (4 * DW_CH));
   A.slices = std::min(want, max_slices);
   A.rows_per = ((rows + A.slices - 1) / A.slices + DW_CH - 1) / DW_CH * DW_CH;
@@ -666,7 +708,7 @@ int tgfr_tail_pack_elems(void) { return PACK_ELEMS; }
 int tgfr_tail_pack(const float* W1, const float* W2, const float* Wp, uint16_t* pk,
                    void* stream) {
   if (!W1 || !W2 || !Wp || !pk) return 1001;
-  hipLaunchKernelGGL(tail_pack_kernel, dim3((PACK_ELEMS / 2 + 255) / 256), dim3(256), 0,
+  hipLaunchKernelGGL(tail_pack_kernel, dim3((PACK_ELEMS + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, W1, W2, Wp, pk);
   return (int)hipGetLastError();
 }

@@ -29,9 +29,6 @@ R = torch.empty(rows, 256, device="cuda"); zb = torch.empty(rows, 256, dtype=tor
 H1 = torch.empty(rows, 128, dtype=torch.int16, device="cuda"); H2 = torch.empty(rows, 256, dtype=torch.int16, device="cuda")
 inv = torch.empty(rows, device="cuda")
 call("tgfr_tail_fwd", ptr(z), 256, rows, ptr(pk), ptr(b1), ptr(b2), ptr(bp), 1e-12, ptr(R), 256, ptr(zb), ptr(H1), ptr(H2), ptr(inv), _hip.stream())
-print("pack W1", rel(bf(pk[:32768]).view(128, 256), w1), "W2", rel(bf(pk[32768:65536]).view(256, 128), w2),
-      "Wp", rel(bf(pk[65536:131072]).view(256, 256), wp), "W1T", rel(bf(pk[131072:163840]).view(256, 128), w1.t()),
-      "W2T", rel(bf(pk[163840:196608]).view(128, 256), w2.t()), "WpT", rel(bf(pk[196608:]).view(256, 256), wp.t()))
 print("zb", rel(bf(zb), z), "H1", rel(bf(H1), h1), "H2", rel(bf(H2), h2), "R", rel(R, r), "inv", rel(inv, 1/p.norm(dim=-1)))
 dz = torch.empty(rows, 256, device="cuda"); dP = torch.empty(rows, 256, dtype=torch.int16, device="cuda")
 dH2 = torch.empty(rows, 256, dtype=torch.int16, device="cuda"); dH1 = torch.empty(rows, 128, dtype=torch.int16, device="cuda")

@@ -146,6 +146,13 @@ int tgfr_ce_grad(const float* L, long long ld, int n_r, int n_c, int row_offset,
  * (ksplit <= 4) or by a second, chip-wide launch (ksplit > 4).
  * counters: >= batch * ceil(M/64) * ceil(N/64) zeroed uint32 words, left
  * zeroed on return. */
+/* C = A W^T + bias with a bf16 output (IMIM's packed q/k/v projection in bf16
+ * mode, models/models.py:397-398 -> fusion_nets.py:99-111): A [M][K] fp32 rows
+ * (K = 128 or 256), W [N][K] fp32 (row stride sWn), C [M][N] bf16 (sCm). */
+int tgfr_linear_bf16out(const float* A, long long sAm, int M, int K, const float* W,
+                        long long sWn, const float* bias, int N, uint16_t* C, long long sCm,
+                        void* stream);
+
 int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, const float* B,
                long long sBb, long long sBk, long long sBn, float* C, long long sCb,
                long long sCm, long long sCn, int batch, int M, int N, int K, float alpha,
@@ -159,6 +166,25 @@ int tgfr_attn_softmax(const float* S, float* P, float* lse, long long rows, int 
 /* dS = scale * P * (dP - rowsum(P * dP)). */
 int tgfr_attn_softmax_bwd(const float* P, const float* dP, float* dS, long long rows, int n,
                           long long ld, float scale, void* stream);
+
+/* Fused self-attention for IMIM (fusion_nets.py:93-118 with C' = C = 256,
+ * HW <= 224), bf16 operands / fp32 accumulation, no HW x HW matrix in HBM:
+ *   O = softmax(scale * Q K^T) V  per sample; lse = row log-sum-exp of the
+ *   scaled scores (saved for the backward).
+ * Q, K, V: [B][hw][256] bf16 views (row stride ld, sample stride sb, both
+ * multiples of 8), e.g. the column slices of the packed projection
+ * [B][hw][768] written by tgfr_linear_bf16out.  O: [B][hw][256] fp32 (ldo,
+ * sbo).  The backward recomputes P from lse and writes dQ, dK, dV fp32 (ldg,
+ * sbg; overwritten); dO and O must be dense [B][hw][256] fp32;
+ * ws: tgfr_attn_bwd_ws bytes. */
+int tgfr_attn_fwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long long ld,
+                  long long sb, int B, int hw, float scale, float* O, long long ldo,
+                  long long sbo, float* lse, void* stream);
+int tgfr_attn_bwd_ws(int B, int hw, long long* bytes);
+int tgfr_attn_bwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long long ld,
+                  long long sb, int B, int hw, float scale, const float* O, const float* dO,
+                  long long ldo, long long sbo, const float* lse, float* dQ, float* dK,
+                  float* dV, long long ldg, long long sbg, void* ws, void* stream);
 
 /* y = x / max(|x|, eps) per row (F.normalize; ProjectionHead models/models.py:119,
  * ArcMarginProduct models/metrics.py:44); inv_norm[row] = 1 / max(|x|, eps). */

@@ -1,0 +1,91 @@
+"""Fused IMIM self-attention (csrc/tgfr_attn.hip attn_fwd / attn_bwd_*;
+reference models/fusion_nets.py:93-118 with C' = C = 256) through the C ABI,
+on a packed bf16 projection, against plain PyTorch fp32 on the GPU (inputs =
+the same bf16 values):
+  forward: lse to 1e-3; O against the same math with P rounded to bf16:
+    1e-2 of max|O|;
+  forward and backward against fp32 autograd of softmax(scale Qr Kr^T) V:
+    relative Frobenius 2e-2 on O, dQr, dKr, dV."""
+import pytest
+import torch
+
+from text_guided_face_recognition_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _frob(a, b):
+    return float((a - b).norm() / b.norm())
+
+
+def _attn(pxb, do, scale):
+    """tgfr_attn_fwd / _bwd on a packed bf16 projection [nb, hw, 768]."""
+    import ctypes
+    from text_guided_face_recognition_amd import _hip
+    from text_guided_face_recognition_amd._hip import call, ptr
+    nb, hw, _ = pxb.shape
+    bits = pxb.view(torch.int16)
+    o = torch.empty(nb, hw, 256, device="cuda")
+    lse = torch.empty(nb * hw, device="cuda")
+    call("tgfr_attn_fwd", ptr(bits), ptr(bits[..., 256:]), ptr(bits[..., 512:]), 768, hw * 768,
+         nb, hw, scale, ptr(o), 256, hw * 256, ptr(lse), _hip.stream())
+    out = (ctypes.c_longlong * 1)()
+    assert _hip.lib().tgfr_attn_bwd_ws(nb, hw, ctypes.addressof(out)) == 0
+    ws = torch.empty(int(out[0]), dtype=torch.uint8, device="cuda")
+    g = torch.empty(nb, hw, 768, device="cuda")
+    call("tgfr_attn_bwd", ptr(bits), ptr(bits[..., 256:]), ptr(bits[..., 512:]), 768, hw * 768,
+         nb, hw, scale, ptr(o), ptr(do), 256, hw * 256, ptr(lse), ptr(g), ptr(g[..., 256:]),
+         ptr(g[..., 512:]), 768, hw * 768, ptr(ws), _hip.stream())
+    return o, lse, g
+
+
+@pytest.mark.parametrize("nb,hw", [(64, 196), (3, 196), (2, 37), (1, 224), (4, 5), (5, 161)])
+def test_fused_attention(nb, hw):
+    torch.backends.cuda.matmul.allow_tf32 = False
+    g = torch.Generator(device="cuda").manual_seed(nb * 1000 + hw)
+    pxb = torch.randn(nb, hw, 768, generator=g, device="cuda").to(torch.bfloat16)
+    do = torch.randn(nb, hw, 256, generator=g, device="cuda")
+    scale = 1.0 / 16.0
+    o, lse, dx = _attn(pxb, do, scale)
+
+    px = pxb.float()
+    q, k, v = px[..., :256], px[..., 256:512], px[..., 512:]
+    s = scale * q @ k.transpose(1, 2)
+    assert float((lse.view(nb, hw) - torch.logsumexp(s, -1)).abs().max()) < 1e-3
+    o_em = _bf(torch.softmax(s, dim=-1)) @ v          # P rounded to bf16 as in the kernel
+    assert float((o - o_em).abs().max() / o_em.abs().max()) < 1e-2
+
+    xr = px.clone().requires_grad_()
+    qr, kr, vr = xr[..., :256], xr[..., 256:512], xr[..., 512:]
+    o_ref = torch.softmax(scale * qr @ kr.transpose(1, 2), dim=-1) @ vr
+    (dx_ref,) = torch.autograd.grad(o_ref, xr, do)
+    assert _frob(o, o_ref.detach()) < 2e-2
+    for name, sl in (("dQr", slice(0, 256)), ("dKr", slice(256, 512)), ("dV", slice(512, 768))):
+        e = _frob(dx[..., sl], dx_ref[..., sl])
+        assert e < 2e-2, (name, e)
+
+
+def test_self_attention_golden_bf16(gpu):
+    """SelfAttention module in bf16 mode (the composed bgemm path, used for
+    cross attention and outside IMIM) on the reference golden (C=256,
+    HW=196): relative Frobenius 2e-2 on the output and gradients."""
+    from conftest import load_golden, t
+    from text_guided_face_recognition_amd.models.fusion_nets import SelfAttention
+    g = load_golden("self_attention_c256_hw196")
+    m = SelfAttention(256, scale=1).to(gpu)
+    m.precision = "bf16"
+    for name, key in (("query_proj", "q"), ("key_proj", "k"), ("value_proj", "v")):
+        getattr(m, name).weight.data = t(g[f"{key}_w"]).to(gpu)
+        getattr(m, name).bias.data = t(g[f"{key}_b"]).to(gpu)
+    x = t(g["x"]).to(gpu).requires_grad_()
+    out = m(x, x)
+    ref = t(g["out"]).to(gpu)
+    assert _frob(out.detach(), ref) < 2e-2
+    (out * t(g["probe"]).to(gpu)).sum().backward()
+    assert _frob(x.grad, t(g["d_x"]).to(gpu)) < 2e-2
+    assert _frob(m.value_proj.weight.grad, t(g["d_v_w"]).to(gpu)) < 2e-2
+    assert _frob(m.query_proj.weight.grad, t(g["d_q_w"]).to(gpu)) < 2e-2

@@ -49,6 +49,10 @@ SIGNATURES = {
     "tgfr_focal_ce": [P, I, I, P, F, P, P, P, P],
     "tgfr_focal_ce_bwd": [P, I, I, P, F, P, P, P, P],
     "tgfr_attn_softmax_bwd": [P, P, P, L, I, L, F, P],
+    "tgfr_attn_fwd": [P, P, P, L, L, I, I, F, P, L, L, P, P],
+    "tgfr_linear_bf16out": [P, L, I, I, P, L, P, I, P, L, P],
+    "tgfr_attn_bwd_ws": [I, I, P],
+    "tgfr_attn_bwd": [P, P, P, L, L, I, I, F, P, P, L, L, P, P, P, P, L, L, P, P],
     "tgfr_ln_ws_floats": [I, L, I, I, P],
     "tgfr_loss_mix": [I, P, I, P, P, P],
     "tgfr_bn_fwd_cl": [P, I, I, I, F, F, I, P, P, P, P, P, P, P],

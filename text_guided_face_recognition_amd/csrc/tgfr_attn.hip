@@ -9,7 +9,27 @@
 //   attn_softmax   P = softmax(scale * S) per row over the valid keys + row LSE.
 //   attn_softmax_bwd  dS = scale * P (dP - rowsum(P dP)).
 // The attention matrices are HW x HW per sample (196^2 fp32 = 150 KB for IMIM,
-// 36^2 for FCFM), so they are materialised instead of recomputed.
+// 36^2 for FCFM); on the composed path they are materialised.
+//
+// Fused self-attention (bf16 mode, IMIM: C' = C = 256, HW <= 224), reading the
+// packed fp32 projections [Qr | Kr | V] of each sample in place:
+//   attn_fwd      per (sample, 32-query tile), online softmax over the key
+//                 tiles.  S^T = Kr Qr^T puts ONE query on each lane (its MFMA
+//                 column): the running max / sum are lane-local plus one
+//                 cross-half combine, and P^T as it stands is the B operand of
+//                 O^T = V^T P^T (the MFMA k axis permuted to the accumulator's
+//                 row order; V read through LDS with ds_read_b64_tr_b16 in
+//                 the same order).  Writes O [HW][256] and the row LSE.
+//   attn_bwd_kv   one 2-wave workgroup per (sample, 32-key tile), each wave
+//                 owning half of the d / dv columns.  Per query tile it
+//                 recomputes S = Qr Kr^T and dP = dO V^T (lane = key column,
+//                 so P^T and dS^T are A operands as they stand), then
+//                 dV += P^T dO and dKr += dS^T Qr with dO / Qr read through
+//                 LDS transposed; dS (bf16) goes to HBM for
+//   attn_bwd_q    one wave per (sample, 32-query tile): dQr = dS Kr, Kr staged
+//                 per key tile in LDS.
+// No HW x HW fp32 matrix is ever written; D = rowsum(dO * O) comes from
+// attn_bwd_prep.
 #include "tgfr_common.h"
 
 using namespace tgfr;
@@ -54,6 +74,399 @@ __global__ __launch_bounds__(256) void attn_softmax_bwd_kernel(const float* __re
   for (int j = lane; j < n; j += WAVE) ds[j] = scale * p[j] * (dp[j] - dot);
 }
 
+// ------------------------------------------------------ fused (IMIM) ---
+constexpr int AD = 256;                  // Qr/Kr width = V width
+constexpr int AT = 7;                    // max 32-position tiles (HW <= 224)
+constexpr int IMG = 32 * AD * 2;         // one 32-row bf16 tile image (16 KiB)
+
+__device__ __attribute__((aligned(16))) uint16_t attn_zero16[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+// Tile image: 32 rows x 256 bf16, 512-B rows, 16-B chunk c of row r stored at
+// chunk c ^ f(r), f(r) = 4 (r & 3) + ((r >> 2) & 3).  Both read shapes are
+// conflict-free on it: a ds_read_b128 operand fragment (16 lanes of a group =
+// 16 rows, one logical chunk: f is a bijection on r mod 16) and a
+// ds_read_b64_tr_b16 transposed fragment (32 lanes = 4 rows x 4 chunks: the
+// rows' high swizzle bits differ).
+__device__ __forceinline__ int tsw(int r) { return 4 * (r & 3) + ((r >> 2) & 3); }
+__device__ __forceinline__ uint32_t tix(int r, int c) {
+  return (uint32_t)(r * (AD * 2) + ((c ^ tsw(r)) << 4));
+}
+__device__ __forceinline__ bf16x8 zero8() { return as_bf8(make_uint4(0, 0, 0, 0)); }
+
+// Wait until at most `younger` ring stages of 8 DMA pieces (this wave's
+// share) are outstanding, then meet the workgroup.
+__device__ __forceinline__ void ring_wait8(int younger) {
+  switch (younger) {
+    case 0: ring_barrier<0>(); break;
+    case 1: ring_barrier<8>(); break;
+    case 2: ring_barrier<16>(); break;
+    case 3: ring_barrier<24>(); break;
+    case 4: ring_barrier<32>(); break;
+    default: ring_barrier<40>(); break;
+  }
+}
+
+// Operand fragment, lane row lr: columns 16 s + 8 h .. +7.
+__device__ __forceinline__ bf16x8 frag(uint32_t base, int s, int lane) {
+  return as_bf8(lds_ld16(base + tix(lane & 31, 2 * s + (lane >> 5))));
+}
+// Transposed fragment: lane gets column c0 + lane%32 at rows r0 + 0..3
+// (elements 0-3) and r1 + 0..3 (elements 4-7).
+__device__ __forceinline__ bf16x8 trf(uint32_t base, int r0, int r1, int c0, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
+  const int col = c0 + 16 * (g & 1) + 4 * p;
+  const uint32_t o = ((col >> 2) & 1) * 8;
+  return join_tr(lds_tr4(base + tix(r0 + q, col >> 3) + o),
+                 lds_tr4(base + tix(r1 + q, col >> 3) + o));
+}
+
+// DMA of bf16 rows [row0, row0 + 32) x 256 (row stride ld) into a tile image:
+// 16 one-KiB pieces (two image rows each); this wave issues pieces
+// wv, wv + nw, ...  Each lane's source is the logical chunk its swizzled slot
+// holds; rows >= n read zeros (checked only on a ragged tile: per-piece
+// address VALU rivals the MFMA time of these short kernels).
+__device__ __forceinline__ void dma_tile(const uint16_t* X, long long ld, int row0, int n,
+                                         uint32_t base, int wv, int nw, int lane) {
+  const bool full = row0 + 32 <= n;                  // uniform
+  const uint16_t* X0 = X + (long long)row0 * ld;
+  const int r1 = lane >> 5, l31 = lane & 31;
+#pragma unroll 4
+  for (int p = wv; p < 16; p += nw) {
+    const int r = 2 * p + r1, c = l31 ^ tsw(r);
+    const uint16_t* src = X0 + r * (int)ld + 8 * c;
+    if (!full && row0 + r >= n) src = attn_zero16;
+    glds16(src, base + p * 1024);
+  }
+}
+
+// Forward: one 2-wave workgroup per (sample, pair of query tiles), online
+// softmax over the key tiles in a ROLLED loop (a fully unrolled run-once
+// kernel of ~40 KB spent its time on instruction-cache misses).  The Kr and
+// V tiles stream, interleaved, through a DMA ring shared by both waves.
+// Per key tile: S^T = Kr Qr^T (lane = query, so the running max / sum are
+// per lane plus one cross-half combine), then O^T += V^T P^T with P^T the
+// accumulator as it stands (k axis in the accumulator's key order, V read
+// transposed in the same order) -- O^T keeps the query on the lane too, so the
+// online-softmax rescale is one scalar per lane.
+// LDS: [0, 2 IMG) the waves' Qr tiles, then the ring.
+constexpr int FWD_NS = 7;
+constexpr int FWD_LDS = (2 + FWD_NS) * IMG;
+
+__global__ __launch_bounds__(128) void attn_fwd_kernel(const uint16_t* __restrict__ Qp,
+                                                       const uint16_t* __restrict__ Kp,
+                                                       const uint16_t* __restrict__ Vp,
+                                                       long long ld, long long sb, int hw,
+                                                       float scale, float* __restrict__ O,
+                                                       long long ldo, long long sbo,
+                                                       float* __restrict__ lse) {
+  const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE, lr = lane & 31, h = lane >> 5;
+  const int nt = (hw + 31) / 32, np = (nt + 1) / 2;
+  // the workgroups of one sample run on one XCD (its Kr / V stay in that L2)
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = wid / np, qt = 2 * (wid % np) + w;
+  const bool active = qt < nt;                       // uniform per wave
+  const uint32_t qimg = w * IMG, ring = 2 * IMG;
+  const int n_st = 2 * nt;                           // stages: Kr 0, V 0, Kr 1, V 1, ...
+  auto issue = [&](int st) {
+    const uint16_t* X = ((st & 1) ? Vp : Kp) + b * sb;
+    dma_tile(X, ld, 32 * (st >> 1), hw, ring + (st % FWD_NS) * IMG, w, 2, lane);
+  };
+  // stage st has landed (this wave's pieces) and every wave got here
+  auto wait = [&](int st) { ring_wait8(min(FWD_NS - 2, n_st - 1 - st)); };
+  dma_tile(Qp + b * sb, ld, 32 * qt, active ? hw : 0, qimg, 0, 1, lane);
+  for (int st = 0; st < FWD_NS - 1 && st < n_st; ++st) issue(st);
+  wait(0);                                           // also covers the Qr tile
+  if (FWD_NS - 1 < n_st) issue(FWD_NS - 1);
+  bf16x8 qf[AD / 16];
+#pragma unroll
+  for (int s = 0; s < AD / 16; ++s) qf[s] = frag(qimg, s, lane);
+
+  const float c = scale * 1.4426950408889634f;
+  float m = -INFINITY, l = 0.f;
+  f32x16 oacc[AD / 32];
+#pragma unroll
+  for (int t = 0; t < AD / 32; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[t][r] = 0.f;
+  for (int kt = 0; kt < nt; ++kt) {
+    const int sk = 2 * kt;
+    if (kt > 0) {
+      wait(sk);
+      if (sk + FWD_NS - 1 < n_st) issue(sk + FWD_NS - 1);
+    }
+    const uint32_t kbuf = ring + (sk % FWD_NS) * IMG;
+    f32x16 sc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < AD / 16; ++s)
+      sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(kbuf, s, lane), qf[s], sc, 0, 0, 0);
+    // keys 32 kt + acc_row(r, h) of query 32 qt + lr
+    if (32 * kt + 32 > hw) {                         // ragged last tile (uniform)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        sc[r] = 32 * kt + acc_row(r, h) < hw ? sc[r] : -INFINITY;
+    }
+    float tmax = sc[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, sc[r]);
+    tmax = xhalf_max(tmax);
+    // lazy rescale: the reference max m only moves when some query's tile
+    // max exceeds it by more than 8 / c (P then stays <= 2^8, exact in the
+    // fp32 sums and fine in bf16); otherwise O and l keep their scale and the
+    // 128-register rescale of O (AGPR read-modify-write) is skipped
+    if (kt == 0) {
+      m = tmax;
+    } else if (__builtin_amdgcn_ballot_w64((tmax - m) * c > 8.f)) {
+      mfma_drain();
+      const float mn = fmaxf(m, tmax);
+      const float alpha = __builtin_amdgcn_exp2f((m - mn) * c);
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int t = 0; t < AD / 32; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[t][r] *= alpha;
+    }
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sc[r] = __builtin_amdgcn_exp2f((sc[r] - m) * c);
+      ps += sc[r];
+    }
+    l += ps;
+    bf16x8 pb[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      pb[s2] = as_bf8(make_uint4(pk_bf16(sc[8 * s2], sc[8 * s2 + 1]),
+                                 pk_bf16(sc[8 * s2 + 2], sc[8 * s2 + 3]),
+                                 pk_bf16(sc[8 * s2 + 4], sc[8 * s2 + 5]),
+                                 pk_bf16(sc[8 * s2 + 6], sc[8 * s2 + 7])));
+    wait(sk + 1);
+    if (sk + FWD_NS < n_st) issue(sk + FWD_NS);
+    const uint32_t vbuf = ring + ((sk + 1) % FWD_NS) * IMG;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int t = 0; t < AD / 32; ++t) {
+        const bf16x8 va = trf(vbuf, 16 * s2 + 4 * h, 16 * s2 + 8 + 4 * h, 32 * t, lane);
+        mma_agpr<MODE_BF16>(oacc[t], va, va, pb[s2], pb[s2]);
+      }
+  }
+  l = xhalf_sum(l);
+  mfma_drain();
+  if (!active) return;
+  const int q = 32 * qt + lr;
+  if (q >= hw) return;
+  if (h == 0) lse[(long long)b * hw + q] = m * scale + __logf(l);
+  const float inv = 1.f / l;
+  // lane: query q; register r of tile t: column 32 t + acc_row(r, h)
+  float* orow = O + b * sbo + (long long)q * ldo;
+#pragma unroll
+  for (int t = 0; t < AD / 32; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *(float4*)(orow + 32 * t + 8 * g + 4 * h) =
+          make_float4(oacc[t][4 * g] * inv, oacc[t][4 * g + 1] * inv, oacc[t][4 * g + 2] * inv,
+                      oacc[t][4 * g + 3] * inv);
+}
+
+// D[row] = sum_c dO[row][c] O[row][c] and dO in bf16 (the backward's operand);
+// one wave per row
+__global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const float* __restrict__ dO,
+                                                            const float* __restrict__ O,
+                                                            long long ld, long long rows,
+                                                            float* __restrict__ D,
+                                                            uint16_t* __restrict__ dOb) {
+  const long long row = blockIdx.x * 4LL + threadIdx.x / WAVE;
+  const int lane = threadIdx.x % WAVE;
+  if (row >= rows) return;
+  const float4 a = *(const float4*)(dO + row * ld + 4 * lane);
+  const float4 o = *(const float4*)(O + row * ld + 4 * lane);
+  *(uint2*)(dOb + row * AD + 4 * lane) = make_uint2(pk_bf16(a.x, a.y), pk_bf16(a.z, a.w));
+  const float v = wave_sum(a.x * o.x + a.y * o.y + a.z * o.z + a.w * o.w);
+  if (lane == 0) D[row] = v;
+}
+
+// dK / dV: one 4-wave workgroup per (sample, pair of key tiles); wave
+// (kk, half) = (w >> 1, w & 1) owns columns [128 half, +128) of dKr and dV
+// for key tile 2 j + kk; all four recompute S and dP of their key tile in
+// full.  The Qr and dO tiles of each query tile are DMA-staged once for the
+// four waves (double buffer).  LDS: Kr and V images of both key tiles
+// [0, 4 IMG), then 2 stages x (Qr, dO) [4 IMG, 8 IMG), then lse / D.
+constexpr int KV_LDS = 8 * IMG + 2 * 32 * AT * 4;
+
+__global__ __launch_bounds__(256) void attn_bwd_kv_kernel(
+    const uint16_t* __restrict__ Qp, const uint16_t* __restrict__ Kp,
+    const uint16_t* __restrict__ Vp, long long ld, long long sb, int hw, float scale,
+    const uint16_t* __restrict__ dOb, const float* __restrict__ lse, const float* __restrict__ D,
+    float* __restrict__ dK, float* __restrict__ dV, long long ldg, long long sbg,
+    uint16_t* __restrict__ dS) {
+  const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE, lr = lane & 31, h = lane >> 5;
+  const int nt = (hw + 31) / 32, kp = 32 * nt, np = (nt + 1) / 2;
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = wid / np, kk = w >> 1, half = w & 1, kt = 2 * (wid % np) + kk;
+  const uint16_t* Qb = Qp + b * sb;
+  const uint16_t* dOs = dOb + (long long)b * hw * AD;
+  const uint32_t KI = kk * 2 * IMG, VI = KI + IMG, ST = 4 * IMG, LS = 8 * IMG;
+  const int key = 32 * kt + lr;
+  const bool kv = key < hw;
+
+  // Kr / V tiles of both key tiles (wave w: tile w >> 1, Kr if w even), then
+  // query-tile stage 0
+  dma_tile((half ? Vp : Kp) + b * sb, ld, 32 * kt, kt < nt ? hw : 0, KI + half * IMG, 0, 1, lane);
+  auto issue = [&](int qt) {
+    const uint32_t base = ST + (qt & 1) * 2 * IMG;
+    dma_tile(Qb, ld, 32 * qt, hw, base, w, 4, lane);
+    dma_tile(dOs, AD, 32 * qt, hw, base + IMG, w, 4, lane);
+  };
+  issue(0);
+  for (int i = tid; i < 32 * nt; i += 256) {
+    lds_stf(LS + i * 4, i < hw ? lse[(long long)b * hw + i] : 0.f);
+    lds_stf(LS + (32 * AT + i) * 4, i < hw ? D[(long long)b * hw + i] : 0.f);
+  }
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[t][r] = dv[t][r] = 0.f;
+  // the key tile's Kr / V operand fragments, held for the whole loop
+  bf16x8 kf[AD / 16], vf[AD / 16];
+
+  for (int qt = 0; qt < nt; ++qt) {
+    // every outstanding op of this wave is this stage's DMA or older
+    ring_barrier<0>();
+    if (qt == 0) {
+#pragma unroll
+      for (int s = 0; s < AD / 16; ++s) {
+        kf[s] = frag(KI, s, lane);
+        vf[s] = frag(VI, s, lane);
+      }
+    }
+    if (qt + 1 < nt) issue(qt + 1);
+    const uint32_t QI = ST + (qt & 1) * 2 * IMG, OI = QI + IMG;
+    f32x16 sacc, pacc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[r] = pacc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < AD / 16; ++s) {
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(QI, s, lane), kf[s], sacc, 0, 0, 0);
+      pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(OI, s, lane), vf[s], pacc, 0, 0, 0);
+    }
+    // lane: key column; register r: query 32 qt + acc_row(r, h)
+    float pv[16], ds[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qq = 32 * qt + acc_row(r, h);
+      const bool ok = kv && qq < hw;
+      const float l = lds_ldf(LS + qq * 4), dd = lds_ldf(LS + (32 * AT + qq) * 4);
+      pv[r] = ok ? __builtin_amdgcn_exp2f((sacc[r] * scale - l) * 1.4426950408889634f) : 0.f;
+      ds[r] = pv[r] * (pacc[r] - dd) * scale;
+    }
+    if (half == 0 && kt < nt) {
+      uint16_t* dsb = dS + ((long long)b * hw) * kp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qq = 32 * qt + acc_row(r, h);
+        if (qq < hw) dsb[(long long)qq * kp + key] = bf_bits(ds[r]);
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      uint32_t up[4], us[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        up[j] = pk_bf16(pv[8 * s2 + 2 * j], pv[8 * s2 + 2 * j + 1]);
+        us[j] = pk_bf16(ds[8 * s2 + 2 * j], ds[8 * s2 + 2 * j + 1]);
+      }
+      const bf16x8 pa = as_bf8(make_uint4(up[0], up[1], up[2], up[3]));
+      const bf16x8 sa = as_bf8(make_uint4(us[0], us[1], us[2], us[3]));
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int c0 = 128 * half + 32 * t;
+        const bf16x8 obf = trf(OI, 16 * s2 + 4 * h, 16 * s2 + 8 + 4 * h, c0, lane);
+        const bf16x8 qbf = trf(QI, 16 * s2 + 4 * h, 16 * s2 + 8 + 4 * h, c0, lane);
+        mma_agpr<MODE_BF16>(dv[t], pa, pa, obf, obf);
+        mma_agpr<MODE_BF16>(dk[t], sa, sa, qbf, qbf);
+      }
+    }
+  }
+  mfma_drain();
+  if (kt >= nt) return;
+  // lane: column 128 half + 32 t + lr; register r: key 32 kt + acc_row(r, h)
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kq = 32 * kt + acc_row(r, h);
+      if (kq < hw) {
+        const long long o = b * sbg + (long long)kq * ldg + 128 * half + 32 * t + lr;
+        dK[o] = dk[t][r];
+        dV[o] = dv[t][r];
+      }
+    }
+}
+
+// dQr = dS Kr: one 2-wave workgroup per (sample, pair of query tiles), the Kr
+// tiles through a DMA ring (rolled loop); each wave's dS rows are staged in
+// LDS first (464-B rows: conflict-free ds_read_b128).
+constexpr int Q_NS = 7;
+constexpr int DS_PITCH = 464;
+constexpr int Q_LDS = Q_NS * IMG + 2 * 32 * DS_PITCH;
+
+__global__ __launch_bounds__(128) void attn_bwd_q_kernel(const uint16_t* __restrict__ Kp,
+                                                         long long ld, long long sb, int hw,
+                                                         const uint16_t* __restrict__ dS,
+                                                         float* __restrict__ dQ, long long ldg,
+                                                         long long sbg) {
+  const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE, lr = lane & 31, h = lane >> 5;
+  const int nt = (hw + 31) / 32, kp = 32 * nt, np = (nt + 1) / 2;
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = wid / np, qt = 2 * (wid % np) + w;
+  const uint16_t* Kb = Kp + b * sb;
+  const uint32_t dsimg = Q_NS * IMG + w * 32 * DS_PITCH;
+  // this wave's 32 dS rows (kp bf16 each) -> LDS; plain loads, drained before
+  // the ring starts so its counted waits see only DMA
+  for (int i = lane; i < 32 * (kp / 8); i += 64) {
+    const int r = i / (kp / 8), c8 = i % (kp / 8), q = 32 * qt + r;
+    const uint4 v = q < hw ? *(const uint4*)(dS + ((long long)b * hw + q) * kp + 8 * c8)
+                           : make_uint4(0, 0, 0, 0);
+    lds_st16(dsimg + r * DS_PITCH + 16 * c8, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  f32x16 acc[AD / 32];
+#pragma unroll
+  for (int t = 0; t < AD / 32; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  for (int st = 0; st < Q_NS - 1 && st < nt; ++st)
+    dma_tile(Kb, ld, 32 * st, hw, st * IMG, w, 2, lane);
+  for (int kt = 0; kt < nt; ++kt) {
+    ring_wait8(min(Q_NS - 2, nt - 1 - kt));
+    if (kt + Q_NS - 1 < nt)
+      dma_tile(Kb, ld, 32 * (kt + Q_NS - 1), hw, ((kt + Q_NS - 1) % Q_NS) * IMG, w, 2, lane);
+    const uint32_t buf = (kt % Q_NS) * IMG;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 a = as_bf8(lds_ld16(dsimg + lr * DS_PITCH + 2 * (32 * kt + 16 * s2 + 8 * h)));
+#pragma unroll
+      for (int t = 0; t < AD / 32; ++t) {
+        const bf16x8 kb = trf(buf, 16 * s2 + 8 * h, 16 * s2 + 8 * h + 4, 32 * t, lane);
+        mma_agpr<MODE_BF16>(acc[t], a, a, kb, kb);
+      }
+    }
+  }
+  mfma_drain();
+  if (qt >= nt) return;
+#pragma unroll
+  for (int t = 0; t < AD / 32; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qq = 32 * qt + acc_row(r, h);
+      if (qq < hw) dQ[b * sbg + (long long)qq * ldg + 32 * t + lr] = acc[t][r];
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -71,6 +484,59 @@ int tgfr_attn_softmax_bwd(const float* P, const float* dP, float* dS, long long 
   if (rows <= 0 || n <= 0) return 1001;
   hipLaunchKernelGGL(attn_softmax_bwd_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
                      (hipStream_t)stream, P, dP, dS, rows, n, ld, scale);
+  return (int)hipGetLastError();
+}
+
+// Fused IMIM self-attention (bf16 operands, fp32 accumulate): Qr, Kr, V are
+// [B][hw][256] bf16 views (row stride ld, sample stride sb, 16-B aligned
+// rows) -- the column slices of the packed projection; O [B][hw][256] fp32
+// (ldo, sbo); lse [B*hw].
+int tgfr_attn_fwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long long ld,
+                  long long sb, int B, int hw, float scale, float* O, long long ldo,
+                  long long sbo, float* lse, void* stream) {
+  if (B <= 0 || hw <= 0 || hw > 32 * AT || (ld & 7) || (sb & 7) || (ldo & 3)) return 1001;
+  if (((uintptr_t)Q | (uintptr_t)K | (uintptr_t)V | (uintptr_t)O) & 15) return 1001;
+  const int np = ((hw + 31) / 32 + 1) / 2;
+  if (const int e = set_max_lds((const void*)attn_fwd_kernel, FWD_LDS)) return e;
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * np), dim3(128), FWD_LDS, (hipStream_t)stream, Q, K,
+                     V, ld, sb, hw, scale, O, ldo, sbo, lse);
+  return (int)hipGetLastError();
+}
+
+int tgfr_attn_bwd_ws(int B, int hw, long long* bytes) {
+  if (B <= 0 || hw <= 0 || !bytes) return 1001;
+  const long long rows = (long long)B * hw, kp = 32LL * ((hw + 31) / 32);
+  // D (fp32), dO (bf16), dS (bf16), each 16-B aligned
+  *bytes = (rows * 4 + 15) / 16 * 16 + rows * AD * 2 + rows * kp * 2;
+  return 0;
+}
+
+// Gradients into dQ / dK / dV [B][hw][256] fp32 (ldg, sbg; typically the
+// column slices of one packed [B][hw][768] gradient), overwritten.  O and dO
+// dense fp32 [B][hw][256].
+int tgfr_attn_bwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long long ld,
+                  long long sb, int B, int hw, float scale, const float* O, const float* dO,
+                  long long ldo, long long sbo, const float* lse, float* dQ, float* dK,
+                  float* dV, long long ldg, long long sbg, void* ws, void* stream) {
+  if (B <= 0 || hw <= 0 || hw > 32 * AT || (ld & 7) || (sb & 7) || !ws) return 1001;
+  if (ldo != AD || sbo != (long long)hw * AD) return 1001;     // dO / O dense rows
+  if (((uintptr_t)Q | (uintptr_t)K | (uintptr_t)V | (uintptr_t)O | (uintptr_t)dO |
+       (uintptr_t)ws) & 15)
+    return 1001;
+  const int nt = (hw + 31) / 32, np = (nt + 1) / 2;
+  auto* s = (hipStream_t)stream;
+  const long long rows = (long long)B * hw;
+  float* D = (float*)ws;
+  auto* dOb = (uint16_t*)((char*)ws + (rows * 4 + 15) / 16 * 16);
+  uint16_t* dS = dOb + rows * AD;
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, dO,
+                     O, (long long)AD, rows, D, dOb);
+  if (const int e = set_max_lds((const void*)attn_bwd_kv_kernel, KV_LDS)) return e;
+  hipLaunchKernelGGL(attn_bwd_kv_kernel, dim3(B * np), dim3(256), KV_LDS, s, Q, K, V, ld, sb, hw,
+                     scale, dOb, lse, D, dK, dV, ldg, sbg, dS);
+  if (const int e = set_max_lds((const void*)attn_bwd_q_kernel, Q_LDS)) return e;
+  hipLaunchKernelGGL(attn_bwd_q_kernel, dim3(B * np), dim3(128), Q_LDS, s, K, ld, sb, hw, dS, dQ,
+                     ldg, sbg);
   return (int)hipGetLastError();
 }
 

@@ -489,7 +489,7 @@ __device__ __forceinline__ void wres_load_b(const float* __restrict__ B, long lo
   }
 }
 
-template <int K>
+template <int K, bool OBF = false>
 __global__ __launch_bounds__(64 * WR_NW) void bgemm_wres_kernel(
     const float* __restrict__ A, long long sAm, const float* __restrict__ B, long long sBk,
     long long sBn, float* __restrict__ Cm, long long sCm, long long sCn, int M, int N,
@@ -571,8 +571,14 @@ __global__ __launch_bounds__(64 * WR_NW) void bgemm_wres_kernel(
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const int m = m0 + wm * 32 + acc_row(q, lane >> 5);
-            const float v = alpha * acc[j][q] + bcol[j];
-            if (m < M) Cm[m * sCm + n * sCn] = relu ? fmaxf(v, 0.f) : v;
+            float v = alpha * acc[j][q] + bcol[j];
+            v = relu ? fmaxf(v, 0.f) : v;
+            if (m < M) {
+              if constexpr (OBF)
+                ((uint16_t*)Cm)[m * sCm + n * sCn] = bf_bits(v);   // bf16 output image
+              else
+                Cm[m * sCm + n * sCn] = v;
+            }
           }
         }
 #pragma unroll
@@ -695,6 +701,28 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
                        slab, ksplit, TM, TN, (int)grid.y, (int)grid.x, tiles, C, sCb, sCm, sCn,
                        M, N, alpha, accumulate, bias, relu);
   }
+  return (int)hipGetLastError();
+}
+
+// C = A W^T + bias with a bf16 output (the packed attention projection of
+// IMIM in bf16 mode, read by tgfr_attn_fwd / _bwd as bf16): A [M][K] fp32
+// rows (K = 128 or 256, 16-B aligned, sAm % 4 == 0), W [N][K] fp32
+// (row stride sWn), C [M][N] bf16 (row stride sCm).
+int tgfr_linear_bf16out(const float* A, long long sAm, int M, int K, const float* W,
+                        long long sWn, const float* bias, int N, uint16_t* C, long long sCm,
+                        void* stream) {
+  if (M <= 0 || N <= 0 || (K != 128 && K != 256) || !dma_ok(A, LAY_K, 0, sAm, 1, M, K, 1) ||
+      !al16(W) || (sWn & 3))
+    return 1001;
+  const int n_slices = (N + WR_TN - 1) / WR_TN;
+  const int m_tiles = (M + WR_TM - 1) / WR_TM;
+  const int per_slice = std::max(1, std::min(m_tiles, 256 / n_slices));
+  const int lds = WR_TN * K * 2 + WR_NS * WR_STG;
+  auto fn = K == 256 ? &bgemm_wres_kernel<256, true> : &bgemm_wres_kernel<128, true>;
+  if (const int e = set_max_lds((const void*)fn, lds)) return e;
+  hipLaunchKernelGGL(fn, dim3(n_slices * per_slice), dim3(64 * WR_NW), lds, (hipStream_t)stream,
+                     A, sAm, W, (long long)1, sWn, (float*)C, sCm, (long long)1, M, N, 1.f, bias,
+                     0, n_slices, per_slice);
   return (int)hipGetLastError();
 }
 

@@ -499,6 +499,83 @@ def attention_core(px, py, cq, ck, cv, scale, mode="fp32"):
 
 
 # ------------------------------------------------- batch norm -> linear ---
+def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf16=False):
+    """BatchNorm2d (batch or running statistics) folded into the following
+    1x1 projection; returns y [N, HW, O] (fp32, or bf16 with out_bf16) and
+    stores what _bn_linear_bwd needs on ctx."""
+    n, c, h, w_ = x.shape
+    hw, o = h * w_, weight.shape[0]
+    x = x.float().contiguous()
+    dev = x.device
+    mean = torch.empty(c, dtype=torch.float32, device=dev)
+    rstd = torch.empty_like(mean)
+    xhat = torch.empty(n, hw, c, dtype=torch.float32, device=dev)
+    track = training and bn.track_running_stats and bn.running_mean is not None
+    if training and track and bn.momentum is None:
+        raise NotImplementedError("cumulative-average BatchNorm (momentum=None)")
+    use_batch = training or bn.running_mean is None
+    call("tgfr_bn_fwd_cl", ptr(x), n, c, hw, float(bn.eps),
+         float(bn.momentum or 0.0), int(use_batch),
+         ptr(bn.running_mean) if (track or not use_batch) else None,
+         ptr(bn.running_var) if (track or not use_batch) else None,
+         ptr(bn.num_batches_tracked) if track else None, ptr(mean), ptr(rstd), ptr(xhat),
+         _hip.stream())
+    w2 = weight.reshape(o, c).float().contiguous()
+    g = gamma.float().contiguous()
+    wf = torch.empty_like(w2)
+    bf = torch.empty(o, dtype=torch.float32, device=dev)
+    call("tgfr_bn_fold", ptr(w2), ptr(None if bias is None else bias.float().contiguous()),
+         o, c, ptr(g), ptr(beta.float().contiguous()), ptr(wf), ptr(bf), _hip.stream())
+    rows = n * hw
+    if out_bf16:
+        y = torch.empty(rows, o, dtype=torch.int16, device=dev)
+        call("tgfr_linear_bf16out", ptr(xhat), c, rows, c, ptr(wf), c, ptr(bf), o, ptr(y), o,
+             _hip.stream())
+    else:
+        mb = -(-rows // 64) * -(-o // 64)
+        y = bgemm(xhat.view(1, rows, c), wf.t().unsqueeze(0), bias=bf, mode=mode,
+                  ksplit=_ksplit(c, mb))[0]
+    ctx.bn_saved = (xhat, w2, wf, g, beta.float().contiguous(), rstd)
+    ctx.bn_cfg = (mode, bias is not None, x.shape, weight.shape, use_batch)
+    return y.view(n, hw, o)
+
+
+def _bn_linear_bwd(ctx, dy, want_dx):
+    """(dx, dgamma, dbeta, dweight, dbias) of _bn_linear_fwd given dy [N, HW, O]."""
+    xhat, w2, wf, g, bt, rstd = ctx.bn_saved
+    mode, has_bias, xshape, wshape, use_batch = ctx.bn_cfg
+    n, hw, c = xhat.shape
+    o = w2.shape[0]
+    rows = n * hw
+    dp = dy.reshape(rows, o).float()
+    if dp.stride(1) != 1 or dp.stride(0) != o:
+        dp = dp.contiguous()
+    dev = dp.device
+    s = torch.empty(o, dtype=torch.float32, device=dev)
+    ws = torch.empty(-(-rows // 128) * o, dtype=torch.float32, device=dev)
+    call("tgfr_bias_grad", ptr(dp), o, rows, o, None, 0, None, 0, ptr(s), ptr(ws),
+         ptr(_hip.counters(dev)), _hip.stream())
+    mb = -(-o // 64) * -(-c // 64)
+    gm = bgemm(dp.t().unsqueeze(0), xhat.view(1, rows, c), mode=mode,
+               ksplit=_ksplit(rows, mb))[0]
+    dw = torch.empty_like(w2)
+    dgamma = torch.empty(c, dtype=torch.float32, device=dev)
+    dbeta = torch.empty_like(dgamma)
+    uws = torch.empty(2 * -(-o // 64) * c, dtype=torch.float32, device=dev)
+    call("tgfr_bn_unfold", ptr(gm), ptr(s), ptr(w2), o, c, ptr(g), ptr(bt), ptr(dw),
+         ptr(dgamma), ptr(dbeta), ptr(uws), ptr(_hip.counters(dev)), _hip.stream())
+    dx = None
+    if want_dx:
+        # d xhat = dp W'; BN input gradient (only when the map itself is trained)
+        dxh = bgemm(dp.unsqueeze(0), wf.unsqueeze(0), mode=mode)[0].view(n, hw, c)
+        if use_batch:
+            m1 = dxh.mean((0, 1))
+            m2 = (dxh * xhat).mean((0, 1))
+            dxh = dxh - m1 - xhat * m2
+        dx = (dxh * rstd).permute(0, 2, 1).reshape(xshape)
+    return dx, dgamma, dbeta, dw.reshape(wshape), (s if has_bias else None)
+
+
 class BNLinear(torch.autograd.Function):
     """y[n, hw] = W bn(x)[n, :, hw] + b for x [N, C, H, W] (NCHW), returned
     channels-last [N, HW, O]: nn.BatchNorm2d followed by a 1x1 projection
@@ -507,72 +584,56 @@ class BNLinear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, weight, bias, bn, training, mode):
-        n, c, h, w_ = x.shape
-        hw, o = h * w_, weight.shape[0]
-        x = x.float().contiguous()
-        dev = x.device
-        mean = torch.empty(c, dtype=torch.float32, device=dev)
-        rstd = torch.empty_like(mean)
-        xhat = torch.empty(n, hw, c, dtype=torch.float32, device=dev)
-        track = training and bn.track_running_stats and bn.running_mean is not None
-        if training and track and bn.momentum is None:
-            raise NotImplementedError("cumulative-average BatchNorm (momentum=None)")
-        use_batch = training or bn.running_mean is None
-        call("tgfr_bn_fwd_cl", ptr(x), n, c, hw, float(bn.eps),
-             float(bn.momentum or 0.0), int(use_batch),
-             ptr(bn.running_mean) if (track or not use_batch) else None,
-             ptr(bn.running_var) if (track or not use_batch) else None,
-             ptr(bn.num_batches_tracked) if track else None, ptr(mean), ptr(rstd), ptr(xhat),
-             _hip.stream())
-        w2 = weight.reshape(o, c).float().contiguous()
-        g = gamma.float().contiguous()
-        wf = torch.empty_like(w2)
-        bf = torch.empty(o, dtype=torch.float32, device=dev)
-        call("tgfr_bn_fold", ptr(w2), ptr(None if bias is None else bias.float().contiguous()),
-             o, c, ptr(g), ptr(beta.float().contiguous()), ptr(wf), ptr(bf), _hip.stream())
-        rows = n * hw
-        mb = -(-rows // 64) * -(-o // 64)
-        y = bgemm(xhat.view(1, rows, c), wf.t().unsqueeze(0), bias=bf, mode=mode,
-                  ksplit=_ksplit(c, mb))[0]
-        ctx.save_for_backward(xhat, w2, wf, g, beta.float().contiguous(), rstd)
-        ctx.cfg = (mode, bias is not None, x.shape, weight.shape, use_batch)
-        return y.view(n, hw, o)
+        return _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode)
 
     @staticmethod
     def backward(ctx, dy):
-        xhat, w2, wf, g, bt, rstd = ctx.saved_tensors
-        mode, has_bias, xshape, wshape, use_batch = ctx.cfg
-        n, hw, c = xhat.shape
-        o = w2.shape[0]
-        rows = n * hw
-        dp = dy.reshape(rows, o).float()
-        if dp.stride(1) != 1 or dp.stride(0) != o:
-            dp = dp.contiguous()
-        dev = dp.device
-        s = torch.empty(o, dtype=torch.float32, device=dev)
-        ws = torch.empty(-(-rows // 128) * o, dtype=torch.float32, device=dev)
-        call("tgfr_bias_grad", ptr(dp), o, rows, o, None, 0, None, 0, ptr(s), ptr(ws),
-             ptr(_hip.counters(dev)), _hip.stream())
-        mb = -(-o // 64) * -(-c // 64)
-        gm = bgemm(dp.t().unsqueeze(0), xhat.view(1, rows, c), mode=mode,
-                   ksplit=_ksplit(rows, mb))[0]
-        dw = torch.empty_like(w2)
-        dgamma = torch.empty(c, dtype=torch.float32, device=dev)
-        dbeta = torch.empty_like(dgamma)
-        uws = torch.empty(2 * -(-o // 64) * c, dtype=torch.float32, device=dev)
-        call("tgfr_bn_unfold", ptr(gm), ptr(s), ptr(w2), o, c, ptr(g), ptr(bt), ptr(dw),
-             ptr(dgamma), ptr(dbeta), ptr(uws), ptr(_hip.counters(dev)), _hip.stream())
-        dx = None
-        if ctx.needs_input_grad[0]:
-            # d xhat = dp W'; BN input gradient (only when the map itself is trained)
-            dxh = bgemm(dp.unsqueeze(0), wf.unsqueeze(0), mode=mode)[0].view(n, hw, c)
-            if use_batch:
-                m1 = dxh.mean((0, 1))
-                m2 = (dxh * xhat).mean((0, 1))
-                dxh = dxh - m1 - xhat * m2
-            dx = (dxh * rstd).permute(0, 2, 1).reshape(xshape)
-        return (dx, dgamma, dbeta, dw.reshape(wshape), s if has_bias else None, None, None,
-                None)
+        return _bn_linear_bwd(ctx, dy, ctx.needs_input_grad[0]) + (None, None, None)
+
+
+class ImimAttention(torch.autograd.Function):
+    """IMIM's bn_img -> SelfAttention (models/models.py:397-398,
+    fusion_nets.py:93-118) in bf16 mode as one autograd node: BN folded into
+    the packed [Qr | Kr | V] projection, which is written in bf16 and read in
+    place by the fused attention kernels (tgfr_attn_fwd / _bwd); the packed
+    projection never exists in fp32.  Returns O [N, HW, 256] fp32."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, weight, bias, bn, training, scale):
+        px = _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, "bf16",
+                            out_bf16=True)
+        nb, hw, _ = px.shape
+        o = torch.empty(nb, hw, 256, dtype=torch.float32, device=px.device)
+        lse = torch.empty(nb * hw, dtype=torch.float32, device=px.device)
+        call("tgfr_attn_fwd", ptr(px), ptr(px[..., 256:]), ptr(px[..., 512:]), px.stride(1),
+             px.stride(0), nb, hw, float(scale), ptr(o), o.stride(1), o.stride(0), ptr(lse),
+             _hip.stream())
+        ctx.save_for_backward(px, o, lse)
+        ctx.scale = float(scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        px, o, lse = ctx.saved_tensors
+        nb, hw, _ = px.shape
+        do = do.float().contiguous()
+        out = (ctypes.c_longlong * 1)()
+        rc = _hip.lib().tgfr_attn_bwd_ws(nb, hw, ctypes.addressof(out))
+        if rc != 0:
+            raise RuntimeError(f"tgfr_attn_bwd_ws failed with code {rc}")
+        ws = torch.empty(int(out[0]), dtype=torch.uint8, device=px.device)
+        dpx = torch.empty(nb, hw, 768, dtype=torch.float32, device=px.device)
+        call("tgfr_attn_bwd", ptr(px), ptr(px[..., 256:]), ptr(px[..., 512:]), px.stride(1),
+             px.stride(0), nb, hw, ctx.scale, ptr(o), ptr(do), do.stride(1), do.stride(0),
+             ptr(lse), ptr(dpx), ptr(dpx[..., 256:]), ptr(dpx[..., 512:]), dpx.stride(1),
+             dpx.stride(0), ptr(ws), _hip.stream())
+        return _bn_linear_bwd(ctx, dpx, ctx.needs_input_grad[0]) + (None, None, None)
+
+
+def imim_attention(x, bn, weight, bias, scale):
+    """bf16 mode: bn -> packed q/k/v projection (weight [768, 256], bias) ->
+    fused self-attention; returns O [N, HW, 256]."""
+    return ImimAttention.apply(x, bn.weight, bn.bias, weight, bias, bn, bn.training, scale)
 
 
 def bn_linear(x, bn, weight, bias, mode="fp32"):

@@ -59,8 +59,12 @@ class IMIM(nn.Module):
         n, c, h, w = img.shape
         # bn_img folded into the packed q/k/v projection of the self-attention
         wq, bq = self.sa.packed_self()
-        px = K.bn_linear(img, self.bn_img, wq, bq, mode=self.precision)   # [B, HW, 3C]
-        z = self.sa.core_self(px)
+        if self.precision == "bf16" and c == 256 and h * w <= 224:
+            # packed projection in bf16 straight into the fused attention kernels
+            z = K.imim_attention(img, self.bn_img, wq, bq, 1.0 / float(self.sa.sqrt_dim))
+        else:
+            px = K.bn_linear(img, self.bn_img, wq, bq, mode=self.precision)   # [B, HW, 3C]
+            z = self.sa.core_self(px)
         # LayerNorm over (C, H, W) of each sample == over the channels-last
         # [HW, C] rows; the [C, H, W] affine maps are read channel-major in place
         z = K.layer_norm_rows(z, self.ln.weight, self.ln.bias, self.ln.eps, ch=c)

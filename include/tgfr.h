@@ -92,6 +92,26 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 long long s_r, long long s_d, float* ws, unsigned* counters, int bounded,
                 int t_pad, int mode, void* stream);
 
+/* Standalone func_attention (models/attention.py:10-43), exact fp32, one
+ * workgroup per sample (R = ih*iw <= 256, T <= 64, D <= 256):
+ *   S = ctx^T q, A1 = softmax_T(S), A2 = softmax_R(gamma1 A1^T), C = ctx A2^T.
+ * query element (b, d, t) at q[b*qsb + d*qsd + t*qst]; context (b, d, r) at
+ * ctx[b*csb + d*csd + r*csr]; C at the given strides; A1 [B][R][T] (kept for
+ * the backward) and attn = A2 [B][T][R] dense.  The backward takes dC (any
+ * strides) and dattn ([B][T][R] dense, nullable) and overwrites dq [B][D][T]
+ * and dctx [B][D][R] (dense).  The trainers reach this arithmetic through
+ * tgfr_wr_fwd/_bwd; this is the per-call API. */
+int tgfr_func_attention_fwd(const float* q, long long qsb, long long qsd, long long qst,
+                            const float* ctx, long long csb, long long csd, long long csr, int B,
+                            int D, int T, int R, float gamma1, float* C, long long Csb,
+                            long long Csd, long long Cst, float* A1, float* attn, void* stream);
+int tgfr_func_attention_bwd(const float* q, long long qsb, long long qsd, long long qst,
+                            const float* ctx, long long csb, long long csd, long long csr,
+                            const float* dC, long long dsb, long long dsd, long long dst,
+                            const float* dattn, int B, int D, int T, int R, float gamma1,
+                            const float* A1, const float* attn, float* dq, float* dctx,
+                            void* stream);
+
 /* Dynamic LDS bytes of the streaming forward (which = 0), the fp32-mode
  * backward (1) and the resident-R bf16 forward (2). */
 int tgfr_wr_lds_bytes(int which);

@@ -89,3 +89,46 @@ def test_self_attention_golden_bf16(gpu):
     assert _frob(x.grad, t(g["d_x"]).to(gpu)) < 2e-2
     assert _frob(m.value_proj.weight.grad, t(g["d_v_w"]).to(gpu)) < 2e-2
     assert _frob(m.query_proj.weight.grad, t(g["d_q_w"]).to(gpu)) < 2e-2
+
+
+@pytest.mark.parametrize("tag", ["small", "t22"])
+def test_func_attention_golden(gpu, tag):
+    """Standalone func_attention (csrc/tgfr_fa.hip, exact fp32) against the
+    reference's fixtures (weighted context, attn, d_context through the
+    probe) and the oracle's query gradient: 1e-5 / 1e-5 / 1e-4 absolute."""
+    import numpy as np
+    from conftest import load_golden, t
+    from text_guided_face_recognition_amd.models.attention import func_attention
+    import oracle.tgfr_oracle as O
+    g = load_golden(f"func_attention_{tag}")
+    q = t(g["query"]).to(gpu).requires_grad_()
+    ctx = t(g["context"]).to(gpu).requires_grad_()
+    wc, attn = func_attention(q, ctx, float(g["gamma1"]))
+    assert np.abs(wc.detach().cpu().numpy() - g["weighted"]).max() < 1e-5
+    assert np.abs(attn.detach().cpu().numpy() - g["attn"]).max() < 1e-5
+    (wc * t(g["probe"]).to(gpu)).sum().backward()
+    assert np.abs(ctx.grad.cpu().numpy() - g["d_context"]).max() < 1e-4
+    qo = t(g["query"]).requires_grad_()
+    wo, _ = O.func_attention(qo, t(g["context"]), float(g["gamma1"]))
+    (wo * t(g["probe"])).sum().backward()
+    assert np.abs(q.grad.cpu().numpy() - qo.grad.numpy()).max() < 1e-4
+
+
+def test_func_attention_attn_grad(gpu):
+    """Gradient through the returned attention map as well (dattn path):
+    against torch fp32 autograd of the oracle on the GPU, 1e-4 relative."""
+    import oracle.tgfr_oracle as O
+    from text_guided_face_recognition_amd.models.attention import func_attention
+    g = torch.Generator(device="cuda").manual_seed(3)
+    q = torch.randn(3, 64, 17, generator=g, device="cuda")
+    c = torch.randn(3, 64, 7, 9, generator=g, device="cuda")
+    pw = torch.randn(3, 64, 17, generator=g, device="cuda")
+    pa = torch.randn(3, 17, 7, 9, generator=g, device="cuda")
+    outs = []
+    for fn in (func_attention, O.func_attention):
+        qq, cc = q.clone().requires_grad_(), c.clone().requires_grad_()
+        w, a = fn(qq, cc, 4.0)
+        ((w * pw).sum() + (a * pa).sum()).backward()
+        outs.append((w.detach(), a.detach(), qq.grad, cc.grad))
+    for x, y in zip(*outs):
+        assert float((x - y).abs().max() / y.abs().max()) < 1e-4

@@ -62,6 +62,9 @@ SIGNATURES = {
     "tgfr_bias_grad": [P, L, I, I, P, L, P, L, P, P, P, P],
     "tgfr_ln_fwd": [P, I, L, P, P, F, I, P, P, P],
     "tgfr_ln_bwd": [P, P, I, L, P, I, P, P, P, P, P],
+    "tgfr_func_attention_fwd": [P, L, L, L, P, L, L, L, I, I, I, I, F, P, L, L, L, P, P, P],
+    "tgfr_func_attention_bwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, I, I, I, I, F, P, P, P,
+                                P, P],
     "tgfr_tail_pack_elems": [],
     "tgfr_tail_pack": [P, P, P, P, P],
     "tgfr_tail_fwd": [P, L, I, P, P, P, P, F, P, L, P, P, P, P, P],

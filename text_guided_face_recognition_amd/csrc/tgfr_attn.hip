@@ -102,7 +102,8 @@ __device__ __forceinline__ void ring_wait8(int younger) {
     case 2: ring_barrier<16>(); break;
     case 3: ring_barrier<24>(); break;
     case 4: ring_barrier<32>(); break;
-    default: ring_barrier<40>(); break;
+    case 5: ring_barrier<40>(); break;
+    default: ring_barrier<48>(); break;
   }
 }
 
@@ -214,11 +215,10 @@ __global__ __launch_bounds__(128) void attn_fwd_kernel(const uint16_t* __restric
     // lazy rescale: the reference max m only moves when some query's tile
     // max exceeds it by more than 8 / c (P then stays <= 2^8, exact in the
     // fp32 sums and fine in bf16); otherwise O and l keep their scale and the
-    // 128-register rescale of O (AGPR read-modify-write) is skipped
+    // 128-register rescale of O is skipped
     if (kt == 0) {
       m = tmax;
     } else if (__builtin_amdgcn_ballot_w64((tmax - m) * c > 8.f)) {
-      mfma_drain();
       const float mn = fmaxf(m, tmax);
       const float alpha = __builtin_amdgcn_exp2f((m - mn) * c);
       m = mn;
@@ -250,11 +250,10 @@ __global__ __launch_bounds__(128) void attn_fwd_kernel(const uint16_t* __restric
 #pragma unroll
       for (int t = 0; t < AD / 32; ++t) {
         const bf16x8 va = trf(vbuf, 16 * s2 + 4 * h, 16 * s2 + 8 + 4 * h, 32 * t, lane);
-        mma_agpr<MODE_BF16>(oacc[t], va, va, pb[s2], pb[s2]);
+        oacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb[s2], oacc[t], 0, 0, 0);
       }
   }
   l = xhalf_sum(l);
-  mfma_drain();
   if (!active) return;
   const int q = 32 * qt + lr;
   if (q >= hw) return;
@@ -386,12 +385,11 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(
         const int c0 = 128 * half + 32 * t;
         const bf16x8 obf = trf(OI, 16 * s2 + 4 * h, 16 * s2 + 8 + 4 * h, c0, lane);
         const bf16x8 qbf = trf(QI, 16 * s2 + 4 * h, 16 * s2 + 8 + 4 * h, c0, lane);
-        mma_agpr<MODE_BF16>(dv[t], pa, pa, obf, obf);
-        mma_agpr<MODE_BF16>(dk[t], sa, sa, qbf, qbf);
+        dv[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, obf, dv[t], 0, 0, 0);
+        dk[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, qbf, dk[t], 0, 0, 0);
       }
     }
   }
-  mfma_drain();
   if (kt >= nt) return;
   // lane: column 128 half + 32 t + lr; register r: key 32 kt + acc_row(r, h)
 #pragma unroll
@@ -452,11 +450,10 @@ __global__ __launch_bounds__(128) void attn_bwd_q_kernel(const uint16_t* __restr
 #pragma unroll
       for (int t = 0; t < AD / 32; ++t) {
         const bf16x8 kb = trf(buf, 16 * s2 + 8 * h, 16 * s2 + 8 * h + 4, 32 * t, lane);
-        mma_agpr<MODE_BF16>(acc[t], a, a, kb, kb);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, kb, acc[t], 0, 0, 0);
       }
     }
   }
-  mfma_drain();
   if (qt >= nt) return;
 #pragma unroll
   for (int t = 0; t < AD / 32; ++t)

@@ -159,6 +159,53 @@ def word_region_logits(img_features, words, lens, gamma1, gamma2, gamma3,
                                   bool(bounded))
 
 
+# -------------------------------------------------------- func_attention ---
+class FuncAttention(torch.autograd.Function):
+    """models/attention.py:10-43 for matched query / context batches, exact
+    fp32 (tgfr_func_attention_fwd / _bwd), differentiable in both inputs."""
+
+    @staticmethod
+    def forward(ctx, query, context, gamma1):
+        b, d, t = query.shape
+        ih, iw = context.shape[2], context.shape[3]
+        r = ih * iw
+        q = query.float()
+        c = context.float().reshape(b, context.shape[1], r)
+        dev = q.device
+        out = torch.empty(b, d, t, dtype=torch.float32, device=dev)
+        a1 = torch.empty(b, r, t, dtype=torch.float32, device=dev)
+        attn = torch.empty(b, t, r, dtype=torch.float32, device=dev)
+        call("tgfr_func_attention_fwd", ptr(q), q.stride(0), q.stride(1), q.stride(2), ptr(c),
+             c.stride(0), c.stride(1), c.stride(2), b, d, t, r, float(gamma1), ptr(out),
+             out.stride(0), out.stride(1), out.stride(2), ptr(a1), ptr(attn), _hip.stream())
+        ctx.save_for_backward(q, c, a1, attn)
+        ctx.cfg = (float(gamma1), context.shape)
+        return out, attn.view(b, t, ih, iw)
+
+    @staticmethod
+    def backward(ctx, d_out, d_attn):
+        q, c, a1, attn = ctx.saved_tensors
+        gamma1, cshape = ctx.cfg
+        b, d, t = q.shape
+        r = c.shape[2]
+        if d_out is None:
+            d_out = torch.zeros_like(q)
+        d_out = d_out.float()
+        da = None if d_attn is None else d_attn.float().reshape(b, t, r).contiguous()
+        dq = torch.empty(b, d, t, dtype=torch.float32, device=q.device)
+        dc = torch.empty(b, d, r, dtype=torch.float32, device=q.device)
+        call("tgfr_func_attention_bwd", ptr(q), q.stride(0), q.stride(1), q.stride(2), ptr(c),
+             c.stride(0), c.stride(1), c.stride(2), ptr(d_out), d_out.stride(0),
+             d_out.stride(1), d_out.stride(2), ptr(da), b, d, t, r, gamma1, ptr(a1), ptr(attn),
+             ptr(dq), ptr(dc), _hip.stream())
+        return dq, dc.view(cshape), None
+
+
+def func_attention(query, context, gamma1):
+    """(weightedContext [B, D, T], attn [B, T, ih, iw]); device tensors only."""
+    return FuncAttention.apply(query, context, gamma1)
+
+
 # ------------------------------------------------------------ cos logits ---
 class CosLogits(torch.autograd.Function):
     """scale * cos(x_b, y_i) (or scale * x_b.y_i) for all pairs, optional

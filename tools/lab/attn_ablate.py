@@ -27,12 +27,13 @@ VARIANTS = {
     "f_stamps": [
         ("  const uint32_t qimg = w * IMG, ring = 2 * IMG;\n  const int n_st = 2 * nt;",
          "  const uint32_t qimg = w * IMG, ring = 2 * IMG;\n  const int n_st = 2 * nt;\n"
-         "  long long* stp = (long long*)lse + (long long)blockIdx.x * 16; int nst = 0;\n"
-         "  auto STAMP = [&]() { long long t = __builtin_amdgcn_s_memtime(); if (w == 0 && lane == nst) stp[nst] = t; ++nst; };\n"
+         "  long long* stp = (long long*)lse + (long long)blockIdx.x * 24; int nst = 0;\n"
+         "  auto STAMP = [&]() { long long t = __builtin_amdgcn_s_memtime(); if (w == 0 && lane == nst && nst < 24) stp[nst] = t; ++nst; };\n"
          "  STAMP();"),
         ("  wait(0);                                           // also covers the Qr tile",
          "  wait(0);                                           // also covers the Qr tile\n  STAMP();"),
-        ("    wait(sk + 1);", "    STAMP();\n    wait(sk + 1);\n    STAMP();"),
+        ("    if (kt > 0) {\n      wait(sk);", "    if (kt > 0) {\n      STAMP();\n      wait(sk);\n      STAMP();"),
+        ("    wait(sk + 1);", "    STAMP();\n    wait(sk + 1);"),
         ("  l = xhalf_sum(l);\n  mfma_drain();", "  STAMP();\n  l = xhalf_sum(l);\n  mfma_drain();"),
         ("  if (h == 0) lse[(long long)b * hw + q] = m * scale + __logf(l);", "  if (h == 0 && lse == nullptr) lse[0] = m;"),
     ],
@@ -106,19 +107,15 @@ if __name__ == "__main__":
         lib.tgfr_attn_fwd.argtypes = [P, P, P, L, L, I, I, F, P, L, L, P, P]
         px = torch.randn(nb, hw, 768, device="cuda").to(torch.bfloat16).view(torch.int16)
         o = torch.empty(nb, hw, 256, device="cuda")
-        lse = torch.zeros(nb * hw * 2, device="cuda")
+        lse = torch.zeros(nb * hw * 4, device="cuda")
         st = torch.cuda.current_stream().cuda_stream
         lib.tgfr_attn_fwd(px.data_ptr(), px[..., 256:].data_ptr(), px[..., 512:].data_ptr(), 768,
                           hw * 768, nb, hw, 0.0625, o.data_ptr(), 256, hw * 256, lse.data_ptr(), st)
         torch.cuda.synchronize()
-        t = lse.view(torch.int64)[:256 * 16].view(256, 16).cpu()
-        t0 = t[:, 0].min()
-        rel = (t - t0).float()
-        print("start spread", float(rel[:, 0].max()))
-        for wg in (0, 1, 100, 255):
-            print(wg, [int(x) for x in rel[wg, :16]])
-        d = (t[:, 1:16] - t[:, 0:15]).float().mean(0)
-        print("mean deltas", [round(float(x)) for x in d])
+        t = lse.view(torch.int64)[:256 * 24].view(256, 24).cpu()
+        d = (t[:, 1:20] - t[:, 0:19]).float()
+        print("median deltas", [round(float(x)) for x in d.median(0).values])
+        print("wg 1", [round(float(x)) for x in d[1]])
     elif args[0] == "sweep":
         so = build("base")
         for nb in (8, 16, 32, 64, 128):

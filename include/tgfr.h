@@ -92,6 +92,11 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 long long s_r, long long s_d, float* ws, unsigned* counters, int bounded,
                 int t_pad, int mode, void* stream);
 
+/* Verification pair scores (utils/modules.py:152-153): out[i] = x_i.y_i /
+ * max(|x_i| |y_i|, eps) for matched rows of x [rows][d] (ldx) and y (ldy). */
+int tgfr_pair_cosine(const float* x, long long ldx, const float* y, long long ldy, int rows,
+                     int d, float eps, float* out, void* stream);
+
 /* Standalone func_attention (models/attention.py:10-43), exact fp32, one
  * workgroup per sample (R = ih*iw <= 256, T <= 64, D <= 256):
  *   S = ctx^T q, A1 = softmax_T(S), A2 = softmax_R(gamma1 A1^T), C = ctx A2^T.

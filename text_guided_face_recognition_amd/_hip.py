@@ -62,6 +62,7 @@ SIGNATURES = {
     "tgfr_bias_grad": [P, L, I, I, P, L, P, L, P, P, P, P],
     "tgfr_ln_fwd": [P, I, L, P, P, F, I, P, P, P],
     "tgfr_ln_bwd": [P, P, I, L, P, I, P, P, P, P, P],
+    "tgfr_pair_cosine": [P, L, P, L, I, I, F, P, P],
     "tgfr_func_attention_fwd": [P, L, L, L, P, L, L, L, I, I, I, I, F, P, L, L, L, P, P, P],
     "tgfr_func_attention_bwd": [P, L, L, L, P, L, L, L, P, L, L, L, P, I, I, I, I, F, P, P, P,
                                 P, P],

@@ -326,6 +326,31 @@ __global__ void loss_mix_bwd_kernel(const float* __restrict__ g, MixArgs a, int 
   if (i < n) dloss[i] = g[0] * a.w[0][i];
 }
 
+// Verification score of a matched pair (utils/modules.py:152-153,
+// nn.CosineSimilarity(dim=1, eps)): x.y / max(|x| |y|, eps), one wave per row.
+__global__ __launch_bounds__(256) void pair_cosine_kernel(const float* __restrict__ x,
+                                                          long long ldx,
+                                                          const float* __restrict__ y,
+                                                          long long ldy, int rows, int d,
+                                                          float eps, float* __restrict__ out) {
+  const long long row = blockIdx.x * 4LL + threadIdx.x / WAVE;
+  const int lane = threadIdx.x % WAVE;
+  if (row >= rows) return;
+  const float* a = x + row * ldx;
+  const float* b = y + row * ldy;
+  float xy = 0.f, xx = 0.f, yy = 0.f;
+  for (int c = lane; c < d; c += WAVE) {
+    const float u = a[c], v = b[c];
+    xy = fmaf(u, v, xy);
+    xx = fmaf(u, u, xx);
+    yy = fmaf(v, v, yy);
+  }
+  xy = wave_sum(xy);
+  xx = wave_sum(xx);
+  yy = wave_sum(yy);
+  if (lane == 0) out[row] = xy / fmaxf(sqrtf(xx * yy), eps);
+}
+
 }  // namespace
 
 extern "C" {
@@ -335,6 +360,14 @@ int tgfr_l2norm_rows(const float* x, long long ldx, int rows, int d, float eps, 
   if (rows <= 0 || d <= 0) return 1001;
   hipLaunchKernelGGL(l2norm_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0,
                      (hipStream_t)stream, x, ldx, rows, d, eps, y, ldy, inv_norm);
+  return (int)hipGetLastError();
+}
+
+int tgfr_pair_cosine(const float* x, long long ldx, const float* y, long long ldy, int rows,
+                     int d, float eps, float* out, void* stream) {
+  if (rows <= 0 || d <= 0 || !x || !y || !out) return 1001;
+  hipLaunchKernelGGL(pair_cosine_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     x, ldx, y, ldy, rows, d, eps, out);
   return (int)hipGetLastError();
 }
 

@@ -199,17 +199,17 @@ int tgfr_attn_softmax_bwd(const float* P, const float* dP, float* dS, long long 
  * Q, K, V: [B][hw][256] bf16 views (row stride ld, sample stride sb, both
  * multiples of 8), e.g. the column slices of the packed projection
  * [B][hw][768] written by tgfr_linear_bf16out.  O: [B][hw][256] fp32 (ldo,
- * sbo).  The backward recomputes P from lse and writes dQ, dK, dV fp32 (ldg,
- * sbg; overwritten); dO and O must be dense [B][hw][256] fp32;
- * ws: tgfr_attn_bwd_ws bytes. */
+ * sbo).  The backward recomputes P from lse and writes dQ, dK, dV in bf16
+ * (ldg, sbg; overwritten: the operand of tgfr_dw_bf16); dO and O must be
+ * dense [B][hw][256] fp32; ws: tgfr_attn_bwd_ws bytes. */
 int tgfr_attn_fwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long long ld,
                   long long sb, int B, int hw, float scale, float* O, long long ldo,
                   long long sbo, float* lse, void* stream);
 int tgfr_attn_bwd_ws(int B, int hw, long long* bytes);
 int tgfr_attn_bwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long long ld,
                   long long sb, int B, int hw, float scale, const float* O, const float* dO,
-                  long long ldo, long long sbo, const float* lse, float* dQ, float* dK,
-                  float* dV, long long ldg, long long sbg, void* ws, void* stream);
+                  long long ldo, long long sbo, const float* lse, uint16_t* dQ, uint16_t* dK,
+                  uint16_t* dV, long long ldg, long long sbg, void* ws, void* stream);
 
 /* y = x / max(|x|, eps) per row (F.normalize; ProjectionHead models/models.py:119,
  * ArcMarginProduct models/metrics.py:44); inv_norm[row] = 1 / max(|x|, eps). */
@@ -285,6 +285,14 @@ int tgfr_tail_bwd(const float* dR, long long lddr, const float* R, long long ldr
                   const uint16_t* H2b, float* dZ, long long lddz, uint16_t* dPb, uint16_t* dH2b,
                   uint16_t* dH1b, void* stream);
 int tgfr_tail_dw_ws(int rows, long long* floats);
+/* Generic bf16 weight gradient of a row-wise linear map: dW [N][K] = X^T Y,
+ * db [N] = column sums of X, for dense X [rows][N] bf16 and Y [rows][K]
+ * (bf16, or fp32 when y_f32); N, K multiples of 128; fp32 outputs
+ * overwritten; ws: tgfr_dw_bf16_ws floats (row-slice partials, summed in
+ * slice order by a second launch). */
+int tgfr_dw_bf16_ws(int rows, int N, int K, long long* floats);
+int tgfr_dw_bf16(const uint16_t* X, const void* Y, int y_f32, int rows, int N, int K, float* dW,
+                 float* db, float* ws, void* stream);
 int tgfr_tail_dw(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
                  const uint16_t* H1b, const uint16_t* dH1b, const uint16_t* Zb, int rows,
                  float* dWp, float* dbp, float* dW2, float* db2, float* dW1, float* db1, float* ws,

@@ -36,11 +36,11 @@ def _attn(pxb, do, scale):
     out = (ctypes.c_longlong * 1)()
     assert _hip.lib().tgfr_attn_bwd_ws(nb, hw, ctypes.addressof(out)) == 0
     ws = torch.empty(int(out[0]), dtype=torch.uint8, device="cuda")
-    g = torch.empty(nb, hw, 768, device="cuda")
+    g = torch.empty(nb, hw, 768, dtype=torch.int16, device="cuda")      # bf16 gradients
     call("tgfr_attn_bwd", ptr(bits), ptr(bits[..., 256:]), ptr(bits[..., 512:]), 768, hw * 768,
          nb, hw, scale, ptr(o), ptr(do), 256, hw * 256, ptr(lse), ptr(g), ptr(g[..., 256:]),
          ptr(g[..., 512:]), 768, hw * 768, ptr(ws), _hip.stream())
-    return o, lse, g
+    return o, lse, (g.to(torch.int32) << 16).view(torch.float32)
 
 
 @pytest.mark.parametrize("nb,hw", [(64, 196), (3, 196), (2, 37), (1, 224), (4, 5), (5, 161)])

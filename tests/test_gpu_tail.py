@@ -141,3 +141,30 @@ def test_tail_deterministic():
     a, b = _run(*ins), _run(*ins)
     for n, x, y in zip(NAMES, a, b):
         assert torch.equal(x, y), n
+
+
+@pytest.mark.parametrize("rows,n,k,yf32", [(12544, 768, 256, True), (1000, 128, 384, False),
+                                           (37, 256, 128, True)])
+def test_dw_bf16_generic(rows, n, k, yf32):
+    """tgfr_dw_bf16 (the q/k/v projection's weight gradient): dW = X^T Y and
+    db = colsum(X) against torch on the same bf16-rounded operands, 1e-2 of
+    the max magnitude (fp32 accumulation in a different order)."""
+    from text_guided_face_recognition_amd import _hip
+    from text_guided_face_recognition_amd._hip import call, ptr
+    torch.backends.cuda.matmul.allow_tf32 = False
+    g = torch.Generator(device="cuda").manual_seed(rows + n)
+    x = torch.randn(rows, n, generator=g, device="cuda").to(torch.bfloat16)
+    y = torch.randn(rows, k, generator=g, device="cuda")
+    yb = y.to(torch.bfloat16)
+    import ctypes
+    out = (ctypes.c_longlong * 1)()
+    assert _hip.lib().tgfr_dw_bf16_ws(rows, n, k, ctypes.addressof(out)) == 0
+    ws = torch.empty(int(out[0]), device="cuda")
+    dw = torch.empty(n, k, device="cuda")
+    db = torch.empty(n, device="cuda")
+    yarg = y if yf32 else yb.view(torch.int16)
+    call("tgfr_dw_bf16", ptr(x.view(torch.int16)), ptr(yarg), int(yf32), rows, n, k, ptr(dw),
+         ptr(db), ptr(ws), _hip.stream())
+    ref = x.float().t() @ yb.float()
+    assert _maxrel(dw, ref) <= 1e-2
+    assert _maxrel(db, x.float().sum(0)) <= 1e-2

@@ -71,6 +71,8 @@ SIGNATURES = {
     "tgfr_tail_fwd": [P, L, I, P, P, P, P, F, P, L, P, P, P, P, P],
     "tgfr_tail_bwd": [P, L, P, L, P, I, F, P, P, P, P, L, P, P, P, P],
     "tgfr_tail_dw_ws": [I, P],
+    "tgfr_dw_bf16_ws": [I, I, I, P],
+    "tgfr_dw_bf16": [P, P, I, I, I, I, P, P, P, P],
     "tgfr_tail_dw": [P, P, P, P, P, P, I, P, P, P, P, P, P, P, P],
     "tgfr_optim_step": [P, I, P, I, P, P, P],
     "tgfr_arc_fwd": [P, L, I, I, P, L, I, P, F, F, I, F, P, P, P, P, P, P],

@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(
     const uint16_t* __restrict__ Qp, const uint16_t* __restrict__ Kp,
     const uint16_t* __restrict__ Vp, long long ld, long long sb, int hw, float scale,
     const uint16_t* __restrict__ dOb, const float* __restrict__ lse, const float* __restrict__ D,
-    float* __restrict__ dK, float* __restrict__ dV, long long ldg, long long sbg,
+    uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, long long ldg, long long sbg,
     uint16_t* __restrict__ dS) {
   const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE, lr = lane & 31, h = lane >> 5;
   const int nt = (hw + 31) / 32, kp = 32 * nt, np = (nt + 1) / 2;
@@ -399,8 +399,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(
       const int kq = 32 * kt + acc_row(r, h);
       if (kq < hw) {
         const long long o = b * sbg + (long long)kq * ldg + 128 * half + 32 * t + lr;
-        dK[o] = dk[t][r];
-        dV[o] = dv[t][r];
+        dK[o] = bf_bits(dk[t][r]);
+        dV[o] = bf_bits(dv[t][r]);
       }
     }
 }
@@ -415,7 +415,7 @@ constexpr int Q_LDS = Q_NS * IMG + 2 * 32 * DS_PITCH;
 __global__ __launch_bounds__(128) void attn_bwd_q_kernel(const uint16_t* __restrict__ Kp,
                                                          long long ld, long long sb, int hw,
                                                          const uint16_t* __restrict__ dS,
-                                                         float* __restrict__ dQ, long long ldg,
+                                                         uint16_t* __restrict__ dQ, long long ldg,
                                                          long long sbg) {
   const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE, lr = lane & 31, h = lane >> 5;
   const int nt = (hw + 31) / 32, kp = 32 * nt, np = (nt + 1) / 2;
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(128) void attn_bwd_q_kernel(const uint16_t* __restr
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qq = 32 * qt + acc_row(r, h);
-      if (qq < hw) dQ[b * sbg + (long long)qq * ldg + 32 * t + lr] = acc[t][r];
+      if (qq < hw) dQ[b * sbg + (long long)qq * ldg + 32 * t + lr] = bf_bits(acc[t][r]);
     }
 }
 
@@ -508,13 +508,14 @@ int tgfr_attn_bwd_ws(int B, int hw, long long* bytes) {
   return 0;
 }
 
-// Gradients into dQ / dK / dV [B][hw][256] fp32 (ldg, sbg; typically the
-// column slices of one packed [B][hw][768] gradient), overwritten.  O and dO
-// dense fp32 [B][hw][256].
+// Gradients into dQ / dK / dV [B][hw][256] bf16 (ldg, sbg; typically the
+// column slices of one packed [B][hw][768] gradient -- the operand of the
+// projection's weight-gradient GEMM), overwritten.  O and dO dense fp32
+// [B][hw][256].
 int tgfr_attn_bwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long long ld,
                   long long sb, int B, int hw, float scale, const float* O, const float* dO,
-                  long long ldo, long long sbo, const float* lse, float* dQ, float* dK,
-                  float* dV, long long ldg, long long sbg, void* ws, void* stream) {
+                  long long ldo, long long sbo, const float* lse, uint16_t* dQ, uint16_t* dK,
+                  uint16_t* dV, long long ldg, long long sbg, void* ws, void* stream) {
   if (B <= 0 || hw <= 0 || hw > 32 * AT || (ld & 7) || (sb & 7) || !ws) return 1001;
   if (ldo != AD || sbo != (long long)hw * AD) return 1001;     // dO / O dense rows
   if (((uintptr_t)Q | (uintptr_t)K | (uintptr_t)V | (uintptr_t)O | (uintptr_t)dO |

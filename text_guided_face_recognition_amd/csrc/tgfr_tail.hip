@@ -495,7 +495,8 @@ constexpr int DW_LDS = 6 * DW_IMG;                     // X, Y, three buffers
 
 struct DwProb {
   const uint16_t* X;
-  const uint16_t* Y;
+  const void* Y;     // bf16, or fp32 when yf32 (converted while staging)
+  int yf32;
   int N, K;          // X row width (= ld), Y row width (= ld)
   int nb_n, nb_k;    // 128-blocks
   int first;         // first workgroup of this product
@@ -516,6 +517,16 @@ __device__ __forceinline__ bf16x8 tr_frag(uint32_t base, int col0, int s, int la
   return join_tr(lds_tr4(a), lds_tr4(a + 4 * DW_PITCH));
 }
 
+// raw Y staging registers: fp32 Y is kept as loaded until it is stored to
+// LDS (converting at load time would wait on the load and defeat the
+// prefetch ring)
+struct YF32Piece {
+  float4 a, b;
+};
+template <bool YF32>
+using YPiece = typename std::conditional<YF32, YF32Piece, uint4>::type;
+
+template <bool YF32>
 __global__ __launch_bounds__(256) void tail_dw_kernel(DwArgs A, float* __restrict__ ws) {
   const int tid = threadIdx.x, wv = tid / WAVE, lane = tid % WAVE;
   const int total = gridDim.x;
@@ -543,24 +554,37 @@ __global__ __launch_bounds__(256) void tail_dw_kernel(DwArgs A, float* __restric
   float cs[2] = {0.f, 0.f};
 
   // staging: thread t loads 16 B of X and 16 B of Y per pass; 2 passes per chunk
-  auto load = [&](int c, uint4 (&vx)[2], uint4 (&vy)[2]) {
+  using YP = YPiece<YF32>;
+  auto load = [&](int c, uint4 (&vx)[2], YP (&vy)[2]) {
 #pragma unroll
     for (int ps = 0; ps < 2; ++ps) {
       const int i = tid + 256 * ps, r = i / 16, c16 = i % 16;
       const int row = r_begin + c * DW_CH + r;
-      vx[ps] = vy[ps] = make_uint4(0, 0, 0, 0);
-      if (row < r_end) {
-        vx[ps] = *(const uint4*)(P.X + (long long)row * P.N + bn * DW_NB + 8 * c16);
-        vy[ps] = *(const uint4*)(P.Y + (long long)row * P.K + bk * DW_NB + 8 * c16);
+      const long long yo = (long long)row * P.K + bk * DW_NB + 8 * c16;
+      const bool ok = row < r_end;
+      vx[ps] = ok ? *(const uint4*)(P.X + (long long)row * P.N + bn * DW_NB + 8 * c16)
+                  : make_uint4(0, 0, 0, 0);
+      if constexpr (YF32) {
+        const float* yp = (const float*)P.Y + yo;
+        vy[ps].a = ok ? *(const float4*)yp : make_float4(0.f, 0.f, 0.f, 0.f);
+        vy[ps].b = ok ? *(const float4*)(yp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        vy[ps] = ok ? *(const uint4*)((const uint16_t*)P.Y + yo) : make_uint4(0, 0, 0, 0);
       }
     }
   };
-  auto store = [&](int buf, const uint4 (&vx)[2], const uint4 (&vy)[2]) {
+  auto store = [&](int buf, const uint4 (&vx)[2], const YP (&vy)[2]) {
 #pragma unroll
     for (int ps = 0; ps < 2; ++ps) {
       const int i = tid + 256 * ps, r = i / 16, c16 = i % 16;
       lds_st16(buf * 2 * DW_IMG + r * DW_PITCH + 16 * c16, vx[ps]);
-      lds_st16(buf * 2 * DW_IMG + DW_IMG + r * DW_PITCH + 16 * c16, vy[ps]);
+      uint4 y;
+      if constexpr (YF32)
+        y = make_uint4(pk_bf16(vy[ps].a.x, vy[ps].a.y), pk_bf16(vy[ps].a.z, vy[ps].a.w),
+                       pk_bf16(vy[ps].b.x, vy[ps].b.y), pk_bf16(vy[ps].b.z, vy[ps].b.w));
+      else
+        y = vy[ps];
+      lds_st16(buf * 2 * DW_IMG + DW_IMG + r * DW_PITCH + 16 * c16, y);
     }
   };
   auto compute = [&](int buf) {
@@ -588,7 +612,8 @@ __global__ __launch_bounds__(256) void tail_dw_kernel(DwArgs A, float* __restric
   // three chunks in flight: chunk c sits in register slot c % 3 from its load
   // (issued three steps ahead) until it is stored to LDS buffer c % 3 one
   // step before it is used
-  uint4 rx[3][2], ry[3][2];
+  uint4 rx[3][2];
+  YP ry[3][2];
 #pragma unroll
   for (int j = 0; j < 3; ++j)
     if (j < n_chunks) load(j, rx[j], ry[j]);
@@ -670,21 +695,22 @@ __global__ __launch_bounds__(256) void tail_dw_reduce_kernel(DwArgs A, DwOut O,
   *(float4*)dst = s;
 }
 
-void dw_plan(int rows, DwArgs& A, long long& ws_floats, int& n_wg) {
-  const int NS[3] = {TD, TC, TH}, KS[3] = {TC, TH, TC};   // dWp, dW2, dW1
+// n products (N[i] x K[i], multiples of 128) over `rows` rows; wg_budget:
+// workgroups to aim for (the slabs, slices x sum N K floats, are written and
+// read back once more by the reduce, so fewer slices trade chip fill for
+// traffic)
+void dw_plan_n(int rows, int n, const int* NS, const int* KS, int wg_budget, DwArgs& A,
+               long long& ws_floats, int& n_wg) {
   int blocks = 0;
-  for (int i = 0; i < 3; ++i) blocks += (NS[i] / DW_NB) * (KS[i] / DW_NB);
-  // slices: one workgroup per CU (the slabs, slices x 0.53 MB written here
-  // and read back by the reduce, are then ~half the 32 MB of operands at the
-  // step's 12544 rows); at least 4 chunks per slice
-  const int want = std::max(1, 256 / blocks);
+  for (int i = 0; i < n; ++i) blocks += (NS[i] / DW_NB) * (KS[i] / DW_NB);
+  const int want = std::max(1, wg_budget / blocks);
   const int max_slices = std::max(1, rows / (4 * DW_CH));
   A.slices = std::min(want, max_slices);
   A.rows_per = ((rows + A.slices - 1) / A.slices + DW_CH - 1) / DW_CH * DW_CH;
   A.rows = rows;
   long long slab = 0;
   int first = 0;
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < n; ++i) {
     DwProb& p = A.p[i];
     p.N = NS[i];
     p.K = KS[i];
@@ -692,11 +718,35 @@ void dw_plan(int rows, DwArgs& A, long long& ws_floats, int& n_wg) {
     p.nb_k = KS[i] / DW_NB;
     p.first = first;
     p.slab = slab;
+    p.yf32 = 0;
     first += p.nb_n * p.nb_k * A.slices;
     slab += (long long)A.slices * (p.N * (long long)p.K + p.N);
   }
+  for (int i = n; i < 3; ++i) {        // unused: no workgroup, nothing to reduce
+    A.p[i] = DwProb{nullptr, nullptr, 0, 0, 0, 0, 0, first, slab};
+  }
   ws_floats = slab;
   n_wg = first;
+}
+
+void dw_plan(int rows, DwArgs& A, long long& ws_floats, int& n_wg) {
+  // slices: one workgroup per CU (the slabs, slices x 0.53 MB written here
+  // and read back by the reduce, are then ~half the 32 MB of operands at the
+  // step's 12544 rows); at least 4 chunks per slice
+  const int NS[3] = {TD, TC, TH}, KS[3] = {TC, TH, TC};   // dWp, dW2, dW1
+  dw_plan_n(rows, 3, NS, KS, 256, A, ws_floats, n_wg);
+}
+
+int dw_launch(const DwArgs& A, int n_wg, const DwOut& O, float* ws, hipStream_t s) {
+  const bool yf32 = A.p[0].yf32 != 0;      // uniform over the launch's products
+  auto fn = yf32 ? &tail_dw_kernel<true> : &tail_dw_kernel<false>;
+  if (const int e = set_max_lds((const void*)fn, DW_LDS)) return e;
+  hipLaunchKernelGGL(fn, dim3(n_wg), dim3(256), DW_LDS, s, A, ws);
+  long long e_total = 0;
+  for (int i = 0; i < 3; ++i) e_total += (long long)A.p[i].N * A.p[i].K + A.p[i].N;
+  hipLaunchKernelGGL(tail_dw_reduce_kernel, dim3((unsigned)((e_total / 4 + 255) / 256)),
+                     dim3(256), 0, s, A, O, ws, e_total);
+  return (int)hipGetLastError();
 }
 
 }  // namespace
@@ -763,17 +813,45 @@ int tgfr_tail_dw(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
   A.p[0].X = dPb;  A.p[0].Y = H2b;
   A.p[1].X = dH2b; A.p[1].Y = H1b;
   A.p[2].X = dH1b; A.p[2].Y = Zb;
-  if (const int e = set_max_lds((const void*)tail_dw_kernel, DW_LDS)) return e;
-  hipLaunchKernelGGL(tail_dw_kernel, dim3(n_wg), dim3(256), DW_LDS, (hipStream_t)stream, A, ws);
   DwOut O;
   O.dW[0] = dWp; O.db[0] = dbp;
   O.dW[1] = dW2; O.db[1] = db2;
   O.dW[2] = dW1; O.db[2] = db1;
-  long long e_total = 0;
-  for (int i = 0; i < 3; ++i) e_total += (long long)A.p[i].N * A.p[i].K + A.p[i].N;
-  hipLaunchKernelGGL(tail_dw_reduce_kernel, dim3((unsigned)((e_total / 4 + 255) / 256)),
-                     dim3(256), 0, (hipStream_t)stream, A, O, ws, e_total);
-  return (int)hipGetLastError();
+  return dw_launch(A, n_wg, O, ws, (hipStream_t)stream);
+}
+
+// Generic weight gradient of a row-wise linear map with bf16 operands:
+// dW[n][k] = sum_rows X[row][n] Y[row][k], db[n] = sum_rows X[row][n], for
+// dense X [rows][N] bf16 and Y [rows][K] (bf16, or fp32 when y_f32: rounded
+// to bf16 while staged); N, K multiples of 128.  dW [N][K] and db [N] fp32,
+// overwritten; ws: tgfr_dw_bf16_ws floats.  (IMIM's packed q/k/v projection:
+// X = the attention's bf16 gradient, Y = the BN output.)
+static int dw_generic_plan(int rows, int N, int K, DwArgs& A, long long& wsf, int& n_wg) {
+  if (rows <= 0 || N <= 0 || K <= 0 || N % DW_NB || K % DW_NB) return 1001;
+  const int NS[1] = {N}, KS[1] = {K};
+  dw_plan_n(rows, 1, NS, KS, 256, A, wsf, n_wg);
+  return 0;
+}
+
+int tgfr_dw_bf16_ws(int rows, int N, int K, long long* floats) {
+  if (!floats) return 1001;
+  DwArgs A;
+  int n_wg;
+  return dw_generic_plan(rows, N, K, A, *floats, n_wg);
+}
+
+int tgfr_dw_bf16(const uint16_t* X, const void* Y, int y_f32, int rows, int N, int K, float* dW,
+                 float* db, float* ws, void* stream) {
+  if (!X || !Y || !dW || !db || !ws) return 1001;
+  DwArgs A;
+  long long wsf;
+  int n_wg;
+  if (const int e = dw_generic_plan(rows, N, K, A, wsf, n_wg)) return e;
+  A.p[0].X = X;
+  A.p[0].Y = Y;
+  A.p[0].yf32 = y_f32 ? 1 : 0;
+  DwOut O = {{dW, nullptr, nullptr}, {db, nullptr, nullptr}};
+  return dw_launch(A, n_wg, O, ws, (hipStream_t)stream);
 }
 
 }  // extern "C"

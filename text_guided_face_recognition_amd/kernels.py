@@ -605,12 +605,7 @@ def _bn_linear_bwd(ctx, dy, want_dx):
     mb = -(-o // 64) * -(-c // 64)
     gm = bgemm(dp.t().unsqueeze(0), xhat.view(1, rows, c), mode=mode,
                ksplit=_ksplit(rows, mb))[0]
-    dw = torch.empty_like(w2)
-    dgamma = torch.empty(c, dtype=torch.float32, device=dev)
-    dbeta = torch.empty_like(dgamma)
-    uws = torch.empty(2 * -(-o // 64) * c, dtype=torch.float32, device=dev)
-    call("tgfr_bn_unfold", ptr(gm), ptr(s), ptr(w2), o, c, ptr(g), ptr(bt), ptr(dw),
-         ptr(dgamma), ptr(dbeta), ptr(uws), ptr(_hip.counters(dev)), _hip.stream())
+    _, dgamma, dbeta, dw, db = _bn_unfold(ctx, gm, s)
     dx = None
     if want_dx:
         # d xhat = dp W'; BN input gradient (only when the map itself is trained)
@@ -620,7 +615,23 @@ def _bn_linear_bwd(ctx, dy, want_dx):
             m2 = (dxh * xhat).mean((0, 1))
             dxh = dxh - m1 - xhat * m2
         dx = (dxh * rstd).permute(0, 2, 1).reshape(xshape)
-    return dx, dgamma, dbeta, dw.reshape(wshape), (s if has_bias else None)
+    return dx, dgamma, dbeta, dw, db
+
+
+def _bn_unfold(ctx, gm, s):
+    """(None, dgamma, dbeta, dweight, dbias) from G = dy^T xhat [O, C] and
+    s = colsum(dy) [O] (tgfr_bn_unfold)."""
+    xhat, w2, wf, g, bt, rstd = ctx.bn_saved
+    mode, has_bias, xshape, wshape, use_batch = ctx.bn_cfg
+    o, c = w2.shape
+    dev = gm.device
+    dw = torch.empty_like(w2)
+    dgamma = torch.empty(c, dtype=torch.float32, device=dev)
+    dbeta = torch.empty_like(dgamma)
+    uws = torch.empty(2 * -(-o // 64) * c, dtype=torch.float32, device=dev)
+    call("tgfr_bn_unfold", ptr(gm), ptr(s), ptr(w2), o, c, ptr(g), ptr(bt), ptr(dw),
+         ptr(dgamma), ptr(dbeta), ptr(uws), ptr(_hip.counters(dev)), _hip.stream())
+    return None, dgamma, dbeta, dw.reshape(wshape), (s if has_bias else None)
 
 
 class BNLinear(torch.autograd.Function):
@@ -669,12 +680,30 @@ class ImimAttention(torch.autograd.Function):
         if rc != 0:
             raise RuntimeError(f"tgfr_attn_bwd_ws failed with code {rc}")
         ws = torch.empty(int(out[0]), dtype=torch.uint8, device=px.device)
-        dpx = torch.empty(nb, hw, 768, dtype=torch.float32, device=px.device)
+        dpx = torch.empty(nb, hw, 768, dtype=torch.int16, device=px.device)     # bf16
         call("tgfr_attn_bwd", ptr(px), ptr(px[..., 256:]), ptr(px[..., 512:]), px.stride(1),
              px.stride(0), nb, hw, ctx.scale, ptr(o), ptr(do), do.stride(1), do.stride(0),
              ptr(lse), ptr(dpx), ptr(dpx[..., 256:]), ptr(dpx[..., 512:]), dpx.stride(1),
              dpx.stride(0), ptr(ws), _hip.stream())
-        return _bn_linear_bwd(ctx, dpx, ctx.needs_input_grad[0]) + (None, None, None)
+        if ctx.needs_input_grad[0]:
+            # the BN input gradient needs dp W' (the reference's frozen-backbone
+            # step never asks for it): the fp32 path
+            dpf = (dpx.to(torch.int32) << 16).view(torch.float32)
+            return _bn_linear_bwd(ctx, dpf, True) + (None, None, None)
+        # G = dp^T xhat and colsum(dp) in one bf16 weight-gradient launch
+        xhat = ctx.bn_saved[0]
+        rows, c = nb * hw, xhat.shape[2]
+        n = dpx.shape[2]
+        out = (ctypes.c_longlong * 1)()
+        rc = _hip.lib().tgfr_dw_bf16_ws(rows, n, c, ctypes.addressof(out))
+        if rc != 0:
+            raise RuntimeError(f"tgfr_dw_bf16_ws failed with code {rc}")
+        gws = torch.empty(int(out[0]), dtype=torch.float32, device=px.device)
+        gm = torch.empty(n, c, dtype=torch.float32, device=px.device)
+        s = torch.empty(n, dtype=torch.float32, device=px.device)
+        call("tgfr_dw_bf16", ptr(dpx), ptr(xhat), 1, rows, n, c, ptr(gm), ptr(s), ptr(gws),
+             _hip.stream())
+        return _bn_unfold(ctx, gm, s) + (None, None, None)
 
 
 def imim_attention(x, bn, weight, bias, scale):

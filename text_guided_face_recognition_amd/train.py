@@ -80,12 +80,16 @@ class _Branches:
     caching allocator must not recycle them under it).  Inside HIP-graph
     capture this forks and joins the captured graph.  Disabled (everything on
     the current stream) when `enabled` is false, e.g. under data parallelism,
-    where StepCapture cuts graphs at the collectives."""
+    where StepCapture cuts graphs at the collectives, and while a KernelTimer
+    is active."""
 
     _streams = {}
 
     def __init__(self, enabled):
-        self.enabled = enabled and torch.cuda.is_available()
+        from ._hip import KernelTimer
+        # a KernelTimer pass (bench.py's per-kernel timing) runs serially so
+        # the timed kernels do not share the chip with the other branches
+        self.enabled = enabled and torch.cuda.is_available() and KernelTimer.active is None
 
     def __enter__(self):
         if self.enabled:

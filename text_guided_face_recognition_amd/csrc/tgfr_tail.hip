@@ -7,7 +7,7 @@
 //   R  = P / max(|P|, eps)      F.normalize               (:117)
 //
 // over the channels-last rows of the LayerNorm output Z [rows = B*196][256].
-// One workgroup owns 64 rows and runs the whole chain: the intermediate
+// One workgroup owns 32 rows and runs the whole chain: the intermediate
 // activations never leave LDS, only the bf16 copies the backward needs (Z, H1,
 // H2) and R go to HBM.  Layers 1 and 2 are computed transposed
 // (Out^T = W In^T): the MFMA accumulator of a lane then holds 4 consecutive
@@ -16,7 +16,13 @@
 // The last layer is computed upright so that its fp32 result is stored as
 // 128-B row segments and its row norms reduce across lanes (rs16).
 //
-// Backward (one workgroup per 64 rows again):
+// 32-row workgroups at ~120 registers per lane put several workgroups on a
+// CU, which hides the operand latency better than 64-row workgroups with the
+// weight fragments prefetched into registers (13 / 19 us against 17 / 25 us
+// forward / backward at 12544 rows, tools/lab/tail_ablate.py); the weights'
+// fragment-order pack keeps each fragment load one coalesced KiB.
+//
+// Backward (one workgroup per 32 rows again):
 //   dP  = (dR - R (R.dR)) / max(|P|, eps)        (clamped rows: dR / eps)
 //   dH2 = (dP Wp) * [H2 > 0],  dH1 = (dH2 W2) * [H1 > 0],  dZ = dH1 W1
 // writing dZ in fp32 (the LayerNorm backward's input) and dP, dH2, dH1 in
@@ -37,7 +43,8 @@ namespace {
 constexpr int TC = 256;   // IMIM channels (LayerNorm / conv1x1_1 input, conv1x1_2 output)
 constexpr int TH = 128;   // conv1x1_1 output
 constexpr int TD = 256;   // projection dim (aux_feat_dim_per_granularity)
-constexpr int TM = 64;    // rows per workgroup
+constexpr int TM = 32;    // rows per workgroup
+constexpr int MT = TM / 32;  // 32-row MFMA tiles per workgroup
 
 // packed bf16 weights (uint16 element offsets)
 constexpr int OFF_W1 = 0;                     // W1  [TH][TC]
@@ -118,7 +125,8 @@ __global__ __launch_bounds__(256) void tail_pack_kernel(const float* __restrict_
 // ------------------------------------------------------------ forward ---
 // LDS: [0, 32K) Z image (later the H2 image), [32K, 48K) H1 image,
 //      [48K, 49K) row sum-of-squares partials [4 waves][64], [49K, 49.25K) 1/norm
-constexpr int F_Z = 0, F_H2 = 0, F_H1 = 32768, F_SS = 49152, F_INV = F_SS + 4 * TM * 4;
+constexpr int F_Z = 0, F_H2 = 0, F_H1 = TM * TC * 2, F_SS = F_H1 + TM * TH * 2,
+              F_INV = F_SS + 4 * TM * 4;
 constexpr int F_LDS = F_INV + TM * 4;
 
 __global__ __launch_bounds__(256) void tail_fwd_kernel(
@@ -129,18 +137,6 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
   const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE;
   const int lr = lane & 31, h = lane >> 5;
   const int row0 = blockIdx.x * TM;
-
-  // every weight fragment of layers 1 and 2 is issued up front (they do not
-  // depend on the activations): one memory latency per kernel instead of one
-  // per k-step -- with one 4-wave workgroup per CU nothing else would hide it
-  bf16x8 w1f[TC / 16], w2f[TH / 16][2];
-#pragma unroll
-  for (int s = 0; s < TC / 16; ++s) w1f[s] = gld16(frag_ptr(pk, OFF_W1, TC, w, s, lane));
-#pragma unroll
-  for (int s = 0; s < TH / 16; ++s)
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-      w2f[s][jt] = gld16(frag_ptr(pk, OFF_W2, TH, 2 * w + jt, s, lane));
 
   // Z rows -> bf16 image (and the bf16 copy for dW1); rows past the end are 0
 #pragma unroll
@@ -159,17 +155,17 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
 
   // layer 1, transposed: H1^T[i][m] = sum_c W1[i][c] Z[m][c]; wave w: i in [32w, 32w+32)
   {
-    f32x16 acc[2];
+    f32x16 acc[MT];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < MT; ++t)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
 #pragma unroll
     for (int s = 0; s < TC / 16; ++s) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
+      for (int mt = 0; mt < MT; ++mt) {
         const bf16x8 b = as_bf8(lds_ld16(F_Z + img<TC>(32 * mt + lr, 2 * s + h)));
-        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[s], b, acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gld16(frag_ptr(pk, OFF_W1, TC, w, s, lane)), b, acc[mt], 0, 0, 0);
       }
     }
 #pragma unroll
@@ -177,7 +173,7 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
       const int i0 = 32 * w + 8 * g + 4 * h;
       const float4 bb = *(const float4*)(b1 + i0);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
+      for (int mt = 0; mt < MT; ++mt) {
         const f32x16& a = acc[mt];
         lds_st8(F_H1 + img_at<TH>(32 * mt + lr, i0),
                 pk4(fmaxf(a[4 * g] + bb.x, 0.f), fmaxf(a[4 * g + 1] + bb.y, 0.f),
@@ -185,37 +181,30 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
       }
     }
   }
-  // layer 3's weight fragments, issued while layer 2 runs
-  bf16x8 wpf[TC / 16][2];
-#pragma unroll
-  for (int s = 0; s < TC / 16; ++s)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-      wpf[s][nt] = gld16(frag_ptr(pk, OFF_WP, TC, 2 * w + nt, s, lane));
   __syncthreads();
   copy_out<TH>(F_H1, H1b, TH, row0, rows, tid);
 
   // layer 2, transposed: H2^T[j][m] = sum_i W2[j][i] H1[m][i]; wave w: j in [64w, 64w+64)
   {
-    f32x16 acc[2][2];
+    f32x16 acc[2][MT];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < MT; ++u)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
 #pragma unroll
     for (int s = 0; s < TH / 16; ++s) {
-      bf16x8 b[2];
+      bf16x8 b[MT];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
         b[mt] = as_bf8(lds_ld16(F_H1 + img<TH>(32 * mt + lr, 2 * s + h)));
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
+        for (int mt = 0; mt < MT; ++mt)
           acc[jt][mt] =
-              __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2f[s][jt], b[mt], acc[jt][mt], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_32x32x16_bf16(gld16(frag_ptr(pk, OFF_W2, TH, 2 * w + jt, s, lane)), b[mt], acc[jt][mt], 0, 0, 0);
     }
     // the Z image is dead (every wave passed the barrier after layer 1): H2 reuses it
 #pragma unroll
@@ -225,7 +214,7 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
         const int j0 = 64 * w + 32 * jt + 8 * g + 4 * h;
         const float4 bb = *(const float4*)(b2 + j0);
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
+        for (int mt = 0; mt < MT; ++mt) {
           const f32x16& a = acc[jt][mt];
           lds_st8(F_H2 + img_at<TC>(32 * mt + lr, j0),
                   pk4(fmaxf(a[4 * g] + bb.x, 0.f), fmaxf(a[4 * g + 1] + bb.y, 0.f),
@@ -237,24 +226,24 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
   copy_out<TC>(F_H2, H2b, TC, row0, rows, tid);
 
   // layer 3, upright: P[m][n] = sum_j H2[m][j] Wp[n][j] + bp[n]; wave w: n in [64w, 64w+64)
-  f32x16 acc[2][2];
+  f32x16 acc[MT][2];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
 #pragma unroll
   for (int s = 0; s < TC / 16; ++s) {
-    bf16x8 a[2];
+    bf16x8 a[MT];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
       a[mt] = as_bf8(lds_ld16(F_H2 + img<TC>(32 * mt + lr, 2 * s + h)));
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mt], wpf[s][nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mt], gld16(frag_ptr(pk, OFF_WP, TC, 2 * w + nt, s, lane)), acc[mt][nt], 0, 0, 0);
   }
   // bias, then the row sums of squares: lane-local over this wave's two
   // column tiles, then over the 32 columns of each half-wave (rs16)
@@ -262,12 +251,12 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
   for (int nt = 0; nt < 2; ++nt) {
     const float bb = bp[64 * w + 32 * nt + lr];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[mt][nt][q] += bb;
   }
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
+  for (int mt = 0; mt < MT; ++mt) {
     float sq[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q)
@@ -286,7 +275,7 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
   }
   __syncthreads();
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int m = 32 * mt + acc_row(q, h);
@@ -301,7 +290,7 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
 
 // ----------------------------------------------------------- backward ---
 // LDS: [0, 32K) dP image (later the dH1 image), [32K, 64K) dH2 image
-constexpr int B_DP = 0, B_DH1 = 0, B_DH2 = 32768, B_LDS = 65536;
+constexpr int B_DP = 0, B_DH1 = 0, B_DH2 = TM * TD * 2, B_LDS = 2 * TM * TD * 2;
 
 __global__ __launch_bounds__(256) void tail_bwd_kernel(
     const float* __restrict__ dR, long long lddr, const float* __restrict__ R, long long ldr,
@@ -313,21 +302,10 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
   const int lr = lane & 31, h = lane >> 5;
   const int row0 = blockIdx.x * TM;
 
-  // the first two GEMMs' weight fragments, issued before anything else
-  bf16x8 wptf[TD / 16][2], w2tf[TC / 16];
-#pragma unroll
-  for (int s = 0; s < TD / 16; ++s)
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-      wptf[s][jt] = gld16(frag_ptr(pk, OFF_WPT, TD, 2 * w + jt, s, lane));
-#pragma unroll
-  for (int s = 0; s < TC / 16; ++s)
-    w2tf[s] = gld16(frag_ptr(pk, OFF_W2T, TC, w, s, lane));
-
   // F.normalize backward, one row per wave pass (lane: 4 columns)
 #pragma unroll 2
   for (int r = 0; r < TM / 4; ++r) {
-    const int m = 16 * w + r, row = row0 + m;
+    const int m = (TM / 4) * w + r, row = row0 + m;
     float4 g = make_float4(0.f, 0.f, 0.f, 0.f), y = g;
     float iv = 0.f;
     if (row < rows) {
@@ -347,41 +325,41 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
   // dH2^T[j][m] = sum_n Wp[n][j] dP[m][n] (A = Wp^T rows); wave w: j in [64w, 64w+64)
   {
     // relu masks first: H2[m][j0..j0+3] for this lane's accumulator quads
-    uint2 msk[2][2][4];
+    uint2 msk[2][MT][4];
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int row = row0 + 32 * mt + lr, j0 = 64 * w + 32 * jt + 8 * g + 4 * h;
           msk[jt][mt][g] = row < rows ? *(const uint2*)(H2b + (long long)row * TC + j0)
                                       : make_uint2(0, 0);
         }
-    f32x16 acc[2][2];
+    f32x16 acc[2][MT];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < MT; ++u)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
 #pragma unroll
     for (int s = 0; s < TD / 16; ++s) {
-      bf16x8 b[2];
+      bf16x8 b[MT];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
         b[mt] = as_bf8(lds_ld16(B_DP + img<TD>(32 * mt + lr, 2 * s + h)));
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
+        for (int mt = 0; mt < MT; ++mt)
           acc[jt][mt] =
-              __builtin_amdgcn_mfma_f32_32x32x16_bf16(wptf[s][jt], b[mt], acc[jt][mt], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_32x32x16_bf16(gld16(frag_ptr(pk, OFF_WPT, TD, 2 * w + jt, s, lane)), b[mt], acc[jt][mt], 0, 0, 0);
     }
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int j0 = 64 * w + 32 * jt + 8 * g + 4 * h;
@@ -395,43 +373,36 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
           lds_st8(B_DH2 + img_at<TC>(32 * mt + lr, j0), pk4(v0, v1, v2, v3));
         }
   }
-  // the last GEMM's weight fragments, issued while dH1 is computed
-  bf16x8 w1tf[TH / 16][2];
-#pragma unroll
-  for (int s = 0; s < TH / 16; ++s)
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-      w1tf[s][ct] = gld16(frag_ptr(pk, OFF_W1T, TH, 2 * w + ct, s, lane));
   __syncthreads();
   copy_out<TC>(B_DH2, dH2b, TC, row0, rows, tid);
 
   // dH1^T[i][m] = sum_j W2[j][i] dH2[m][j] (A = W2^T rows); wave w: i in [32w, 32w+32)
   {
-    uint2 msk[2][4];
+    uint2 msk[MT][4];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int row = row0 + 32 * mt + lr, i0 = 32 * w + 8 * g + 4 * h;
         msk[mt][g] = row < rows ? *(const uint2*)(H1b + (long long)row * TH + i0)
                                 : make_uint2(0, 0);
       }
-    f32x16 acc[2];
+    f32x16 acc[MT];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < MT; ++t)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
 #pragma unroll
     for (int s = 0; s < TC / 16; ++s) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
+      for (int mt = 0; mt < MT; ++mt) {
         const bf16x8 b = as_bf8(lds_ld16(B_DH2 + img<TC>(32 * mt + lr, 2 * s + h)));
-        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2tf[s], b, acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gld16(frag_ptr(pk, OFF_W2T, TC, w, s, lane)), b, acc[mt], 0, 0, 0);
       }
     }
     // the dP image is dead (every wave passed the barrier before this GEMM)
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int i0 = 32 * w + 8 * g + 4 * h;
@@ -448,27 +419,27 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
   copy_out<TH>(B_DH1, dH1b, TH, row0, rows, tid);
 
   // dZ[m][c] = sum_i dH1[m][i] W1[i][c] (B = W1^T rows); wave w: c in [64w, 64w+64)
-  f32x16 acc[2][2];
+  f32x16 acc[MT][2];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
 #pragma unroll
   for (int s = 0; s < TH / 16; ++s) {
-    bf16x8 a[2];
+    bf16x8 a[MT];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
       a[mt] = as_bf8(lds_ld16(B_DH1 + img<TH>(32 * mt + lr, 2 * s + h)));
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
-        acc[mt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mt], w1tf[s][ct], acc[mt][ct], 0, 0, 0);
+        acc[mt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mt], gld16(frag_ptr(pk, OFF_W1T, TH, 2 * w + ct, s, lane)), acc[mt][ct], 0, 0, 0);
   }
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int row = row0 + 32 * mt + acc_row(q, h);

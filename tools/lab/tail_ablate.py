@@ -25,6 +25,49 @@ VARIANTS = {
              "w2f[s][jt] = as_bf8(make_uint4(s, lr, jt, w));"),
             ("wpf[s][nt] = gld16(frag_ptr(pk, OFF_WP, TC, 2 * w + nt, s, lane));",
              "wpf[s][nt] = as_bf8(make_uint4(s, lr, nt, h));")],
+    # weight fragments loaded at each use instead of prefetched per layer
+    # (fewer VGPRs: two waves per SIMD)
+    "nopf": [
+        ("""  bf16x8 w1f[TC / 16], w2f[TH / 16][2];
+#pragma unroll
+  for (int s = 0; s < TC / 16; ++s) w1f[s] = gld16(frag_ptr(pk, OFF_W1, TC, w, s, lane));
+#pragma unroll
+  for (int s = 0; s < TH / 16; ++s)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+      w2f[s][jt] = gld16(frag_ptr(pk, OFF_W2, TH, 2 * w + jt, s, lane));
+""", ""),
+        ("w1f[s]", "gld16(frag_ptr(pk, OFF_W1, TC, w, s, lane))"),
+        ("w2f[s][jt]", "gld16(frag_ptr(pk, OFF_W2, TH, 2 * w + jt, s, lane))"),
+        ("""  bf16x8 wpf[TC / 16][2];
+#pragma unroll
+  for (int s = 0; s < TC / 16; ++s)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      wpf[s][nt] = gld16(frag_ptr(pk, OFF_WP, TC, 2 * w + nt, s, lane));
+""", ""),
+        ("wpf[s][nt]", "gld16(frag_ptr(pk, OFF_WP, TC, 2 * w + nt, s, lane))"),
+        ("""  bf16x8 wptf[TD / 16][2], w2tf[TC / 16];
+#pragma unroll
+  for (int s = 0; s < TD / 16; ++s)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+      wptf[s][jt] = gld16(frag_ptr(pk, OFF_WPT, TD, 2 * w + jt, s, lane));
+#pragma unroll
+  for (int s = 0; s < TC / 16; ++s)
+    w2tf[s] = gld16(frag_ptr(pk, OFF_W2T, TC, w, s, lane));
+""", ""),
+        ("wptf[s][jt]", "gld16(frag_ptr(pk, OFF_WPT, TD, 2 * w + jt, s, lane))"),
+        ("w2tf[s]", "gld16(frag_ptr(pk, OFF_W2T, TC, w, s, lane))"),
+        ("""  bf16x8 w1tf[TH / 16][2];
+#pragma unroll
+  for (int s = 0; s < TH / 16; ++s)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+      w1tf[s][ct] = gld16(frag_ptr(pk, OFF_W1T, TH, 2 * w + ct, s, lane));
+""", ""),
+        ("w1tf[s][ct]", "gld16(frag_ptr(pk, OFF_W1T, TH, 2 * w + ct, s, lane))"),
+    ],
     "bwd_nocopy": [("  copy_out<TC>(B_DH2, dH2b, TC, row0, rows, tid);\n", ""),
                    ("  copy_out<TH>(B_DH1, dH1b, TH, row0, rows, tid);\n", "")],
     "bwd_nodz": [("        o[0] = acc[mt][0][q];\n        o[32] = acc[mt][1][q];",

@@ -416,6 +416,33 @@ int tgfr_text_heading(const float* X, int B, int L1, const uint16_t* taps,
                       const float* const* conv_b, float* ws, float* words, long long s_wb,
                       long long s_wt, float* sent, long long s_sb, int mode, void* stream);
 
+/* ---- FCFM image branch (models/fusion_nets.py:236-237) ----------------------
+ * relu(Conv2d(256, 36, 3, padding=0)(x)) -> MaxPool2d(2), fused, and its
+ * backward.  x: the [B, 256, 14, 14] input read as channels-last rows
+ * [B][196][256] (sample stride s_b, row stride s_p, channels contiguous,
+ * 16-byte aligned; ImageHeading's physical layout).  mode 0 = bf16, 1 = fp32
+ * (split bf16 pairs).
+ *   tgfr_fcfm_pack: the Conv2d weight [36][256][3][3] fp32 -> pk,
+ *     tgfr_fcfm_pack_elems() uint16 (bf16 MFMA fragments of both directions,
+ *     opaque); re-pack after every update.
+ *   tgfr_fcfm_conv_fwd: pooled [B][36][6][6] fp32 and code [B][36][6][6]
+ *     (argmax 0..3 = dy*2+dx of the 2x2 window, -1 when the max is <= 0).
+ *   tgfr_fcfm_conv_dx: dX rows [B][196][256] (strides s_b, s_p; overwritten)
+ *     from gpool [B][36][6][6] (contiguous) and code.
+ *   tgfr_fcfm_conv_dw: dW [36][256][3][3], db [36] (overwritten); ws:
+ *     tgfr_fcfm_conv_dw_ws floats (sample-group partials summed in group
+ *     order by a second launch). */
+int tgfr_fcfm_pack_elems(void);
+int tgfr_fcfm_pack(const float* W, uint16_t* pk, void* stream);
+int tgfr_fcfm_conv_fwd(const float* x, long long s_b, long long s_p, int B, const uint16_t* pk,
+                       const float* bias, float* pooled, int8_t* code, int mode, void* stream);
+int tgfr_fcfm_conv_dx(const float* gpool, const int8_t* code, int B, const uint16_t* pk,
+                      float* dx, long long s_b, long long s_p, int mode, void* stream);
+int tgfr_fcfm_conv_dw_ws(int B, long long* floats);
+int tgfr_fcfm_conv_dw(const float* x, long long s_b, long long s_p, const float* gpool,
+                      const int8_t* code, int B, float* dW, float* db, float* ws, int mode,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

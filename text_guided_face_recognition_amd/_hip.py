@@ -82,6 +82,12 @@ SIGNATURES = {
     "tgfr_text_pack": [P, P, I, P],
     "tgfr_text_heading_ws": [I, I, P],
     "tgfr_text_heading": [P, I, I, P, P, P, P, L, L, P, L, I, P],
+    "tgfr_fcfm_pack_elems": [],
+    "tgfr_fcfm_pack": [P, P, P],
+    "tgfr_fcfm_conv_fwd": [P, L, L, I, P, P, P, P, I, P],
+    "tgfr_fcfm_conv_dx": [P, P, I, P, P, L, L, I, P],
+    "tgfr_fcfm_conv_dw_ws": [I, P],
+    "tgfr_fcfm_conv_dw": [P, L, L, P, P, I, P, P, P, I, P],
 }
 
 

@@ -356,83 +356,80 @@ def _ksplit(k, mn_blocks):
     return int(max(1, min(k // chunk, -(-512 // mn_blocks))))
 
 
-class Conv3x3Rows(torch.autograd.Function):
-    """relu(Conv2d(Cin, Cout, 3, padding=0)(x)) of the FCFM image branch
-    (fusion_nets.py:236, 14x14 -> 12x12) as implicit GEMMs on tgfr_bgemm over the
-    channels-last rows of x, with no im2col copy.
+class ConvReluPool(torch.autograd.Function):
+    """MaxPool2d(2)(relu(Conv2d(256, 36, 3, padding=0)(x))) of the FCFM image
+    branch (models/fusion_nets.py:236-237) in one launch each way
+    (csrc/tgfr_fcfm.hip): x [B, 256, 14, 14] -> [B, 36, 6, 6].
 
-    With X the [B*H*W, Cin] rows and q = b*H*W + y*W + x, the output row q is
-    sum over (dy, dx) of X[q + W*dy + dx] . W_{dy,dx}.  For one dy the (dx, e)
-    pairs of the window are 3*Cin CONTIGUOUS floats of X starting at row
-    q + W*dy, so each dy is one GEMM whose A operand is an overlapping-row
-    stride view of X (row stride Cin, K = 3*Cin): three accumulating launches,
-    bias + ReLU in the last one's epilogue.  Rows whose window leaves the image
-    (x >= W-2, y >= H-2) are computed and discarded.
-
-    Backward: the masked output gradient G is scattered into a zero row buffer
-    with 2W+2 leading pad rows; then per dy
-      dX[r] += sum_{dx', c} Gp[r - W*dy - 2 + dx', c] W[c, :, dy, 2 - dx']
-    (again a contiguous 3*Cout window per row: K = 3*Cout), and
-      dW_dy = X_dy^T G (K = the row count, split-K)."""
+    x is read as channels-last rows [B][196][256] (ImageHeading's physical
+    layout, no copy); other layouts are made channels-last first.  The forward
+    keeps the 2x2 argmax (with the ReLU folded in) for the backward, which
+    returns dx (channels-last strides), dW and db."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, mode):
         b, cin, h, w = x.shape
-        cout = weight.shape[0]
-        xr = x.permute(0, 2, 3, 1).contiguous().float()          # [B, H, W, Cin] rows
-        rows = b * h * w
-        m = rows - (2 * w + 2)                                    # last row with an in-buffer window
-        wt = weight.float().permute(2, 3, 1, 0).reshape(3, 3 * cin, cout).contiguous()
-        out = torch.empty(rows, cout, dtype=torch.float32, device=x.device)
-        mb = -(-m // 64) * -(-cout // 64)
-        for dy in range(3):
-            a = xr.as_strided((1, m, 3 * cin), (0, cin, 1), xr.storage_offset() + dy * w * cin)
-            last = dy == 2
-            bgemm(a, wt[dy].unsqueeze(0), out=out[:m].unsqueeze(0), accumulate=dy > 0,
-                  mode=mode, bias=bias.float().contiguous() if last else None, relu=last,
-                  ksplit=_ksplit(3 * cin, mb))
-        y = out.view(b, h, w, cout)[:, :h - 2, :w - 2].permute(0, 3, 1, 2)
-        ctx.save_for_backward(xr, weight, y)
-        ctx.cfg = (b, cin, h, w, cout, mode)
-        return y
+        if (cin, h, w) != (256, 14, 14) or tuple(weight.shape) != (36, 256, 3, 3):
+            raise ValueError("FCFM conv: x [B, 256, 14, 14], weight [36, 256, 3, 3] "
+                             f"(got {tuple(x.shape)}, {tuple(weight.shape)})")
+        rows = x.float().permute(0, 2, 3, 1)                       # [B, 14, 14, 256]
+        if not (rows.stride(3) == 1 and rows.stride(2) == 256 and rows.stride(1) == 14 * 256
+                and rows.stride(0) % 4 == 0 and rows.data_ptr() % 16 == 0):
+            rows = rows.contiguous()
+        m = _mode(mode)
+        pk = torch.empty(_hip.lib().tgfr_fcfm_pack_elems(), dtype=torch.int16, device=x.device)
+        call("tgfr_fcfm_pack", ptr(weight.float().contiguous()), ptr(pk), _hip.stream())
+        pooled = torch.empty(b, 36, 6, 6, dtype=torch.float32, device=x.device)
+        code = torch.empty(b, 36, 6, 6, dtype=torch.int8, device=x.device)
+        call("tgfr_fcfm_conv_fwd", ptr(rows), rows.stride(0), 256, b, ptr(pk),
+             ptr(bias.float().contiguous()), ptr(pooled), ptr(code), m, _hip.stream())
+        ctx.save_for_backward(rows, pk, code)
+        ctx.cfg = (b, m, weight.dtype)
+        ctx.mark_non_differentiable(code)
+        return pooled
 
     @staticmethod
-    def backward(ctx, gy):
-        xr, weight, y = ctx.saved_tensors
-        b, cin, h, w, cout, mode = ctx.cfg
-        rows, pad = b * h * w, 2 * w + 2
-        g = gy.float() * (y > 0)                                  # ReLU backward
-        gp = torch.zeros(pad + rows, cout, dtype=torch.float32, device=gy.device)
-        gp[pad:].view(b, h, w, cout)[:, :h - 2, :w - 2] = g.permute(0, 2, 3, 1)
+    def backward(ctx, gpool):
+        rows, pk, code = ctx.saved_tensors
+        b, m, wdtype = ctx.cfg
+        gpool = gpool.float().contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            # B'_dy[(2 - dx) * Cout + c, e] = W[c, e, dy, dx]
-            wb = weight.float().flip(3).permute(2, 3, 0, 1).reshape(3, 3 * cout, cin).contiguous()
-            dxr = torch.empty(rows, cin, dtype=torch.float32, device=gy.device)
-            mb = -(-rows // 64) * -(-cin // 64)
-            for dy in range(3):
-                a = gp.as_strided((1, rows, 3 * cout), (0, cout, 1),
-                                  gp.storage_offset() + (pad - w * dy - 2) * cout)
-                bgemm(a, wb[dy].unsqueeze(0), out=dxr.unsqueeze(0), accumulate=dy > 0,
-                      mode=mode, ksplit=_ksplit(3 * cout, mb))
-            dx = dxr.view(b, h, w, cin).permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1]:
-            m = rows - pad
-            gm = gp[pad:pad + m].unsqueeze(0)
-            dwt = torch.empty(3, 3 * cin, cout, dtype=torch.float32, device=gy.device)
-            mb = -(-(3 * cin) // 64) * -(-cout // 64)
-            for dy in range(3):
-                at = xr.as_strided((1, 3 * cin, m), (0, 1, cin),
-                                   xr.storage_offset() + dy * w * cin)
-                bgemm(at, gm, out=dwt[dy].unsqueeze(0), mode=mode, ksplit=_ksplit(m, mb))
-            dw = dwt.view(3, 3, cin, cout).permute(3, 2, 0, 1).to(weight.dtype)
-        if ctx.needs_input_grad[2]:
-            db = g.sum(dim=(0, 2, 3))
+            dxr = torch.empty(b, 14, 14, 256, dtype=torch.float32, device=gpool.device)
+            call("tgfr_fcfm_conv_dx", ptr(gpool), ptr(code), b, ptr(pk), ptr(dxr),
+                 dxr.stride(0), 256, m, _hip.stream())
+            dx = dxr.permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            n = (ctypes.c_longlong * 1)()
+            rc = _hip.lib().tgfr_fcfm_conv_dw_ws(b, ctypes.addressof(n))
+            if rc != 0:
+                raise RuntimeError(f"tgfr_fcfm_conv_dw_ws failed with code {rc}")
+            ws = torch.empty(int(n[0]), dtype=torch.float32, device=gpool.device)
+            dwf = torch.empty(36, 256, 3, 3, dtype=torch.float32, device=gpool.device)
+            dbf = torch.empty(36, dtype=torch.float32, device=gpool.device)
+            call("tgfr_fcfm_conv_dw", ptr(rows), rows.stride(0), 256, ptr(gpool), ptr(code), b,
+                 ptr(dwf), ptr(dbf), ptr(ws), m, _hip.stream())
+            dw = dwf.to(wdtype) if ctx.needs_input_grad[1] else None
+            db = dbf if ctx.needs_input_grad[2] else None
         return dx, dw, db, None
 
 
-def conv3x3_relu(x, weight, bias, mode="fp32"):
-    return Conv3x3Rows.apply(x, weight, bias, mode)
+def conv_relu_pool(x, weight, bias, mode="fp32"):
+    return ConvReluPool.apply(x, weight, bias, mode)
+
+
+def conv_relu_pool_code(x, weight, bias, mode="fp32"):
+    """The forward kernel alone (no autograd): (pooled, code), code the 2x2
+    argmax 0..3 = dy*2+dx of each window, -1 where the ReLU blocks it."""
+    with torch.no_grad():
+        rows = x.float().permute(0, 2, 3, 1).contiguous()
+        pk = torch.empty(_hip.lib().tgfr_fcfm_pack_elems(), dtype=torch.int16, device=x.device)
+        call("tgfr_fcfm_pack", ptr(weight.float().contiguous()), ptr(pk), _hip.stream())
+        pooled = torch.empty(x.shape[0], 36, 6, 6, dtype=torch.float32, device=x.device)
+        code = torch.empty(x.shape[0], 36, 6, 6, dtype=torch.int8, device=x.device)
+        call("tgfr_fcfm_conv_fwd", ptr(rows), rows.stride(0), 256, x.shape[0], ptr(pk),
+             ptr(bias.float().contiguous()), ptr(pooled), ptr(code), _mode(mode), _hip.stream())
+    return pooled, code
 
 
 class LinearRows(torch.autograd.Function):

@@ -102,18 +102,11 @@ class Working(nn.Module):
         self.ln_gl_image = nn.LayerNorm([256])
         self.ln_sent = nn.LayerNorm([256])
         self.linear = nn.Linear(324, 128)
-        self.native_conv = False
 
     def forward(self, img, word, gl_img, sent):
-        # conv3x3 + ReLU (:236).  native_conv runs it as implicit GEMMs on
-        # tgfr_bgemm (K.conv3x3_relu, parity-tested); it is off by default
-        # because at config 4 it measured 600 us fwd+bwd per step against
-        # MIOpen's 453 us
-        if self.native_conv:
-            img = K.conv3x3_relu(img, self.conv.weight, self.conv.bias, mode=self.sa.precision)
-        else:
-            img = self.relu(self.conv(img))
-        img = self.maxpool(img)
+        # conv3x3 + ReLU + maxpool (:236-237): one fused kernel each way
+        # (K.conv_relu_pool, csrc/tgfr_fcfm.hip)
+        img = K.conv_relu_pool(img, self.conv.weight, self.conv.bias, mode=self.sa.precision)
         img = self.bn_img(img)
         word = K.linear_rows(word.transpose(1, 2), self.projection.weight,
                              self.projection.bias, mode=self.sa.precision)

@@ -324,6 +324,11 @@ int tgfr_loss_mix_bwd(const float* g, int n, const float* W, float* dloss, void*
 int tgfr_bn_fwd_cl(const float* x, int N, int C, int HW, float eps, float momentum,
                    int training, float* running_mean, float* running_var, long long* nbt,
                    float* mean, float* rstd, float* xhat, void* stream);
+/* BatchNorm2d input gradient: dx [N][C][HW] from the channels-last gradient
+ * of xhat, dxh [N][HW][C], xhat and rstd of tgfr_bn_fwd_cl; training = batch
+ * statistics (rstd (dxh - mean dxh - xhat mean(dxh xhat))), else rstd dxh. */
+int tgfr_bn_bwd_cl(const float* dxh, const float* xhat, const float* rstd, int N, int C, int HW,
+                   int training, float* dx, void* stream);
 /* Wf = W diag(gamma), bf = b + W beta (W [O][C]; b nullable). */
 int tgfr_bn_fold(const float* W, const float* b, int O, int C, const float* gamma,
                  const float* beta, float* Wf, float* bf, void* stream);
@@ -432,6 +437,13 @@ int tgfr_text_heading(const float* X, int B, int L1, const uint16_t* taps,
  *   tgfr_fcfm_conv_dw: dW [36][256][3][3], db [36] (overwritten); ws:
  *     tgfr_fcfm_conv_dw_ws floats (sample-group partials summed in group
  *     order by a second launch). */
+/* Working's second MaxPool2d(2) (fusion_nets.py:252) on a channels-last map:
+ * x [B][H*W][C] -> y [B][C][H/2][W/2] (NCHW) and idx (argmax 0..3 = dy*2+dx,
+ * first maximum); the backward writes every element of dx [B][H*W][C]. */
+int tgfr_maxpool2_cl(const float* x, int B, int H, int W, int C, float* y, uint8_t* idx,
+                     void* stream);
+int tgfr_maxpool2_cl_bwd(const float* dy, const uint8_t* idx, int B, int H, int W, int C,
+                         float* dx, void* stream);
 int tgfr_fcfm_pack_elems(void);
 int tgfr_fcfm_pack(const float* W, uint16_t* pk, void* stream);
 int tgfr_fcfm_conv_fwd(const float* x, long long s_b, long long s_p, int B, const uint16_t* pk,

@@ -83,6 +83,9 @@ SIGNATURES = {
     "tgfr_text_heading_ws": [I, I, P],
     "tgfr_text_heading": [P, I, I, P, P, P, P, L, L, P, L, I, P],
     "tgfr_fcfm_pack_elems": [],
+    "tgfr_maxpool2_cl": [P, I, I, I, I, P, P, P],
+    "tgfr_maxpool2_cl_bwd": [P, P, I, I, I, I, P, P],
+    "tgfr_bn_bwd_cl": [P, P, P, I, I, I, I, P, P],
     "tgfr_fcfm_pack": [P, P, P],
     "tgfr_fcfm_conv_fwd": [P, L, L, I, P, P, P, P, I, P],
     "tgfr_fcfm_conv_dx": [P, P, I, P, P, L, L, I, P],
@@ -176,13 +179,22 @@ N_COUNTERS = 1 << 20
 
 
 def counters(device):
-    """Per-device zeroed uint32 words for the kernels' in-launch last-arriver
-    hand-offs; every kernel leaves the words it used at zero again, and calls
-    on one stream run one at a time, so all calls share the buffer."""
-    key = torch.device(device).index
+    """Zeroed uint32 words for the kernels' in-launch last-arriver hand-offs,
+    one buffer per (device, stream): kernels on one stream run one at a time
+    and every kernel leaves the words it used at zero again, so the calls of a
+    stream share its buffer, while kernels of different streams (the
+    trainer's concurrent loss branches, train._Branches) never share a word.
+    A stream's buffer is made eagerly on first use; a stream that is being
+    captured into a HIP graph must have been given its buffer before the
+    capture began (dist.StepCapture does this for its capture stream)."""
+    dev = torch.device(device)
+    stream = torch.cuda.current_stream(dev)
+    key = (dev.index, stream.cuda_stream)
     buf = _counters.get(key)
     if buf is None:
-        buf = torch.zeros(N_COUNTERS, dtype=torch.int32, device=device)
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("tgfr counters for a stream first used inside a graph capture")
+        buf = torch.zeros(N_COUNTERS, dtype=torch.int32, device=dev)
         _counters[key] = buf
     return buf
 

@@ -97,6 +97,43 @@ __global__ __launch_bounds__(256) void bn_norm_cl_kernel(const float* __restrict
   }
 }
 
+// BatchNorm2d input gradient from the channels-last gradient of xhat:
+//   dx[n][c][hw] = rstd_c (dxh - mean(dxh) - xhat mean(dxh xhat))   (batch stats)
+//   dx[n][c][hw] = rstd_c dxh                                        (running stats)
+// means over (N, HW) of channel c; grid C, 256 threads, fixed-order sums.
+__global__ __launch_bounds__(256) void bn_bwd_cl_kernel(const float* __restrict__ dxh,
+                                                        const float* __restrict__ xhat,
+                                                        const float* __restrict__ rstd, int N,
+                                                        int C, int HW, int training,
+                                                        float* __restrict__ dx) {
+  __shared__ float red[2][4];
+  const int c = blockIdx.x, tid = threadIdx.x, wid = tid / WAVE, lane = tid % WAVE;
+  const long long cnt = (long long)N * HW;
+  float m1 = 0.f, m2 = 0.f;
+  if (training) {
+    float s1 = 0.f, s2 = 0.f;
+    for (long long e = tid; e < cnt; e += 256) {
+      const float g = dxh[e * C + c];
+      s1 += g;
+      s2 += g * xhat[e * C + c];
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) {
+      red[0][wid] = s1;
+      red[1][wid] = s2;
+    }
+    __syncthreads();
+    m1 = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / (float)cnt;
+    m2 = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)cnt;
+  }
+  const float r = rstd[c];
+  for (long long e = tid; e < cnt; e += 256) {
+    const long long n = e / HW, hw = e % HW;
+    dx[(n * C + c) * HW + hw] = r * (dxh[e * C + c] - m1 - xhat[e * C + c] * m2);
+  }
+}
+
 // one wave per output row o
 __global__ __launch_bounds__(256) void bn_fold_kernel(const float* __restrict__ W,
                                                       const float* __restrict__ b, int O, int C,
@@ -164,6 +201,14 @@ __global__ __launch_bounds__(256) void bn_unfold_kernel(
 }  // namespace
 
 extern "C" {
+
+int tgfr_bn_bwd_cl(const float* dxh, const float* xhat, const float* rstd, int N, int C, int HW,
+                   int training, float* dx, void* stream) {
+  if (!dxh || !xhat || !rstd || !dx || N <= 0 || C <= 0 || HW <= 0) return 1001;
+  hipLaunchKernelGGL(bn_bwd_cl_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dxh, xhat,
+                     rstd, N, C, HW, training, dx);
+  return (int)hipGetLastError();
+}
 
 int tgfr_bn_fwd_cl(const float* x, int N, int C, int HW, float eps, float momentum,
                    int training, float* running_mean, float* running_var, long long* nbt,

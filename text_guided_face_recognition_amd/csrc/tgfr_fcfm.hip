@@ -484,6 +484,58 @@ __global__ __launch_bounds__(256) void fcfm_dw_reduce_kernel(const float* __rest
   }
 }
 
+// ------------------------------------------------- 2x2 max pool, channels last ---
+// Working's second MaxPool2d (fusion_nets.py:252) on the LayerNorm output,
+// which the attention leaves channels-last: x [B][H*W][C] -> y [B][C][H/2][W/2]
+// (NCHW, the order the following flatten + Linear read, :253-254) and the
+// argmax (0..3 = dy*2 + dx, first maximum in scan order as MaxPool2d).  One
+// thread per output element, reads coalesced along C.
+__global__ __launch_bounds__(256) void maxpool2_cl_kernel(const float* __restrict__ x, int B,
+                                                          int H, int W, int C,
+                                                          float* __restrict__ y,
+                                                          uint8_t* __restrict__ idx) {
+  const int ph = H / 2, pw = W / 2;
+  const long long n = (long long)B * ph * pw * C;
+  const long long o = blockIdx.x * 256LL + threadIdx.x;
+  if (o >= n) return;
+  const int c = o % C, px = (o / C) % pw, py = (o / ((long long)C * pw)) % ph;
+  const int b = o / ((long long)C * pw * ph);
+  const float* xb = x + (long long)b * H * W * C + c;
+  float best = xb[((2 * py) * W + 2 * px) * C];
+  int bi = 0;
+#pragma unroll
+  for (int e = 1; e < 4; ++e) {
+    const float v = xb[((2 * py + (e >> 1)) * W + 2 * px + (e & 1)) * C];
+    if (v > best) {
+      best = v;
+      bi = e;
+    }
+  }
+  const long long oy = (((long long)b * C + c) * ph + py) * pw + px;
+  y[oy] = best;
+  idx[oy] = (uint8_t)bi;
+}
+
+// dx [B][H*W][C] (every element written: the gradient at the argmax, 0 elsewhere)
+__global__ __launch_bounds__(256) void maxpool2_cl_bwd_kernel(const float* __restrict__ dy,
+                                                              const uint8_t* __restrict__ idx,
+                                                              int B, int H, int W, int C,
+                                                              float* __restrict__ dx) {
+  const int ph = H / 2, pw = W / 2;
+  const long long n = (long long)B * ph * pw * C;
+  const long long o = blockIdx.x * 256LL + threadIdx.x;
+  if (o >= n) return;
+  const int c = o % C, px = (o / C) % pw, py = (o / ((long long)C * pw)) % ph;
+  const int b = o / ((long long)C * pw * ph);
+  const long long oy = (((long long)b * C + c) * ph + py) * pw + px;
+  const float g = dy[oy];
+  const int bi = idx[oy];
+  float* xb = dx + (long long)b * H * W * C + c;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    xb[((2 * py + (e >> 1)) * W + 2 * px + (e & 1)) * C] = e == bi ? g : 0.f;
+}
+
 bool rows_ok(const float* x, long long s_b, long long s_p) {
   return x && ((uintptr_t)x & 15) == 0 && s_b % 4 == 0 && s_p % 4 == 0 && s_p >= CIN;
 }
@@ -493,6 +545,24 @@ bool rows_ok(const float* x, long long s_b, long long s_p) {
 extern "C" {
 
 int tgfr_fcfm_pack_elems(void) { return PK_ELEMS; }
+
+int tgfr_maxpool2_cl(const float* x, int B, int H, int W, int C, float* y, uint8_t* idx,
+                     void* stream) {
+  if (!x || !y || !idx || B <= 0 || C <= 0 || H < 2 || W < 2 || (H & 1) || (W & 1)) return 1001;
+  const long long n = (long long)B * (H / 2) * (W / 2) * C;
+  hipLaunchKernelGGL(maxpool2_cl_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, x, B, H, W, C, y, idx);
+  return (int)hipGetLastError();
+}
+
+int tgfr_maxpool2_cl_bwd(const float* dy, const uint8_t* idx, int B, int H, int W, int C,
+                         float* dx, void* stream) {
+  if (!dy || !idx || !dx || B <= 0 || C <= 0 || H < 2 || W < 2 || (H & 1) || (W & 1)) return 1001;
+  const long long n = (long long)B * (H / 2) * (W / 2) * C;
+  hipLaunchKernelGGL(maxpool2_cl_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, dy, idx, B, H, W, C, dx);
+  return (int)hipGetLastError();
+}
 
 int tgfr_fcfm_pack(const float* W, uint16_t* pk, void* stream) {
   if (!W || !pk || ((uintptr_t)pk & 15)) return 1001;

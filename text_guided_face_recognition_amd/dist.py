@@ -66,8 +66,10 @@ class StepCapture:
         """Record `step(*args)` (on a side stream); returns its outputs, whose
         storage the replays rewrite."""
         global _CAPTURE
+        from ._hip import counters
         self.stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.stream):
+            counters(torch.cuda.current_device())      # the capture stream's own words
             self._begin()
             _CAPTURE = self
             try:

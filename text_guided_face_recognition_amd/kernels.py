@@ -432,6 +432,64 @@ def conv_relu_pool_code(x, weight, bias, mode="fp32"):
     return pooled, code
 
 
+class MaxPool2CL(torch.autograd.Function):
+    """MaxPool2d(2) of a channels-last map x [B, H*W, C] (Working's pool after
+    its LayerNorm, fusion_nets.py:252) -> [B, C, H/2, W/2] (NCHW)."""
+
+    @staticmethod
+    def forward(ctx, x, h, w):
+        b, hw, c = x.shape
+        assert hw == h * w
+        x = _aligned(x)
+        y = torch.empty(b, c, h // 2, w // 2, dtype=torch.float32, device=x.device)
+        idx = torch.empty(b, c, h // 2, w // 2, dtype=torch.uint8, device=x.device)
+        call("tgfr_maxpool2_cl", ptr(x), b, h, w, c, ptr(y), ptr(idx), _hip.stream())
+        ctx.save_for_backward(idx)
+        ctx.cfg = (b, h, w, c)
+        ctx.mark_non_differentiable(idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        idx, = ctx.saved_tensors
+        b, h, w, c = ctx.cfg
+        dy = _aligned(dy)
+        dx = torch.empty(b, h * w, c, dtype=torch.float32, device=dy.device)
+        call("tgfr_maxpool2_cl_bwd", ptr(dy), ptr(idx), b, h, w, c, ptr(dx), _hip.stream())
+        return dx, None, None
+
+
+def maxpool2_cl(x, h, w):
+    return MaxPool2CL.apply(x, h, w)
+
+
+class Gram(torch.autograd.Function):
+    """G = alpha * X^T X per sample for X [B, T, C] -> [B, C, C]: Working's
+    word Gram matrix (fusion_nets.py:241), on the batched MFMA GEMM; the
+    backward dX = alpha X (dG + dG^T) as two accumulating GEMMs."""
+
+    @staticmethod
+    def forward(ctx, x, alpha, mode):
+        x = x.float()
+        g = bgemm(x.transpose(1, 2), x, alpha=alpha, mode=mode)
+        ctx.save_for_backward(x)
+        ctx.cfg = (float(alpha), mode)
+        return g
+
+    @staticmethod
+    def backward(ctx, dg):
+        x, = ctx.saved_tensors
+        alpha, mode = ctx.cfg
+        dg = dg.float()
+        dx = bgemm(x, dg, alpha=alpha, mode=mode)
+        bgemm(x, dg.transpose(1, 2), out=dx, alpha=alpha, accumulate=True, mode=mode)
+        return dx, None, None
+
+
+def gram(x, alpha=1.0, mode="fp32"):
+    return Gram.apply(x, alpha, mode)
+
+
 class LinearRows(torch.autograd.Function):
     """y = x W^T + b (optionally ReLU) over the rows of x [..., K]: every
     nn.Linear / 1x1 conv of the head, on the split-bf16 MFMA GEMM."""
@@ -606,12 +664,10 @@ def _bn_linear_bwd(ctx, dy, want_dx):
     dx = None
     if want_dx:
         # d xhat = dp W'; BN input gradient (only when the map itself is trained)
-        dxh = bgemm(dp.unsqueeze(0), wf.unsqueeze(0), mode=mode)[0].view(n, hw, c)
-        if use_batch:
-            m1 = dxh.mean((0, 1))
-            m2 = (dxh * xhat).mean((0, 1))
-            dxh = dxh - m1 - xhat * m2
-        dx = (dxh * rstd).permute(0, 2, 1).reshape(xshape)
+        dxh = bgemm(dp.unsqueeze(0), wf.unsqueeze(0), mode=mode)[0]
+        dx = torch.empty(xshape, dtype=torch.float32, device=dev)
+        call("tgfr_bn_bwd_cl", ptr(dxh), ptr(xhat), ptr(rstd), n, c, hw, int(use_batch),
+             ptr(dx), _hip.stream())
     return dx, dgamma, dbeta, dw, db
 
 

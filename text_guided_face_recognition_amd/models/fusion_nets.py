@@ -104,22 +104,32 @@ class Working(nn.Module):
         self.linear = nn.Linear(324, 128)
 
     def forward(self, img, word, gl_img, sent):
+        mode = self.sa.precision
+        sa = self.sa
         # conv3x3 + ReLU + maxpool (:236-237): one fused kernel each way
-        # (K.conv_relu_pool, csrc/tgfr_fcfm.hip)
-        img = K.conv_relu_pool(img, self.conv.weight, self.conv.bias, mode=self.sa.precision)
-        img = self.bn_img(img)
-        word = K.linear_rows(word.transpose(1, 2), self.projection.weight,
-                             self.projection.bias, mode=self.sa.precision)
-        word = torch.bmm(word.transpose(1, 2), word) / np.sqrt(36)
-        word = word.unsqueeze(-1).view(word.size(0), word.size(1), 6, 6)
-        word = self.bn_word(word)
-        iw = self.sa(img, word)
-        iw = self.ln(iw)
-        iw = self.maxpool(iw)
-        iw = iw.reshape(iw.size(0), -1)
-        iw = K.linear_rows(iw, self.linear.weight, self.linear.bias, mode=self.sa.precision)
-        gl_img = self.ln_gl_image(gl_img)
-        sent = self.ln_sent(sent)
+        img = K.conv_relu_pool(img, self.conv.weight, self.conv.bias, mode=mode)   # [B,36,6,6]
+        # word projection and its Gram matrix / 6 (:240-242)
+        wd = K.linear_rows(word.transpose(1, 2), self.projection.weight, self.projection.bias,
+                           mode=mode)                                    # [B, T, 36]
+        wd = K.gram(wd, 1.0 / np.sqrt(36), mode=mode)                    # [B, 36, 36]
+        wd = wd.view(wd.size(0), wd.size(1), 6, 6)
+        # bn_img / bn_word (:237, :243) folded into the attention's 1x1
+        # projections (query role = key_proj(img), value = value_proj(img),
+        # key role = query_proj(word), :248 -> :97-99)
+        wx = torch.cat([sa._w(sa.key_proj), sa._w(sa.value_proj)], 0)
+        bx = torch.cat([sa.key_proj.bias, sa.value_proj.bias])
+        px = K.bn_linear(img, self.bn_img, wx, bx, mode=mode)                # [B, 36, Qr | V]
+        py = K.bn_linear(wd, self.bn_word, sa._w(sa.query_proj), sa.query_proj.bias,
+                         mode=mode)                                        # [B, 36, Kr]
+        cq = sa.key_proj.weight.shape[0]
+        iw = K.attention_core(px, py, cq, 0, cq, 1.0 / float(sa.sqrt_dim), mode)   # [B, HW, C]
+        # LayerNorm [36, 6, 6] on the channels-last rows, maxpool, flatten (:249-253)
+        iw = K.layer_norm_rows(iw, self.ln.weight, self.ln.bias, self.ln.eps, ch=iw.shape[2])
+        iw = K.maxpool2_cl(iw, 6, 6).reshape(iw.size(0), -1)             # [B, 324]
+        iw = K.linear_rows(iw, self.linear.weight, self.linear.bias, mode=mode)
+        gl_img = K.layer_norm_rows(gl_img, self.ln_gl_image.weight, self.ln_gl_image.bias,
+                                   self.ln_gl_image.eps)
+        sent = K.layer_norm_rows(sent, self.ln_sent.weight, self.ln_sent.bias, self.ln_sent.eps)
         return torch.concat((iw, gl_img, sent), dim=1)
 
 

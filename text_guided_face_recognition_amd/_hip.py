@@ -182,8 +182,8 @@ def counters(device):
     """Zeroed uint32 words for the kernels' in-launch last-arriver hand-offs,
     one buffer per (device, stream): kernels on one stream run one at a time
     and every kernel leaves the words it used at zero again, so the calls of a
-    stream share its buffer, while kernels of different streams (the
-    trainer's concurrent loss branches, train._Branches) never share a word.
+    stream share its buffer, while kernels of different streams never share
+    a word.
     A stream's buffer is made eagerly on first use; a stream that is being
     captured into a HIP graph must have been given its buffer before the
     capture began (dist.StepCapture does this for its capture stream)."""

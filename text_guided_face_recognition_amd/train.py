@@ -73,53 +73,6 @@ def synthetic_batch_lstm(b, max_words, device, seed, n_ids=1000):
             cls.to(**to), lens.to(device=device, dtype=torch.int32))
 
 
-class _Branches:
-    """Independent parts of a step on side streams: each branch waits for
-    the work enqueued so far, the caller's stream waits for every branch at
-    join(), and tensors handed back are recorded on the caller's stream (the
-    caching allocator must not recycle them under it).  Inside HIP-graph
-    capture this forks and joins the captured graph.  Disabled (everything on
-    the current stream) when `enabled` is false, e.g. under data parallelism,
-    where StepCapture cuts graphs at the collectives, and while a KernelTimer
-    is active."""
-
-    _streams = {}
-
-    def __init__(self, enabled):
-        from ._hip import KernelTimer
-        # a KernelTimer pass (bench.py's per-kernel timing) runs serially so
-        # the timed kernels do not share the chip with the other branches
-        self.enabled = enabled and torch.cuda.is_available() and KernelTimer.active is None
-
-    def __enter__(self):
-        if self.enabled:
-            self.main = torch.cuda.current_stream()
-            dev = self.main.device
-            pool = _Branches._streams.setdefault(dev, [torch.cuda.Stream(dev) for _ in range(3)])
-            self.side = pool
-            for st in self.side:
-                st.wait_stream(self.main)
-        return self
-
-    def stream(self, i):
-        import contextlib
-        if not self.enabled:
-            return contextlib.nullcontext()
-        return torch.cuda.stream(self.side[i])
-
-    def join(self, *tensors):
-        if not self.enabled:
-            return
-        for st in self.side:
-            self.main.wait_stream(st)
-        for t in tensors:
-            if isinstance(t, torch.Tensor):
-                t.record_stream(self.main)
-
-    def __exit__(self, *exc):
-        return False
-
-
 class Train:
     """Stage-1 BERT trainer step (src/train_encoders_bert.py)."""
 
@@ -159,35 +112,44 @@ class Train:
         img_features, words_features = self.image_head(g, local)   # :265
         self.optimizer.zero_grad(set_to_none=True)
 
-        # the loss branches are independent: on one GPU they run on side
-        # streams (their backward follows them there), so the small
-        # contrastive / identity kernels overlap the word-region kernels
-        with _Branches(not ctx.active) as br:
-            with br.stream(0):
-                w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
-            with br.stream(1):
-                s0, s1 = sent_loss(img_features, sent_g, labels, cls_g, b, args)
-                cl = global_loss(img_features, sent_g, args=args)  # :310
-            with br.stream(2):
-                # :293-306, both focal losses from the global-batch mean CE
-                tid, iid = K.focal_ce_multi(
-                    [(self.text_cls(sent, class_ids), class_ids),
-                     (self.image_cls(img_features, class_ids), class_ids)],
-                    self.ident_loss.gamma, ctx.group if ctx.active else None, ctx.n_global)
-            br.join(w0, w1, s0, s1, cl, tid, iid)
-        # total = damsm + lambda_clip * cl + lambda_id * (tid + iid)
-        # (:279, :316-323) and the logged terms, as one launch each way
-        wi = float(args.lambda_id)
-        total, report = K.loss_mix(
-            (w0, w1, s0, s1, cl, tid, iid),
-            [(1, 1, 1, 1, args.lambda_clip, wi, wi),              # objective
-             (1, 1, 1, 1, 0, 0, 0),                               # damsm
-             (0, 0, 0, 0, 1, 0, 0),                               # clip
-             (0, 0, 0, 0, 0, wi, wi)])                            # ident
-        total.backward()                                           # :323
+        # total = damsm + lambda_clip * cl + lambda_id * (tid + iid) (:279,
+        # :316-323) is linear in the terms, so each term's gradient is its
+        # constant weight: every branch runs its backward right after its own
+        # forward (no loss-mix backward launch, no join).  One stream: on
+        # MI355X the step replays faster as a linear graph than with the
+        # branches forked onto side streams (0.665 vs 0.694 ms at config 2,
+        # tools/lab/branch_ab.py) -- the word<->region kernels fill the chip.
+        wi, lc = float(args.lambda_id), float(args.lambda_clip)
+        s0, s1 = sent_loss(img_features, sent_g, labels, cls_g, b, args)
+        cl = global_loss(img_features, sent_g, args=args)      # :310
+        # :293-306, both focal losses from the global-batch mean CE
+        tid, iid = K.focal_ce_multi(
+            [(self.text_cls(sent, class_ids), class_ids),
+             (self.image_cls(img_features, class_ids), class_ids)],
+            self.ident_loss.gamma, ctx.group if ctx.active else None, ctx.n_global)
+        torch.autograd.backward((s0, s1, cl, tid, iid),
+                                self._weights((1.0, 1.0, lc, wi, wi), g.device))
+        w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
+        torch.autograd.backward((w0, w1), self._weights((1.0, 1.0), g.device))
+        # the logged terms (and the objective) in one launch
+        with torch.no_grad():
+            _, report = K.loss_mix(
+                (w0, w1, s0, s1, cl, tid, iid),
+                [(1, 1, 1, 1, lc, wi, wi),                            # objective
+                 (1, 1, 1, 1, 0, 0, 0),                               # damsm
+                 (0, 0, 0, 0, 1, 0, 0),                               # clip
+                 (0, 0, 0, 0, 0, wi, wi)])                            # ident
         ctx.reduce_grads(self.params)
         self.optimizer.step()
         return {"damsm": report[0], "clip": report[1], "ident": report[2]}
+
+    def _weights(self, values, device):
+        """Constant device scalars (the loss terms' weights, cached)."""
+        cache = self.__dict__.setdefault("_wcache", {})
+        key = (tuple(values), device)
+        if key not in cache:
+            cache[key] = tuple(torch.full((), float(v), device=device) for v in values)
+        return cache[key]
 
     def _labels(self, n, device):
         lab = getattr(self, "_lab", None)

@@ -147,6 +147,23 @@ int tgfr_ce_stats(const float* L, long long ld, int n_r, int n_c, float* row_lse
                   float* col_max, float* col_sum, float* col_lse, int row_offset, float inv_n,
                   float* loss, unsigned* counters, void* stream);
 
+/* sent_loss + global_loss of one process holding the whole batch (n <= 64,
+ * models/losses.py:19-57 and :329-351): x = img [n][256], y = sent [n][256]
+ * (16-byte aligned rows), cls [n] class ids; logits s_sent * cos with the
+ * same-class off-diagonal mask and s_glob * cos without.  loss [3] = (sent
+ * loss0, sent loss1, global loss0 + loss1); saves cosv [n][n], stats [4][n]
+ * (row / column log-sum-exps of both logit sets) and nrm [2][n] for the
+ * backward, which writes dx [n][256] (row stride lddx) from the upstream
+ * gradients gs0, gs1, ggl (device scalars, each nullable = 0). */
+int tgfr_sent_global(const float* x, long long ldx, const float* y, long long ldy, int n,
+                     const long long* cls, float s_sent, float s_glob, float eps, float* cosv,
+                     float* stats, float* nrm, float* loss, void* stream);
+int tgfr_sent_global_bwd(const float* gs0, const float* gs1, const float* ggl, const float* x,
+                         long long ldx, const float* y, long long ldy, int n,
+                         const long long* cls, float s_sent, float s_glob, float eps,
+                         const float* cosv, const float* stats, const float* nrm, float* dx,
+                         long long lddx, void* stream);
+
 /* loss[0] = inv_n * sum_b (row_lse[b] - L[b][b+off]), loss[1] = inv_n * sum_b
  * (col_lse[b+off] - L[b][b+off]): this rank's share of nn.CrossEntropyLoss on
  * the rows and on the transposed matrix (models/losses.py:52-53, 131-132). */
@@ -236,6 +253,12 @@ int tgfr_arc_margin_bwd(const float* cosv, const long long* label, const float* 
  * word (left zeroed). */
 int tgfr_focal_ce(const float* L, int rows, int cols, const long long* label, float gamma,
                   float* ws, unsigned* counters, float* loss, void* stream);
+/* Two focal losses on the same labels in one launch (the trainer's text and
+ * image identity heads): (L, ws, loss) and (L2, ws2, loss2); counters: 2
+ * zeroed words (left zeroed). */
+int tgfr_focal_ce2(const float* L, const float* L2, int rows, int cols, const long long* label,
+                   float gamma, float* ws, float* ws2, unsigned* counters, float* loss,
+                   float* loss2, void* stream);
 
 /* dL = gscale[0] * dloss/dlogp * (softmax(L_b) - onehot) / rows. */
 int tgfr_focal_ce_bwd(const float* L, int rows, int cols, const long long* label, float gamma,
@@ -361,6 +384,33 @@ int tgfr_arc_bwd(const float* dlogits, const float* cosv, const long long* label
                  int D, int C, float s, float m, int easy, float eps, float* dW, long long lddw,
                  float* dcs, float* ws, void* stream);
 int tgfr_arc_bwd_ws(int B, int D, int C, long long* floats);
+/* Several ArcMarginProduct heads of the same (B, D, C) (the trainer's text and
+ * image identity classifiers, src/train_encoders_bert.py:293-306) in one
+ * launch each way, n_heads <= 2.  Per head: x [B][D], W [C][D] (dense rows,
+ * 16-byte aligned), label, scale s; outputs as tgfr_arc_fwd.  The backward
+ * (B <= 64) takes the head's focal loss (tgfr_focal_ce_heads) instead of
+ * dlogits: its logit gradient g f'(logp) / B (softmax - onehot) is formed in
+ * place from logits, focal_ws and the upstream gradient g (device scalar,
+ * nullable = 1); writes dW and, when dcs is non-NULL, dcs as tgfr_arc_bwd. */
+typedef struct {
+  const float* x;
+  const float* W;
+  const long long* label;
+  float s;
+  float* logits;
+  float* cosv;
+  float* xn;
+  float* inv_nx;
+  float* inv_nw;
+  const float* focal_ws;
+  const float* g;
+  float* dW;
+  float* dcs;
+} tgfr_arc_head;
+int tgfr_arc_fwd_heads(const tgfr_arc_head* heads, int n_heads, int B, int D, int C, float m,
+                       int easy, float eps, void* stream);
+int tgfr_arc_focal_bwd_heads(const tgfr_arc_head* heads, int n_heads, int B, int D, int C,
+                             float m, int easy, float eps, float gamma, void* stream);
 
 /* ---- optimiser step ------------------------------------------------------
  * Every trainable tensor of a trainer in one launch (replaces the two torch

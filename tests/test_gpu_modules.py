@@ -72,6 +72,41 @@ def test_sent_global_clip(gpu):
     assert abs(fl.item() - float(g["loss"])) < 1e-5
 
 
+@pytest.mark.parametrize("n", [8, 37, 64])
+def test_sent_global_fused(gpu, n):
+    """sent_loss + global_loss in one fused launch each way (kernels.SentGlobal,
+    the single-process stage-1 path) against the oracle's two losses on the
+    same inputs (duplicate class ids exercise the sent mask): losses 1e-4,
+    the image-side gradient of s0 + 2 s1 + 3 gl 1e-4 of its max; and the
+    reference's own sent_loss fixture."""
+    from oracle import tgfr_oracle as O
+    from text_guided_face_recognition_amd.models import losses as L
+    gen = torch.Generator().manual_seed(n)
+    x = torch.randn(n, 256, generator=gen)
+    y = torch.randn(n, 256, generator=gen)
+    cls = torch.randint(0, max(2, n // 3), (n,), generator=gen)
+    xo = x.clone().requires_grad_()
+    r0, r1, _ = O.sent_loss(xo, y, torch.arange(n), cls.numpy(), 10.0)
+    rg, _ = O.global_loss(xo, y)
+    (r0 + 2 * r1 + 3 * rg).backward()
+    xg = x.to(gpu).requires_grad_()
+    s0, s1, gl = L.sent_global_loss(xg, y.to(gpu), torch.arange(n, device=gpu), cls.numpy(), n,
+                                    _args())
+    for a, b in ((s0, r0), (s1, r1), (gl, rg)):
+        assert abs(a.item() - b.item()) < 1e-4
+    (s0 + 2 * s1 + 3 * gl).backward()
+    assert _relerr(xg.grad, xo.grad.numpy()) < 1e-4
+    if n == 8:
+        g = load_golden("sent_loss_b8")
+        xg = t(g["cnn_code"]).to(gpu).requires_grad_()
+        s0, s1, _ = L.sent_global_loss(xg, t(g["rnn_code"]).to(gpu), torch.arange(8, device=gpu),
+                                       g["class_ids"], 8, _args())
+        assert abs(s0.item() - float(g["loss0"])) < 1e-4
+        assert abs(s1.item() - float(g["loss1"])) < 1e-4
+        (s0 + s1).backward()
+        assert _relerr(xg.grad, g["d_cnn"]) < 1e-4
+
+
 @pytest.mark.parametrize("tag", ["c256_hw196", "c36_hw36"])
 def test_self_attention(gpu, tag):
     from text_guided_face_recognition_amd.models.fusion_nets import SelfAttention
@@ -338,6 +373,40 @@ def test_arc_head_fused(gpu, b, d, c, easy, precision):
     out2 = head(x.to(gpu), lab.to(gpu))
     (out2 * probe.to(gpu)).sum().backward()
     assert _relerr(head.weight.grad, wo.grad.numpy()) < 1e-4
+
+
+@pytest.mark.parametrize("b,c,precision", [(64, 4500, "fp32"), (64, 4500, "bf16"),
+                                             (17, 300, "fp32")])
+def test_identity_heads(gpu, b, c, precision):
+    """Both identity heads of the stage-1 step in one launch per direction
+    (kernels.IdentityHeads: two ArcMargin heads, two focal losses, the focal
+    gradient formed inside the ArcMargin backward) against the oracle's
+    focal_loss(arc_margin(...)) per head (src/train_encoders_bert.py:293-306):
+    losses 1e-5, dW of both heads 1e-4, dx of the trained (image) input 1e-4
+    (fp32) / 1e-2 (the bf16 dx GEMM); the text input stays frozen."""
+    from oracle import tgfr_oracle as O
+    from text_guided_face_recognition_amd import kernels as K
+    from text_guided_face_recognition_amd.models.metrics import ArcMarginProduct
+    gen = torch.Generator().manual_seed(b + c)
+    sent = torch.randn(b, 256, generator=gen)
+    img = torch.randn(b, 256, generator=gen)
+    lab = torch.randint(0, c, (b,), generator=gen)
+    tc = ArcMarginProduct(256, c, s=35, m=0.5).to(gpu)
+    ic = ArcMarginProduct(256, c, s=30, m=0.5).to(gpu)
+    tc.precision = ic.precision = precision
+    wt = tc.weight.detach().cpu().clone().requires_grad_()
+    wi = ic.weight.detach().cpu().clone().requires_grad_()
+    xo = img.clone().requires_grad_()
+    rt = O.focal_loss(O.arc_margin(sent, wt, lab, s=35), lab)
+    ri = O.focal_loss(O.arc_margin(xo, wi, lab, s=30), lab)
+    (rt + 3.0 * ri).backward()
+    xg = img.to(gpu).requires_grad_()
+    tid, iid = K.identity_heads(sent.to(gpu), tc, xg, ic, lab.to(gpu), 2.0)
+    assert abs(tid.item() - rt.item()) < 1e-5 and abs(iid.item() - ri.item()) < 1e-5
+    (tid + 3.0 * iid).backward()
+    assert _relerr(tc.weight.grad, wt.grad.numpy()) < 1e-4
+    assert _relerr(ic.weight.grad, wi.grad.numpy()) < 1e-4
+    assert _relerr(xg.grad, xo.grad.numpy()) < (1e-4 if precision == "fp32" else 1e-2)
 
 
 def test_l2norm_rows(gpu):

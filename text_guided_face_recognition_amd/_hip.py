@@ -82,6 +82,11 @@ SIGNATURES = {
     "tgfr_text_pack": [P, P, I, P],
     "tgfr_text_heading_ws": [I, I, P],
     "tgfr_text_heading": [P, I, I, P, P, P, P, L, L, P, L, I, P],
+    "tgfr_sent_global": [P, L, P, L, I, P, F, F, F, P, P, P, P, P],
+    "tgfr_sent_global_bwd": [P, P, P, P, L, P, L, I, P, F, F, F, P, P, P, P, L, P],
+    "tgfr_focal_ce2": [P, P, I, I, P, F, P, P, P, P, P, P],
+    "tgfr_arc_fwd_heads": [P, I, I, I, I, F, I, F, P],
+    "tgfr_arc_focal_bwd_heads": [P, I, I, I, I, F, I, F, F, P],
     "tgfr_fcfm_pack_elems": [],
     "tgfr_maxpool2_cl": [P, I, I, I, I, P, P, P],
     "tgfr_maxpool2_cl_bwd": [P, P, I, I, I, I, P, P],

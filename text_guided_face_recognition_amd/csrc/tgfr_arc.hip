@@ -14,6 +14,7 @@
 // classes (32 in the forward); the class tile of W and a chunk of x rows sit in LDS (rows padded
 // by 4 floats so the 16 classes of a 16-lane group read distinct banks).
 #include "tgfr_common.h"
+#include "../../include/tgfr.h"
 
 #include <math.h>
 
@@ -115,12 +116,36 @@ constexpr int CBF = 32;         // classes per forward block
 constexpr int FRB = 64;         // x rows per forward block
 // FK: k chunk (256 when D <= 256 and B <= 64: one chunk, no re-staging barriers;
 // 128 else, so that several blocks share a CU)
+// Second head (blockIdx.z == 1) of a two-head launch: the trainer's image and
+// text identity classifiers (src/train_encoders_bert.py:293-306) share
+// (B, D, C) and run as one grid.
+struct ArcHead2 {
+  const float* x;
+  const float* W;
+  float* logits;
+  float* cosv;
+  float* xn;
+  float* inv_nx;
+  float* inv_nw;
+  Margin M;
+};
+
 template <int FK>
 __global__ __launch_bounds__(NT) void arc_fwd_kernel(
     const float* __restrict__ x, long long ldx, int B, int D, const float* __restrict__ W,
     long long ldw, int C, const long long* __restrict__ label, Margin M, float eps,
     float* __restrict__ logits, float* __restrict__ cosv, float* __restrict__ xn,
-    float* __restrict__ inv_nx, float* __restrict__ inv_nw) {
+    float* __restrict__ inv_nx, float* __restrict__ inv_nw, ArcHead2 h2) {
+  if (blockIdx.z) {
+    x = h2.x;
+    W = h2.W;
+    logits = h2.logits;
+    cosv = h2.cosv;
+    xn = h2.xn;
+    inv_nx = h2.inv_nx;
+    inv_nw = h2.inv_nw;
+    M = h2.M;
+  }
   float* lds_f = (float*)g_smem;
   const uint32_t w_off = 0, x_off = CBF * (FK + 4) * 4;
   float* nw = lds_f + (CBF + FRB) * (FK + 4);
@@ -245,13 +270,51 @@ __device__ __forceinline__ void arc_dw_epilogue(const float4 (&acc)[MAXJ],
 
 // LDS: dcos [rows_per][CB] | xn chunk [RB][D+4]
 // thread: class c = tid / 16, d-group g = tid % 16 owns dims 4 g + 64 j
+// The head's focal loss (models/losses.py:313-325) as the source of the logit
+// gradient (dlogits == NULL): dlogits[b][c] = g f'(logp) / B (softmax(L_b)[c]
+// - [c == label_b]) formed in place from the logits L, the focal workspace
+// (ws[b] = row LSE, ws[B] = logp) and the upstream gradient g (nullable = 1).
+struct FocalSrc {
+  const float* L;
+  const float* ws;
+  const float* g;
+  float gamma;
+};
+struct ArcBwd2 {
+  const float* cosv;
+  const float* xn;
+  const float* W;
+  const float* inv_nw;
+  float* dW;
+  float* dcs;
+  FocalSrc F;
+  Margin M;
+};
+
 template <int NJ>   // float4 columns per thread: D = 64 NJ (NJ = 0: any D <= 1024)
 __global__ __launch_bounds__(NT) void arc_bwd_kernel(
     const float* __restrict__ dlogits, const float* __restrict__ cosv,
     const long long* __restrict__ label, const float* __restrict__ xn,
     const float* __restrict__ W, long long ldw, const float* __restrict__ inv_nw, int B, int D,
     int C, Margin M, float eps, int RB, float* __restrict__ dW, long long lddw,
-    float* __restrict__ dcs, int rows_per, float* __restrict__ part) {
+    float* __restrict__ dcs, int rows_per, float* __restrict__ part, FocalSrc F, ArcBwd2 h2) {
+  if (blockIdx.z) {
+    cosv = h2.cosv;
+    xn = h2.xn;
+    W = h2.W;
+    inv_nw = h2.inv_nw;
+    dW = h2.dW;
+    dcs = h2.dcs;
+    F = h2.F;
+    M = h2.M;
+  }
+  float fscale = 0.f;
+  if (!dlogits) {
+    const float logp = F.ws[B], p = __expf(-logp), q = 1.f - p;
+    float dfl = powf(q, F.gamma);
+    if (F.gamma != 0.f) dfl += F.gamma * powf(q, F.gamma - 1.f) * p * logp;
+    fscale = (F.g ? F.g[0] : 1.f) * dfl / (float)B;
+  }
   // block row y owns rows [rb0, rb1); with gridDim.y > 1 the raw sums go to
   // part[y][C][D] and arc_bwd_finish_kernel applies the l2-norm backward
   const int rb0 = blockIdx.y * rows_per, rb1 = min(B, rb0 + rows_per), nbs = rb1 - rb0;
@@ -279,7 +342,8 @@ __global__ __launch_bounds__(NT) void arc_bwd_kernel(
       const int i = min(base + u * NT, nbs * CB - 1);
       const int b = rb0 + i / CB, col = min(c0 + i % CB, C - 1);
       const long long e = (long long)b * C + col;
-      gl[u] = dlogits[e];
+      gl[u] = dlogits ? dlogits[e]
+                      : fscale * (__expf(F.L[e] - F.ws[b]) - (label[b] == col ? 1.f : 0.f));
       cv[u] = cosv[e];
       iw[u] = inv_nw[col];
       tg[u] = label[b] == col;
@@ -395,7 +459,7 @@ int tgfr_arc_fwd(const float* x, long long ldx, int B, int D, const float* W, lo
   if (const int e = set_max_lds((const void*)fn, lds)) return e;
   hipLaunchKernelGGL(fn, dim3((C + CBF - 1) / CBF, (B + FRB - 1) / FRB), dim3(NT),
                      lds, (hipStream_t)stream, x, ldx, B, D, W, ldw, C, label,
-                     make_margin(s, m, easy), eps, logits, cosv, xn, inv_nx, inv_nw);
+                     make_margin(s, m, easy), eps, logits, cosv, xn, inv_nx, inv_nw, ArcHead2{});
   return (int)hipGetLastError();
 }
 
@@ -419,7 +483,7 @@ int tgfr_arc_bwd(const float* dlogits, const float* cosv, const long long* label
   if (const int e = set_max_lds((const void*)fn, lds)) return e;
   hipLaunchKernelGGL(fn, dim3((C + CB - 1) / CB, S), dim3(NT), lds, (hipStream_t)stream, dlogits,
                      cosv, label, xn, W, ldw, inv_nw, B, D, C, make_margin(s, m, easy), eps, RB,
-                     dW, lddw, dcs, rows_per, ws);
+                     dW, lddw, dcs, rows_per, ws, FocalSrc{}, ArcBwd2{});
   if (S > 1) {
     using Gn = decltype(&arc_bwd_finish_kernel<0>);
     Gn gn = D == 128 ? &arc_bwd_finish_kernel<2> : D == 256 ? &arc_bwd_finish_kernel<4>
@@ -428,6 +492,59 @@ int tgfr_arc_bwd(const float* dlogits, const float* cosv, const long long* label
     hipLaunchKernelGGL(gn, dim3((C + CB - 1) / CB), dim3(NT), 0, (hipStream_t)stream, ws, S, W,
                        ldw, inv_nw, D, C, eps, dW, lddw);
   }
+  return (int)hipGetLastError();
+}
+
+int tgfr_arc_fwd_heads(const tgfr_arc_head* heads, int n_heads, int B, int D, int C, float m,
+                       int easy, float eps, void* stream) {
+  if (!heads || n_heads < 1 || n_heads > 2 || B <= 0 || B > 4096 || C <= 0 || D <= 0 || D % 8 ||
+      D > 1024)
+    return 1001;
+  for (int k = 0; k < n_heads; ++k)
+    if (!a16(heads[k].x) || !a16(heads[k].W) || !a16(heads[k].xn)) return 1001;
+  const tgfr_arc_head& a = heads[0];
+  ArcHead2 h2{};
+  if (n_heads == 2) {
+    const tgfr_arc_head& b = heads[1];
+    h2 = ArcHead2{b.x, b.W, b.logits, b.cosv, b.xn, b.inv_nx, b.inv_nw, make_margin(b.s, m, easy)};
+  }
+  const int fk = D <= 256 && B <= FRB ? 256 : 128;
+  const int lds = ((CBF + FRB) * (fk + 4) + CBF + 2 * FRB) * 4;
+  auto fn = fk == 256 ? &arc_fwd_kernel<256> : &arc_fwd_kernel<128>;
+  if (const int e = set_max_lds((const void*)fn, lds)) return e;
+  hipLaunchKernelGGL(fn, dim3((C + CBF - 1) / CBF, (B + FRB - 1) / FRB, n_heads), dim3(NT), lds,
+                     (hipStream_t)stream, a.x, (long long)D, B, D, a.W, (long long)D, C, a.label,
+                     make_margin(a.s, m, easy), eps, a.logits, a.cosv, a.xn, a.inv_nx, a.inv_nw,
+                     h2);
+  return (int)hipGetLastError();
+}
+
+int tgfr_arc_focal_bwd_heads(const tgfr_arc_head* heads, int n_heads, int B, int D, int C,
+                             float m, int easy, float eps, float gamma, void* stream) {
+  if (!heads || n_heads < 1 || n_heads > 2 || B <= 0 || B > 64 || C <= 0 || D <= 0 || D % 4 ||
+      D > 1024)
+    return 1001;
+  for (int k = 0; k < n_heads; ++k)
+    if (!a16(heads[k].W) || !a16(heads[k].dW) || !a16(heads[k].xn) || !heads[k].logits ||
+        !heads[k].focal_ws || heads[k].label != heads[0].label)
+      return 1001;
+  const tgfr_arc_head& a = heads[0];
+  ArcBwd2 h2{};
+  if (n_heads == 2) {
+    const tgfr_arc_head& b = heads[1];
+    h2 = ArcBwd2{b.cosv, b.xn, b.W, b.inv_nw, b.dW, b.dcs, FocalSrc{b.logits, b.focal_ws, b.g, gamma},
+                 make_margin(b.s, m, easy)};
+  }
+  const int RB = chunk_rows(B, D, B * CB);
+  const int lds = (B * CB + RB * (D + 4)) * 4;
+  using Fn = decltype(&arc_bwd_kernel<0>);
+  Fn fn = D == 128 ? &arc_bwd_kernel<2> : D == 256 ? &arc_bwd_kernel<4>
+        : D == 512 ? &arc_bwd_kernel<8> : D == 640 ? &arc_bwd_kernel<10> : &arc_bwd_kernel<0>;
+  if (const int e = set_max_lds((const void*)fn, lds)) return e;
+  hipLaunchKernelGGL(fn, dim3((C + CB - 1) / CB, 1, n_heads), dim3(NT), lds, (hipStream_t)stream,
+                     nullptr, a.cosv, a.label, a.xn, a.W, (long long)D, a.inv_nw, B, D, C,
+                     make_margin(a.s, m, easy), eps, RB, a.dW, (long long)D, a.dcs, B, nullptr,
+                     FocalSrc{a.logits, a.focal_ws, a.g, gamma}, h2);
   return (int)hipGetLastError();
 }
 

@@ -198,6 +198,198 @@ __global__ __launch_bounds__(256) void ce_grad_kernel(const float* __restrict__ 
   dL[b * ldd + c] = g0 * (__expf(v - row_lse[b]) - onehot) + g1 * (__expf(v - col_lse[c]) - onehot);
 }
 
+// ------------------------------------- sent_loss + global_loss, one rank ---
+// The two contrastive losses of the stage-1 step on the same pair of feature
+// sets (sent_loss, models/losses.py:19-57, and global_loss, :329-351: both
+// are cos(img_b, sent_i) / max(|img||sent|, eps) logits, the first scaled by
+// gamma3 with the same-class mask, the second by temp3 without) when one
+// process holds the whole batch (n <= 64): one workgroup forms the n x n
+// cosines (split-bf16 MFMA, ~fp32 products; fp32 norms), both logit sets,
+// their row / column log-sum-exps and the four cross-entropies; the
+// backward is one launch of n row workgroups (softmax gradients of both
+// losses folded into one dcos, then the cosine backward to img).
+constexpr int SG_N = 64;
+
+// 8 fp32 -> bf16x8 hi and lo = bf16(x - hi) by packed conversions
+__device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8& hi, bf16x8& lo) {
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    h[k] = pk_bf16(v[2 * k], v[2 * k + 1]);
+    l[k] = pk_bf16(v[2 * k] - __uint_as_float(h[k] << 16),
+                   v[2 * k + 1] - __uint_as_float(h[k] & 0xffff0000u));
+  }
+  hi = as_bf8(make_uint4(h[0], h[1], h[2], h[3]));
+  lo = as_bf8(make_uint4(l[0], l[1], l[2], l[3]));
+}
+
+constexpr int SG_LD = D + 4;                 // padded fp32 LDS rows (bank spread)
+constexpr int SG_LDS = 2 * SG_N * SG_LD * 4 + SG_N * (SG_N + 1) * 4;
+
+__global__ __launch_bounds__(256) void sg_fwd_kernel(
+    const float* __restrict__ x, long long ldx, const float* __restrict__ y, long long ldy, int n,
+    const long long* __restrict__ cls, float s_sent, float s_glob, float eps,
+    float* __restrict__ cosv, float* __restrict__ stats, float* __restrict__ nrm,
+    float* __restrict__ loss) {
+  // LDS: x rows | y rows (fp32, padded) | cos [64][65]
+  float* xs = (float*)g_smem;
+  float* ys = xs + SG_N * SG_LD;
+  float* cs = ys + SG_N * SG_LD;
+  __shared__ float nx2[SG_N], ny2[SG_N];
+  __shared__ long long cl[SG_N];
+  __shared__ float red[8];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 31, h = lane >> 5;
+  if (tid < n) cl[tid] = cls[tid];
+  // stage both row sets, 8 + 8 float4 loads of a thread in flight per round
+  // (rows >= n are left unwritten: an output element reads only its own row
+  // of each operand, and those outputs are discarded)
+  {
+    constexpr int NQ = SG_N * D / 4 / 256;   // float4 per thread per matrix
+    constexpr int U = 8;
+    const uint32_t yoff = SG_N * SG_LD * 4;
+#pragma unroll
+    for (int u0 = 0; u0 < NQ; u0 += U) {
+      uint4 vx[U], vy[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = (u0 + u) * 256 + tid, r = min(i / (D / 4), n - 1), k = i % (D / 4);
+        vx[u] = *(const uint4*)(x + r * ldx + 4 * k);
+        vy[u] = *(const uint4*)(y + r * ldy + 4 * k);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = (u0 + u) * 256 + tid, r = i / (D / 4), k = i % (D / 4);
+        const uint32_t o = (uint32_t)(r * SG_LD + 4 * k) * 4;
+        lds_st16(o, vx[u]);
+        lds_st16(yoff + o, vy[u]);
+      }
+    }
+  }
+  __syncthreads();
+  // n x n cosines: wave w owns the 32 x 32 tile (w >> 1, w & 1)
+  const int rt = w >> 1, ct = w & 1;
+  if (32 * rt < n && 32 * ct < n) {
+    const int ra = 32 * rt + lr, rb = 32 * ct + lr;
+    f32x16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    float sx = 0.f, sy = 0.f;
+#pragma unroll 4
+    for (int s = 0; s < D / 16; ++s) {
+      const int k0 = 16 * s + 8 * h;
+      const float4 a0 = *(const float4*)(xs + ra * SG_LD + k0);
+      const float4 a1 = *(const float4*)(xs + ra * SG_LD + k0 + 4);
+      const float4 b0 = *(const float4*)(ys + rb * SG_LD + k0);
+      const float4 b1 = *(const float4*)(ys + rb * SG_LD + k0 + 4);
+      sx = fmaf(a0.x, a0.x, fmaf(a0.y, a0.y, fmaf(a0.z, a0.z, fmaf(a0.w, a0.w, sx))));
+      sx = fmaf(a1.x, a1.x, fmaf(a1.y, a1.y, fmaf(a1.z, a1.z, fmaf(a1.w, a1.w, sx))));
+      sy = fmaf(b0.x, b0.x, fmaf(b0.y, b0.y, fmaf(b0.z, b0.z, fmaf(b0.w, b0.w, sy))));
+      sy = fmaf(b1.x, b1.x, fmaf(b1.y, b1.y, fmaf(b1.z, b1.z, fmaf(b1.w, b1.w, sy))));
+      bf16x8 ah, al, bh, bl;
+      split8(a0, a1, ah, al);
+      split8(b0, b1, bh, bl);
+      mma<MODE_SPLIT>(acc, ah, al, bh, bl);
+    }
+    sx += __shfl_xor(sx, 32);
+    sy += __shfl_xor(sy, 32);
+    if (h == 0 && ct == 0 && ra < n) nx2[ra] = sx;
+    if (h == 0 && rt == 0 && rb < n) ny2[rb] = sy;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r = 32 * rt + acc_row(q, h), c = rb;
+      if (r < n && c < n) {
+        const float cv = acc[q] / fmaxf(sqrtf(nx2[r]) * sqrtf(ny2[c]), eps);
+        cs[r * (SG_N + 1) + c] = cv;
+        cosv[r * n + c] = cv;
+      }
+    }
+  } else {
+    __syncthreads();
+  }
+  __syncthreads();
+  // wave 0: sent rows, 1: sent columns, 2: global rows, 3: global columns;
+  // lane j < n owns row / column j (online log-sum-exp)
+  const bool glob = w >= 2, col = w & 1;
+  const float sc = glob ? s_glob : s_sent;
+  float term = 0.f;
+  if (lane < n) {
+    const int j = lane;
+    float m = -INFINITY, sum = 0.f;
+    for (int k = 0; k < n; ++k) {
+      const int b = col ? k : j, i = col ? j : k;
+      if (!glob && cl[b] == cl[i] && b != i) continue;
+      const float L = sc * cs[b * (SG_N + 1) + i];
+      if (L > m) {
+        sum = sum * __expf(m - L) + 1.f;
+        m = L;
+      } else {
+        sum += __expf(L - m);
+      }
+    }
+    const float lse = m + __logf(sum);
+    stats[w * n + j] = lse;
+    term = lse - sc * cs[j * (SG_N + 1) + j];
+  }
+  term = wave_sum(term);
+  if (lane == 0) red[w] = term;
+  if (tid < n) {
+    nrm[tid] = sqrtf(nx2[tid]);
+    nrm[n + tid] = sqrtf(ny2[tid]);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const float inv = 1.f / (float)n;
+    loss[0] = red[0] * inv;                  // sent loss0 (rows)
+    loss[1] = red[1] * inv;                  // sent loss1 (columns)
+    loss[2] = (red[2] + red[3]) * inv;       // global loss0 + loss1
+  }
+}
+
+// grid n (row b of img), 256 threads (thread = feature d)
+__global__ __launch_bounds__(256) void sg_bwd_kernel(
+    const float* __restrict__ gs0, const float* __restrict__ gs1, const float* __restrict__ ggl,
+    const float* __restrict__ x, long long ldx, const float* __restrict__ y, long long ldy, int n,
+    const long long* __restrict__ cls, float s_sent, float s_glob, float eps,
+    const float* __restrict__ cosv, const float* __restrict__ stats, const float* __restrict__ nrm,
+    float* __restrict__ dx, long long lddx) {
+  __shared__ float cf[SG_N];
+  __shared__ float red[4];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float a0 = gs0 ? *gs0 : 0.f, a1 = gs1 ? *gs1 : 0.f, ag = ggl ? *ggl : 0.f;
+  const float inv_n = 1.f / (float)n, nxb = nrm[b];
+  float xcoef = 0.f;
+  if (tid < n) {
+    const int i = tid;
+    const float cv = cosv[b * n + i];
+    const float dg = i == b ? 1.f : 0.f;
+    const bool masked = cls[b] == cls[i] && b != i;
+    float dls = 0.f;
+    if (!masked) {
+      const float L = s_sent * cv;
+      dls = a0 * (__expf(L - stats[b]) - dg) + a1 * (__expf(L - stats[n + i]) - dg);
+    }
+    const float Lg = s_glob * cv;
+    const float dlg = ag * ((__expf(Lg - stats[2 * n + b]) - dg) + (__expf(Lg - stats[3 * n + i]) - dg));
+    const float dcos = (s_sent * dls + s_glob * dlg) * inv_n;
+    const float den = nxb * nrm[n + i];
+    if (den >= eps) {
+      cf[i] = dcos / den;
+      xcoef = -dcos * cv / (nxb * nxb);
+    } else {
+      cf[i] = dcos / eps;
+    }
+  }
+  xcoef = wave_sum(xcoef);
+  if ((tid & 63) == 0) red[tid >> 6] = xcoef;
+  __syncthreads();
+  xcoef = red[0] + red[1] + red[2] + red[3];
+  float acc = xcoef * x[b * ldx + tid];
+  for (int i = 0; i < n; ++i) acc = fmaf(cf[i], y[i * ldy + tid], acc);
+  dx[b * lddx + tid] = acc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -232,6 +424,30 @@ int tgfr_ce_stats(const float* L, long long ld, int n_r, int n_c, float* row_lse
   hipLaunchKernelGGL(ce_stats_kernel, dim3(gx, 2), dim3(256), 0, (hipStream_t)stream, L, ld,
                      n_r, n_c, row_lse, col_max, col_sum, col_lse, row_offset, inv_n, loss,
                      counters);
+  return (int)hipGetLastError();
+}
+
+int tgfr_sent_global(const float* x, long long ldx, const float* y, long long ldy, int n,
+                     const long long* cls, float s_sent, float s_glob, float eps, float* cosv,
+                     float* stats, float* nrm, float* loss, void* stream) {
+  if (n <= 0 || n > SG_N || !x || !y || !cls || !cosv || !stats || !nrm || !loss || ldx % 4 ||
+      ldy % 4 || ((uintptr_t)x & 15) || ((uintptr_t)y & 15))
+    return 1001;
+  if (const int e = set_max_lds((const void*)sg_fwd_kernel, SG_LDS)) return e;
+  hipLaunchKernelGGL(sg_fwd_kernel, dim3(1), dim3(256), SG_LDS, (hipStream_t)stream, x, ldx, y,
+                     ldy, n,
+                     cls, s_sent, s_glob, eps, cosv, stats, nrm, loss);
+  return (int)hipGetLastError();
+}
+
+int tgfr_sent_global_bwd(const float* gs0, const float* gs1, const float* ggl, const float* x,
+                         long long ldx, const float* y, long long ldy, int n,
+                         const long long* cls, float s_sent, float s_glob, float eps,
+                         const float* cosv, const float* stats, const float* nrm, float* dx,
+                         long long lddx, void* stream) {
+  if (n <= 0 || n > SG_N || !x || !y || !cls || !cosv || !stats || !nrm || !dx) return 1001;
+  hipLaunchKernelGGL(sg_bwd_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, gs0, gs1, ggl, x,
+                     ldx, y, ldy, n, cls, s_sent, s_glob, eps, cosv, stats, nrm, dx, lddx);
   return (int)hipGetLastError();
 }
 

@@ -106,13 +106,24 @@ __global__ __launch_bounds__(256) void arc_margin_bwd_kernel(const float* __rest
 
 // one block per row: ws[b] = row LSE, ws[rows + 1 + b] = row NLL; the last
 // block forms ws[rows] = logp = mean NLL (row order) and the focal loss
+// blockIdx.y = 1: a second head (L2, ws2, loss2, the next counter word) on
+// the same labels, so the trainer's two identity losses take one launch
 __global__ __launch_bounds__(256) void focal_ce_kernel(const float* __restrict__ L, int cols,
                                                        const long long* __restrict__ label,
                                                        int rows, float gamma,
                                                        float* __restrict__ ws,
                                                        unsigned* __restrict__ counter,
-                                                       float* __restrict__ loss) {
+                                                       float* __restrict__ loss,
+                                                       const float* __restrict__ L2,
+                                                       float* __restrict__ ws2,
+                                                       float* __restrict__ loss2) {
   __shared__ float red[5];
+  if (blockIdx.y) {
+    L = L2;
+    ws = ws2;
+    loss = loss2;
+    counter += 1;
+  }
   const int b = blockIdx.x, wid = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
   const float* r = L + (long long)b * cols;
   float m = -INFINITY;
@@ -406,7 +417,16 @@ int tgfr_focal_ce(const float* L, int rows, int cols, const long long* label, fl
                   float* ws, unsigned* counters, float* loss, void* stream) {
   if (rows <= 0 || cols <= 0 || !counters) return 1001;
   hipLaunchKernelGGL(focal_ce_kernel, dim3(rows), dim3(256), 0, (hipStream_t)stream, L, cols,
-                     label, rows, gamma, ws, counters, loss);
+                     label, rows, gamma, ws, counters, loss, nullptr, nullptr, nullptr);
+  return (int)hipGetLastError();
+}
+
+int tgfr_focal_ce2(const float* L, const float* L2, int rows, int cols, const long long* label,
+                   float gamma, float* ws, float* ws2, unsigned* counters, float* loss,
+                   float* loss2, void* stream) {
+  if (rows <= 0 || cols <= 0 || !counters || !L2 || !ws2 || !loss2) return 1001;
+  hipLaunchKernelGGL(focal_ce_kernel, dim3(rows, 2), dim3(256), 0, (hipStream_t)stream, L, cols,
+                     label, rows, gamma, ws, counters, loss, L2, ws2, loss2);
   return (int)hipGetLastError();
 }
 

@@ -322,6 +322,49 @@ def contrastive_ce(logits, row_offset=0, n_global=None, group=None):
     return ContrastiveCE.apply(logits, row_offset, n_global, group)
 
 
+class SentGlobal(torch.autograd.Function):
+    """(sent loss0, sent loss1, global loss) of one process holding the whole
+    batch (n <= 64): sent_loss (models/losses.py:19-57, gamma3, same-class
+    mask) and global_loss (:329-351, temp3) share one cosine matrix, one
+    forward launch and one backward launch (tgfr_sent_global).  Gradient to
+    the image side only (the text side is detached, utils/dataset_utils.py:42)."""
+
+    @staticmethod
+    def forward(ctx, x, y, cls, s_sent, s_glob, eps):
+        x = _aligned(x)
+        y = _aligned(y)
+        n = x.shape[0]
+        dev = x.device
+        cls = cls.to(device=dev, dtype=torch.int64).contiguous()
+        cosv = torch.empty(n, n, dtype=torch.float32, device=dev)
+        stats = torch.empty(4, n, dtype=torch.float32, device=dev)
+        nrm = torch.empty(2, n, dtype=torch.float32, device=dev)
+        loss = torch.empty(3, dtype=torch.float32, device=dev)
+        call("tgfr_sent_global", ptr(x), x.stride(0), ptr(y), y.stride(0), n, ptr(cls),
+             float(s_sent), float(s_glob), float(eps), ptr(cosv), ptr(stats), ptr(nrm), ptr(loss),
+             _hip.stream())
+        ctx.save_for_backward(x, y, cls, cosv, stats, nrm)
+        ctx.cfg = (float(s_sent), float(s_glob), float(eps))
+        ctx.set_materialize_grads(False)
+        return loss[0], loss[1], loss[2]
+
+    @staticmethod
+    def backward(ctx, gs0, gs1, ggl):
+        x, y, cls, cosv, stats, nrm = ctx.saved_tensors
+        s_sent, s_glob, eps = ctx.cfg
+        n = x.shape[0]
+        dx = torch.empty_like(x)
+        g = [None if v is None else v.float().contiguous() for v in (gs0, gs1, ggl)]
+        call("tgfr_sent_global_bwd", ptr(g[0]), ptr(g[1]), ptr(g[2]), ptr(x), x.stride(0),
+             ptr(y), y.stride(0), n, ptr(cls), s_sent, s_glob, eps, ptr(cosv), ptr(stats),
+             ptr(nrm), ptr(dx), dx.stride(0), _hip.stream())
+        return dx, None, None, None, None, None
+
+
+def sent_global(x, y, cls, s_sent, s_glob, eps=1e-8):
+    return SentGlobal.apply(x, y, cls, s_sent, s_glob, eps)
+
+
 # ------------------------------------------------------------------ bgemm ---
 def bgemm(a, b, out=None, alpha=1.0, accumulate=False, mode="fp32", bias=None,
           relu=False, ksplit=1):
@@ -1025,6 +1068,100 @@ def arc_bwd_ws_floats(b, d, c):
 
 def arc_head(x, weight, label, s, m, easy_margin=False, eps=1e-12, mode="fp32"):
     return ArcHead.apply(x, weight, label, s, m, easy_margin, eps, mode)
+
+
+class _ArcHeadArgs(ctypes.Structure):
+    """tgfr_arc_head (include/tgfr.h)."""
+    _fields_ = [("x", ctypes.c_void_p), ("W", ctypes.c_void_p), ("label", ctypes.c_void_p),
+                ("s", ctypes.c_float), ("logits", ctypes.c_void_p), ("cosv", ctypes.c_void_p),
+                ("xn", ctypes.c_void_p), ("inv_nx", ctypes.c_void_p),
+                ("inv_nw", ctypes.c_void_p), ("focal_ws", ctypes.c_void_p),
+                ("g", ctypes.c_void_p), ("dW", ctypes.c_void_p), ("dcs", ctypes.c_void_p)]
+
+
+class IdentityHeads(torch.autograd.Function):
+    """The stage-1 step's two identity losses, focal(ArcMargin_text(sent)) and
+    focal(ArcMargin_image(img)) (src/train_encoders_bert.py:293-306, one
+    process, B <= 64, heads of one (D, C)): both heads' cosine + margin in one
+    launch, both focal losses in one launch; backward: the focal logit
+    gradient formed inside the ArcMargin backward of both heads (one launch),
+    then dx of the heads whose input is trained (dcs W GEMM + l2-norm
+    backward, as ArcHead)."""
+
+    @staticmethod
+    def forward(ctx, x_t, w_t, x_i, w_i, label, s_t, s_i, m, easy, eps, gamma, mode):
+        xs = [_aligned(x_t), _aligned(x_i)]
+        ws_ = [_aligned(w_t), _aligned(w_i)]
+        label = label.to(torch.int64).contiguous()
+        b, d = xs[0].shape
+        c = ws_[0].shape[0]
+        dev = xs[0].device
+        out = []
+        heads = (_ArcHeadArgs * 2)()
+        for k, sc in enumerate((s_t, s_i)):
+            t = {"logits": torch.empty(b, c, dtype=torch.float32, device=dev),
+                 "cosv": torch.empty(b, c, dtype=torch.float32, device=dev),
+                 "xn": torch.empty_like(xs[k]),
+                 "inv_nx": torch.empty(b, dtype=torch.float32, device=dev),
+                 "inv_nw": torch.empty(c, dtype=torch.float32, device=dev),
+                 "fws": torch.empty(2 * b + 1, dtype=torch.float32, device=dev),
+                 "loss": torch.empty(1, dtype=torch.float32, device=dev)}
+            out.append(t)
+            heads[k] = _ArcHeadArgs(ptr(xs[k]), ptr(ws_[k]), ptr(label), float(sc),
+                                    ptr(t["logits"]), ptr(t["cosv"]), ptr(t["xn"]),
+                                    ptr(t["inv_nx"]), ptr(t["inv_nw"]), None, None, None, None)
+        call("tgfr_arc_fwd_heads", ctypes.addressof(heads), 2, b, d, c, float(m), int(easy),
+             float(eps), _hip.stream())
+        call("tgfr_focal_ce2", ptr(out[0]["logits"]), ptr(out[1]["logits"]), b, c, ptr(label),
+             float(gamma), ptr(out[0]["fws"]), ptr(out[1]["fws"]), ptr(_hip.counters(dev)),
+             ptr(out[0]["loss"]), ptr(out[1]["loss"]), _hip.stream())
+        ctx.save_for_backward(ws_[0], ws_[1], label,
+                              *[out[k][n] for k in range(2)
+                                for n in ("logits", "cosv", "xn", "inv_nx", "inv_nw", "fws")])
+        ctx.cfg = (float(s_t), float(s_i), float(m), int(easy), float(eps), float(gamma), mode)
+        return out[0]["loss"][0], out[1]["loss"][0]
+
+    @staticmethod
+    def backward(ctx, g_t, g_i):
+        w_t, w_i, label, *rest = ctx.saved_tensors
+        s_t, s_i, m, easy, eps, gamma, mode = ctx.cfg
+        per = [dict(zip(("logits", "cosv", "xn", "inv_nx", "inv_nw", "fws"), rest[6 * k:6 * k + 6]))
+               for k in range(2)]
+        ws_ = (w_t, w_i)
+        b, d = per[0]["xn"].shape
+        c = w_t.shape[0]
+        dev = w_t.device
+        want_dx = (ctx.needs_input_grad[0], ctx.needs_input_grad[2])
+        gs = [g.float().reshape(1).contiguous() for g in (g_t, g_i)]
+        dws = [torch.empty_like(w) for w in ws_]
+        dcs = [torch.empty(b, c, dtype=torch.float32, device=dev) if want_dx[k] else None
+               for k in range(2)]
+        heads = (_ArcHeadArgs * 2)()
+        for k, sc in enumerate((s_t, s_i)):
+            t = per[k]
+            heads[k] = _ArcHeadArgs(None, ptr(ws_[k]), ptr(label), sc, ptr(t["logits"]),
+                                    ptr(t["cosv"]), ptr(t["xn"]), ptr(t["inv_nx"]),
+                                    ptr(t["inv_nw"]), ptr(t["fws"]), ptr(gs[k]), ptr(dws[k]),
+                                    ptr(dcs[k]))
+        call("tgfr_arc_focal_bwd_heads", ctypes.addressof(heads), 2, b, d, c, m, easy, eps, gamma,
+             _hip.stream())
+        dx = [None, None]
+        for k in range(2):
+            if want_dx[k]:
+                mb = -(-b // 64) * -(-d // 64)
+                dxn = bgemm(dcs[k].unsqueeze(0), ws_[k].unsqueeze(0), mode=mode,
+                            ksplit=_ksplit(c, mb))[0]
+                dx[k] = torch.empty_like(per[k]["xn"])
+                call("tgfr_l2norm_rows_bwd", ptr(dxn), d, ptr(per[k]["xn"]), d,
+                     ptr(per[k]["inv_nx"]), b, d, eps, ptr(dx[k]), d, _hip.stream())
+        return (dx[0], dws[0], dx[1], dws[1]) + (None,) * 8
+
+
+def identity_heads(x_t, head_t, x_i, head_i, label, gamma, eps=1e-12):
+    """(focal(head_t(x_t)), focal(head_i(x_i))) for two ArcMarginProduct
+    modules of one (D, C) and margin: kernels.IdentityHeads."""
+    return IdentityHeads.apply(x_t, head_t.weight, x_i, head_i.weight, label, head_t.s, head_i.s,
+                               head_t.m, head_t.easy_margin, eps, gamma, head_t.precision)
 
 
 class FocalCE(torch.autograd.Function):

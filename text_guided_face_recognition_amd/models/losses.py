@@ -140,6 +140,22 @@ def global_loss(cnn_code, rnn_code, eps=1e-8, temp3=10.0, args=None):
     return l0 + l1
 
 
+def sent_global_loss(cnn_code, rnn_code, labels, class_ids, batch_size, args, eps=1e-8,
+                     temp3=10.0):
+    """(sent loss0, sent loss1, global loss) = sent_loss(...) and
+    global_loss(..., temp3) of the trainer (src/train_encoders_bert.py:276-277,
+    :310) on the same features.  One process with the whole batch (n <= 64):
+    one fused kernel each way (kernels.SentGlobal); otherwise the two losses
+    as above."""
+    row_offset, n_global, group = _dist(args)
+    n = cnn_code.shape[0]
+    if group is None and n == rnn_code.shape[0] and n <= 64 and labels is not None:
+        cls = _class_tensor(class_ids, cnn_code.device)
+        return K.sent_global(cnn_code, rnn_code, cls, args.TRAIN.SMOOTH.GAMMA3, temp3, eps)
+    s0, s1 = sent_loss(cnn_code, rnn_code, labels, class_ids, batch_size, args, eps)
+    return s0, s1, global_loss(cnn_code, rnn_code, eps, temp3, args)
+
+
 class ClipLoss(nn.Module):
     """losses.py:268-309: un-normalised logits, mean of the two CEs."""
 

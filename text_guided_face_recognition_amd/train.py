@@ -33,7 +33,7 @@ import torch
 from . import kernels as K
 from .dist import DistContext, StepCapture
 from .models.fusion_nets import Working, set_precision
-from .models.losses import ClipLoss, FocalLoss, global_loss, sent_loss, words_loss
+from .models.losses import ClipLoss, FocalLoss, sent_global_loss, words_loss
 from .models.metrics import ArcMarginProduct
 from .models.models import ImageHeading
 from .optim import FusedOptimizer, adam_group, sgd_group
@@ -120,13 +120,9 @@ class Train:
         # branches forked onto side streams (0.665 vs 0.694 ms at config 2,
         # tools/lab/branch_ab.py) -- the word<->region kernels fill the chip.
         wi, lc = float(args.lambda_id), float(args.lambda_clip)
-        s0, s1 = sent_loss(img_features, sent_g, labels, cls_g, b, args)
-        cl = global_loss(img_features, sent_g, args=args)      # :310
+        s0, s1, cl = sent_global_loss(img_features, sent_g, labels, cls_g, b, args)  # :276, :310
         # :293-306, both focal losses from the global-batch mean CE
-        tid, iid = K.focal_ce_multi(
-            [(self.text_cls(sent, class_ids), class_ids),
-             (self.image_cls(img_features, class_ids), class_ids)],
-            self.ident_loss.gamma, ctx.group if ctx.active else None, ctx.n_global)
+        tid, iid = self._identity(sent, img_features, class_ids, ctx)
         torch.autograd.backward((s0, s1, cl, tid, iid),
                                 self._weights((1.0, 1.0, lc, wi, wi), g.device))
         w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
@@ -142,6 +138,18 @@ class Train:
         ctx.reduce_grads(self.params)
         self.optimizer.step()
         return {"damsm": report[0], "clip": report[1], "ident": report[2]}
+
+    def _identity(self, sent, img_features, class_ids, ctx):
+        """(focal(text_cls(sent)), focal(image_cls(img))): one launch per
+        direction for both heads on one process (kernels.IdentityHeads),
+        else the per-head path with the global-batch focal factor."""
+        tc, ic = self.text_cls, self.image_cls
+        if (not ctx.active and sent.shape[0] <= 64 and tc.weight.shape == ic.weight.shape
+                and tc.m == ic.m and tc.easy_margin == ic.easy_margin):
+            return K.identity_heads(sent, tc, img_features, ic, class_ids, self.ident_loss.gamma)
+        return K.focal_ce_multi(
+            [(tc(sent, class_ids), class_ids), (ic(img_features, class_ids), class_ids)],
+            self.ident_loss.gamma, ctx.group if ctx.active else None, ctx.n_global)
 
     def _weights(self, values, device):
         """Constant device scalars (the loss terms' weights, cached)."""

@@ -361,6 +361,15 @@ int tgfr_bn_fold(const float* W, const float* b, int O, int C, const float* gamm
 int tgfr_bn_unfold(const float* G, const float* s, const float* W, int O, int C,
                    const float* gamma, const float* beta, float* dW, float* dgamma, float* dbeta,
                    float* ws, unsigned* counters, void* stream);
+/* tgfr_bn_fold / tgfr_bn_unfold with W (and b) given as 3 row blocks of
+ * `rows` rows each (host arrays of 3 device pointers; b nullable, and each
+ * of its entries nullable): the three 1x1 projections of a self-attention
+ * (key, query, value) read in place.  Wf, bf, dW are the packed [3 rows][C]. */
+int tgfr_bn_fold3(const float* const* W, const float* const* b, int rows, int C,
+                  const float* gamma, const float* beta, float* Wf, float* bf, void* stream);
+int tgfr_bn_unfold3(const float* G, const float* s, const float* const* W, int rows, int C,
+                    const float* gamma, const float* beta, float* dW, float* dgamma,
+                    float* dbeta, float* ws, unsigned* counters, void* stream);
 
 /* ---- ArcMarginProduct (models/metrics.py:17-60), fused --------------------
  * tgfr_arc_fwd: logits[b][c] = s * margin(cos[b][c]) with cos = normalize(x_b)

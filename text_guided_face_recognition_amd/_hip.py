@@ -87,6 +87,8 @@ SIGNATURES = {
     "tgfr_focal_ce2": [P, P, I, I, P, F, P, P, P, P, P, P],
     "tgfr_arc_fwd_heads": [P, I, I, I, I, F, I, F, P],
     "tgfr_arc_focal_bwd_heads": [P, I, I, I, I, F, I, F, F, P],
+    "tgfr_bn_fold3": [P, P, I, I, P, P, P, P, P],
+    "tgfr_bn_unfold3": [P, P, P, I, I, P, P, P, P, P, P, P, P],
     "tgfr_fcfm_pack_elems": [],
     "tgfr_maxpool2_cl": [P, I, I, I, I, P, P, P],
     "tgfr_maxpool2_cl_bwd": [P, P, I, I, I, I, P, P],

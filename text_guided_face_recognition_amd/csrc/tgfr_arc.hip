@@ -508,9 +508,11 @@ int tgfr_arc_fwd_heads(const tgfr_arc_head* heads, int n_heads, int B, int D, in
     const tgfr_arc_head& b = heads[1];
     h2 = ArcHead2{b.x, b.W, b.logits, b.cosv, b.xn, b.inv_nx, b.inv_nw, make_margin(b.s, m, easy)};
   }
-  const int fk = D <= 256 && B <= FRB ? 256 : 128;
+  // 128-wide k chunks (~51 KB LDS): several blocks per CU, so both heads'
+  // class blocks run in one round
+  constexpr int fk = 128;
   const int lds = ((CBF + FRB) * (fk + 4) + CBF + 2 * FRB) * 4;
-  auto fn = fk == 256 ? &arc_fwd_kernel<256> : &arc_fwd_kernel<128>;
+  auto fn = &arc_fwd_kernel<fk>;
   if (const int e = set_max_lds((const void*)fn, lds)) return e;
   hipLaunchKernelGGL(fn, dim3((C + CBF - 1) / CBF, (B + FRB - 1) / FRB, n_heads), dim3(NT), lds,
                      (hipStream_t)stream, a.x, (long long)D, B, D, a.W, (long long)D, C, a.label,
@@ -535,7 +537,8 @@ int tgfr_arc_focal_bwd_heads(const tgfr_arc_head* heads, int n_heads, int B, int
     h2 = ArcBwd2{b.cosv, b.xn, b.W, b.inv_nw, b.dW, b.dcs, FocalSrc{b.logits, b.focal_ws, b.g, gamma},
                  make_margin(b.s, m, easy)};
   }
-  const int RB = chunk_rows(B, D, B * CB);
+  // 16-row x chunks (~21 KB LDS at D = 256): both heads' class blocks in one round
+  const int RB = std::min(16, B);
   const int lds = (B * CB + RB * (D + 4)) * 4;
   using Fn = decltype(&arc_bwd_kernel<0>);
   Fn fn = D == 128 ? &arc_bwd_kernel<2> : D == 256 ? &arc_bwd_kernel<4>

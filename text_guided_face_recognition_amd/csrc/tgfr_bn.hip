@@ -135,22 +135,40 @@ __global__ __launch_bounds__(256) void bn_bwd_cl_kernel(const float* __restrict_
 }
 
 // one wave per output row o
-__global__ __launch_bounds__(256) void bn_fold_kernel(const float* __restrict__ W,
-                                                      const float* __restrict__ b, int O, int C,
+// A weight [O][C] given as up to 3 row blocks of `rows` rows each (the
+// three 1x1 projections of a self-attention, read in place: no concatenated
+// copy), and their biases (each nullable).
+struct Parts {
+  const float* w[3];
+  const float* b[3];
+  int rows;
+  __device__ __forceinline__ const float* row(int o, int C) const {
+    const int p = o / rows;
+    return (p == 0 ? w[0] : p == 1 ? w[1] : w[2]) + (long long)(o - p * rows) * C;
+  }
+  __device__ __forceinline__ float bias(int o) const {
+    const int p = o / rows;
+    const float* bp = p == 0 ? b[0] : p == 1 ? b[1] : b[2];
+    return bp ? bp[o - p * rows] : 0.f;
+  }
+};
+
+__global__ __launch_bounds__(256) void bn_fold_kernel(Parts P, int O, int C,
                                                       const float* __restrict__ gamma,
                                                       const float* __restrict__ beta,
                                                       float* __restrict__ Wf,
                                                       float* __restrict__ bf) {
   const int o = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
   if (o >= O) return;
+  const float* wr = P.row(o, C);
   float acc = 0.f;
   for (int c = lane; c < C; c += WAVE) {
-    const float w = W[(long long)o * C + c];
+    const float w = wr[c];
     Wf[(long long)o * C + c] = w * gamma[c];
     acc += w * beta[c];
   }
   acc = wave_sum(acc);
-  if (lane == 0) bf[o] = (b ? b[o] : 0.f) + acc;
+  if (lane == 0) bf[o] = P.bias(o) + acc;
 }
 
 // grid (ceil(C / 64), ceil(O / 64)); block = 64 columns x 4 row lanes over a
@@ -158,7 +176,7 @@ __global__ __launch_bounds__(256) void bn_fold_kernel(const float* __restrict__ 
 // chunks are combined by the last chunk of each column group (chunk order).
 constexpr int UF_ROWS = 64;
 __global__ __launch_bounds__(256) void bn_unfold_kernel(
-    const float* __restrict__ G, const float* __restrict__ s, const float* __restrict__ W, int O,
+    const float* __restrict__ G, const float* __restrict__ s, Parts W, int O,
     int C, const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dW,
     float* __restrict__ part, unsigned* __restrict__ counters, float* __restrict__ dgamma,
     float* __restrict__ dbeta) {
@@ -172,7 +190,7 @@ __global__ __launch_bounds__(256) void bn_unfold_kernel(
 #pragma unroll 4
     for (int o = o0 + ry; o < o1; o += 4) {
       const long long e = (long long)o * C + c;
-      const float gv = G[e], w = W[e], so = s[o];
+      const float gv = G[e], w = W.row(o, C)[c], so = s[o];
       dW[e] = gv * g + so * bt;
       ag += w * gv;
       ab += w * so;
@@ -229,20 +247,45 @@ int tgfr_bn_fwd_cl(const float* x, int N, int C, int HW, float eps, float moment
 int tgfr_bn_fold(const float* W, const float* b, int O, int C, const float* gamma,
                  const float* beta, float* Wf, float* bf, void* stream) {
   if (O <= 0 || C <= 0) return 1001;
-  hipLaunchKernelGGL(bn_fold_kernel, dim3((O + 3) / 4), dim3(256), 0, (hipStream_t)stream, W, b,
-                     O, C, gamma, beta, Wf, bf);
+  hipLaunchKernelGGL(bn_fold_kernel, dim3((O + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     Parts{{W, W, W}, {b, b, b}, O}, O, C, gamma, beta, Wf, bf);
+  return (int)hipGetLastError();
+}
+
+int tgfr_bn_fold3(const float* const* W, const float* const* b, int rows, int C,
+                  const float* gamma, const float* beta, float* Wf, float* bf, void* stream) {
+  if (!W || rows <= 0 || C <= 0 || !W[0] || !W[1] || !W[2]) return 1001;
+  const Parts P{{W[0], W[1], W[2]}, {b ? b[0] : nullptr, b ? b[1] : nullptr, b ? b[2] : nullptr},
+                rows};
+  hipLaunchKernelGGL(bn_fold_kernel, dim3((3 * rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     P, 3 * rows, C, gamma, beta, Wf, bf);
   return (int)hipGetLastError();
 }
 
 // ws: 2 * ceil(O / 64) * C floats; counters: ceil(C / 64) zeroed words.
-int tgfr_bn_unfold(const float* G, const float* s, const float* W, int O, int C,
-                   const float* gamma, const float* beta, float* dW, float* dgamma, float* dbeta,
-                   float* ws, unsigned* counters, void* stream) {
+static int bn_unfold_launch(const float* G, const float* s, const Parts& W, int O, int C,
+                            const float* gamma, const float* beta, float* dW, float* dgamma,
+                            float* dbeta, float* ws, unsigned* counters, void* stream) {
   if (O <= 0 || C <= 0 || !ws || !counters) return 1001;
   hipLaunchKernelGGL(bn_unfold_kernel, dim3((C + 63) / 64, (O + UF_ROWS - 1) / UF_ROWS),
                      dim3(256), 0, (hipStream_t)stream, G, s, W, O, C, gamma, beta, dW, ws,
                      counters, dgamma, dbeta);
   return (int)hipGetLastError();
+}
+
+int tgfr_bn_unfold(const float* G, const float* s, const float* W, int O, int C,
+                   const float* gamma, const float* beta, float* dW, float* dgamma, float* dbeta,
+                   float* ws, unsigned* counters, void* stream) {
+  return bn_unfold_launch(G, s, Parts{{W, W, W}, {nullptr, nullptr, nullptr}, O}, O, C, gamma,
+                          beta, dW, dgamma, dbeta, ws, counters, stream);
+}
+
+int tgfr_bn_unfold3(const float* G, const float* s, const float* const* W, int rows, int C,
+                    const float* gamma, const float* beta, float* dW, float* dgamma,
+                    float* dbeta, float* ws, unsigned* counters, void* stream) {
+  if (!W || !W[0] || !W[1] || !W[2]) return 1001;
+  return bn_unfold_launch(G, s, Parts{{W[0], W[1], W[2]}, {nullptr, nullptr, nullptr}, rows},
+                          3 * rows, C, gamma, beta, dW, dgamma, dbeta, ws, counters, stream);
 }
 
 }  // extern "C"

@@ -226,98 +226,101 @@ __device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8&
 
 constexpr int SG_LD = D + 4;                 // padded fp32 LDS rows (bank spread)
 constexpr int SG_LDS = 2 * SG_N * SG_LD * 4 + SG_N * (SG_N + 1) * 4;
+constexpr int SG_T = 1024;                   // 16 waves
 
-__global__ __launch_bounds__(256) void sg_fwd_kernel(
+// 16 waves: staging 8 float4 loads per thread; wave w computes tile w & 3 of
+// the 64 x 64 cosines over k quarter w >> 2 (the quarters summed through LDS);
+// each logit set's LSEs by 4 waves, 4 lanes per row / column.
+__global__ __launch_bounds__(SG_T) void sg_fwd_kernel(
     const float* __restrict__ x, long long ldx, const float* __restrict__ y, long long ldy, int n,
     const long long* __restrict__ cls, float s_sent, float s_glob, float eps,
     float* __restrict__ cosv, float* __restrict__ stats, float* __restrict__ nrm,
     float* __restrict__ loss) {
-  // LDS: x rows | y rows (fp32, padded) | cos [64][65]
+  // LDS: x rows | y rows (fp32, padded) | cos [64][65]; the MFMA partials
+  // reuse the row area once the products are done
   float* xs = (float*)g_smem;
   float* ys = xs + SG_N * SG_LD;
   float* cs = ys + SG_N * SG_LD;
-  __shared__ float nx2[SG_N], ny2[SG_N];
+  float* part = xs;                            // [16 waves][16][64]
+  __shared__ float nxp[4][SG_N], nyp[4][SG_N];
   __shared__ long long cl[SG_N];
-  __shared__ float red[8];
+  __shared__ float red[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 31, h = lane >> 5;
   if (tid < n) cl[tid] = cls[tid];
-  // stage both row sets, 8 + 8 float4 loads of a thread in flight per round
-  // (rows >= n are left unwritten: an output element reads only its own row
-  // of each operand, and those outputs are discarded)
   {
-    constexpr int NQ = SG_N * D / 4 / 256;   // float4 per thread per matrix
-    constexpr int U = 8;
+    constexpr int NQ = SG_N * D / 4 / SG_T;    // 4 float4 per thread per matrix
     const uint32_t yoff = SG_N * SG_LD * 4;
+    uint4 vx[NQ], vy[NQ];
 #pragma unroll
-    for (int u0 = 0; u0 < NQ; u0 += U) {
-      uint4 vx[U], vy[U];
+    for (int u = 0; u < NQ; ++u) {
+      const int i = u * SG_T + tid, r = min(i / (D / 4), n - 1), k = i % (D / 4);
+      vx[u] = *(const uint4*)(x + r * ldx + 4 * k);
+      vy[u] = *(const uint4*)(y + r * ldy + 4 * k);
+    }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = (u0 + u) * 256 + tid, r = min(i / (D / 4), n - 1), k = i % (D / 4);
-        vx[u] = *(const uint4*)(x + r * ldx + 4 * k);
-        vy[u] = *(const uint4*)(y + r * ldy + 4 * k);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = (u0 + u) * 256 + tid, r = i / (D / 4), k = i % (D / 4);
-        const uint32_t o = (uint32_t)(r * SG_LD + 4 * k) * 4;
-        lds_st16(o, vx[u]);
-        lds_st16(yoff + o, vy[u]);
-      }
+    for (int u = 0; u < NQ; ++u) {
+      const int i = u * SG_T + tid, r = i / (D / 4), k = i % (D / 4);
+      const uint32_t o = (uint32_t)(r * SG_LD + 4 * k) * 4;
+      lds_st16(o, vx[u]);
+      lds_st16(yoff + o, vy[u]);
     }
   }
   __syncthreads();
-  // n x n cosines: wave w owns the 32 x 32 tile (w >> 1, w & 1)
-  const int rt = w >> 1, ct = w & 1;
-  if (32 * rt < n && 32 * ct < n) {
-    const int ra = 32 * rt + lr, rb = 32 * ct + lr;
-    f32x16 acc;
+  const int t = w & 3, kq = w >> 2, rt = t >> 1, ct = t & 1;
+  const int ra = 32 * rt + lr, rb = 32 * ct + lr;
+  f32x16 acc;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-    float sx = 0.f, sy = 0.f;
-#pragma unroll 4
-    for (int s = 0; s < D / 16; ++s) {
-      const int k0 = 16 * s + 8 * h;
-      const float4 a0 = *(const float4*)(xs + ra * SG_LD + k0);
-      const float4 a1 = *(const float4*)(xs + ra * SG_LD + k0 + 4);
-      const float4 b0 = *(const float4*)(ys + rb * SG_LD + k0);
-      const float4 b1 = *(const float4*)(ys + rb * SG_LD + k0 + 4);
-      sx = fmaf(a0.x, a0.x, fmaf(a0.y, a0.y, fmaf(a0.z, a0.z, fmaf(a0.w, a0.w, sx))));
-      sx = fmaf(a1.x, a1.x, fmaf(a1.y, a1.y, fmaf(a1.z, a1.z, fmaf(a1.w, a1.w, sx))));
-      sy = fmaf(b0.x, b0.x, fmaf(b0.y, b0.y, fmaf(b0.z, b0.z, fmaf(b0.w, b0.w, sy))));
-      sy = fmaf(b1.x, b1.x, fmaf(b1.y, b1.y, fmaf(b1.z, b1.z, fmaf(b1.w, b1.w, sy))));
-      bf16x8 ah, al, bh, bl;
-      split8(a0, a1, ah, al);
-      split8(b0, b1, bh, bl);
-      mma<MODE_SPLIT>(acc, ah, al, bh, bl);
-    }
-    sx += __shfl_xor(sx, 32);
-    sy += __shfl_xor(sy, 32);
-    if (h == 0 && ct == 0 && ra < n) nx2[ra] = sx;
-    if (h == 0 && rt == 0 && rb < n) ny2[rb] = sy;
-    __syncthreads();
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  float sx = 0.f, sy = 0.f;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int r = 32 * rt + acc_row(q, h), c = rb;
-      if (r < n && c < n) {
-        const float cv = acc[q] / fmaxf(sqrtf(nx2[r]) * sqrtf(ny2[c]), eps);
-        cs[r * (SG_N + 1) + c] = cv;
-        cosv[r * n + c] = cv;
-      }
-    }
-  } else {
-    __syncthreads();
+  for (int s = 4 * kq; s < 4 * kq + 4; ++s) {
+    const int k0 = 16 * s + 8 * h;
+    const float4 a0 = *(const float4*)(xs + ra * SG_LD + k0);
+    const float4 a1 = *(const float4*)(xs + ra * SG_LD + k0 + 4);
+    const float4 b0 = *(const float4*)(ys + rb * SG_LD + k0);
+    const float4 b1 = *(const float4*)(ys + rb * SG_LD + k0 + 4);
+    sx = fmaf(a0.x, a0.x, fmaf(a0.y, a0.y, fmaf(a0.z, a0.z, fmaf(a0.w, a0.w, sx))));
+    sx = fmaf(a1.x, a1.x, fmaf(a1.y, a1.y, fmaf(a1.z, a1.z, fmaf(a1.w, a1.w, sx))));
+    sy = fmaf(b0.x, b0.x, fmaf(b0.y, b0.y, fmaf(b0.z, b0.z, fmaf(b0.w, b0.w, sy))));
+    sy = fmaf(b1.x, b1.x, fmaf(b1.y, b1.y, fmaf(b1.z, b1.z, fmaf(b1.w, b1.w, sy))));
+    bf16x8 ah, al, bh, bl;
+    split8(a0, a1, ah, al);
+    split8(b0, b1, bh, bl);
+    mma<MODE_SPLIT>(acc, ah, al, bh, bl);
+  }
+  sx += __shfl_xor(sx, 32);
+  sy += __shfl_xor(sy, 32);
+  if (h == 0 && ct == 0) nxp[kq][ra] = sx;
+  if (h == 0 && rt == 0) nyp[kq][rb] = sy;
+  __syncthreads();                             // the row area is free now
+#pragma unroll
+  for (int q = 0; q < 16; ++q) part[(w * 16 + q) * 64 + lane] = acc[q];
+  __syncthreads();
+  // cos[r][c] = sum of the 4 quarter partials / max(|x_r||y_c|, eps)
+  for (int e = tid; e < SG_N * SG_N; e += SG_T) {
+    const int r = e >> 6, c = e & 63;
+    if (r >= n || c >= n) continue;
+    const int tt = (r >> 5) * 2 + (c >> 5), rr = r & 31;
+    const int hh = (rr >> 2) & 1, q = (rr & 3) | ((rr >> 3) << 2), ln = (c & 31) + 32 * hh;
+    float v = 0.f;
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4) v += part[((tt + 4 * k4) * 16 + q) * 64 + ln];
+    const float nx = nxp[0][r] + nxp[1][r] + nxp[2][r] + nxp[3][r];
+    const float ny = nyp[0][c] + nyp[1][c] + nyp[2][c] + nyp[3][c];
+    const float cv = v / fmaxf(sqrtf(nx) * sqrtf(ny), eps);
+    cs[r * (SG_N + 1) + c] = cv;
+    cosv[r * n + c] = cv;
   }
   __syncthreads();
-  // wave 0: sent rows, 1: sent columns, 2: global rows, 3: global columns;
-  // lane j < n owns row / column j (online log-sum-exp)
-  const bool glob = w >= 2, col = w & 1;
+  // logit set ls = w >> 2 (0: sent rows, 1: sent columns, 2: global rows,
+  // 3: global columns); row / column j = 16 (w & 3) + lane / 4, four lanes
+  // per row each taking every fourth element (online log-sum-exp, combined)
+  const int ls = w >> 2, j = 16 * (w & 3) + (lane >> 2), sub = lane & 3;
+  const bool glob = ls >= 2, col = ls & 1;
   const float sc = glob ? s_glob : s_sent;
-  float term = 0.f;
-  if (lane < n) {
-    const int j = lane;
-    float m = -INFINITY, sum = 0.f;
-    for (int k = 0; k < n; ++k) {
+  float m = -INFINITY, sum = 0.f;
+  if (j < n) {
+    for (int k = sub; k < n; k += 4) {
       const int b = col ? k : j, i = col ? j : k;
       if (!glob && cl[b] == cl[i] && b != i) continue;
       const float L = sc * cs[b * (SG_N + 1) + i];
@@ -328,22 +331,35 @@ __global__ __launch_bounds__(256) void sg_fwd_kernel(
         sum += __expf(L - m);
       }
     }
+  }
+#pragma unroll
+  for (int msk = 1; msk <= 2; msk <<= 1) {
+    const float m2 = __shfl_xor(m, msk), s2 = __shfl_xor(sum, msk);
+    const float mm = fmaxf(m, m2);
+    sum = (m == -INFINITY ? 0.f : sum * __expf(m - mm)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mm));
+    m = mm;
+  }
+  float term = 0.f;
+  if (j < n && sub == 0) {
     const float lse = m + __logf(sum);
-    stats[w * n + j] = lse;
+    stats[ls * n + j] = lse;
     term = lse - sc * cs[j * (SG_N + 1) + j];
   }
   term = wave_sum(term);
   if (lane == 0) red[w] = term;
   if (tid < n) {
-    nrm[tid] = sqrtf(nx2[tid]);
-    nrm[n + tid] = sqrtf(ny2[tid]);
+    nrm[tid] = sqrtf(nxp[0][tid] + nxp[1][tid] + nxp[2][tid] + nxp[3][tid]);
+    nrm[n + tid] = sqrtf(nyp[0][tid] + nyp[1][tid] + nyp[2][tid] + nyp[3][tid]);
   }
   __syncthreads();
   if (tid == 0) {
+    float l4[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) l4[k] = (red[4 * k] + red[4 * k + 1]) + (red[4 * k + 2] + red[4 * k + 3]);
     const float inv = 1.f / (float)n;
-    loss[0] = red[0] * inv;                  // sent loss0 (rows)
-    loss[1] = red[1] * inv;                  // sent loss1 (columns)
-    loss[2] = (red[2] + red[3]) * inv;       // global loss0 + loss1
+    loss[0] = l4[0] * inv;                   // sent loss0 (rows)
+    loss[1] = l4[1] * inv;                   // sent loss1 (columns)
+    loss[2] = (l4[2] + l4[3]) * inv;         // global loss0 + loss1
   }
 }
 
@@ -434,7 +450,7 @@ int tgfr_sent_global(const float* x, long long ldx, const float* y, long long ld
       ldy % 4 || ((uintptr_t)x & 15) || ((uintptr_t)y & 15))
     return 1001;
   if (const int e = set_max_lds((const void*)sg_fwd_kernel, SG_LDS)) return e;
-  hipLaunchKernelGGL(sg_fwd_kernel, dim3(1), dim3(256), SG_LDS, (hipStream_t)stream, x, ldx, y,
+  hipLaunchKernelGGL(sg_fwd_kernel, dim3(1), dim3(SG_T), SG_LDS, (hipStream_t)stream, x, ldx, y,
                      ldy, n,
                      cls, s_sent, s_glob, eps, cosv, stats, nrm, loss);
   return (int)hipGetLastError();

@@ -151,6 +151,20 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_off) {
                : "memory", "m0");
 }
 
+// glds16 with a wave-uniform 64-bit base in SGPRs and a per-lane 32-bit byte
+// offset (the saddr form): no 64-bit address arithmetic per piece on the VALU.
+__device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32_t lds_off) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(lds_base() + lds_off));
+  // (readfirstlane returns int: zero-extend each half, never sign-extend)
+  const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)sbase);
+  const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)sbase >> 32));
+  const uint64_t sb = lo | (hi << 32);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff),
+               "s"(sb), "s"(m0)
+               : "memory", "m0");
+}
+
 // Retire this wave's DMA down to N outstanding ops and its LDS reads, then
 // meet the other waves.  One asm statement: nothing moves across it.
 template <int N>

@@ -1005,7 +1005,7 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
     } else {
       // wr_bwd_pipe_kernel: scores S' = log2(e) S, rows W' = log2(e) W, C-hat
       constexpr float L2E = 1.4426950408889634f;
-      o[0] = g1 * iz / L2E;             // E -> g1 A2 / log2e
+      o[0] = __log2f(g1 * iz / L2E);    // E -> g1 A2 / log2e, as an exp2 offset
       o[1] = alpha / L2E;               // coefficient of S' in dA2
       o[2] = beta * iz;                 // coefficient of Q-hat in dA2
       o[3] = sigma;
@@ -1014,6 +1014,7 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
     }
   }
   if (layout != 0) {
+    if (!valid) o[0] = -INFINITY;       // exp2 offset of a padding token: A2 = 0
     o[6] = valid ? 0.f : -1e30f;        // G1's initial value row (word bias)
     if ((threadIdx.x % WAVE) < 32) {
 #pragma unroll
@@ -1553,10 +1554,34 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
   }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
+  // DMA pieces of one caption (bwd_stage's layout, MODE_BF16): wave wid
+  // issues pieces k = wid + 4 j (j < 8); rows 4 (k % 16) + lane / 16 are W'
+  // rows for j % 4 < 2 and C-hat rows otherwise, so each piece's source is a
+  // caption-uniform base (SGPRs) plus a per-lane byte offset fixed here
+  uint32_t dma_off[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = wid + 4 * j, p = k % 32, half = p / 16;
+    const int row = 4 * (p % 16) + lane / 16, pc = lane % 16;
+    const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
+    const int c = half * 16 + (pc ^ sw);
+    dma_off[j] = (j % 4 < 2) ? (uint32_t)((row * D + c * 8) * 2)
+                             : (uint32_t)(((c * 32) + (row - 32)) * 8 * 2);
+  }
   auto stage_dma = [&](int k) {     // caption c0 + k -> ring slot k % 4
-    if (k < K)
-      bwd_stage<MODE_BF16>((k % BP_NB) * BP_BUF, Whi, nullptr, Chi, nullptr, tok,
-                           (long long)b * B_cap + c0 + k, c0 + k, wid, lane);
+    if (k < K) {
+      const uint32_t base = (k % BP_NB) * BP_BUF;
+      const long long pair = (long long)b * B_cap + c0 + k;
+      const uint16_t* wsrc = Whi + (long long)(c0 + k) * TPAD * D;
+      const uint16_t* csrc = Chi + pair * 32 * 32 * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kk = wid + 4 * j, p = kk % 32;
+        glds16s(j % 4 < 2 ? (const void*)wsrc : (const void*)csrc, dma_off[j],
+                base + (p / 16) * (64 * 256) + 4 * (p % 16) * 256);
+      }
+      glds16s(tok + pair * TPAD * 8, lane * 16, base + B_XIMG);
+    }
   };
   stage_dma(0);
   stage_dma(1);
@@ -1665,7 +1690,7 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
       const u32x4* f = fb[g & 1];
       if (((c - 13) & 1) == 0) {
         a1[q] = p[q] * inv;                                   // A1
-        ax[q] = __builtin_amdgcn_exp2f(p[q] * kq) * fl(f[0], q);   // g1 A2 / log2e
+        ax[q] = __builtin_amdgcn_exp2f(fmaf(p[q], kq, fl(f[0], q)));   // g1 A2 / log2e
       } else {
         // (dA2 - sigma) = (alpha / log2e) S' + (beta / Z) Q-hat - sigma
         const float du = fmaf(fl(f[1], q), A0[q], fmaf(fl(f[2], q), A1[q], -fl(f[3], q)));

@@ -649,7 +649,8 @@ def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf
     1x1 projection; returns y [N, HW, O] (fp32, or bf16 with out_bf16) and
     stores what _bn_linear_bwd needs on ctx."""
     n, c, h, w_ = x.shape
-    hw, o = h * w_, weight.shape[0]
+    hw = h * w_
+    o = sum(t.shape[0] for t in weight) if isinstance(weight, tuple) else weight.shape[0]
     x = x.float().contiguous()
     dev = x.device
     mean = torch.empty(c, dtype=torch.float32, device=dev)
@@ -665,12 +666,23 @@ def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf
          ptr(bn.running_var) if (track or not use_batch) else None,
          ptr(bn.num_batches_tracked) if track else None, ptr(mean), ptr(rstd), ptr(xhat),
          _hip.stream())
-    w2 = weight.reshape(o, c).float().contiguous()
     g = gamma.float().contiguous()
-    wf = torch.empty_like(w2)
     bf = torch.empty(o, dtype=torch.float32, device=dev)
-    call("tgfr_bn_fold", ptr(w2), ptr(None if bias is None else bias.float().contiguous()),
-         o, c, ptr(g), ptr(beta.float().contiguous()), ptr(wf), ptr(bf), _hip.stream())
+    if isinstance(weight, tuple):
+        # three projections read in place (tgfr_bn_fold3), no concatenated copy
+        rows = weight[0].shape[0]
+        w2 = tuple(w_.reshape(rows, c).float().contiguous() for w_ in weight)
+        b2 = tuple(None if b_ is None else b_.float().contiguous() for b_ in bias)
+        wf = torch.empty(o, c, dtype=torch.float32, device=dev)
+        wp = (ctypes.c_void_p * 3)(*[ptr(t) for t in w2])
+        bp = (ctypes.c_void_p * 3)(*[ptr(t) for t in b2])
+        call("tgfr_bn_fold3", ctypes.addressof(wp), ctypes.addressof(bp), rows, c, ptr(g),
+             ptr(beta.float().contiguous()), ptr(wf), ptr(bf), _hip.stream())
+    else:
+        w2 = weight.reshape(o, c).float().contiguous()
+        wf = torch.empty_like(w2)
+        call("tgfr_bn_fold", ptr(w2), ptr(None if bias is None else bias.float().contiguous()),
+             o, c, ptr(g), ptr(beta.float().contiguous()), ptr(wf), ptr(bf), _hip.stream())
     rows = n * hw
     if out_bf16:
         y = torch.empty(rows, o, dtype=torch.int16, device=dev)
@@ -681,7 +693,8 @@ def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf
         y = bgemm(xhat.view(1, rows, c), wf.t().unsqueeze(0), bias=bf, mode=mode,
                   ksplit=_ksplit(c, mb))[0]
     ctx.bn_saved = (xhat, w2, wf, g, beta.float().contiguous(), rstd)
-    ctx.bn_cfg = (mode, bias is not None, x.shape, weight.shape, use_batch)
+    wshape = tuple(t.shape for t in weight) if isinstance(weight, tuple) else weight.shape
+    ctx.bn_cfg = (mode, bias is not None, x.shape, wshape, use_batch)
     return y.view(n, hw, o)
 
 
@@ -690,7 +703,7 @@ def _bn_linear_bwd(ctx, dy, want_dx):
     xhat, w2, wf, g, bt, rstd = ctx.bn_saved
     mode, has_bias, xshape, wshape, use_batch = ctx.bn_cfg
     n, hw, c = xhat.shape
-    o = w2.shape[0]
+    o = wf.shape[0]
     rows = n * hw
     dp = dy.reshape(rows, o).float()
     if dp.stride(1) != 1 or dp.stride(0) != o:
@@ -716,15 +729,24 @@ def _bn_linear_bwd(ctx, dy, want_dx):
 
 def _bn_unfold(ctx, gm, s):
     """(None, dgamma, dbeta, dweight, dbias) from G = dy^T xhat [O, C] and
-    s = colsum(dy) [O] (tgfr_bn_unfold)."""
+    s = colsum(dy) [O] (tgfr_bn_unfold); with the weight in 3 parts, dweight
+    and dbias are tuples of the parts' slices of the packed gradients."""
     xhat, w2, wf, g, bt, rstd = ctx.bn_saved
     mode, has_bias, xshape, wshape, use_batch = ctx.bn_cfg
-    o, c = w2.shape
+    o, c = wf.shape
     dev = gm.device
-    dw = torch.empty_like(w2)
+    dw = torch.empty(o, c, dtype=torch.float32, device=dev)
     dgamma = torch.empty(c, dtype=torch.float32, device=dev)
     dbeta = torch.empty_like(dgamma)
     uws = torch.empty(2 * -(-o // 64) * c, dtype=torch.float32, device=dev)
+    if isinstance(w2, tuple):
+        rows = w2[0].shape[0]
+        wp = (ctypes.c_void_p * 3)(*[ptr(t) for t in w2])
+        call("tgfr_bn_unfold3", ptr(gm), ptr(s), ctypes.addressof(wp), rows, c, ptr(g), ptr(bt),
+             ptr(dw), ptr(dgamma), ptr(dbeta), ptr(uws), ptr(_hip.counters(dev)), _hip.stream())
+        dws = tuple(dw[k * rows:(k + 1) * rows].view(wshape[k]) for k in range(3))
+        dbs = tuple(s[k * rows:(k + 1) * rows] for k in range(3)) if has_bias else None
+        return None, dgamma, dbeta, dws, dbs
     call("tgfr_bn_unfold", ptr(gm), ptr(s), ptr(w2), o, c, ptr(g), ptr(bt), ptr(dw),
          ptr(dgamma), ptr(dbeta), ptr(uws), ptr(_hip.counters(dev)), _hip.stream())
     return None, dgamma, dbeta, dw.reshape(wshape), (s if has_bias else None)
@@ -753,9 +775,9 @@ class ImimAttention(torch.autograd.Function):
     projection never exists in fp32.  Returns O [N, HW, 256] fp32."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, weight, bias, bn, training, scale):
-        px = _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, "bf16",
-                            out_bf16=True)
+    def forward(ctx, x, gamma, beta, wk, wq, wv, bk, bq, bv, bn, training, scale):
+        px = _bn_linear_fwd(ctx, x, gamma, beta, (wk, wq, wv), (bk, bq, bv), bn, training,
+                            "bf16", out_bf16=True)
         nb, hw, _ = px.shape
         o = torch.empty(nb, hw, 256, dtype=torch.float32, device=px.device)
         lse = torch.empty(nb * hw, dtype=torch.float32, device=px.device)
@@ -785,7 +807,7 @@ class ImimAttention(torch.autograd.Function):
             # the BN input gradient needs dp W' (the reference's frozen-backbone
             # step never asks for it): the fp32 path
             dpf = (dpx.to(torch.int32) << 16).view(torch.float32)
-            return _bn_linear_bwd(ctx, dpf, True) + (None, None, None)
+            return _imim_grads(_bn_linear_bwd(ctx, dpf, True))
         # G = dp^T xhat and colsum(dp) in one bf16 weight-gradient launch
         xhat = ctx.bn_saved[0]
         rows, c = nb * hw, xhat.shape[2]
@@ -799,13 +821,24 @@ class ImimAttention(torch.autograd.Function):
         s = torch.empty(n, dtype=torch.float32, device=px.device)
         call("tgfr_dw_bf16", ptr(dpx), ptr(xhat), 1, rows, n, c, ptr(gm), ptr(s), ptr(gws),
              _hip.stream())
-        return _bn_unfold(ctx, gm, s) + (None, None, None)
+        return _imim_grads(_bn_unfold(ctx, gm, s))
 
 
-def imim_attention(x, bn, weight, bias, scale):
-    """bf16 mode: bn -> packed q/k/v projection (weight [768, 256], bias) ->
-    fused self-attention; returns O [N, HW, 256]."""
-    return ImimAttention.apply(x, bn.weight, bn.bias, weight, bias, bn, bn.training, scale)
+def _imim_grads(g):
+    """(dx, dgamma, dbeta, (dwk, dwq, dwv), (dbk, dbq, dbv) or None) ->
+    ImimAttention.backward's flat tuple."""
+    dx, dgamma, dbeta, dws, dbs = g
+    return (dx, dgamma, dbeta) + tuple(dws) + (tuple(dbs) if dbs else (None,) * 3) + \
+        (None, None, None)
+
+
+def imim_attention(x, bn, sa, scale):
+    """bf16 mode: bn -> q/k/v projections of SelfAttention `sa` (key role,
+    query role, value; read in place) -> fused self-attention; returns
+    O [N, HW, 256]."""
+    return ImimAttention.apply(x, bn.weight, bn.bias, sa.key_proj.weight, sa.query_proj.weight,
+                               sa.value_proj.weight, sa.key_proj.bias, sa.query_proj.bias,
+                               sa.value_proj.bias, bn, bn.training, scale)
 
 
 def bn_linear(x, bn, weight, bias, mode="fp32"):

@@ -58,11 +58,11 @@ class IMIM(nn.Module):
     def forward(self, img):
         n, c, h, w = img.shape
         # bn_img folded into the packed q/k/v projection of the self-attention
-        wq, bq = self.sa.packed_self()
         if self.precision == "bf16" and c == 256 and h * w <= 224:
             # packed projection in bf16 straight into the fused attention kernels
-            z = K.imim_attention(img, self.bn_img, wq, bq, 1.0 / float(self.sa.sqrt_dim))
+            z = K.imim_attention(img, self.bn_img, self.sa, 1.0 / float(self.sa.sqrt_dim))
         else:
+            wq, bq = self.sa.packed_self()
             px = K.bn_linear(img, self.bn_img, wq, bq, mode=self.precision)   # [B, HW, 3C]
             z = self.sa.core_self(px)
         # LayerNorm over (C, H, W) of each sample == over the channels-last

@@ -395,6 +395,142 @@ __global__ __launch_bounds__(NT) void arc_bwd_kernel(
   arc_dw_epilogue<MAXJ>(acc, wv, nj, inv_nw[col], eps, g, dW + (long long)col * lddw);
 }
 
+// The same backward with dWn = dcos^T xn on the matrix core: block = 32
+// classes; v_mfma_f32_32x32x2f32 (fp32 operands, exact products) with A =
+// dcos [rows][32 classes] and B = xn [rows][d] read straight from LDS (lane
+// l takes row l / 32 of the k pair and class / d column l % 32: no
+// transposes); wave w owns d tiles w NTW .. w NTW + NTW - 1 (D = 128 NTW).
+// The l2-norm backward's per-class dot is reduced across lanes and waves
+// through LDS.  LDS: dcos [rows_per + RB][33] (rows past the slice zero) |
+// xn chunk [RB][D + 4].
+constexpr int CBM = 32;
+constexpr int RBM = 16;         // xn rows per staged chunk
+template <int NTW>
+__global__ __launch_bounds__(NT) void arc_bwd_mma_kernel(
+    const float* __restrict__ dlogits, const float* __restrict__ cosv,
+    const long long* __restrict__ label, const float* __restrict__ xn,
+    const float* __restrict__ W, long long ldw, const float* __restrict__ inv_nw, int B, int D,
+    int C, Margin M, float eps, float* __restrict__ dW, long long lddw, float* __restrict__ dcs,
+    int rows_per, float* __restrict__ part, FocalSrc F, ArcBwd2 h2) {
+  if (blockIdx.z) {
+    cosv = h2.cosv;
+    xn = h2.xn;
+    W = h2.W;
+    inv_nw = h2.inv_nw;
+    dW = h2.dW;
+    dcs = h2.dcs;
+    F = h2.F;
+    M = h2.M;
+  }
+  float fscale = 0.f;
+  if (!dlogits) {
+    const float logp = F.ws[B], p = __expf(-logp), q = 1.f - p;
+    float dfl = powf(q, F.gamma);
+    if (F.gamma != 0.f) dfl += F.gamma * powf(q, F.gamma - 1.f) * p * logp;
+    fscale = (F.g ? F.g[0] : 1.f) * dfl / (float)B;
+  }
+  constexpr int LDC = CBM + 1;
+  const int rb0 = blockIdx.y * rows_per, rb1 = min(B, rb0 + rows_per), nbs = rb1 - rb0;
+  float* dc = (float*)g_smem;
+  const uint32_t x_off = (uint32_t)(((rows_per + RBM) * LDC * 4 + 15) & ~15);
+  const float* xs = (const float*)(g_smem + x_off);
+  const int c0 = blockIdx.x * CBM, tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6, lr = lane & 31, h = lane >> 5;
+  // dcos of the block's columns; rows past the slice (up to one chunk) zero
+  for (int base = tid; base < (rows_per + RBM) * CBM; base += NT * 4) {
+    float gl[4], cv[4], iw[4];
+    bool tg[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = min(base + u * NT, max(nbs * CBM - 1, 0));
+      const int b = rb0 + i / CBM, col = min(c0 + i % CBM, C - 1);
+      const long long e = (long long)b * C + col;
+      gl[u] = dlogits ? dlogits[e]
+                      : fscale * (__expf(F.L[e] - F.ws[b]) - (label[b] == col ? 1.f : 0.f));
+      cv[u] = cosv[e];
+      iw[u] = inv_nw[col];
+      tg[u] = label[b] == col;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = base + u * NT;
+      if (i < (rows_per + RBM) * CBM) {
+        const int r = i / CBM, cc = i % CBM, col = c0 + cc;
+        float d = 0.f;
+        if (r < nbs && col < C) {
+          d = margin_bwd(gl[u], cv[u], tg[u], M);
+          if (dcs) dcs[(long long)(rb0 + r) * C + col] = d * iw[u];
+        }
+        dc[r * LDC + cc] = d;
+      }
+    }
+  }
+  f32x16 acc[NTW];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+  const int dbase = 32 * NTW * w + lr;
+  for (int b0 = rb0; b0 < rb1; b0 += RBM) {
+    const int nb = min(RBM, rb1 - b0);
+    __syncthreads();
+    stage_rows(xn, D, b0, RBM, B, D, x_off);   // rows past B staged as zeros
+    __syncthreads();
+    for (int k = 0; k < nb; k += 2) {
+      const float a = dc[(b0 - rb0 + k + h) * LDC + lr];
+      const float* xr = xs + (k + h) * (D + 4) + dbase;
+#pragma unroll
+      for (int t = 0; t < NTW; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xr[32 * t], acc[t], 0, 0, 0);
+    }
+  }
+  if (gridDim.y > 1) {                       // raw dWn partials: part[y][C][D]
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int col = c0 + acc_row(q, h);
+      if (col < C) {
+        float* pr = part + ((long long)blockIdx.y * C + col) * D + dbase;
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) pr[32 * t] = acc[t][q];
+      }
+    }
+    return;
+  }
+  // l2-norm backward: dW_c = (dWn_c - wn_c (wn_c . dWn_c)) / |W_c|
+  __syncthreads();                           // dc / xs no longer read
+  float* red = (float*)g_smem;               // [4 waves][32 classes]
+  float part_dot[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int col = min(c0 + acc_row(q, h), C - 1);
+    const float* wr = W + (long long)col * ldw + dbase;
+    float sdot = 0.f;
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) sdot = fmaf(wr[32 * t], acc[t][q], sdot);
+#pragma unroll
+    for (int m = 16; m >= 1; m >>= 1) sdot += __shfl_xor(sdot, m);
+    part_dot[q] = sdot;
+  }
+  if (lr == 0) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) red[w * CBM + acc_row(q, h)] = part_dot[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int cc = acc_row(q, h), col = c0 + cc;
+    if (col >= C) continue;
+    const float inv = inv_nw[col];
+    const bool clamped = inv >= 1.f / eps;   // |W_c| <= eps: y = W / eps, no projection
+    const float dot = clamped ? 0.f
+                              : inv * (red[cc] + red[CBM + cc] + red[2 * CBM + cc] + red[3 * CBM + cc]);
+    const float* wr = W + (long long)col * ldw + dbase;
+    float* o = dW + (long long)col * lddw + dbase;
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) o[32 * t] = (acc[t][q] - wr[32 * t] * inv * dot) * inv;
+  }
+}
+
 // Sums the block rows' partial dWn in fixed order and applies the l2-norm
 // backward; the thread layout of arc_bwd_kernel (16 classes x 16 lanes).
 template <int NJ>
@@ -442,6 +578,26 @@ int chunk_rows(int B, int D, int fixed_floats) {
   return std::max(1, std::min(B, budget / (D + 4)));
 }
 
+// The MFMA backward for D in {128, 256, 512, 640}: returns -1 when D has no
+// instance (the caller takes the VALU kernel), else the launch status.
+int launch_arc_bwd_mma(const float* dlogits, const float* cosv, const long long* label,
+                       const float* xn, const float* W, long long ldw, const float* inv_nw,
+                       int B, int D, int C, Margin M, float eps, float* dW, long long lddw,
+                       float* dcs, int S, int rows_per, float* part, FocalSrc F, ArcBwd2 h2,
+                       int n_heads, void* stream) {
+  using Fn = decltype(&arc_bwd_mma_kernel<1>);
+  Fn fn = D == 128 ? &arc_bwd_mma_kernel<1> : D == 256 ? &arc_bwd_mma_kernel<2>
+        : D == 512 ? &arc_bwd_mma_kernel<4> : D == 640 ? &arc_bwd_mma_kernel<5> : nullptr;
+  if (!fn || ldw % 4 || lddw % 4) return -1;
+  const int lds = (((rows_per + RBM) * (CBM + 1) * 4 + 15) & ~15) + RBM * (D + 4) * 4;
+  if (lds > 160 * 1024) return -1;
+  if (const int e = set_max_lds((const void*)fn, lds)) return e;
+  hipLaunchKernelGGL(fn, dim3((C + CBM - 1) / CBM, S, n_heads), dim3(NT), lds,
+                     (hipStream_t)stream, dlogits, cosv, label, xn, W, ldw, inv_nw, B, D, C, M,
+                     eps, dW, lddw, dcs, rows_per, part, F, h2);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
@@ -477,13 +633,20 @@ int tgfr_arc_bwd(const float* dlogits, const float* cosv, const long long* label
   const int rows_per = (B + S - 1) / S;
   const int RB = S > 1 ? std::min(16, rows_per) : chunk_rows(B, D, B * CB);
   const int lds = (rows_per * CB + RB * (D + 4)) * 4;
-  using Fn = decltype(&arc_bwd_kernel<0>);
-  Fn fn = D == 128 ? &arc_bwd_kernel<2> : D == 256 ? &arc_bwd_kernel<4>
-        : D == 512 ? &arc_bwd_kernel<8> : D == 640 ? &arc_bwd_kernel<10> : &arc_bwd_kernel<0>;
-  if (const int e = set_max_lds((const void*)fn, lds)) return e;
-  hipLaunchKernelGGL(fn, dim3((C + CB - 1) / CB, S), dim3(NT), lds, (hipStream_t)stream, dlogits,
-                     cosv, label, xn, W, ldw, inv_nw, B, D, C, make_margin(s, m, easy), eps, RB,
-                     dW, lddw, dcs, rows_per, ws, FocalSrc{}, ArcBwd2{});
+  if (const int e = launch_arc_bwd_mma(dlogits, cosv, label, xn, W, ldw, inv_nw, B, D, C,
+                                       make_margin(s, m, easy), eps, dW, lddw, dcs, S, rows_per,
+                                       ws, FocalSrc{}, ArcBwd2{}, 1, stream);
+      e != -1) {
+    if (e) return e;
+  } else {
+    using Fn = decltype(&arc_bwd_kernel<0>);
+    Fn fn = D == 128 ? &arc_bwd_kernel<2> : D == 256 ? &arc_bwd_kernel<4>
+          : D == 512 ? &arc_bwd_kernel<8> : D == 640 ? &arc_bwd_kernel<10> : &arc_bwd_kernel<0>;
+    if (const int e = set_max_lds((const void*)fn, lds)) return e;
+    hipLaunchKernelGGL(fn, dim3((C + CB - 1) / CB, S), dim3(NT), lds, (hipStream_t)stream,
+                       dlogits, cosv, label, xn, W, ldw, inv_nw, B, D, C, make_margin(s, m, easy),
+                       eps, RB, dW, lddw, dcs, rows_per, ws, FocalSrc{}, ArcBwd2{});
+  }
   if (S > 1) {
     using Gn = decltype(&arc_bwd_finish_kernel<0>);
     Gn gn = D == 128 ? &arc_bwd_finish_kernel<2> : D == 256 ? &arc_bwd_finish_kernel<4>
@@ -537,6 +700,13 @@ int tgfr_arc_focal_bwd_heads(const tgfr_arc_head* heads, int n_heads, int B, int
     h2 = ArcBwd2{b.cosv, b.xn, b.W, b.inv_nw, b.dW, b.dcs, FocalSrc{b.logits, b.focal_ws, b.g, gamma},
                  make_margin(b.s, m, easy)};
   }
+  const FocalSrc fa{a.logits, a.focal_ws, a.g, gamma};
+  if (const int e = launch_arc_bwd_mma(nullptr, a.cosv, a.label, a.xn, a.W, (long long)D,
+                                       a.inv_nw, B, D, C, make_margin(a.s, m, easy), eps, a.dW,
+                                       (long long)D, a.dcs, 1, B, nullptr, fa, h2, n_heads,
+                                       stream);
+      e != -1)
+    return e;
   // 16-row x chunks (~21 KB LDS at D = 256): both heads' class blocks in one round
   const int RB = std::min(16, B);
   const int lds = (B * CB + RB * (D + 4)) * 4;
@@ -547,7 +717,7 @@ int tgfr_arc_focal_bwd_heads(const tgfr_arc_head* heads, int n_heads, int B, int
   hipLaunchKernelGGL(fn, dim3((C + CB - 1) / CB, 1, n_heads), dim3(NT), lds, (hipStream_t)stream,
                      nullptr, a.cosv, a.label, a.xn, a.W, (long long)D, a.inv_nw, B, D, C,
                      make_margin(a.s, m, easy), eps, RB, a.dW, (long long)D, a.dcs, B, nullptr,
-                     FocalSrc{a.logits, a.focal_ws, a.g, gamma}, h2);
+                     fa, h2);
   return (int)hipGetLastError();
 }
 

@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=64, help="images per GPU")
     p.add_argument("--words", type=int, default=32, help="bert_words_num (T = words-2)")
-    p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp16"])
     p.add_argument("--alt-precision", default="fp32",
                    help="also time this precision mode ('' to skip)")
     p.add_argument("--cpu-steps", type=int, default=6)

@@ -18,7 +18,10 @@
  *   - Return 0 on success, a hipError_t from the launch, or
  *     1001 (bad shape/argument) / 1002 (bad precision mode).
  *   - mode: 0 = bf16 MFMA operands, 1 = fp32 operands carried as bf16 hi/lo
- *     pairs (three MFMAs per product; the fp32-parity mode).
+ *     pairs (three MFMAs per product; the fp32-parity mode); the word-region
+ *     entry points (tgfr_wr_fwd / tgfr_wr_bwd, general kernels) also take
+ *     2 = fp16 operands (v_mfma_f32_32x32x16_f16, fp32 accumulation;
+ *     BASELINE config 5's precision), with operands from tgfr_prep_rows_f16.
  *   - bf16 buffers are uint16_t bit patterns.
  *   - Feature dim D is 256 (aux_feat_dim_per_granularity, cfg/train_bert.yml:28);
  *     regions R = 196 (14x14, padded to 224 in the split images); words per
@@ -46,6 +49,11 @@ int tgfr_version(void);
 int tgfr_prep_rows(const float* x, long long s_item, long long s_row, long long s_col,
                    int n_items, int n_rows, int n_cols, int rows_pad, const int* lens,
                    float scale, uint16_t* hi, uint16_t* lo, float* norms, void* stream);
+/* tgfr_prep_rows for the fp16 operand mode (mode 2 of tgfr_wr_fwd / _bwd):
+ * hi receives fp16 bits of scale * x (no lo plane). */
+int tgfr_prep_rows_f16(const float* x, long long s_item, long long s_row, long long s_col,
+                       int n_items, int n_rows, int n_cols, int rows_pad, const int* lens,
+                       float scale, uint16_t* hi, float* norms, void* stream);
 
 /* Forward of words_loss's similarity matrix for all (image b, caption i) pairs:
  * replaces the per-caption loop of models/losses.py:73-122 together with

@@ -30,6 +30,7 @@ F = C.c_float
 SIGNATURES = {
     "tgfr_version": [],
     "tgfr_prep_rows": [P, L, L, L, I, I, I, I, P, F, P, P, P, P],
+    "tgfr_prep_rows_f16": [P, L, L, L, I, I, I, I, P, F, P, P, P],
     "tgfr_wr_fwd": [P, P, P, P, P, P, P, I, I, I, F, F, F, F, P, I, P, P, P, P, I, I, I, I, P],
     "tgfr_wr_bwd_tok": [P, P, P, I, I, F, F, F, F, P, I, I, I, P, P],
     "tgfr_wr_bwd_ws": [I, I, I, I, I, P],

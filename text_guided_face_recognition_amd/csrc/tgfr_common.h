@@ -23,7 +23,10 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-enum { MODE_BF16 = 0, MODE_SPLIT = 1 };
+// MODE_F16: fp16 operands (v_mfma_f32_32x32x16_f16, fp32 accumulation), hi
+// only -- the BASELINE config-5 precision for the word-region contraction.
+enum { MODE_BF16 = 0, MODE_SPLIT = 1, MODE_F16 = 2 };
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 namespace tgfr {
 
@@ -34,6 +37,17 @@ __device__ __forceinline__ uint16_t bf_bits(float x) {
 }
 __device__ __forceinline__ float bf_val(uint16_t u) {
   return __uint_as_float(((uint32_t)u) << 16);
+}
+__device__ __forceinline__ uint16_t f16_bits(float x) {
+  return __builtin_bit_cast(uint16_t, (_Float16)x);
+}
+// the single-operand (non-split) encoding of a mode: bf16 or fp16 bits
+template <int MODE>
+__device__ __forceinline__ uint16_t lowp_bits(float x) {
+  if constexpr (MODE == MODE_F16)
+    return f16_bits(x);
+  else
+    return bf_bits(x);
 }
 // fp32 -> (hi, lo) bf16 pair with x ~= hi + lo to ~2^-17 relative.
 __device__ __forceinline__ void split2(float x, uint16_t& hi, uint16_t& lo) {
@@ -53,6 +67,11 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
 template <int MODE>
 __device__ __forceinline__ void mma(f32x16& acc, const bf16x8& ahi, const bf16x8& alo,
                                     const bf16x8& bhi, const bf16x8& blo) {
+  if constexpr (MODE == MODE_F16) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, ahi),
+                                                  __builtin_bit_cast(f16x8, bhi), acc, 0, 0, 0);
+    return;
+  }
   if constexpr (MODE == MODE_SPLIT) {
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc, 0, 0, 0);
@@ -68,6 +87,10 @@ __device__ __forceinline__ void mma(f32x16& acc, const bf16x8& ahi, const bf16x8
 template <int MODE>
 __device__ __forceinline__ void mma_agpr(f32x16& acc, const bf16x8& ahi, const bf16x8& alo,
                                          const bf16x8& bhi, const bf16x8& blo) {
+  if constexpr (MODE == MODE_F16) {
+    asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(ahi), "v"(bhi));
+    return;
+  }
   if constexpr (MODE == MODE_SPLIT) {
     asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(alo), "v"(bhi));
     asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(ahi), "v"(blo));
@@ -94,8 +117,8 @@ __device__ __forceinline__ void frag8(const float* v, bf16x8& hi, bf16x8& lo) {
       split2(v[2 * k], a0, b0);
       split2(v[2 * k + 1], a1, b1);
     } else {
-      a0 = bf_bits(v[2 * k]);
-      a1 = bf_bits(v[2 * k + 1]);
+      a0 = lowp_bits<MODE>(v[2 * k]);
+      a1 = lowp_bits<MODE>(v[2 * k + 1]);
     }
     hp[k] = pack2(a0, a1);
     lp[k] = pack2(b0, b1);

@@ -45,7 +45,7 @@ constexpr int NRT = 7;         // region tiles
 __global__ __launch_bounds__(256) void prep_rows_kernel(
     const float* __restrict__ x, long long s_item, long long s_row, long long s_col,
     int n_items, int n_rows, int rows_pad, const int* __restrict__ lens, float scale,
-    uint16_t* __restrict__ hi, uint16_t* __restrict__ lo, float* __restrict__ norms) {
+    uint16_t* __restrict__ hi, uint16_t* __restrict__ lo, float* __restrict__ norms, int f16) {
   const int wave = (blockIdx.x * 256 + threadIdx.x) / WAVE;
   const int lane = threadIdx.x % WAVE;
   if (wave >= n_items * rows_pad) return;
@@ -63,10 +63,17 @@ __global__ __launch_bounds__(256) void prep_rows_kernel(
   }
   uint16_t h[4], l[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) split2(scale * v[k], h[k], l[k]);
+  for (int k = 0; k < 4; ++k) {
+    if (f16) {
+      h[k] = f16_bits(scale * v[k]);
+      l[k] = 0;
+    } else {
+      split2(scale * v[k], h[k], l[k]);
+    }
+  }
   const long long o = ((long long)item * rows_pad + row) * D + lane * 4;
   *(uint2*)(hi + o) = make_uint2(pack2(h[0], h[1]), pack2(h[2], h[3]));
-  *(uint2*)(lo + o) = make_uint2(pack2(l[0], l[1]), pack2(l[2], l[3]));
+  if (lo) *(uint2*)(lo + o) = make_uint2(pack2(l[0], l[1]), pack2(l[2], l[3]));
   ss = wave_sum(ss);
   if (lane == 0 && norms) norms[(long long)item * rows_pad + row] = sqrtf(ss);
 }
@@ -155,7 +162,7 @@ __device__ __forceinline__ void store_cq(uint16_t* Chi, uint16_t* Clo, long long
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if constexpr (MODE == MODE_SPLIT) split2(C[dt][4 * g + k], hh[k], ll[k]);
-        else hh[k] = bf_bits(C[dt][4 * g + k]);
+        else hh[k] = lowp_bits<MODE>(C[dt][4 * g + k]);
       }
       const long long o = ((pair * 32 + (4 * dt + g)) * TPS + t) * 8 + 4 * h;
       *(uint2*)(Chi + o) = make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3]));
@@ -180,7 +187,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_kernel(
     uint16_t* __restrict__ Clo, float* __restrict__ att, int att_T) {
   constexpr int CPW = 4 / TT;              // captions per workgroup
   constexpr int TP = 32 * TT;              // token stride of W, stats, C
-  constexpr bool SCALED = MODE == MODE_BF16;
+  constexpr bool SCALED = MODE != MODE_SPLIT;
   constexpr float L2E = 1.4426950408889634f;
   const int groups = (B_cap + CPW - 1) / CPW;
   const int work = xcd_remap(blockIdx.x, groups * B_img);
@@ -329,7 +336,10 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_kernel(
       for (int g = 0; g < 4; ++g) {
         uint16_t hh[4], ll[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) split2(E[j][4 * g + k], hh[k], ll[k]);
+        for (int k = 0; k < 4; ++k) {
+          if constexpr (MODE == MODE_SPLIT) split2(E[j][4 * g + k], hh[k], ll[k]);
+          else hh[k] = lowp_bits<MODE>(E[j][4 * g + k]);
+        }
         const uint32_t o = et + lr * 64 + (8 * g + 4 * h) * 2;
         lds_st8(o, make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3])));
         if (MODE == MODE_SPLIT)
@@ -1048,7 +1058,7 @@ struct BwdCfg {
   // bf16: each wave's R tile (32 x 256 bf16) lives in LDS instead of 64
   // VGPRs, which keeps the caption loop's live set inside the VGPR file (no
   // AGPR shuttling); split mode keeps hi/lo R fragments in registers.
-  static constexpr bool R_LDS = MODE == MODE_BF16;
+  static constexpr bool R_LDS = MODE != MODE_SPLIT;
   static constexpr int R_BASE = NB * BUF;
   static constexpr int R_TILE = 32 * D * 2;
   static constexpr int LDS = NB * BUF + (R_LDS ? 4 * R_TILE : 0);
@@ -1580,7 +1590,8 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
         glds16s(j % 4 < 2 ? (const void*)wsrc : (const void*)csrc, dma_off[j],
                 base + (p / 16) * (64 * 256) + 4 * (p % 16) * 256);
       }
-      glds16s(tok + pair * TPAD * 8, lane * 16, base + B_XIMG);
+      // the token table (1 KiB) by one wave, rotating with the caption
+      if (wid == (k & 3)) glds16s(tok + pair * TPAD * 8, lane * 16, base + B_XIMG);
     }
   };
   stage_dma(0);
@@ -1834,7 +1845,18 @@ int tgfr_prep_rows(const float* x, long long s_item, long long s_row, long long 
   const int waves = n_items * rows_pad;
   hipLaunchKernelGGL(prep_rows_kernel, dim3((waves + 3) / 4), dim3(256), 0,
                      (hipStream_t)stream, x, s_item, s_row, s_col, n_items, n_rows, rows_pad,
-                     lens, scale, hi, lo, norms);
+                     lens, scale, hi, lo, norms, 0);
+  return (int)hipGetLastError();
+}
+
+int tgfr_prep_rows_f16(const float* x, long long s_item, long long s_row, long long s_col,
+                       int n_items, int n_rows, int n_cols, int rows_pad, const int* lens,
+                       float scale, uint16_t* hi, float* norms, void* stream) {
+  if (n_cols != D || n_rows > rows_pad || n_items <= 0 || !hi) return 1001;
+  const int waves = n_items * rows_pad;
+  hipLaunchKernelGGL(prep_rows_kernel, dim3((waves + 3) / 4), dim3(256), 0,
+                     (hipStream_t)stream, x, s_item, s_row, s_col, n_items, n_rows, rows_pad,
+                     lens, scale, hi, nullptr, norms, 1);
   return (int)hipGetLastError();
 }
 
@@ -1844,13 +1866,21 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 int img_offset, float gamma1, float gamma2, float gamma3, float eps,
                 float* logits, int ld_logits, float* stats, uint16_t* Chi, uint16_t* Clo,
                 float* att, int att_T, int bounded, int t_pad, int mode, void* stream) {
-  if (B_img <= 0 || B_cap <= 0 || ld_logits < B_cap) return 1001;
+  if (B_img <= 0 || B_cap <= 0 || ld_logits < B_cap || !Rhi || !Whi) return 1001;
   if (t_pad != 32 && t_pad != 64) return 1001;
+  // the general kernels stage the R lo plane in every mode (read only in
+  // split mode): single-operand modes without one stage hi twice
+  if (!Rlo) {
+    if (mode == MODE_SPLIT) return 1001;
+    Rlo = Rhi;
+  }
   const int grid = ((B_cap + 3) / 4) * B_img;
   auto* s = (hipStream_t)stream;
   if (const int e = allow_lds(wr_fwd_kernel<MODE_SPLIT, 1>, F_LDS)) return e;
   if (const int e = allow_lds(wr_fwd_kernel<MODE_SPLIT, 2>, F_LDS2)) return e;
   if (const int e = allow_lds(wr_fwd_kernel<MODE_BF16, 2>, F_LDS2)) return e;
+  if (const int e = allow_lds(wr_fwd_kernel<MODE_F16, 1>, F_LDS)) return e;
+  if (const int e = allow_lds(wr_fwd_kernel<MODE_F16, 2>, F_LDS2)) return e;
   if (const int e = allow_lds(wr_fwd_res_kernel, FR_LDS)) return e;
   if (const int e = allow_lds(wr_fwd_pipe_kernel, FR_LDS)) return e;
   if (t_pad == 64) {
@@ -1866,12 +1896,21 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                          Rhi, Rlo, Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1,
                          gamma2, gamma3, eps, logits, ld_logits, (float4*)stats, Chi, Clo, att,
                          att_T);
+    else if (mode == MODE_F16)
+      hipLaunchKernelGGL((wr_fwd_kernel<MODE_F16, 2>), dim3(grid2), dim3(256), F_LDS2, s,
+                         Rhi, Rlo, Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1,
+                         gamma2, gamma3, eps, logits, ld_logits, (float4*)stats, Chi, Clo, att,
+                         att_T);
     else
       return 1002;
     return (int)hipGetLastError();
   }
   if (mode == MODE_SPLIT)
     hipLaunchKernelGGL((wr_fwd_kernel<MODE_SPLIT, 1>), dim3(grid), dim3(256), F_LDS, s, Rhi, Rlo,
+                       Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1, gamma2, gamma3,
+                       eps, logits, ld_logits, (float4*)stats, Chi, Clo, att, att_T);
+  else if (mode == MODE_F16)
+    hipLaunchKernelGGL((wr_fwd_kernel<MODE_F16, 1>), dim3(grid), dim3(256), F_LDS, s, Rhi, Rlo,
                        Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1, gamma2, gamma3,
                        eps, logits, ld_logits, (float4*)stats, Chi, Clo, att, att_T);
   else if (mode == MODE_BF16) {
@@ -1924,7 +1963,7 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 int t_pad, int mode, void* stream) {
   (void)counters;
   if (B_img <= 0 || B_cap <= 0 || !dR || !ws) return 1001;
-  if (mode != MODE_SPLIT && mode != MODE_BF16) return 1002;
+  if (mode != MODE_SPLIT && mode != MODE_BF16 && mode != MODE_F16) return 1002;
   auto* s = (hipStream_t)stream;
   // caption-chunk partial slabs in ws, summed into dR by wr_reduce_kernel
   const int n_chunks = slab_chunks(B_img, B_cap);
@@ -1940,9 +1979,14 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   } else if (t_pad == 64) {
     if (const int e = allow_lds(wr_bwd_wide_kernel<MODE_SPLIT>, BwdWCfg<MODE_SPLIT>::LDS)) return e;
     if (const int e = allow_lds(wr_bwd_wide_kernel<MODE_BF16>, BwdWCfg<MODE_BF16>::LDS)) return e;
+    if (const int e = allow_lds(wr_bwd_wide_kernel<MODE_F16>, BwdWCfg<MODE_F16>::LDS)) return e;
     if (mode == MODE_SPLIT)
       hipLaunchKernelGGL(wr_bwd_wide_kernel<MODE_SPLIT>, dim3(grid), dim3(256),
                          BwdWCfg<MODE_SPLIT>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
+                         gamma1, tok_ws, Chi, Clo, ws);
+    else if (mode == MODE_F16)
+      hipLaunchKernelGGL(wr_bwd_wide_kernel<MODE_F16>, dim3(grid), dim3(256),
+                         BwdWCfg<MODE_F16>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
                          gamma1, tok_ws, Chi, Clo, ws);
     else
       hipLaunchKernelGGL(wr_bwd_wide_kernel<MODE_BF16>, dim3(grid), dim3(256),
@@ -1951,9 +1995,14 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   } else if (t_pad == 32) {
     if (const int e = allow_lds(wr_bwd_kernel<MODE_SPLIT>, BwdCfg<MODE_SPLIT>::LDS)) return e;
     if (const int e = allow_lds(wr_bwd_kernel<MODE_BF16>, BwdCfg<MODE_BF16>::LDS)) return e;
+    if (const int e = allow_lds(wr_bwd_kernel<MODE_F16>, BwdCfg<MODE_F16>::LDS)) return e;
     if (mode == MODE_SPLIT)
       hipLaunchKernelGGL(wr_bwd_kernel<MODE_SPLIT>, dim3(grid), dim3(256),
                          BwdCfg<MODE_SPLIT>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
+                         gamma1, tok_ws, Chi, Clo, ws);
+    else if (mode == MODE_F16)
+      hipLaunchKernelGGL(wr_bwd_kernel<MODE_F16>, dim3(grid), dim3(256),
+                         BwdCfg<MODE_F16>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
                          gamma1, tok_ws, Chi, Clo, ws);
     else
       hipLaunchKernelGGL(wr_bwd_kernel<MODE_BF16>, dim3(grid), dim3(256),

@@ -18,10 +18,20 @@ RPAD = 224
 NREG = 196
 TPAD = 32
 
-MODES = {"bf16": 0, "fp32": 1}
+MODES = {"bf16": 0, "fp32": 1, "fp16": 2}
 
 
 def _mode(mode):
+    """C-ABI precision of the generic kernels: "fp16" (the word-region
+    contraction in fp16, BASELINE config 5) runs everything else in bf16."""
+    try:
+        return min(MODES[mode], 1)
+    except KeyError:
+        raise ValueError(f"precision mode must be one of {sorted(MODES)}") from None
+
+
+def _wr_mode(mode):
+    """C-ABI precision of the word-region kernels (0 bf16, 1 fp32 split, 2 fp16)."""
     try:
         return MODES[mode]
     except KeyError:
@@ -31,9 +41,9 @@ def _mode(mode):
 LOG2E = 1.4426950408889634
 
 
-def prep_rows(x, n_rows, rows_pad, lens=None, want_norms=False, scale=1.0):
+def prep_rows(x, n_rows, rows_pad, lens=None, want_norms=False, scale=1.0, f16=False):
     """fp32 [items, rows, 256] (any strides) -> bf16 hi/lo of scale * x
-    [items, rows_pad, 256].
+    [items, rows_pad, 256] (f16: fp16 bits in hi, no lo).
 
     Rows >= n_rows (or >= lens[item]) are zero.  Optional fp32 norms of the
     unscaled rows.
@@ -41,10 +51,14 @@ def prep_rows(x, n_rows, rows_pad, lens=None, want_norms=False, scale=1.0):
     assert x.dtype == torch.float32 and x.dim() == 3 and x.shape[2] == D
     n_items = x.shape[0]
     hi = torch.empty(n_items, rows_pad, D, dtype=torch.int16, device=x.device)
-    lo = torch.empty_like(hi)
     norms = torch.empty(n_items, rows_pad, dtype=torch.float32, device=x.device) \
         if want_norms else None
     s0, s1, s2 = x.stride()
+    if f16:
+        call("tgfr_prep_rows_f16", ptr(x), s0, s1, s2, n_items, n_rows, D, rows_pad,
+             ptr(lens), float(scale), ptr(hi), ptr(norms), _hip.stream())
+        return hi, None, norms
+    lo = torch.empty_like(hi)
     call("tgfr_prep_rows", ptr(x), s0, s1, s2, n_items, n_rows, D, rows_pad,
          ptr(lens), float(scale), ptr(hi), ptr(lo), ptr(norms), _hip.stream())
     return hi, lo, norms
@@ -92,17 +106,20 @@ class WordRegionLogits(torch.autograd.Function):
         # token stride: 32, or 64 for 64-token captions (general kernels only)
         t_pad = TPAD if t_words <= TPAD else 2 * TPAD
         lens = lens.to(device=dev, dtype=torch.int32).contiguous()
-        m = _mode(mode)
-        bf16 = m == MODES["bf16"]
+        m = _wr_mode(mode)
+        f16 = m == MODES["fp16"]
+        bf16 = m != MODES["fp32"]          # single-operand modes (bf16, fp16)
         # the bounded bf16 path runs the pipelined kernels both ways
-        fast = bf16 and bool(bounded) and not att_T and t_pad == TPAD
-        r_hi, r_lo, r_norm = prep_rows(regions, NREG, RPAD, want_norms=bf16)
+        fast = m == MODES["bf16"] and bool(bounded) and not att_T and t_pad == TPAD
+        r_hi, r_lo, r_norm = prep_rows(regions, NREG, RPAD, want_norms=bf16, f16=f16)
         if bf16:
-            # the bf16 forward takes log2(e)-scaled words (tgfr.h, tgfr_wr_fwd),
-            # and so does the pipelined backward; the other backward the plain ones
+            # the bf16 / fp16 forward takes log2(e)-scaled words (tgfr.h,
+            # tgfr_wr_fwd), and so does the pipelined backward; the other
+            # backward the plain ones
             w_fwd, _, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,
-                                         want_norms=True, scale=LOG2E)
-            w_hi = w_fwd if fast else prep_rows(words.float(), t_words, t_pad, lens=lens)[0]
+                                         want_norms=True, scale=LOG2E, f16=f16)
+            w_hi = w_fwd if fast else prep_rows(words.float(), t_words, t_pad, lens=lens,
+                                                f16=f16)[0]
             w_lo = None
         else:
             w_hi, w_lo, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,

@@ -58,7 +58,7 @@ class IMIM(nn.Module):
     def forward(self, img):
         n, c, h, w = img.shape
         # bn_img folded into the packed q/k/v projection of the self-attention
-        if self.precision == "bf16" and c == 256 and h * w <= 224:
+        if self.precision in ("bf16", "fp16") and c == 256 and h * w <= 224:
             # packed projection in bf16 straight into the fused attention kernels
             z = K.imim_attention(img, self.bn_img, self.sa, 1.0 / float(self.sa.sqrt_dim))
         else:
@@ -68,7 +68,7 @@ class IMIM(nn.Module):
         # LayerNorm over (C, H, W) of each sample == over the channels-last
         # [HW, C] rows; the [C, H, W] affine maps are read channel-major in place
         z = K.layer_norm_rows(z, self.ln.weight, self.ln.bias, self.ln.eps, ch=c)
-        if self.precision == "bf16":
+        if self.precision in ("bf16", "fp16"):
             # conv1x1_1 -> ReLU -> conv1x1_2 -> ReLU -> project_local, fused
             z = K.imim_tail(z, self.conv1x1_1, self.conv1x1_2, self.project_local.projection)
             return z.reshape(n, h, w, -1).permute(0, 3, 1, 2)

@@ -625,6 +625,224 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
   }
 }
 
+// ------------------------------------------ fwd, 64-token captions, R resident ---
+// wr_fwd_res_kernel for T <= 64 (BASELINE configs[4], T = 62) in the
+// single-operand modes (bf16 / fp16, log2(e)-scaled words): the image's R
+// stays in LDS (roff swizzle) for the workgroup's whole caption chunk, and the
+// chunk's captions go two at a time, one wave per (caption, 32-token tile).
+// The two waves of a caption exchange through LDS the per-region max and sum
+// of the softmax over its 64 words and the per-token sum of the final
+// log-sum-exp: three workgroup barriers per caption pair, so every wave runs
+// the same number of iterations (a missing second caption computes on a
+// clamped one and stores nothing).
+constexpr int FR2_OFF_XM = FR_LDS;                         // [wave][7][32] region max
+constexpr int FR2_OFF_XS = FR2_OFF_XM + 4 * NRT * 128;     // [wave][7][32] region sum
+constexpr int FR2_OFF_XL = FR2_OFF_XS + 4 * NRT * 128;     // [wave] per-tile exp sum
+constexpr int FR2_LDS = FR2_OFF_XL + 4 * 16;
+
+template <int MODE, bool ATT>
+__global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
+    const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi,
+    const float* __restrict__ Wnorm, const int* __restrict__ lens, int B_img, int B_cap,
+    int n_chunks, int img_offset, float g1, float g2, float g3, float eps,
+    float* __restrict__ logits, int ld_logits, float4* __restrict__ stats,
+    uint16_t* __restrict__ Chi, float* __restrict__ att, int att_T) {
+  constexpr int TP = 64;
+  constexpr float L2E = 1.4426950408889634f;
+  const int work = xcd_remap(blockIdx.x, n_chunks * B_img);
+  const int b = work / n_chunks, chunk = work % n_chunks;
+  const int per = (B_cap + n_chunks - 1) / n_chunks;
+  const int c0 = chunk * per, c1 = min(B_cap, c0 + per);
+  const int tid = threadIdx.x, lane = tid % WAVE;
+  const int wid = __builtin_amdgcn_readfirstlane(tid / WAVE);
+  const int lr = lane & 31, h = lane >> 5;
+  const int g16 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const int tt = wid & 1, slot = wid >> 1;       // token tile, caption slot
+
+  {
+    const uint16_t* src = Rhi + (long long)b * RPAD * D;
+    for (int piece = wid; piece < FR_IMG / 1024; piece += 4) {
+      const int o = piece * 1024 + lane * 16;
+      const int half = o / (RPAD * 256), rem = o % (RPAD * 256);
+      const int row = rem / 256, pc = (rem % 256) / 16;
+      const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
+      const int col = half * 128 + ((pc ^ sw) << 3);
+      __builtin_amdgcn_global_load_lds((const void*)(src + row * D + col),
+                                       (LDS_AS void*)(lds_base() + piece * 1024), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (c0 >= c1) return;                          // workgroup-uniform
+  const uint32_t et = FR_OFF_ET + wid * 4096;
+  const uint32_t tok = FR_OFF_TOK + wid * 256;
+  uint32_t f1o[8], f2o[2][4];
+  {
+    const int sw1 = ((lr & 3) << 2) | ((lr >> 2) & 3);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f1o[k] = lr * 256 + (((2 * k + h) ^ sw1) << 4);
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd)
+        f2o[bb][dd] = (8 * h + q4 + 4 * bb) * 256 + ((dd ^ q4) << 6) +
+                      (((2 * (g16 & 1) + (p4 >> 1)) ^ ((2 * h + bb) & 3)) << 4) + (p4 & 1) * 8;
+  }
+  bf16x8 Wc[16];
+  auto load_w = [&](int ii) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      Wc[s] = as_bf8(
+          *(const uint4*)(Whi + ((long long)ii * TP + 32 * tt + lr) * D + s * 16 + h * 8));
+  };
+  const int npairs = (c1 - c0 + 1) / 2;
+  load_w(min(c0 + slot, c1 - 1));
+  for (int k = 0; k < npairs; ++k) {
+    const int i = c0 + 2 * k + slot;
+    const bool active = i < c1;
+    const int ic = active ? i : c1 - 1;
+    const int tl = lens[ic] - 32 * tt;           // valid words of this tile
+    // ---- GEMM1: S'^T[t][r] = W'[t][d] R[r][d]
+    // (accumulators start at the word bias: 0, or -1e30 for padding words,
+    // whose E = exp(0) = 1 then only feeds their own unused statistics and
+    // C-hat rows, as in wr_fwd_pipe_kernel)
+    f32x16 S[NRT];
+#pragma unroll
+    for (int j = 0; j < NRT; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) S[j][q] = acc_row(q, h) < tl ? 0.f : -1e30f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+#pragma unroll
+      for (int j = 0; j < NRT; ++j) {
+        const bf16x8 bb = as_bf8(lds_ld16(f1o[s & 7] + (s >> 3) * (RPAD * 256) + j * 32 * 256));
+        mma<MODE>(S[j], Wc[s], Wc[s], bb, bb);
+      }
+    // ---- softmax over the caption's words, per region: max and sum over
+    // both token tiles (partner wave = wid ^ 1)
+    float mj[NRT];
+#pragma unroll
+    for (int j = 0; j < NRT; ++j) {
+      float m = S[j][0];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) m = __builtin_fmaxf(m, S[j][q]);
+      mj[j] = __builtin_fmaxf(m, __shfl_xor(m, 32));
+    }
+    if (h == 0)
+#pragma unroll
+      for (int j = 0; j < NRT; ++j) lds_stf(FR2_OFF_XM + (wid * NRT + j) * 128 + lr * 4, mj[j]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NRT; ++j)
+      mj[j] = __builtin_fmaxf(mj[j], lds_ldf(FR2_OFF_XM + ((wid ^ 1) * NRT + j) * 128 + lr * 4));
+    float sj[NRT];
+#pragma unroll
+    for (int j = 0; j < NRT; ++j) {
+      float sum = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) sum += __builtin_amdgcn_exp2f(S[j][q] - mj[j]);
+      sj[j] = sum + __shfl_xor(sum, 32);
+    }
+    if (h == 0)
+#pragma unroll
+      for (int j = 0; j < NRT; ++j) lds_stf(FR2_OFF_XS + (wid * NRT + j) * 128 + lr * 4, sj[j]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NRT; ++j)
+      sj[j] += lds_ldf(FR2_OFF_XS + ((wid ^ 1) * NRT + j) * 128 + lr * 4);
+    // ---- per region tile: E = exp(gamma1 A1), per-token Z and N, E^T via LDS,
+    // C^T[d][t] += R[r][d] E[t][r] (p recomputed: S stays live for N)
+    float zp[16], np[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) zp[q] = np[q] = 0.f;
+    f32x16 C[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) C[j][q] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NRT; ++j) {
+      const float rb = j * 32 + lr < NREG ? 0.f : -1e30f;   // padding regions
+      const float kj = g1 * L2E * __builtin_amdgcn_rcpf(sj[j]);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float p = __builtin_amdgcn_exp2f(S[j][q] - mj[j]);
+        const float e = __builtin_amdgcn_exp2f(j == NRT - 1 ? fmaf(p, kj, rb) : p * kj);
+        zp[q] += e;
+        np[q] = fmaf(e, S[j][q], np[q]);
+        S[j][q] = e;
+      }
+      const uint32_t etj = et + (j & 1) * 2048;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint16_t hh[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) hh[kk] = lowp_bits<MODE>(S[j][4 * g + kk]);
+        lds_st8(etj + lr * 64 + (8 * g + 4 * h) * 2,
+                make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3])));
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int rbk = 16 * s + 8 * h;
+        const uint32_t eo = etj + (rbk + q4) * 64 + (16 * (g16 & 1) + 4 * p4) * 2;
+        const bf16x8 bb = join_tr(lds_tr4(eo), lds_tr4(eo + 4 * 64));
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          const uint32_t kb = (dt >> 2) * (RPAD * 256) + (j * 32 + 16 * s) * 256;
+          const bf16x8 aa = join_tr(lds_tr4(kb + f2o[0][dt & 3]), lds_tr4(kb + f2o[1][dt & 3]));
+          mma<MODE>(C[dt], aa, aa, bb, bb);
+        }
+      }
+    }
+    const float zr = rs16(zp, lr), nr = rs16(np, lr);
+    if ((lr & 1) == 0) {
+      const int t = acc_row(rs16_index(lr), h);
+      lds_stf(tok + t * 4, zr);
+      lds_stf(tok + 128 + t * 4, nr);
+    }
+    if (ATT && active && b + img_offset == i) {
+      // attention map of the matching pair: A2[t][r] = E[t][r] / Z_t
+      float* dst = att + (long long)b * att_T * NREG;
+#pragma unroll
+      for (int j = 0; j < NRT; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int tq = acc_row(q, h), tg = 32 * tt + tq, r = j * 32 + lr;
+          if (tq < tl && tg < att_T && r < NREG)
+            dst[tg * NREG + r] = S[j][q] * __builtin_amdgcn_rcpf(lds_ldf(tok + tq * 4));
+        }
+    }
+    if (k + 1 < npairs) load_w(min(i + 2, c1 - 1));
+    // ---- per-token epilogue (lane t = lr), log-sum-exp over both tiles
+    const int t = lr, tg = 32 * tt + lr;
+    float csq = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) csq = fmaf(C[dt][q], C[dt][q], csq);
+    csq += __shfl_xor(csq, 32);
+    const float Z = lds_ldf(tok + t * 4);
+    const float nhat = lds_ldf(tok + 128 + t * 4) * (1.f / L2E);
+    const bool tvalid = t < tl;
+    const float zinv = 1.f / Z;
+    const float cn = sqrtf(csq) * zinv;
+    const float n = nhat * zinv;
+    const float u = Wnorm[(long long)ic * TP + tg];
+    const float cosv = n / fmaxf(u * cn, eps);
+    float ex = half_sum(tvalid ? __expf(g2 * cosv) : 0.f);
+    if (lane == 0) lds_stf(FR2_OFF_XL + wid * 4, ex);
+    __syncthreads();
+    ex += lds_ldf(FR2_OFF_XL + (wid ^ 1) * 4);
+    if (!active) continue;
+    const long long pair = (long long)b * B_cap + i;
+    if (lane == 0 && tt == 0) logits[(long long)b * ld_logits + i] = g3 * __logf(ex);
+    if (stats && h == 0)
+      stats[pair * TP + tg] =
+          tvalid ? make_float4(Z, n, cn, cosv) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (Chi) store_cq<MODE, TP>(Chi, nullptr, pair, tg, h, C);
+  }
+}
+
 // ------------------------------------- fwd, bf16, R resident, pipelined ---
 // Same work split, R image (LDS, roff swizzle) and outputs as
 // wr_fwd_res_kernel, restructured so that the matrix core and the VALU work
@@ -1878,31 +2096,34 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   auto* s = (hipStream_t)stream;
   if (const int e = allow_lds(wr_fwd_kernel<MODE_SPLIT, 1>, F_LDS)) return e;
   if (const int e = allow_lds(wr_fwd_kernel<MODE_SPLIT, 2>, F_LDS2)) return e;
-  if (const int e = allow_lds(wr_fwd_kernel<MODE_BF16, 2>, F_LDS2)) return e;
   if (const int e = allow_lds(wr_fwd_kernel<MODE_F16, 1>, F_LDS)) return e;
-  if (const int e = allow_lds(wr_fwd_kernel<MODE_F16, 2>, F_LDS2)) return e;
   if (const int e = allow_lds(wr_fwd_res_kernel, FR_LDS)) return e;
   if (const int e = allow_lds(wr_fwd_pipe_kernel, FR_LDS)) return e;
   if (t_pad == 64) {
-    // 64-token captions: two waves per caption, two captions per workgroup
+    // 64-token captions: two waves per caption, two captions at a time
     const int grid2 = ((B_cap + 1) / 2) * B_img;
-    if (mode == MODE_SPLIT)
-      hipLaunchKernelGGL((wr_fwd_kernel<MODE_SPLIT, 2>), dim3(grid2), dim3(256), F_LDS2, s,
-                         Rhi, Rlo, Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1,
-                         gamma2, gamma3, eps, logits, ld_logits, (float4*)stats, Chi, Clo, att,
-                         att_T);
-    else if (mode == MODE_BF16)
-      hipLaunchKernelGGL((wr_fwd_kernel<MODE_BF16, 2>), dim3(grid2), dim3(256), F_LDS2, s,
-                         Rhi, Rlo, Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1,
-                         gamma2, gamma3, eps, logits, ld_logits, (float4*)stats, Chi, Clo, att,
-                         att_T);
-    else if (mode == MODE_F16)
-      hipLaunchKernelGGL((wr_fwd_kernel<MODE_F16, 2>), dim3(grid2), dim3(256), F_LDS2, s,
-                         Rhi, Rlo, Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1,
-                         gamma2, gamma3, eps, logits, ld_logits, (float4*)stats, Chi, Clo, att,
-                         att_T);
-    else
-      return 1002;
+    if (mode != MODE_SPLIT) {
+      // R resident in LDS; caption chunks sized for >= ~256 workgroups
+      const int n_chunks = max(1, min((B_cap + 1) / 2, (256 + B_img - 1) / B_img));
+      const dim3 g(n_chunks * B_img);
+#define TGFR_RES2(M, A)                                                                     \
+  do {                                                                                     \
+    if (const int e = allow_lds(wr_fwd_res2_kernel<M, A>, FR2_LDS)) return e;              \
+    hipLaunchKernelGGL((wr_fwd_res2_kernel<M, A>), g, dim3(256), FR2_LDS, s, Rhi, Whi, Wnorm, \
+                       lens, B_img, B_cap, n_chunks, img_offset, gamma1, gamma2, gamma3, eps, \
+                       logits, ld_logits, (float4*)stats, Chi, att, att_T);                \
+  } while (0)
+      if (mode == MODE_BF16 && att) TGFR_RES2(MODE_BF16, true);
+      else if (mode == MODE_BF16) TGFR_RES2(MODE_BF16, false);
+      else if (mode == MODE_F16 && att) TGFR_RES2(MODE_F16, true);
+      else if (mode == MODE_F16) TGFR_RES2(MODE_F16, false);
+      else return 1002;
+#undef TGFR_RES2
+      return (int)hipGetLastError();
+    }
+    hipLaunchKernelGGL((wr_fwd_kernel<MODE_SPLIT, 2>), dim3(grid2), dim3(256), F_LDS2, s, Rhi,
+                       Rlo, Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1, gamma2,
+                       gamma3, eps, logits, ld_logits, (float4*)stats, Chi, Clo, att, att_T);
     return (int)hipGetLastError();
   }
   if (mode == MODE_SPLIT)

@@ -27,7 +27,8 @@
  *     regions R = 196 (14x14, padded to 224 in the split images); words per
  *     caption T <= t_pad, t_pad = 32 or 64 (64-token captions, T = 62): the
  *     token stride of every words / stats / C / token-table buffer.  t_pad =
- *     64 runs the general (running-max) kernels, bounded must be 0.
+ *     64: the forward always takes a running max (two waves per caption);
+ *     bounded selects the backward only (modes 0 and 2, see tgfr_wr_bwd).
  */
 #ifndef TGFR_H
 #define TGFR_H
@@ -86,9 +87,11 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
  * accumulated.  ws: tgfr_wr_bwd_ws floats of workspace: caption-chunk partial
  * slabs, added in chunk order into dR by a reduction launch inside the call;
  * counters: reserved (may be NULL).  The text side is detached in the
- * reference (utils/dataset_utils.py:42).  bounded = 1 (mode 0, t_pad 32,
- * after a bounded forward): both calls must pass it, Whi is the forward's
- * log2(e)-scaled words, and the software-pipelined kernel runs. */
+ * reference (utils/dataset_utils.py:42).  bounded = 1 (mode 0 with t_pad 32
+ * after a bounded forward, or modes 0 / 2 with t_pad 64; scores bounded as
+ * for tgfr_wr_fwd): both calls must pass it, Whi is the forward's
+ * log2(e)-scaled words, and the max-free kernels run (t_pad 32: the
+ * software-pipelined one). */
 int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const int* lens, int B_img,
                     int B_cap, float gamma1, float gamma2, float gamma3, float eps,
                     const float* dlogits, int ld, int bounded, int t_pad, float* tok_ws,

@@ -1244,9 +1244,9 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
   if (layout != 0) {
     if (!valid) o[0] = -INFINITY;       // exp2 offset of a padding token: A2 = 0
     o[6] = valid ? 0.f : -1e30f;        // G1's initial value row (word bias)
-    if ((threadIdx.x % WAVE) < 32) {
+    if ((threadIdx.x % WAVE) < TP) {    // 8 rows of TP tokens per pair
 #pragma unroll
-      for (int k = 0; k < 8; ++k) tok[pair * 256 + k * 32 + t] = o[k];
+      for (int k = 0; k < 8; ++k) tok[pair * 8 * TP + k * TP + t] = o[k];
     }
     return;
   }
@@ -1722,6 +1722,172 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide_kernel(
     for (int q = 0; q < 16; ++q) dst[acc_row(q, h) * D + dt * 32 + lr] = dR[dt][q];
 }
 
+// ------------------------------------ bwd, 64-token captions, bounded scores ---
+// wr_bwd_wide_kernel for the single-operand modes with bounded scores (the
+// BERT path's L2-normalised rows): the words come log2(e)-scaled (W', as the
+// forward's), the token table is wr_tok_kernel's layout 1 with 64-token rows,
+// and the softmax over words needs no running max: G1's accumulators start at
+// the word bias row, p = exp2(S') directly, and each element of the two
+// softmax backwards costs 2 exp2 + ~10 VALU (wr_bwd_pipe_kernel's algebra;
+// the exact-max kernel spends 3 exp + ~25 VALU and four token-table reads).
+template <int MODE>
+__global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
+    const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi, int B_img, int B_cap,
+    int n_chunks, float g1, const float* __restrict__ tok, const uint16_t* __restrict__ Chi,
+    float* __restrict__ slab) {
+  constexpr int BUF = BwdWCfg<MODE>::BUF;
+  static_assert(BwdWCfg<MODE>::NB == 2, "two-deep ring");
+  const int total = n_chunks * 2 * B_img;
+  const int work = xcd_remap(blockIdx.x, total);
+  const int b = work / (2 * n_chunks);
+  const int rem = work % (2 * n_chunks);
+  const int tg = rem / n_chunks, chunk = rem % n_chunks;
+  const int per = (B_cap + n_chunks - 1) / n_chunks;
+  const int c0 = chunk * per, c1 = min(B_cap, c0 + per);
+  const int tid = threadIdx.x, lane = tid % WAVE;
+  const int wid = __builtin_amdgcn_readfirstlane(tid / WAVE);
+  const int lr = lane & 31, h = lane >> 5;
+  const int rt = tg * 4 + wid;                 // region tile (7: padding only)
+  const int g16 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const float gL = g1 * 1.4426950408889634f;
+
+  bf16x8 Rf[16];
+  {
+    const long long roff = ((long long)b * RPAD + min(rt, NRT - 1) * 32 + lr) * D;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) Rf[s] = as_bf8(*(const uint4*)(Rhi + roff + s * 16 + h * 8));
+  }
+  f32x16 dR[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dR[j][q] = 0.f;
+  uint32_t g1o[8], g2o[2][4];
+  {
+    const int sw1 = ((lr & 3) << 2) | ((lr >> 2) & 3);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g1o[k] = lr * 256 + (((2 * k + h) ^ sw1) << 4);
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd)
+        g2o[bb][dd] = (4 * h + q4 + 8 * bb) * 256 + ((dd ^ q4) << 6) +
+                      (((2 * (g16 & 1) + (p4 >> 1)) ^ ((h + 2 * bb) & 3)) << 4) + (p4 & 1) * 8;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (c0 < c1)
+    bwd_stage_wide<MODE>(0, Whi, nullptr, Chi, nullptr, tok, (long long)b * B_cap + c0, c0, wid,
+                         lane);
+  // token scalar k of tile u for the lane's tokens 8g + 4h + 0..3 (q = 4g..4g+3)
+  auto scal = [&](uint32_t tb, int k, int u, int g) {
+    return __builtin_bit_cast(u32x4, lds_ld16(tb + k * 256 + u * 128 + g * 32 + h * 16));
+  };
+  auto fl = [](const u32x4& x, int q) { return __uint_as_float(x[q & 3]); };
+
+  for (int i = c0; i < c1; ++i) {
+    const int it = i - c0;
+    ring_barrier<0>();     // caption i landed; caption i-1's buffer retired
+    if (i + 1 < c1)
+      bwd_stage_wide<MODE>(((it + 1) & 1) * BUF, Whi, nullptr, Chi, nullptr, tok,
+                           (long long)b * B_cap + i + 1, i + 1, wid, lane);
+    const uint32_t base = (it & 1) * BUF;
+    const uint32_t tk = base + W_XIMG;
+    // ---- [S'^T ; Q-hat^T] of both token tiles = [W' ; C-hat] R_tile^T, S'
+    // starting at the word bias (0, or -1e30 for padding words)
+    f32x16 A0[2], A1[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u32x4 x = scal(tk, 6, u, g);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          A0[u][4 * g + k] = __uint_as_float(x[k]);
+          A1[u][4 * g + k] = 0.f;
+        }
+      }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t ow = base + g1o[s & 7] + (s >> 3) * (128 * 256) + u * 32 * 256;
+        const bf16x8 w = as_bf8(lds_ld16(ow)), c = as_bf8(lds_ld16(ow + 64 * 256));
+        mma<MODE>(A0[u], w, w, Rf[s], Rf[s]);
+        mma<MODE>(A1[u], c, c, Rf[s], Rf[s]);
+      }
+    }
+    // ---- softmax over the 64 words (p = exp2(S'), bounded) and both backwards
+    float a1[2][16], ax[2][16], v[2][16];
+    float sum = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        a1[u][q] = __builtin_amdgcn_exp2f(A0[u][q]);
+        sum += a1[u][q];
+      }
+    const float inv = __builtin_amdgcn_rcpf(xhalf_sum(sum));
+    const float kq = gL * inv;
+    float rho = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u32x4 f0 = scal(tk, 0, u, g), f1 = scal(tk, 1, u, g);
+        const u32x4 f2 = scal(tk, 2, u, g), f3 = scal(tk, 3, u, g);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = 4 * g + k;
+          const float p = a1[u][q];
+          a1[u][q] = p * inv;                                               // A1
+          ax[u][q] = __builtin_amdgcn_exp2f(fmaf(p, kq, fl(f0, k)));         // g1 A2 / log2e
+          const float du = fmaf(fl(f1, k), A0[u][q], fmaf(fl(f2, k), A1[u][q], -fl(f3, k)));
+          v[u][q] = a1[u][q] * (ax[u][q] * du);                              // A1 dA1 / log2e
+          rho += v[u][q];
+        }
+      }
+    rho = xhalf_sum(rho);
+    // ---- per token tile: M = [M_w | M_c] fragments, dR GEMM
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float mw[16], mc[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u32x4 f4 = scal(tk, 4, u, g), f5 = scal(tk, 5, u, g);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = 4 * g + k;
+          mw[q] = fmaf(fl(f4, k), ax[u][q], fmaf(-a1[u][q], rho, v[u][q]));
+          mc[q] = fl(f5, k) * ax[u][q];
+        }
+      }
+      bf16x8 M[4], unused;
+      frag8<MODE>(mw, M[0], unused);
+      frag8<MODE>(mw + 8, M[1], unused);
+      frag8<MODE>(mc, M[2], unused);
+      frag8<MODE>(mc + 8, M[3], unused);
+      // k outer: consecutive MFMAs update different accumulators
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          // k block: W' rows (k < 2) or C-hat rows of this tile, 16 tokens each
+          const int ks = (k < 2 ? 0 : 4) + 2 * u + (k & 1);
+          const uint32_t kb = base + (dt >> 2) * (128 * 256) + ks * 16 * 256;
+          const bf16x8 x = join_tr(lds_tr4(kb + g2o[0][dt & 3]), lds_tr4(kb + g2o[1][dt & 3]));
+          mma<MODE>(dR[dt], M[k], M[k], x, x);
+        }
+      }
+    }
+  }
+  if (rt >= NRT) return;
+  float* dst = slab + (((long long)chunk * B_img + b) * RPAD + rt * 32) * D;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dst[acc_row(q, h) * D + dt * 32 + lr] = dR[dt][q];
+}
+
 // -------------------------------------------- bwd, bf16, bounded, pipelined ---
 // Backward of wr_fwd_pipe_kernel (bf16 mode, bounded scores, log2(e)-scaled
 // words W').  Same work split and slab output as wr_bwd_kernel: workgroup =
@@ -2158,10 +2324,10 @@ int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const int* lens, int
                     void* stream) {
   if (B_img <= 0 || B_cap <= 0 || ld < B_cap) return 1001;
   const long long pairs = (long long)B_img * B_cap;
-  if (t_pad == 64 && !bounded)
+  if (t_pad == 64)
     hipLaunchKernelGGL(wr_tok_kernel<64>, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, (const float4*)stats, Wnorm, lens, dlogits, ld,
-                       B_img, B_cap, gamma1, gamma2, gamma3, eps, 0, tok_ws);
+                       B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 1 : 0, tok_ws);
   else if (t_pad == 32)
     hipLaunchKernelGGL(wr_tok_kernel<32>, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, (const float4*)stats, Wnorm, lens, dlogits, ld,
@@ -2189,7 +2355,20 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   // caption-chunk partial slabs in ws, summed into dR by wr_reduce_kernel
   const int n_chunks = slab_chunks(B_img, B_cap);
   const int grid = n_chunks * 2 * B_img;
-  if (bounded) {
+  if (bounded && t_pad == 64) {
+    if (const int e = allow_lds(wr_bwd_wide2_kernel<MODE_BF16>, BwdWCfg<MODE_BF16>::LDS)) return e;
+    if (const int e = allow_lds(wr_bwd_wide2_kernel<MODE_F16>, BwdWCfg<MODE_F16>::LDS)) return e;
+    if (mode == MODE_BF16)
+      hipLaunchKernelGGL(wr_bwd_wide2_kernel<MODE_BF16>, dim3(grid), dim3(256),
+                         BwdWCfg<MODE_BF16>::LDS, s, Rhi, Whi, B_img, B_cap, n_chunks, gamma1,
+                         tok_ws, Chi, ws);
+    else if (mode == MODE_F16)
+      hipLaunchKernelGGL(wr_bwd_wide2_kernel<MODE_F16>, dim3(grid), dim3(256),
+                         BwdWCfg<MODE_F16>::LDS, s, Rhi, Whi, B_img, B_cap, n_chunks, gamma1,
+                         tok_ws, Chi, ws);
+    else
+      return 1002;
+  } else if (bounded) {
     if (t_pad != 32) return 1001;
     if (mode != MODE_BF16) return 1002;
     if (const int e = allow_lds(wr_bwd_pipe_kernel, BP_LDS)) return e;

@@ -109,8 +109,12 @@ class WordRegionLogits(torch.autograd.Function):
         m = _wr_mode(mode)
         f16 = m == MODES["fp16"]
         bf16 = m != MODES["fp32"]          # single-operand modes (bf16, fp16)
-        # the bounded bf16 path runs the pipelined kernels both ways
-        fast = m == MODES["bf16"] and bool(bounded) and not att_T and t_pad == TPAD
+        # bounded scores: the bf16 path runs the pipelined kernels both ways;
+        # 64-token captions (bf16 / fp16) the bounded backward (log2(e)-scaled
+        # words, no running max)
+        fast = bool(bounded) and (
+            (m == MODES["bf16"] and not att_T and t_pad == TPAD) or
+            (m != MODES["fp32"] and t_pad == 2 * TPAD))
         r_hi, r_lo, r_norm = prep_rows(regions, NREG, RPAD, want_norms=bf16, f16=f16)
         if bf16:
             # the bf16 / fp16 forward takes log2(e)-scaled words (tgfr.h,

@@ -54,4 +54,4 @@ print(json.dumps({
     "launch": "eager" if a.eager else "hip-graph",
     "value": round(a.batch * a.steps / el, 1), "unit": "samples/s",
     "ms_per_step": round(el / a.steps * 1e3, 4),
-    "kernels_ms": {k: round(v[1], 4) for k, v in sorted(prof.items())}}), flush=True)
+    "eager_entry_ms": {k: round(v[1], 4) for k, v in sorted(prof.items())}}), flush=True)

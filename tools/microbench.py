@@ -48,7 +48,8 @@ def main(b=64, nw=30, mode="fp32", iters=20):
 if __name__ == "__main__":
     if "--bf16-only" in sys.argv:
         rest = [a for a in sys.argv[1:] if not a.startswith("--")]
-        main(b=int(rest[0]) if rest else 64, mode="bf16", iters=3)
+        main(b=int(rest[0]) if rest else 64, nw=int(rest[1]) if len(rest) > 1 else 30,
+             mode="bf16", iters=3)
         sys.exit(0)
     for mode in ("fp32", "bf16"):
         main(mode=mode)

@@ -198,6 +198,34 @@ def test_words_64_token_captions_vs_oracle(gpu, mode, b_img, b_cap, nw):
     assert err < gtol, err
 
 
+@pytest.mark.parametrize("mode", ["bf16", "fp16", "fp32"])
+def test_words_64_token_ragged_vs_oracle(gpu, mode):
+    """Ragged 64-token captions (cap_lens, losses.py:82): lengths on both sides of
+    the 32-token tile boundary, so the second tile's wave is all padding for
+    some captions and partly valid for others, through the two-tile forward and
+    the bounded backward (bf16 / fp16) or the split kernels (fp32)."""
+    K = _kernels()
+    torch.manual_seed(11)
+    b_img, b_cap = 5, 9
+    lens = torch.tensor([1, 31, 32, 33, 62, 40, 7, 64, 50], dtype=torch.int32)
+    r = _unit(torch.randn(b_img, 14, 14, 256)).permute(0, 3, 1, 2)
+    w = _unit(torch.randn(b_cap, 64, 256)).transpose(1, 2)
+    ro = r.clone().requires_grad_()
+    _, _, _, ref = O.words_loss(ro, w, None, lens, 64, 4.0, 5.0, 10.0, batch_size=b_cap)
+    probe = torch.randn(b_img, b_cap)
+    (ref * probe).sum().backward()
+    rg = r.to(gpu).requires_grad_()
+    logits = K.word_region_logits(rg, K.words_view(w.to(gpu), 64), lens, 4.0, 5.0, 10.0,
+                                  mode=mode, bounded=True)
+    (logits * probe.to(gpu)).sum().backward()
+    got = logits.detach().cpu()
+    assert torch.isfinite(got).all() and torch.isfinite(rg.grad).all()
+    tol, gtol = {"fp32": (1e-3, 2e-3), "bf16": (1e-1, 3e-2), "fp16": (2e-2, 1e-2)}[mode]
+    np.testing.assert_allclose(got.numpy(), ref.detach().numpy(), atol=tol, rtol=0)
+    err = (rg.grad.cpu() - ro.grad).abs().max().item() / ro.grad.abs().max().item()
+    assert err < gtol, err
+
+
 @pytest.mark.parametrize("precision,ltol,mtol", [("fp32", 1e-3, 1e-4), ("bf16", 5e-2, 5e-3),
                                                  ("fp16", 2e-2, 1e-3)])
 def test_words_loss_64_token_captions_attention_maps(gpu, precision, ltol, mtol):

@@ -487,6 +487,11 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
   // this wave's captions i = c0 + wid, +4, ...; the next caption's words are
   // loaded into Wc after the current caption's last MFMA, so the load latency
   // hides behind its epilogue
+  const int ec = 2 * (g16 & 1) + (p4 >> 1);
+  const uint32_t eoa = (8 * h + q4) * 64 + ((ec ^ (2 * h)) << 4) + (p4 & 1) * 8;
+  const uint32_t eob = (8 * h + q4 + 4) * 64 + ((ec ^ (2 * h + 1)) << 4) + (p4 & 1) * 8;
+  const uint32_t ew = lr * 64 + h * 8;
+  const int ewx = (lr >> 2) & 3;
   bf16x8 Wc[16];
   auto load_w = [&](int ii) {
 #pragma unroll
@@ -557,20 +562,19 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
       }
       // E^T tile j (bf16) -> LDS; DS instructions of one wave execute in order,
       // so the transposed reads below see these writes
+      // (swizzled E^T layout of wr_fwd_pipe_kernel: no bank conflicts)
       const uint32_t etj = et + (j & 1) * 2048;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         uint16_t hh[4];
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) hh[kk] = bf_bits(S[j][4 * g + kk]);
-        lds_st8(etj + lr * 64 + (8 * g + 4 * h) * 2,
+        lds_st8(etj + ew + ((g ^ ewx) << 4),
                 make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3])));
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int rbk = 16 * s + 8 * h;
-        const uint32_t eo = etj + (rbk + q4) * 64 + (16 * (g16 & 1) + 4 * p4) * 2;
-        const bf16x8 bb = join_tr(lds_tr4(eo), lds_tr4(eo + 4 * 64));
+        const bf16x8 bb = join_tr(lds_tr4(etj + eoa + s * 1024), lds_tr4(etj + eob + s * 1024));
 #pragma unroll
         for (int dt = 0; dt < 8; ++dt) {
           const uint32_t kb = (dt >> 2) * (RPAD * 256) + (j * 32 + 16 * s) * 256;

@@ -10,7 +10,7 @@ def unit(x):
     return x / x.norm(dim=-1, keepdim=True)
 
 
-def main(b=64, nw=30, mode="fp32", iters=20):
+def main(b=64, nw=30, mode="fp32", iters=20, bounded=True):
     dev = torch.device("cuda")
     torch.manual_seed(0)
     r = unit(torch.randn(b, 14, 14, 256, device=dev)).permute(0, 3, 1, 2).requires_grad_()
@@ -19,7 +19,7 @@ def main(b=64, nw=30, mode="fp32", iters=20):
     labels = torch.arange(b, device=dev)
 
     def step():
-        logits = K.word_region_logits(r, w, lens, 4.0, 5.0, 10.0, mode=mode, bounded=True)
+        logits = K.word_region_logits(r, w, lens, 4.0, 5.0, 10.0, mode=mode, bounded=bounded)
         loss = F.cross_entropy(logits, labels) + F.cross_entropy(logits.t(), labels)
         loss.backward()
         return loss
@@ -41,7 +41,7 @@ def main(b=64, nw=30, mode="fp32", iters=20):
     fwd, bwd = kt.replayed["tgfr_wr_fwd"], kt.replayed["tgfr_wr_bwd"]
     f_tf = 4 * 196 * 256 * nw * b * b / fwd / 1e9
     b_tf = 6 * 196 * 256 * nw * b * b / bwd / 1e9
-    print(f"mode={mode} B={b} T={nw}: {ms:.3f} ms/step  {flop / ms / 1e9:.1f} TFLOP/s algorithmic"
+    print(f"mode={mode} bounded={bounded} B={b} T={nw}: {ms:.3f} ms/step  {flop / ms / 1e9:.1f} TFLOP/s algorithmic"
           f" | fwd {fwd * 1000:.1f} us ({f_tf:.0f} TF)  bwd {bwd * 1000:.1f} us ({b_tf:.0f} TF)")
 
 
@@ -50,6 +50,10 @@ if __name__ == "__main__":
         rest = [a for a in sys.argv[1:] if not a.startswith("--")]
         main(b=int(rest[0]) if rest else 64, nw=int(rest[1]) if len(rest) > 1 else 30,
              mode="bf16", iters=3)
+        sys.exit(0)
+    if "--unbounded" in sys.argv:
+        main(mode="bf16", bounded=False)
+        main(b=128, mode="bf16", bounded=False)
         sys.exit(0)
     for mode in ("fp32", "bf16"):
         main(mode=mode)

@@ -27,8 +27,8 @@
  *     regions R = 196 (14x14, padded to 224 in the split images); words per
  *     caption T <= t_pad, t_pad = 32 or 64 (64-token captions, T = 62): the
  *     token stride of every words / stats / C / token-table buffer.  t_pad =
- *     64: the forward always takes a running max (two waves per caption);
- *     bounded selects the backward only (modes 0 and 2, see tgfr_wr_bwd).
+ *     64 (modes 0 / 2): two waves per caption; bounded = 1 drops the running
+ *     max both ways (scores bounded as below; Rnorm unused).
  */
 #ifndef TGFR_H
 #define TGFR_H

@@ -139,7 +139,7 @@ class WordRegionLogits(torch.autograd.Function):
         call("tgfr_wr_fwd", ptr(r_hi), ptr(r_lo), ptr(w_fwd), ptr(w_lo), ptr(w_norm),
              ptr(r_norm), ptr(lens), b_img, b_cap, img_offset, gamma1, gamma2, gamma3, eps,
              ptr(logits), b_cap, ptr(stats), ptr(c_hi), ptr(c_lo), ptr(att), att_T,
-             int(bool(bounded) and t_pad == TPAD), t_pad, m,
+             int(bool(bounded) and (t_pad == TPAD or m != MODES["fp32"])), t_pad, m,
              _hip.stream())
         ctx.save_for_backward(r_hi, r_lo, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo)
         ctx.cfg = (gamma1, gamma2, gamma3, eps, m, img_features.shape, fast, t_pad)

@@ -1755,6 +1755,8 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide_kernel(
 // the word bias row, p = exp2(S') directly, and each element of the two
 // softmax backwards costs 2 exp2 + ~10 VALU (wr_bwd_pipe_kernel's algebra;
 // the exact-max kernel spends 3 exp + ~25 VALU and four token-table reads).
+constexpr int WPF = 4;      // wr_bwd_wide2_kernel's LDS operand prefetch distance (slots)
+
 template <int MODE>
 __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi, int B_img, int B_cap,
@@ -1831,14 +1833,26 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
           A1[u][4 * g + k] = 0.f;
         }
       }
+    // 64 MFMAs n = (k-step s, tile u, W'/C-hat), operands read WPF slots ahead
+    // through a ring (one wave per SIMD: an LDS read waited on right before
+    // its MFMA stalls the wave for the whole LDS latency)
+    {
+      auto rd1 = [&](int n) {
+        const int s = n >> 2, u = (n >> 1) & 1, c = n & 1;
+        return lds_ld16(base + g1o[s & 7] + (s >> 3) * (128 * 256) + u * 32 * 256 +
+                        c * 64 * 256);
+      };
+      uint4 ring[8];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
+      for (int n = 0; n < WPF; ++n) ring[n] = rd1(n);
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const uint32_t ow = base + g1o[s & 7] + (s >> 3) * (128 * 256) + u * 32 * 256;
-        const bf16x8 w = as_bf8(lds_ld16(ow)), c = as_bf8(lds_ld16(ow + 64 * 256));
-        mma<MODE>(A0[u], w, w, Rf[s], Rf[s]);
-        mma<MODE>(A1[u], c, c, Rf[s], Rf[s]);
+      for (int n = 0; n < 64; ++n) {
+        const int s = n >> 2, u = (n >> 1) & 1;
+        const bf16x8 x = as_bf8(ring[n & 7]);
+        if (n & 1) mma<MODE>(A1[u], x, x, Rf[s], Rf[s]);
+        else mma<MODE>(A0[u], x, x, Rf[s], Rf[s]);
+        if (n + WPF < 64) ring[(n + WPF) & 7] = rd1(n + WPF);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     // ---- softmax over the 64 words (p = exp2(S'), bounded) and both backwards
@@ -1886,22 +1900,30 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
           mc[q] = fl(f5, k) * ax[u][q];
         }
       }
+      // dR GEMM operand n = (k block, d tile): k outer, so consecutive MFMAs
+      // update different accumulators; k block = W' rows (k < 2) or C-hat
+      // rows of this tile, 16 tokens each; read WPF slots ahead (the first
+      // ones before the fragments are packed)
+      auto rd3 = [&](int n) {
+        const int kk = n >> 3, dt = n & 7;
+        const int ks = (kk < 2 ? 0 : 4) + 2 * u + (kk & 1);
+        const uint32_t kb = base + (dt >> 2) * (128 * 256) + ks * 16 * 256;
+        return join_tr(lds_tr4(kb + g2o[0][dt & 3]), lds_tr4(kb + g2o[1][dt & 3]));
+      };
+      bf16x8 ring[8];
+#pragma unroll
+      for (int n = 0; n < WPF; ++n) ring[n] = rd3(n);
       bf16x8 M[4], unused;
       frag8<MODE>(mw, M[0], unused);
       frag8<MODE>(mw + 8, M[1], unused);
       frag8<MODE>(mc, M[2], unused);
       frag8<MODE>(mc + 8, M[3], unused);
-      // k outer: consecutive MFMAs update different accumulators
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-          // k block: W' rows (k < 2) or C-hat rows of this tile, 16 tokens each
-          const int ks = (k < 2 ? 0 : 4) + 2 * u + (k & 1);
-          const uint32_t kb = base + (dt >> 2) * (128 * 256) + ks * 16 * 256;
-          const bf16x8 x = join_tr(lds_tr4(kb + g2o[0][dt & 3]), lds_tr4(kb + g2o[1][dt & 3]));
-          mma<MODE>(dR[dt], M[k], M[k], x, x);
-        }
+      for (int n = 0; n < 32; ++n) {
+        const bf16x8 x = ring[n & 7];
+        mma<MODE>(dR[n & 7], M[n >> 3], M[n >> 3], x, x);
+        if (n + WPF < 32) ring[(n + WPF) & 7] = rd3(n + WPF);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }

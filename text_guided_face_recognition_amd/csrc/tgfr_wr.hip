@@ -1461,6 +1461,29 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
       f32x16 A0, A1;
 #pragma unroll
       for (int q = 0; q < 16; ++q) A0[q] = A1[q] = 0.f;
+      if constexpr (R_LDS) {
+        // single-operand modes: W / C rows and R fragments of k-step s read
+        // two k-steps ahead through a register ring (one wave per SIMD: a read
+        // waited on right before its MFMA exposes the LDS latency)
+        auto rd1 = [&](int s, uint4* o) {
+          const uint32_t ow = base + g1o[s & 7] + (s >> 3) * (64 * 256);
+          o[0] = lds_ld16(ow);
+          o[1] = lds_ld16(ow + 32 * 256);
+          o[2] = lds_ld16(rof[s & 7] + (s >> 3) * 256);
+        };
+        uint4 ring[4][3];
+        rd1(0, ring[0]);
+        rd1(1, ring[1]);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const uint4* o = ring[s & 3];
+          const bf16x8 w = as_bf8(o[0]), c = as_bf8(o[1]), rr = as_bf8(o[2]);
+          mma<MODE>(A0, w, w, rr, rr);
+          mma<MODE>(A1, c, c, rr, rr);
+          if (s + 2 < 16) rd1(s + 2, ring[(s + 2) & 3]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         const uint32_t ow = base + g1o[s & 7] + (s >> 3) * (64 * 256);
@@ -1480,6 +1503,7 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
         }
         mma<MODE>(A0, w_hi, w_lo, rh, rl);
         mma<MODE>(A1, c_hi, c_lo, rh, rl);
+      }
       }
       // sched_barrier fences keep the scheduler from hoisting the LDS reads of
       // later phases (their results would pin registers across the softmax)
@@ -1535,6 +1559,25 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_kernel(
       frag8<MODE>(mc + 8, Mh[3], Ml[3]);
       __builtin_amdgcn_sched_barrier(0);
       // ---- dR_tile[r][d] += sum_k M[r][k] X[k][d]
+      if constexpr (R_LDS) {
+        // operand n = (d tile dt, k block ks) read 4 MFMAs ahead
+        auto rd3 = [&](int n) {
+          const int dt = n >> 2, ks = n & 3;
+          const uint32_t kb =
+              base + (dt >> 2) * (64 * 256) + ((ks >> 1) * 32 + (ks & 1) * 16) * 256;
+          return join_tr(lds_tr4(kb + g2o[0][dt & 3]), lds_tr4(kb + g2o[1][dt & 3]));
+        };
+        bf16x8 ring[8];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) ring[n] = rd3(n);
+#pragma unroll
+        for (int n = 0; n < 32; ++n) {
+          const bf16x8 x = ring[n & 7];
+          mma_agpr<MODE>(dR[n >> 2], Mh[n & 3], Ml[n & 3], x, x);
+          if (n + 4 < 32) ring[(n + 4) & 7] = rd3(n + 4);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) {
 #pragma unroll

@@ -1949,43 +1949,77 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
         }
       }
     rho = xhalf_sum(rho);
-    // ---- per token tile: M = [M_w | M_c] fragments, dR GEMM
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      float mw[16], mc[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const u32x4 f4 = scal(tk, 4, u, g), f5 = scal(tk, 5, u, g);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int q = 4 * g + k;
-          mw[q] = fmaf(fl(f4, k), ax[u][q], fmaf(-a1[u][q], rho, v[u][q]));
-          mc[q] = fl(f5, k) * ax[u][q];
-        }
-      }
-      // dR GEMM operand n = (k block, d tile): k outer, so consecutive MFMAs
-      // update different accumulators; k block = W' rows (k < 2) or C-hat
-      // rows of this tile, 16 tokens each; read WPF slots ahead (the first
-      // ones before the fragments are packed)
+    // ---- dR GEMM over both token tiles: 64 MFMAs n = (tile u, k block, d
+    // tile dt), k outer so consecutive MFMAs update different accumulators; k
+    // block = W' rows (k < 2) or C-hat rows of the tile, 16 tokens each.
+    // Operands read WPF slots ahead; tile 0's M fragments are formed before
+    // the loop, tile 1's in the gaps of tile 0's first 16 MFMAs.
+    {
       auto rd3 = [&](int n) {
-        const int kk = n >> 3, dt = n & 7;
+        const int u = n >> 5, kk = (n >> 3) & 3, dt = n & 7;
         const int ks = (kk < 2 ? 0 : 4) + 2 * u + (kk & 1);
         const uint32_t kb = base + (dt >> 2) * (128 * 256) + ks * 16 * 256;
         return join_tr(lds_tr4(kb + g2o[0][dt & 3]), lds_tr4(kb + g2o[1][dt & 3]));
       };
+      auto pk2 = [](float x, float y) {
+        if constexpr (MODE == MODE_F16) return pack2(f16_bits(x), f16_bits(y));
+        else return pk_bf16(x, y);
+      };
       bf16x8 ring[8];
 #pragma unroll
       for (int n = 0; n < WPF; ++n) ring[n] = rd3(n);
-      bf16x8 M[4], unused;
-      frag8<MODE>(mw, M[0], unused);
-      frag8<MODE>(mw + 8, M[1], unused);
-      frag8<MODE>(mc, M[2], unused);
-      frag8<MODE>(mc + 8, M[3], unused);
+      bf16x8 M0[4], M1[4];
+      {
+        uint32_t w2[8], c2[8];
 #pragma unroll
-      for (int n = 0; n < 32; ++n) {
+        for (int g = 0; g < 4; ++g) {
+          const u32x4 f4 = scal(tk, 4, 0, g), f5 = scal(tk, 5, 0, g);
+#pragma unroll
+          for (int kq = 0; kq < 4; kq += 2) {
+            const int q = 4 * g + kq;
+            const float w0 = fmaf(fl(f4, kq), ax[0][q], fmaf(-a1[0][q], rho, v[0][q]));
+            const float w1 = fmaf(fl(f4, kq + 1), ax[0][q + 1], fmaf(-a1[0][q + 1], rho, v[0][q + 1]));
+            w2[q >> 1] = pk2(w0, w1);
+            c2[q >> 1] = pk2(fl(f5, kq) * ax[0][q], fl(f5, kq + 1) * ax[0][q + 1]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          M0[j] = __builtin_bit_cast(bf16x8, make_uint4(w2[4 * j], w2[4 * j + 1], w2[4 * j + 2], w2[4 * j + 3]));
+          M0[2 + j] = __builtin_bit_cast(bf16x8, make_uint4(c2[4 * j], c2[4 * j + 1], c2[4 * j + 2], c2[4 * j + 3]));
+        }
+      }
+      uint32_t w2[8], c2[8];
+      u32x4 f4 = scal(tk, 4, 1, 0), f5 = scal(tk, 5, 1, 0);
+#pragma unroll
+      for (int n = 0; n < 64; ++n) {
         const bf16x8 x = ring[n & 7];
-        mma<MODE>(dR[n & 7], M[n >> 3], M[n >> 3], x, x);
-        if (n + WPF < 32) ring[(n + WPF) & 7] = rd3(n + WPF);
+        const int kk = (n >> 3) & 3;
+        const bf16x8 m = n < 32 ? M0[kk] : M1[kk];
+        mma<MODE>(dR[n & 7], m, m, x, x);
+        if (n + WPF < 64) ring[(n + WPF) & 7] = rd3(n + WPF);
+        if (n < 16) {                     // tile 1, token pair q = 2 (n >> 1)
+          const int q = n & ~1;
+          if (n & 1) {
+            c2[q >> 1] = pk2(fl(f5, q) * ax[1][q], fl(f5, q + 1) * ax[1][q + 1]);
+            if ((n & 3) == 3 && n < 15) {
+              f4 = scal(tk, 4, 1, (n + 1) >> 2);
+              f5 = scal(tk, 5, 1, (n + 1) >> 2);
+            }
+          } else {
+            const float w0 = fmaf(fl(f4, q), ax[1][q], fmaf(-a1[1][q], rho, v[1][q]));
+            const float w1 =
+                fmaf(fl(f4, q + 1), ax[1][q + 1], fmaf(-a1[1][q + 1], rho, v[1][q + 1]));
+            w2[q >> 1] = pk2(w0, w1);
+          }
+          if (n == 15) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              M1[j] = __builtin_bit_cast(bf16x8, make_uint4(w2[4 * j], w2[4 * j + 1], w2[4 * j + 2], w2[4 * j + 3]));
+              M1[2 + j] = __builtin_bit_cast(bf16x8, make_uint4(c2[4 * j], c2[4 * j + 1], c2[4 * j + 2], c2[4 * j + 3]));
+            }
+          }
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     }

@@ -507,12 +507,22 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res_kernel(
     for (int j = 0; j < NRT; ++j)
 #pragma unroll
       for (int q = 0; q < 16; ++q) S[j][q] = 0.f;
+    {
+      // 112 MFMAs n = (k-step s, region tile j), R operands read 3 slots ahead
+      // through a register ring (wr_fwd_res2_kernel's scheme)
+      auto rd1 = [&](int n) {
+        const int s = n / NRT, j = n % NRT;
+        return lds_ld16(f1o[s & 7] + (s >> 3) * (RPAD * 256) + j * 32 * 256);
+      };
+      uint4 ring[4];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
+      for (int n = 0; n < 3; ++n) ring[n] = rd1(n);
 #pragma unroll
-      for (int j = 0; j < NRT; ++j) {
-        const bf16x8 bb = as_bf8(lds_ld16(f1o[s & 7] + (s >> 3) * (RPAD * 256) + j * 32 * 256));
-        S[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Wc[s], bb, S[j], 0, 0, 0);
+      for (int n = 0; n < 16 * NRT; ++n) {
+        const int s = n / NRT, j = n % NRT;
+        S[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Wc[s], as_bf8(ring[n & 3]), S[j], 0, 0, 0);
+        if (n + 3 < 16 * NRT) ring[(n + 3) & 3] = rd1(n + 3);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     // ---- per region tile j: softmax over words (E overwrites S, per-token Z

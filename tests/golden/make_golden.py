@@ -42,8 +42,9 @@ def _import_reference(root):
     import models.attention as ref_att
     import models.fusion_nets as ref_fus
     import models.losses as ref_loss
+    import models.metrics as ref_metrics
     import models.models as ref_models
-    return ref_att, ref_loss, ref_fus, ref_models
+    return ref_att, ref_loss, ref_fus, ref_models, ref_metrics
 
 
 class _Args:
@@ -272,10 +273,57 @@ def gen_text_heading(ref_models):
               words_emb=words, words_out=w_out.contiguous(), sent_out=s_out)
 
 
+def _cpu_torch_proxy():
+    """A ``torch`` module proxy whose ``zeros`` ignores ``device=``: the one
+    CUDA-only call of ArcMarginProduct.forward is its one-hot buffer
+    (models/metrics.py:53, ``torch.zeros(..., device='cuda')``); everything
+    else is the real torch."""
+    proxy = types.ModuleType("torch_proxy")
+    proxy.__dict__.update(torch.__dict__)
+    real = torch.zeros
+
+    def zeros(*size, device=None, **kw):
+        return real(*size, **kw)
+    proxy.zeros = zeros
+    return proxy
+
+
+def gen_arc_margin(ref_metrics):
+    """ArcMarginProduct (models/metrics.py:17-60) with s = 30 (image head) and
+    35 (text head, src/train_encoders_bert.py:186-191), easy_margin False and
+    True; some rows aligned and some anti-aligned with their class weight so
+    both sides of every torch.where (:47-50) are taken.  Gradients to the input
+    and to the weight through a random probe."""
+    ref_metrics.torch = _cpu_torch_proxy()
+    torch.manual_seed(800)
+    b, d, n_cls = 8, 256, 50
+    label = torch.tensor([3, 17, 3, 49, 0, 22, 8, 31])
+    base = ref_metrics.ArcMarginProduct(d, n_cls, s=30.0, m=0.5)
+    weight0 = base.weight.detach().clone()
+    wn = weight0 / weight0.norm(dim=1, keepdim=True)
+    sign = torch.tensor([1.0, -1.0, 0.3, -1.0, 1.0, 0.0, -0.2, 1.0]).view(-1, 1)
+    x0 = 2.0 * (sign * wn[label] + 0.02 * torch.randn(b, d))
+    probe = torch.randn(b, n_cls)
+    arrays = dict(x=x0, weight=weight0, label=label, probe=probe, m=0.5)
+    for s_ in (30.0, 35.0):
+        for easy in (False, True):
+            net = ref_metrics.ArcMarginProduct(d, n_cls, s=s_, m=0.5, easy_margin=easy)
+            with torch.no_grad():
+                net.weight.copy_(weight0)
+            x = x0.clone().requires_grad_()
+            out = net(x, label)
+            (out * probe).sum().backward()
+            tag = f"s{int(s_)}_{'easy' if easy else 'std'}"
+            arrays[f"out_{tag}"] = out
+            arrays[f"d_x_{tag}"] = x.grad
+            arrays[f"d_w_{tag}"] = net.weight.grad
+    _save("arc_margin_b8", **arrays)
+
+
 def main():
     root = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
     torch.set_num_threads(8)
-    ref_att, ref_loss, ref_fus, ref_models = _import_reference(root)
+    ref_att, ref_loss, ref_fus, ref_models, ref_metrics = _import_reference(root)
     gen_func_attention(ref_att)
     gen_words_loss(ref_loss)
     gen_sent_global_clip(ref_loss)
@@ -283,6 +331,7 @@ def main():
     gen_working(ref_fus)
     gen_image_heading(ref_models)
     gen_text_heading(ref_models)
+    gen_arc_margin(ref_metrics)
 
 
 if __name__ == "__main__":

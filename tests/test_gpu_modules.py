@@ -330,6 +330,48 @@ def test_arc_margin_and_focal(gpu):
     assert _relerr(lg.grad, g["d_logits"]) < 1e-4
 
 
+@pytest.mark.parametrize("tag", ["s30_std", "s35_std", "s30_easy", "s35_easy"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_arc_margin_golden(gpu, tag, precision):
+    """ArcMarginProduct against the REFERENCE's own outputs (models/metrics.py:
+    17-60, tests/golden/arc_margin_b8.npz): logits 1e-5 relative, dW 1e-4,
+    dx 1e-4 (fp32) / 1e-2 (the bf16 dx GEMM); rows on both sides of each
+    margin branch.  Then both identity heads in one launch (kernels.IdentityHeads,
+    text s=35 frozen input, image s=30) give the reference logits' focal losses
+    (FocalLoss pinned by focal_loss_b8)."""
+    from oracle import tgfr_oracle as O
+    from text_guided_face_recognition_amd import kernels as K
+    from text_guided_face_recognition_amd.models.metrics import ArcMarginProduct
+    g = load_golden("arc_margin_b8")
+    s_, kind = tag.split("_")
+    easy = kind == "easy"
+    head = ArcMarginProduct(256, 50, s=float(s_[1:]), m=float(g["m"]), easy_margin=easy).to(gpu)
+    head.precision = precision
+    with torch.no_grad():
+        head.weight.copy_(t(g["weight"]))
+    lab = t(g["label"]).to(gpu)
+    x = t(g["x"]).to(gpu).requires_grad_()
+    out = head(x, lab)
+    (out * t(g["probe"]).to(gpu)).sum().backward()
+    assert _relerr(out, g[f"out_{tag}"]) < 1e-5
+    assert _relerr(head.weight.grad, g[f"d_w_{tag}"]) < 1e-4
+    assert _relerr(x.grad, g[f"d_x_{tag}"]) < (1e-4 if precision == "fp32" else 1e-2)
+    if kind == "std" and s_ == "s30":
+        tc = ArcMarginProduct(256, 50, s=35, m=0.5).to(gpu)
+        ic = ArcMarginProduct(256, 50, s=30, m=0.5).to(gpu)
+        tc.precision = ic.precision = precision
+        with torch.no_grad():
+            tc.weight.copy_(t(g["weight"]))
+            ic.weight.copy_(t(g["weight"]))
+        xs = t(g["x"]).to(gpu)
+        tid, iid = K.identity_heads(xs, tc, xs.clone().requires_grad_(), ic, lab, 2.0)
+        lab_c = t(g["label"])
+        rt = O.focal_loss(t(g["out_s35_std"]), lab_c).item()
+        ri = O.focal_loss(t(g["out_s30_std"]), lab_c).item()
+        assert abs(tid.item() - rt) < 1e-5 * max(1.0, rt)
+        assert abs(iid.item() - ri) < 1e-5 * max(1.0, ri)
+
+
 @pytest.mark.parametrize("b,d,c,easy,precision", [
     (64, 256, 4500, False, "bf16"), (64, 640, 1000, False, "fp32"), (13, 256, 300, True, "fp32"),
     (70, 128, 37, False, "bf16"), (256, 640, 4500, False, "bf16"), (200, 256, 300, True, "fp32")])

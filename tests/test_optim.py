@@ -152,10 +152,43 @@ def test_lr_schedule_between_graph_replays(gpu):
         if epoch in (3, 8):
             for pg in sgd.param_groups:
                 pg["lr"] *= 0.1
-            opt.scale_lr(1, 0.1)
+            # the reference's own pattern (src/train_encoders_bert.py:408-410)
+            for pg in opt.param_groups[1:]:
+                pg["lr"] *= 0.1
         assert abs(opt.get_lr(0) - adam.param_groups[0]["lr"]) < 1e-12
         assert abs(opt.get_lr(1) - sgd.param_groups[0]["lr"]) < 1e-12
     torch.cuda.synchronize()
     for p, q in zip(mine, ref):
         err = ((p - q).abs().max() / q.abs().max()).item()
         assert err < 1e-5, err
+
+
+def test_param_groups_lr_assignment_reaches_the_kernel():
+    """``g['lr'] = x`` on param_groups (the reference's classifier lr cut,
+    src/train_encoders_bert.py:408-410) changes the device lr factor the kernel
+    reads, not only the reported value; indices follow the caller's list even
+    with an empty group; a rejected set_lr leaves the state unchanged."""
+    a = [torch.zeros(4, requires_grad=True)]
+    s = [torch.zeros(3, requires_grad=True)]
+    z = [torch.zeros(2, requires_grad=True)]
+    opt = FusedOptimizer([adam_group(a, lr=2e-4), adam_group([], lr=1.0),
+                          sgd_group(s, lr=0.1), sgd_group(z, lr=0.0)])
+    groups = opt.param_groups
+    assert len(groups) == 4 and groups[2]["lr"] == 0.1
+    for g in groups[2:3]:
+        g["lr"] *= 0.1
+    assert abs(opt.get_lr(2) - 0.01) < 1e-12
+    assert abs(opt.lr_scale[1].item() - 0.1) < 1e-7          # internal slot of group 2
+    assert abs(groups[2]["lr"] - 0.01) < 1e-12
+    opt.scale_lr(0, 0.98)
+    assert abs(opt.param_groups[0]["lr"] - 2e-4 * 0.98) < 1e-12
+    assert abs(opt.lr_scale[0].item() - 0.98) < 1e-7
+    groups[1]["lr"] = 0.5                                     # empty group: host value only
+    assert opt.get_lr(1) == 0.5
+    before = opt.lr_scale.clone()
+    with pytest.raises(ValueError):
+        groups[3]["lr"] = 1e-3                                # base lr 0 cannot be rescaled
+    assert opt.get_lr(3) == 0.0 and groups[3]["lr"] == 0.0
+    assert torch.equal(before, opt.lr_scale)
+    with pytest.raises(ValueError):
+        groups[0]["betas"] = (0.9, 0.9)

@@ -158,3 +158,34 @@ def test_text_heading(tag):
                                  [t(b) for b in g["conv_b"]], int(g["bert_words_num"]))
     close(words, g["words_out"])
     close(sent, g["sent_out"])
+
+
+ARC_TAGS = ["s30_std", "s35_std", "s30_easy", "s35_easy"]
+
+
+@pytest.mark.parametrize("tag", ARC_TAGS)
+def test_arc_margin(tag):
+    """oracle.arc_margin against the reference's ArcMarginProduct
+    (models/metrics.py:17-60, run with its CUDA one-hot buffer on the CPU,
+    make_golden.gen_arc_margin): logits and both gradients, both heads'
+    scales, both margin variants, rows on both sides of each torch.where."""
+    g = load_golden("arc_margin_b8")
+    s_, kind = tag.split("_")
+    x = t(g["x"]).requires_grad_()
+    w = t(g["weight"]).requires_grad_()
+    out = O.arc_margin(x, w, t(g["label"]), s=float(s_[1:]), m=float(g["m"]),
+                       easy_margin=kind == "easy")
+    close(out, g[f"out_{tag}"], atol=2e-5)
+    (out * t(g["probe"])).sum().backward()
+    close(x.grad, g[f"d_x_{tag}"], atol=1e-5, rtol=1e-4)
+    close(w.grad, g[f"d_w_{tag}"], atol=1e-5, rtol=1e-4)
+
+
+def test_arc_margin_fixture_covers_both_branches():
+    g = load_golden("arc_margin_b8")
+    wn = g["weight"] / np.linalg.norm(g["weight"], axis=1, keepdims=True)
+    xn = g["x"] / np.linalg.norm(g["x"], axis=1, keepdims=True)
+    cos_lab = (xn * wn[g["label"]]).sum(1)
+    th = np.cos(np.pi - 0.5)
+    assert (cos_lab > th).any() and (cos_lab <= th).any()      # standard margin branch
+    assert (cos_lab > 0).any() and (cos_lab <= 0).any()        # easy margin branch

@@ -48,8 +48,12 @@ def deps():
                   glob.glob(os.path.join(INCLUDE, "*.h")) + [os.path.abspath(__file__)])
 
 
-def source_hash():
+def source_hash(extra=()):
+    """Hash of every input of the build: the sources and headers, this file,
+    the compiler, the target and any extra flags (a debug / experiment build
+    never carries the default build's stamp)."""
     h = hashlib.sha256()
+    h.update(f"{HIPCC}|{ARCH}|{' '.join(extra)}".encode())
     for p in deps():
         h.update(os.path.relpath(p, os.path.dirname(PKG)).encode())
         with open(p, "rb") as f:
@@ -91,7 +95,7 @@ def build(force=False, verbose=False, extra=()):
 
 
 def _build_locked(verbose, extra):
-    digest = source_hash()
+    digest = source_hash(tuple(extra))
     os.makedirs(OBJ_DIR, exist_ok=True)
     common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
               "-fno-gpu-rdc", "-Wno-unused-result", "-Wno-unused-value", "-I", CSRC, *extra]

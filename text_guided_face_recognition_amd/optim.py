@@ -50,11 +50,42 @@ def sgd_group(params, lr, momentum=0.0, dampening=0.0, weight_decay=0.0):
             "dampening": dampening, "weight_decay": weight_decay}
 
 
+class _GroupView(dict):
+    """One entry of ``FusedOptimizer.param_groups``: a torch.optim-style dict
+    whose ``g['lr'] = x`` goes through ``set_lr`` (the reference cuts the
+    classifier lr that way, src/train_encoders_bert.py:408-410), so the kernel
+    applies exactly the lr the dict reports."""
+
+    def __init__(self, opt, index, group):
+        super().__init__(group)
+        self._opt, self._index = opt, index
+
+    def __setitem__(self, key, value):
+        if key == "lr":
+            self._opt.set_lr(self._index, value)      # validates, then mirrors here
+            return
+        if key in self and self[key] != value:
+            raise ValueError(f"param group key {key!r} is fixed at construction "
+                             "(only 'lr' can change between steps)")
+        super().__setitem__(key, value)
+
+
 class FusedOptimizer:
     def __init__(self, groups):
-        groups = [g for g in groups if g["params"]]
-        if not groups or len(groups) > MAX_GROUPS:
+        groups = list(groups)
+        # caller's group index -> internal index (None for an empty group, which
+        # keeps its slot so set_lr / scale_lr / param_groups indices match the
+        # caller's list, as in torch.optim)
+        self._index = []
+        kept = []
+        for g in groups:
+            self._index.append(len(kept) if g["params"] else None)
+            if g["params"]:
+                kept.append(g)
+        if not kept or len(kept) > MAX_GROUPS:
             raise ValueError(f"1..{MAX_GROUPS} non-empty parameter groups")
+        self._all_groups = groups
+        groups = kept
         self.groups = groups
         self.params = [p for g in groups for p in g["params"]]
         if len(self.params) > MAX_SEGS:
@@ -92,28 +123,41 @@ class FusedOptimizer:
         self._segs_c = (_Seg * len(self.params))()
 
     def get_lr(self, group):
-        """The learning rate group `group` uses at the next step (host value)."""
-        return self.groups[group]["lr"]
+        """The learning rate group `group` (caller's index) uses at the next
+        step (host value)."""
+        return float(self._all_groups[group]["lr"])
 
     def set_lr(self, group, lr):
-        """Set group `group`'s learning rate for the following steps (one tiny
-        device write; no re-capture of a graphed step needed)."""
+        """Set group `group`'s learning rate (caller's index) for the following
+        steps (one tiny device write; no re-capture of a graphed step needed).
+        Validated before anything changes."""
         lr = float(lr)
-        self.groups[group]["lr"] = lr
-        base = self.base_lr[group]
-        with torch.no_grad():
-            self.lr_scale[group].fill_(lr / base if base != 0.0 else 0.0)
-        if base == 0.0 and lr != 0.0:
-            raise ValueError("cannot rescale a group created with lr = 0")
+        gi = self._index[group]
+        if gi is not None:
+            base = self.base_lr[gi]
+            if base == 0.0 and lr != 0.0:
+                raise ValueError("cannot rescale a group created with lr = 0")
+            with torch.no_grad():
+                self.lr_scale[gi].fill_(lr / base if base != 0.0 else 0.0)
+        self._all_groups[group]["lr"] = lr
+        views = self.__dict__.get("_views")
+        if views is not None:
+            dict.__setitem__(views[group], "lr", lr)
 
     def scale_lr(self, group, gamma):
         """lr *= gamma for one group (ExponentialLR.step, the 0.1 cuts)."""
-        self.set_lr(group, self.groups[group]["lr"] * gamma)
+        self.set_lr(group, self.get_lr(group) * gamma)
 
     @property
     def param_groups(self):
-        """torch.optim-style view: one dict per group with its current 'lr'."""
-        return self.groups
+        """torch.optim-style view: one dict per group (the caller's order, empty
+        groups included) with its current 'lr'; ``g['lr'] = x`` is applied to
+        the next step exactly like ``set_lr``."""
+        views = self.__dict__.get("_views")
+        if views is None:
+            views = self._views = [_GroupView(self, i, g)
+                                   for i, g in enumerate(self._all_groups)]
+        return views
 
     @property
     def step_count(self):

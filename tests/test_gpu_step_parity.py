@@ -53,13 +53,15 @@ def _cpu_params(module, keys):
     return {v: named[k].detach().cpu().clone().requires_grad_() for k, v in keys.items()}
 
 
-def _check_adam(param, old, ref_new, grad, lr, name="", g_all=0.0, wd=0.0):
+def _check_adam(param, old, ref_new, grad, lr, name="", g_all=0.0, wd=0.0, gtol=5e-3,
+                utol=1e-4, gfloor=1e-5):
     """Gradient and first Adam update of one parameter against the oracle.
 
-    The gradient (p.grad after the step) must be within 5e-3 of the tensor's
-    largest reference gradient (the IMIM q/k projections reach ~4e-3: their
+    The gradient (p.grad after the step) must be within gtol (5e-3 in fp32
+    mode) of the tensor's largest reference gradient (the IMIM q/k projections reach ~4e-3: their
     gradient runs through the 196-wide attention softmax backward), plus
-    1e-5 of the largest gradient of the whole head (g_all) -- a floor for
+    gfloor (1e-5 in fp32 mode) of the largest gradient of the whole head
+    (g_all) -- a floor for
     tensors whose exact gradient is zero, such as the key-role bias, which
     the attention softmax cancels.  Adam's
     first update is lr * g / (|g| + 1e-8), i.e. +-lr: a sign decision, so it
@@ -71,7 +73,7 @@ def _check_adam(param, old, ref_new, grad, lr, name="", g_all=0.0, wd=0.0):
     g_mine = param.grad.detach().cpu()
     g_err = (g_mine - grad).abs().max().item()
     g_scale = grad.abs().max().item()
-    assert g_err <= 5e-3 * g_scale + 1e-5 * g_all + 1e-12, (
+    assert g_err <= gtol * g_scale + gfloor * g_all + 1e-12, (
         f"{name}: gradient error {g_err:.3e} = {g_err / g_scale:.3e} of max {g_scale:.3e}")
     d_mine, d_ref = new - old, ref_new - old
     assert (d_mine - d_ref).abs().max().item() <= 2 * lr + 1e-7, name
@@ -80,11 +82,13 @@ def _check_adam(param, old, ref_new, grad, lr, name="", g_all=0.0, wd=0.0):
     scale = old.abs().max().clamp(min=1e-3)
     diff = (d_mine - d_ref).abs() * sure
     err = diff.max() / scale
-    if err.item() >= 1e-4:
+    if err.item() >= utol:
         i = int(diff.argmax())
         raise AssertionError(f"{name}: update error {err.item():.3e} of scale at element {i}: "
                              f"ref grad {grad.flatten()[i].item():.3e} (max {g_scale:.3e}), "
                              f"d_mine {d_mine.flatten()[i]:.3e}, d_ref {d_ref.flatten()[i]:.3e}")
+    # relative error, for tensors whose gradient is not ~0 (the floor case)
+    return g_err / g_scale if g_scale > 1e-3 * g_all else 0.0
 
 
 def _check_sgd(new, ref_new):
@@ -103,23 +107,18 @@ def _bert_trainer(dev, b, nw, seed, n_ids):
     return tr, batch, args
 
 
-@pytest.mark.parametrize("b,nw,n_ids", [(8, 22, 5), (16, 30, 200)])
-def test_train_step_matches_oracle(gpu, b, nw, n_ids):
-    """Stage-1 BERT step: duplicate class ids (n_ids = 5) exercise the
-    sent_loss same-class mask."""
-    tr, batch, args = _bert_trainer(gpu, b, nw, 31 + b, n_ids)
-    g, local, words, sent, cls = batch
+def _oracle_bert_step(tr, batch, args, b, nw):
+    """The reference's stage-1 step (src/train_encoders_bert.py:254-331) on the
+    oracle, from the trainer's current weights: loss groups, head gradients,
+    post-step parameters and the word-region logits."""
     hp = _cpu_params(tr.image_head, HEAD_KEYS)
     arc_i = tr.image_cls.weight.detach().cpu().clone().requires_grad_()
     arc_t = tr.text_cls.weight.detach().cpu().clone().requires_grad_()
     old = {k: v.detach().clone() for k, v in hp.items()}
-    old_i, old_t = arc_i.detach().clone(), arc_t.detach().clone()
-
-    # the oracle step (train_encoders_bert.py:254-331)
     gc, lc, wc, sc, cc = (x.cpu() for x in batch)
     labels = torch.arange(b)
     gp, r = O.image_heading(gc, lc, hp)
-    w0, w1, _, _ = O.words_loss(r, wc, labels, None, nw, 4.0, 5.0, 10.0)
+    w0, w1, _, wlogits = O.words_loss(r, wc, labels, None, nw, 4.0, 5.0, 10.0)
     s0, s1, _ = O.sent_loss(gp, sc, labels, cc.numpy(), 10.0)
     tid = O.focal_loss(O.arc_margin(sc, arc_t, cc, s=35), cc)
     iid = O.focal_loss(O.arc_margin(gp, arc_i, cc, s=30), cc)
@@ -129,23 +128,122 @@ def test_train_step_matches_oracle(gpu, b, nw, n_ids):
     grads = {k: v.grad.clone() for k, v in hp.items()}
     torch.optim.Adam(list(hp.values()), lr=args.lr_head, betas=(0.5, 0.999)).step()
     torch.optim.SGD([arc_i, arc_t], lr=0.1, momentum=0.9, weight_decay=5e-5).step()
+    terms = {"w0": w0, "w1": w1, "s0": s0, "s1": s1, "tid": tid, "iid": iid, "global": cl}
+    return dict(hp=hp, old=old, grads=grads, arc_i=arc_i.detach(), arc_t=arc_t.detach(),
+                terms={k: v.item() for k, v in terms.items()},
+                groups={"damsm": (w0 + w1 + s0 + s1).item(), "clip": cl.item(),
+                        "ident": args.lambda_id * (tid + iid).item()},
+                wlogits=wlogits.detach())
+
+
+@pytest.mark.parametrize("b,nw,n_ids", [(8, 22, 5), (16, 30, 200)])
+def test_train_step_matches_oracle(gpu, b, nw, n_ids):
+    """Stage-1 BERT step: duplicate class ids (n_ids = 5) exercise the
+    sent_loss same-class mask."""
+    tr, batch, args = _bert_trainer(gpu, b, nw, 31 + b, n_ids)
+    old_i = tr.image_cls.weight.detach().cpu().clone()
+    old_t = tr.text_cls.weight.detach().cpu().clone()
+    ref = _oracle_bert_step(tr, batch, args, b, nw)
+    hp, grads = ref["hp"], ref["grads"]
 
     out = tr.step(batch)
     torch.cuda.synchronize()
-    ref = {"damsm": (w0 + w1 + s0 + s1).item(), "clip": cl.item(),
-           "ident": args.lambda_id * (tid + iid).item()}
-    for k, v in ref.items():
+    for k, v in ref["groups"].items():
         # ident is 100 x (two focal losses): 1e-3 on each focal term
         tol = 1e-3 * (2 * args.lambda_id if k == "ident" else 1)
         assert abs(out[k].item() - v) < tol, (k, out[k].item(), v)
     named = dict(tr.image_head.named_parameters())
     for k, v in HEAD_KEYS.items():
-        _check_adam(named[k], old[v], hp[v].detach(), grads[v], args.lr_head, k,
+        _check_adam(named[k], ref["old"][v], hp[v].detach(), grads[v], args.lr_head, k,
                     max(x.abs().max().item() for x in grads.values()))
-    _check_sgd(tr.image_cls.weight.detach().cpu(), arc_i.detach())
-    _check_sgd(tr.text_cls.weight.detach().cpu(), arc_t.detach())
+    _check_sgd(tr.image_cls.weight.detach().cpu(), ref["arc_i"])
+    _check_sgd(tr.text_cls.weight.detach().cpu(), ref["arc_t"])
     assert not torch.equal(tr.image_cls.weight.detach().cpu(), old_i)
     assert not torch.equal(tr.text_cls.weight.detach().cpu(), old_t)
+
+
+# Reduced-precision steps (the benchmarked configuration and BASELINE configs[4]'s
+# precision).  Tolerances (measured on MI355X, round 3, in brackets):
+#   word-region terms w0, w1: 1e-2 each -- the bf16 operands carry 2^-9
+#     relative rounding that gamma2 * gamma3 = 50 amplifies in the logits
+#     (DESIGN.md 2); fp16 2^-11  [damsm group 1.8e-4 bf16, 2.0e-4 fp16]
+#   sentence / global / identity terms: 1e-3 (north star): they run on fp32
+#     features (g' by the split-mode projection, the fp32-MFMA ArcMargin)
+#     [<= 1e-6; ident group 1.2e-4 / 9.8e-4 = 100 x focal errors of ~1e-5]
+#   SGD on both classifiers: relative 1e-3 of the tensor's scale  [5e-6]
+#   Adam on the image head: gradients within 1e-1 of each tensor's largest
+#     reference gradient (bf16 IMIM activations, DESIGN.md 2) plus 1e-3 of the
+#     head's largest gradient (the projection bias sums 196 B bf16-rounded rows
+#     whose total nearly cancels: 1.5e-2 absolute against 17 at B = 32, fp16
+#     step), the update's sign wherever the reference gradient exceeds 4x that
+#     error  [worst 1.1e-2 of scale, bf16]
+REDUCED = {
+    "bf16": dict(wtol=1e-2, otol=1e-3, gtol=1e-1),
+    "fp16": dict(wtol=1e-2, otol=1e-3, gtol=1e-1),
+}
+
+
+@pytest.mark.parametrize("precision,b,nw", [("bf16", 64, 30), ("fp16", 32, 62)])
+def test_train_step_reduced_precision_matches_oracle(gpu, precision, b, nw):
+    """The benchmarked step (bf16, BASELINE configs[1]: B = 64, T = 30) and the
+    fp16 step at 64-token captions (configs[4]'s precision and caption length,
+    B = 32) against the oracle's fp32 step on the same weights and batch."""
+    from text_guided_face_recognition_amd.config import make_args
+    from text_guided_face_recognition_amd.models import losses as L
+    from text_guided_face_recognition_amd.train import Train, synthetic_batch
+    tol = REDUCED[precision]
+    torch.manual_seed(41 + b)
+    args = make_args(batch_size=b, bert_words_num=nw + 2, num_classes=4500,
+                     precision=precision)
+    tr = Train(args, gpu)
+    batch = synthetic_batch(b, nw, gpu, seed=42 + b, n_ids=4500)
+    ref = _oracle_bert_step(tr, batch, args, b, nw)
+    # the trainer's own word-region logits on the same weights (before the step)
+    g, local, words, sent, cls = batch
+    with torch.no_grad():
+        gi, ri = tr.image_head(g, local)
+        lens = torch.full((b,), nw, dtype=torch.int32)
+        wl = _words_logits(ri, words, lens, nw, precision).cpu()
+        lab = torch.arange(b, device=gpu)
+        s0, s1, cl = L.sent_global_loss(gi, sent, lab, cls, b, args)
+        mine = {"s0": s0.item(), "s1": s1.item(), "global": cl.item()}
+    out = tr.step(batch)
+    torch.cuda.synchronize()
+    wref = ref["wlogits"]
+    lerr = (wl - wref).abs().max().item()
+    top2 = wref.topk(2, dim=1).values
+    sure = (top2[:, 0] - top2[:, 1]) > 2 * lerr
+    print(f"{precision} step B={b} T={nw}: word-region logit error {lerr:.3e}, "
+          f"rows with a resolvable top-2 gap {int(sure.sum())}/{b}")
+    assert (wl.argmax(1) == wref.argmax(1))[sure].all()
+    for k in ("s0", "s1", "global"):
+        err = abs(mine[k] - ref["terms"][k])
+        print(f"  {k}: error {err:.3e}")
+        assert err < tol["otol"], (k, mine[k], ref["terms"][k])
+    errs = {k: abs(out[k].item() - v) for k, v in ref["groups"].items()}
+    print("  groups:", {k: f"{v:.3e}" for k, v in errs.items()})
+    assert errs["damsm"] < 2 * tol["wtol"] + 2 * tol["otol"], errs
+    assert errs["clip"] < tol["otol"], errs
+    assert errs["ident"] < 2 * args.lambda_id * 1e-3, errs
+    named = dict(tr.image_head.named_parameters())
+    g_all = max(x.abs().max().item() for x in ref["grads"].values())
+    gmax = 0.0
+    for k, v in HEAD_KEYS.items():
+        gmax = max(gmax, _check_adam(named[k], ref["old"][v], ref["hp"][v].detach(),
+                                     ref["grads"][v], args.lr_head, k, g_all,
+                                     gtol=tol["gtol"], utol=1e-3, gfloor=1e-3))
+    print(f"  worst head gradient error {gmax:.3e} of its tensor's scale")
+    for new, want in ((tr.image_cls.weight, ref["arc_i"]), (tr.text_cls.weight, ref["arc_t"])):
+        scale = want.abs().max().clamp(min=1e-6)
+        err = ((new.detach().cpu() - want).abs().max() / scale).item()
+        print(f"  SGD update error {err:.3e} of scale")
+        assert err < 1e-3, err
+
+
+def _words_logits(ri, words, lens, nw, precision):
+    from text_guided_face_recognition_amd import kernels as K
+    return K.word_region_logits(ri, K.words_view(words, nw), lens, 4.0, 5.0, 10.0,
+                                mode=precision, bounded=True)
 
 
 def test_train_step_each_loss_term(gpu):

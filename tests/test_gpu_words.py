@@ -289,3 +289,55 @@ def test_words_config3_rank_shape(gpu, mode):
         sure = (top2[:, 0] - top2[:, 1]) > 2 * err
         print(f"  rows with a resolvable top-2 gap: {int(sure.sum())} / {b_img}")
         assert (got.argmax(1) == refd.argmax(1))[sure].all()
+
+
+@pytest.mark.parametrize("mode,ltol,gtol", [("fp16", 2e-2, 1e-2), ("bf16", 1e-1, 3e-2)])
+def test_words_config5_rank_shape(gpu, mode, ltol, gtol):
+    """BASELINE configs[4] as one rank sees it: B_l = 128 local images against
+    B_g = 1024 all-gathered captions (8 ranks x 128), bert_words_num = 64 ->
+    T = 62 (losses.py:73-132, :83), bounded (unit-norm BERT-path rows): the
+    two-tile forward and the bounded 64-token backward over the full
+    128 x 1024 grid (caption chunks of 1024 / n_chunks).
+
+    The oracle loops over a 128-caption column subset (columns are
+    independent; the subset includes the first and last caption); the
+    gradient is taken through a probe that is zero outside those columns, so
+    the kernel's dR must equal the oracle's for the subset.  fp16 (the
+    config's precision): logits within 2e-2, region gradient 1e-2 of its
+    scale; bf16 1e-1 / 3e-2.  Row argmax over the subset identical wherever
+    the reference top-2 gap exceeds twice the measured error; every logit of
+    the full grid finite."""
+    K = _kernels()
+    b_img, b_cap, nw = 128, 1024, 62
+    gen = torch.Generator().manual_seed(1024)
+    r = _unit(torch.randn(b_img, 14, 14, 256, generator=gen)).permute(0, 3, 1, 2)
+    w = _unit(torch.randn(b_cap, nw, 256, generator=gen)).transpose(1, 2)
+    inner = torch.randperm(b_cap - 2, generator=gen)[:126] + 1
+    cols = torch.cat([torch.tensor([0, b_cap - 1]), inner]).sort().values
+    ro = r.clone().requires_grad_()
+    _, _, _, ref = O.words_loss(ro, w[cols], None, None, nw, 4.0, 5.0, 10.0,
+                                batch_size=len(cols))
+    probe = torch.randn(b_img, len(cols), generator=gen)
+    (ref * probe).sum().backward()
+    probe_full = torch.zeros(b_img, b_cap)
+    probe_full[:, cols] = probe
+    rg = r.to(gpu).requires_grad_()
+    logits = K.word_region_logits(rg, K.words_view(w.to(gpu), nw),
+                                  torch.full((b_cap,), nw, dtype=torch.int32), 4.0, 5.0,
+                                  10.0, mode=mode, bounded=True)
+    (logits * probe_full.to(gpu)).sum().backward()
+    full = logits.detach().cpu()
+    assert torch.isfinite(full).all() and torch.isfinite(rg.grad).all()
+    got = full[:, cols]
+    refd = ref.detach()
+    err = (got - refd).abs().max().item()
+    gerr = ((rg.grad.cpu() - ro.grad).abs().max() / ro.grad.abs().max()).item()
+    top2 = refd.topk(2, dim=1).values
+    sure = (top2[:, 0] - top2[:, 1]) > 2 * err
+    print(f"configs[4] rank shape {mode}: max |logit error| {err:.3e}, gradient error "
+          f"{gerr:.3e} of scale, rows with a resolvable top-2 gap {int(sure.sum())}/{b_img}")
+    assert err < ltol and gerr < gtol
+    assert (got.argmax(1) == refd.argmax(1))[sure].all()
+    top2c = refd.topk(2, dim=0).values
+    surec = (top2c[0] - top2c[1]) > 2 * err
+    assert (got.argmax(0) == refd.argmax(0))[surec].all()

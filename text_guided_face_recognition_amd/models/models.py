@@ -92,8 +92,14 @@ class ImageHeading(nn.Module):
 
     def forward(self, global_image, local_image):
         local_image = self.imim(local_image)
-        global_image = self.project_global(global_image)
-        return global_image, local_image
+        # g' feeds only fp32 consumers (the sentence / global cosine logits and
+        # the fp32-MFMA identity head, whose loss is scaled by s * lambda_id =
+        # 3000): its B x 512 x 256 projection runs in the split (fp32) mode in
+        # every precision -- a few microseconds -- so the reduced-precision
+        # modes leave those terms at fp32 accuracy
+        p = self.project_global
+        y = K.linear_rows(global_image, p.projection.weight, p.projection.bias, mode="fp32")
+        return K.l2norm_rows(y), local_image
 
 
 class Bert_Word_Mapping(nn.Module):  # noqa: N801  (reference class name)

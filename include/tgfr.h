@@ -85,23 +85,27 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
  * fused recompute + both softmax backwards + dR GEMM, writing
  * dR[b][r][d] (r < 196) at dR[b*s_b + r*s_r + d*s_d] -- overwritten, not
  * accumulated.  ws: tgfr_wr_bwd_ws floats of workspace: caption-chunk partial
- * slabs, added in chunk order into dR by a reduction launch inside the call;
- * counters: reserved (may be NULL).  The text side is detached in the
+ * slabs, added in chunk order into dR by a reduction launch inside the call.
+ * Rnorm (bounded only; the forward's |R_r| [B_img][224]): the pair's score
+ * bound c = max|W| max|R| is formed again here, and from c >= 40 on the
+ * max-free backwards shift the recomputed scores by it exactly as the
+ * bounded forward does, so the bounded kernels stay finite past the unit-norm
+ * contract (fp32 range: c < ~58 for any input).  The text side is detached in the
  * reference (utils/dataset_utils.py:42).  bounded = 1 (mode 0 with t_pad 32
  * after a bounded forward, or modes 0 / 2 with t_pad 64; scores bounded as
  * for tgfr_wr_fwd): both calls must pass it, Whi is the forward's
  * log2(e)-scaled words, and the max-free kernels run (t_pad 32: the
  * software-pipelined one). */
-int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const int* lens, int B_img,
-                    int B_cap, float gamma1, float gamma2, float gamma3, float eps,
+int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const float* Rnorm, const int* lens,
+                    int B_img, int B_cap, float gamma1, float gamma2, float gamma3, float eps,
                     const float* dlogits, int ld, int bounded, int t_pad, float* tok_ws,
                     void* stream);
 int tgfr_wr_bwd_ws(int B_img, int B_cap, int bounded, int t_pad, int mode, long long* floats);
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, int B_img, int B_cap, float gamma1, const float* tok_ws,
                 const uint16_t* Chi, const uint16_t* Clo, float* dR, long long s_b,
-                long long s_r, long long s_d, float* ws, unsigned* counters, int bounded,
-                int t_pad, int mode, void* stream);
+                long long s_r, long long s_d, float* ws, int bounded, int t_pad, int mode,
+                void* stream);
 
 /* Verification pair scores (utils/modules.py:152-153): out[i] = x_i.y_i /
  * max(|x_i| |y_i|, eps) for matched rows of x [rows][d] (ldx) and y (ldy). */

@@ -341,3 +341,36 @@ def test_words_config5_rank_shape(gpu, mode, ltol, gtol):
     top2c = refd.topk(2, dim=0).values
     surec = (top2c[0] - top2c[1]) > 2 * err
     assert (got.argmax(0) == refd.argmax(0))[surec].all()
+
+
+@pytest.mark.parametrize("mode,nw,ltol,gtol", [("bf16", 30, 2e-1, 6e-2), ("bf16", 62, 3e-2, 4e-2),
+                                               ("fp16", 62, 5e-3, 1e-2)])
+def test_words_bounded_past_unit_norm(gpu, mode, nw, ltol, gtol):
+    """The max-free (bounded) kernels fed features far from the unit-norm
+    contract (|W| = 6, |R| = 8, so the score bound c = 48 > 40): forward and
+    backward both shift the scores by the device-computed bound, so logits and
+    gradients stay finite and match the oracle (models/losses.py:83-109 on
+    unnormalised BERT-path features).  Measured (MI355X): bf16 T=30 logits
+    1.0e-1 (the t_pad = 32 forward's shift cancels c Z in N),
+    gradients 3.6e-2 of max; bf16 T=62 7.5e-3 / 1.8e-2; fp16 8.7e-4 / 2.7e-3."""
+    K = _kernels()
+    torch.manual_seed(23 + nw)
+    b_img, b_cap = 7, 11
+    r = 8.0 * _unit(torch.randn(b_img, 14, 14, 256)).permute(0, 3, 1, 2)
+    w = 6.0 * _unit(torch.randn(b_cap, nw, 256)).transpose(1, 2)
+    ro = r.clone().requires_grad_()
+    _, _, _, ref = O.words_loss(ro, w, None, None, nw, 4.0, 5.0, 10.0, batch_size=b_cap)
+    probe = torch.randn(b_img, b_cap)
+    (ref * probe).sum().backward()
+    rg = r.to(gpu).requires_grad_()
+    logits = K.word_region_logits(rg, K.words_view(w.to(gpu), nw),
+                                  torch.full((b_cap,), nw, dtype=torch.int32),
+                                  4.0, 5.0, 10.0, mode=mode, bounded=True)
+    (logits * probe.to(gpu)).sum().backward()
+    got = logits.detach().cpu()
+    assert torch.isfinite(got).all() and torch.isfinite(rg.grad).all()
+    lerr = (got - ref.detach()).abs().max().item()
+    gerr = (rg.grad.cpu() - ro.grad).abs().max().item() / ro.grad.abs().max().item()
+    print(f"{mode} T={nw}: logit err {lerr:.3e}, grad err {gerr:.3e}")
+    assert lerr < ltol, lerr
+    assert gerr < gtol, gerr

@@ -630,11 +630,12 @@ struct DwOut {
   float* db[3];
 };
 
-// out = sum over slices, in slice order; thread = 4 consecutive outputs
+// out = sum over slices, in slice order; thread = 2 consecutive outputs (a
+// grid of ~2 workgroups per CU) with 8 slice loads in flight
 __global__ __launch_bounds__(256) void tail_dw_reduce_kernel(DwArgs A, DwOut O,
                                                              const float* __restrict__ ws,
                                                              long long e_total) {
-  const long long e4 = (blockIdx.x * 256LL + threadIdx.x) * 4;
+  const long long e4 = (blockIdx.x * 256LL + threadIdx.x) * 2;
   if (e4 >= e_total) return;
   // which product / region: products laid out as [dW N*K][db N] each
   long long off = e4;
@@ -658,12 +659,14 @@ __global__ __launch_bounds__(256) void tail_dw_reduce_kernel(DwArgs A, DwOut O,
     stride = P.N;
     dst = O.db[pi] + (off - nk);
   }
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  float2 s = make_float2(0.f, 0.f);
+#pragma unroll 8
   for (int z = 0; z < A.slices; ++z) {
-    const float4 v = *(const float4*)(src + z * stride);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    const float2 v = *(const float2*)(src + z * stride);
+    s.x += v.x;
+    s.y += v.y;
   }
-  *(float4*)dst = s;
+  *(float2*)dst = s;
 }
 
 // n products (N[i] x K[i], multiples of 128) over `rows` rows; wg_budget:
@@ -715,7 +718,7 @@ int dw_launch(const DwArgs& A, int n_wg, const DwOut& O, float* ws, hipStream_t 
   hipLaunchKernelGGL(fn, dim3(n_wg), dim3(256), DW_LDS, s, A, ws);
   long long e_total = 0;
   for (int i = 0; i < 3; ++i) e_total += (long long)A.p[i].N * A.p[i].K + A.p[i].N;
-  hipLaunchKernelGGL(tail_dw_reduce_kernel, dim3((unsigned)((e_total / 4 + 255) / 256)),
+  hipLaunchKernelGGL(tail_dw_reduce_kernel, dim3((unsigned)((e_total / 2 + 255) / 256)),
                      dim3(256), 0, s, A, O, ws, e_total);
   return (int)hipGetLastError();
 }

@@ -658,8 +658,8 @@ constexpr int RPF = 3;      // wr_fwd_res2_kernel's LDS operand prefetch distanc
 template <int MODE, bool ATT, bool BOUNDED>
 __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi,
-    const float* __restrict__ Wnorm, const int* __restrict__ lens, int B_img, int B_cap,
-    int n_chunks, int img_offset, float g1, float g2, float g3, float eps,
+    const float* __restrict__ Wnorm, const float* __restrict__ Rnorm, const int* __restrict__ lens,
+    int B_img, int B_cap, int n_chunks, int img_offset, float g1, float g2, float g3, float eps,
     float* __restrict__ logits, int ld_logits, float4* __restrict__ stats,
     uint16_t* __restrict__ Chi, float* __restrict__ att, int att_T) {
   constexpr int TP = 64;
@@ -689,6 +689,14 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
     __syncthreads();
   }
   if (c0 >= c1) return;                          // workgroup-uniform
+  // BOUNDED: max_r |R_r| of this image, the image factor of the per-caption
+  // score bound c (as wr_fwd_pipe_kernel: past 40 the scores are shifted by c)
+  float rmax = 0.f;
+  if (BOUNDED) {
+    const float* rn = Rnorm + (long long)b * RPAD;
+    rmax = wave_max(fmaxf(fmaxf(rn[lane], rn[lane + 64]),
+                          fmaxf(rn[lane + 128], lane < 4 ? rn[lane + 192] : 0.f)));
+  }
   const uint32_t et = FR_OFF_ET + wid * 4096;
   const uint32_t tok = FR_OFF_TOK + wid * 256;
   // (the d >= 128 half has its own GEMM2 bases so every read is base + immediate)
@@ -733,11 +741,19 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
     // (accumulators start at the word bias: 0, or -1e30 for padding words,
     // whose E = exp(0) = 1 then only feeds their own unused statistics and
     // C-hat rows, as in wr_fwd_pipe_kernel)
+    // (BOUNDED: valid words start at -log2(e) c, c = max|W| max|R| of the
+    // caption when >= 40, else 0; both token tiles' waves form the same c)
+    float cb = 0.f;
+    if (BOUNDED) {
+      cb = wave_max(Wnorm[(long long)ic * TP + lane]) * rmax;
+      if (cb < 40.f) cb = 0.f;
+    }
+    const float sh = -L2E * cb;
     f32x16 S[NRT];
 #pragma unroll
     for (int j = 0; j < NRT; ++j)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) S[j][q] = acc_row(q, h) < tl ? 0.f : -1e30f;
+      for (int q = 0; q < 16; ++q) S[j][q] = acc_row(q, h) < tl ? sh : -1e30f;
     {
       // 112 MFMAs n = (k-step s, region tile j), R operands read RPF ahead
       auto rd1 = [&](int n) { return lds_ld16(f1o[(n / NRT) >> 3][(n / NRT) & 7] + (n % NRT) * 32 * 256); };
@@ -877,7 +893,8 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
       for (int q = 0; q < 16; ++q) csq = fmaf(C[dt][q], C[dt][q], csq);
     csq += __shfl_xor(csq, 32);
     const float Z = lds_ldf(tok + t * 4);
-    const float nhat = lds_ldf(tok + 128 + t * 4) * (1.f / L2E);
+    // (np sums E (S' + sh) = log2(e) (N - c Z) over the regions)
+    const float nhat = lds_ldf(tok + 128 + t * 4) * (1.f / L2E) + cb * Z;
     const bool tvalid = t < tl;
     const float zinv = 1.f / Z;
     const float cn = sqrtf(csq) * zinv;
@@ -1249,6 +1266,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
 template <int TP>
 __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ stats,
                                                      const float* __restrict__ Wnorm,
+                                                     const float* __restrict__ Rnorm,
                                                      const int* __restrict__ lens,
                                                      const float* __restrict__ dlogits, int ld,
                                                      int B_img, int B_cap, float g1, float g2,
@@ -1261,6 +1279,19 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
   const int len = lens[i];
   const bool valid = t < len;
   const float4 st = valid ? stats[pair * TP + t] : make_float4(1.f, 0.f, 0.f, 0.f);
+  // layout 1: the pair's score bound c = max_t |W_t| max_r |R_r| (as the
+  // bounded forwards form it); past 40 the max-free backwards shift S' by
+  // -log2(e) c through the G1 initial row, and sigma absorbs alpha c
+  float cb = 0.f;
+  if (layout != 0 && Rnorm) {
+    const float* rn = Rnorm + (long long)b * RPAD;
+    const int l = threadIdx.x % WAVE;
+    float rmax = fmaxf(fmaxf(rn[l], rn[l + 64]), fmaxf(rn[l + 128], l < 4 ? rn[l + 192] : 0.f));
+    rmax = wave_max(rmax);
+    const float wn = Wnorm[(long long)i * TP + t];
+    cb = (TP == 64 ? wave_max(wn) : half_max(wn)) * rmax;
+    if (cb < 40.f) cb = 0.f;
+  }
   const float ex = valid ? __expf(g2 * st.w) : 0.f;
   const float tot = TP == 64 ? wave_sum(ex) : half_sum(ex);
   float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1291,14 +1322,14 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
       o[0] = __log2f(g1 * iz / L2E);    // E -> g1 A2 / log2e, as an exp2 offset
       o[1] = alpha / L2E;               // coefficient of S' in dA2
       o[2] = beta * iz;                 // coefficient of Q-hat in dA2
-      o[3] = sigma;
+      o[3] = sigma - alpha * cb;        // (S' enters as S' - log2(e) c)
       o[4] = alpha / g1;                // M_w = dS / log2e + o4 * (g1 A2 / log2e)
       o[5] = beta * iz * L2E / g1;      // M_c = o5 * (g1 A2 / log2e)
     }
   }
   if (layout != 0) {
     if (!valid) o[0] = -INFINITY;       // exp2 offset of a padding token: A2 = 0
-    o[6] = valid ? 0.f : -1e30f;        // G1's initial value row (word bias)
+    o[6] = valid ? -1.4426950408889634f * cb : -1e30f;   // G1's initial value row
     if ((threadIdx.x % WAVE) < TP) {    // 8 rows of TP tokens per pair
 #pragma unroll
       for (int k = 0; k < 8; ++k) tok[pair * 8 * TP + k * TP + t] = o[k];
@@ -1820,6 +1851,83 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide_kernel(
     for (int q = 0; q < 16; ++q) dst[acc_row(q, h) * D + dt * 32 + lr] = dR[dt][q];
 }
 
+// ------------------------------------------- dR output of the bounded kernels ---
+// One caption chunk (n_chunks == 1, e.g. B_img >= 128 on 256 CUs): the wave's
+// finished dR tile goes straight to the caller's dR (fp32, strides).  Several:
+// each chunk's partial goes to a bf16 slab in MFMA fragment order -- lane l of
+// (chunk, image, region tile, d tile) holds rows acc_row(q, l/32), q < 16, of
+// column 32 dt + l%32 as 32 contiguous bytes, two dwordx4 stores per d tile
+// (the fp32 row-scatter epilogue was 128 dword stores per lane, half the
+// bytes per store of this one and twice the bytes) -- and wr_reduce_frag_kernel
+// adds the chunks in chunk order in fp32.  (bf16 partials: 2^-9 of each
+// chunk's partial, well inside the bf16 mode's gradient error.)
+constexpr long long FRAG_TILE = 8 * 64 * 16;     // bf16 elements per (image, region tile)
+
+__device__ __forceinline__ void store_dr_tile(const f32x16 (&dR)[8], int n_chunks, int chunk,
+                                              int b, int rt, int B_img, int lane,
+                                              float* __restrict__ out, long long s_b,
+                                              long long s_r, long long s_d,
+                                              uint16_t* __restrict__ slab) {
+  const int lr = lane & 31, h = lane >> 5;
+  if (n_chunks == 1) {
+    float* o = out + (long long)b * s_b;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r = rt * 32 + acc_row(q, h);
+      if (r < NREG)
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) o[r * s_r + (dt * 32 + lr) * s_d] = dR[dt][q];
+    }
+    return;
+  }
+  uint16_t* dst = slab + (((long long)chunk * B_img + b) * NRT + rt) * FRAG_TILE + lane * 16;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    const f32x16& a = dR[dt];
+    uint4* d4 = (uint4*)(dst + dt * 64 * 16);
+    d4[0] = make_uint4(pk_bf16(a[0], a[1]), pk_bf16(a[2], a[3]), pk_bf16(a[4], a[5]),
+                       pk_bf16(a[6], a[7]));
+    d4[1] = make_uint4(pk_bf16(a[8], a[9]), pk_bf16(a[10], a[11]), pk_bf16(a[12], a[13]),
+                       pk_bf16(a[14], a[15]));
+  }
+}
+
+// dR[b][r][d] = sum over chunks of the fragment-order bf16 partials; thread =
+// one (image, region tile, d tile, lane): 32 B per chunk in, 16 rows of one
+// column out (a wave's stores are 128-B row segments)
+__global__ __launch_bounds__(256) void wr_reduce_frag_kernel(const uint16_t* __restrict__ slab,
+                                                             int n_chunks, int B_img,
+                                                             float* __restrict__ out,
+                                                             long long s_b, long long s_r,
+                                                             long long s_d) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= B_img * NRT * 8 * 64) return;
+  const int lane = e & 63, dt = (e >> 6) & 7, tile = e >> 9;      // tile = b * NRT + rt
+  const int b = tile / NRT, rt = tile % NRT;
+  const int lr = lane & 31, h = lane >> 5;
+  float acc[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  const long long cstride = (long long)B_img * NRT * FRAG_TILE;
+  const uint16_t* src = slab + (long long)tile * FRAG_TILE + (dt * 64 + lane) * 16;
+  for (int c = 0; c < n_chunks; ++c) {
+    const uint4 v0 = *(const uint4*)(src + c * cstride);
+    const uint4 v1 = *(const uint4*)(src + c * cstride + 8);
+    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      acc[2 * k] += __uint_as_float(w[k] << 16);
+      acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
+  float* o = out + (long long)b * s_b + (dt * 32 + lr) * s_d;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int r = rt * 32 + acc_row(q, h);
+    if (r < NREG) o[r * s_r] = acc[q];
+  }
+}
+
 // ------------------------------------ bwd, 64-token captions, bounded scores ---
 // wr_bwd_wide_kernel for the single-operand modes with bounded scores (the
 // BERT path's L2-normalised rows): the words come log2(e)-scaled (W', as the
@@ -1834,7 +1942,8 @@ template <int MODE>
 __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi, int B_img, int B_cap,
     int n_chunks, float g1, const float* __restrict__ tok, const uint16_t* __restrict__ Chi,
-    float* __restrict__ slab) {
+    float* __restrict__ out, long long s_b, long long s_r, long long s_d,
+    uint16_t* __restrict__ slab) {
   constexpr int BUF = BwdWCfg<MODE>::BUF;
   static_assert(BwdWCfg<MODE>::NB == 2, "two-deep ring");
   const int total = n_chunks * 2 * B_img;
@@ -2035,11 +2144,7 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
     }
   }
   if (rt >= NRT) return;
-  float* dst = slab + (((long long)chunk * B_img + b) * RPAD + rt * 32) * D;
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) dst[acc_row(q, h) * D + dt * 32 + lr] = dR[dt][q];
+  store_dr_tile(dR, n_chunks, chunk, b, rt, B_img, lane, out, s_b, s_r, s_d, slab);
 }
 
 // -------------------------------------------- bwd, bf16, bounded, pipelined ---
@@ -2075,7 +2180,8 @@ constexpr int BP_LDS = BP_ZERO + BP_TOK;
 __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi, int B_img, int B_cap,
     int n_chunks, float g1, const float* __restrict__ tok, const uint16_t* __restrict__ Chi,
-    float* __restrict__ slab) {
+    float* __restrict__ out, long long s_b, long long s_r, long long s_d,
+    uint16_t* __restrict__ slab) {
   const int total = n_chunks * 2 * B_img;
   const int work = xcd_remap(blockIdx.x, total);
   const int b = work / (2 * n_chunks);
@@ -2319,11 +2425,7 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
     stage(t + 1, Ab0, Ab1, Aa0, Aa1, Mb, Ma);
   }
   if (rt >= NRT) return;
-  float* dst = slab + (((long long)chunk * B_img + b) * RPAD + rt * 32) * D;
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) dst[acc_row(q, h) * D + dt * 32 + lr] = dR[dt][q];
+  store_dr_tile(dR, n_chunks, chunk, b, rt, B_img, lane, out, s_b, s_r, s_d, slab);
 }
 
 __global__ __launch_bounds__(256) void wr_reduce_kernel(const float* __restrict__ slab,
@@ -2331,15 +2433,21 @@ __global__ __launch_bounds__(256) void wr_reduce_kernel(const float* __restrict_
                                                         float* __restrict__ out, long long s_b,
                                                         long long s_r, long long s_d,
                                                         int accumulate) {
-  const long long n = (long long)B_img * NREG * D;
-  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
-    const int d = e % D;
-    const long long br = e / D;
+  // thread = 4 consecutive d of one (image, region) row
+  const int n4 = B_img * NREG * (D / 4);
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < n4; e += gridDim.x * 256) {
+    const int d = (e % (D / 4)) * 4;
+    const int br = e / (D / 4);
     const int rr = br % NREG, b = br / NREG;
-    float acc = 0.f;
-    for (int c = 0; c < n_chunks; ++c) acc += slab[(((long long)c * B_img + b) * RPAD + rr) * D + d];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int c = 0; c < n_chunks; ++c) {
+      const float4 v = *(const float4*)(slab + (((long long)c * B_img + b) * RPAD + rr) * D + d);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
     float* o = out + b * s_b + rr * s_r + d * s_d;
-    *o = accumulate ? *o + acc : acc;
+    const float a[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k * s_d] = accumulate ? o[k * s_d] + a[k] : a[k];
   }
 }
 
@@ -2366,6 +2474,18 @@ static int device_cus() {
 static int slab_chunks(int B_img, int B_cap) {
   const int want = std::max(1, (device_cus() + 2 * B_img - 1) / (2 * B_img));
   return std::max(1, std::min(B_cap, want));
+}
+
+// the bounded kernels' dR: written in place by the kernel (one chunk), else
+// the chunks' fragment-order bf16 partials summed by wr_reduce_frag_kernel
+static int frag_reduce(int n_chunks, int B_img, const uint16_t* slab, float* dR, long long s_b,
+                       long long s_r, long long s_d, hipStream_t s) {
+  if (n_chunks > 1) {
+    const int threads = B_img * NRT * 8 * 64;
+    hipLaunchKernelGGL(wr_reduce_frag_kernel, dim3((threads + 255) / 256), dim3(256), 0, s, slab,
+                       n_chunks, B_img, dR, s_b, s_r, s_d);
+  }
+  return (int)hipGetLastError();
 }
 
 template <typename K>
@@ -2430,14 +2550,14 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   do {                                                                                     \
     if (const int e = allow_lds(wr_fwd_res2_kernel<M, A, BD>, FR2_LDS)) return e;          \
     hipLaunchKernelGGL((wr_fwd_res2_kernel<M, A, BD>), g, dim3(256), FR2_LDS, s, Rhi, Whi,   \
-                       Wnorm, lens, B_img, B_cap, n_chunks, img_offset, gamma1, gamma2,      \
+                       Wnorm, Rnorm, lens, B_img, B_cap, n_chunks, img_offset, gamma1, gamma2, \
                        gamma3, eps, logits, ld_logits, (float4*)stats, Chi, att, att_T);   \
   } while (0)
       if (mode == MODE_BF16 && att) TGFR_RES2(MODE_BF16, true, false);
-      else if (mode == MODE_BF16 && bounded) TGFR_RES2(MODE_BF16, false, true);
+      else if (mode == MODE_BF16 && bounded && Rnorm) TGFR_RES2(MODE_BF16, false, true);
       else if (mode == MODE_BF16) TGFR_RES2(MODE_BF16, false, false);
       else if (mode == MODE_F16 && att) TGFR_RES2(MODE_F16, true, false);
-      else if (mode == MODE_F16 && bounded) TGFR_RES2(MODE_F16, false, true);
+      else if (mode == MODE_F16 && bounded && Rnorm) TGFR_RES2(MODE_F16, false, true);
       else if (mode == MODE_F16) TGFR_RES2(MODE_F16, false, false);
       else return 1002;
 #undef TGFR_RES2
@@ -2474,7 +2594,8 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   return (int)hipGetLastError();
 }
 
-int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const int* lens, int B_img,
+int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const float* Rnorm, const int* lens,
+                    int B_img,
                     int B_cap, float gamma1, float gamma2, float gamma3, float eps,
                     const float* dlogits, int ld, int bounded, int t_pad, float* tok_ws,
                     void* stream) {
@@ -2482,11 +2603,11 @@ int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const int* lens, int
   const long long pairs = (long long)B_img * B_cap;
   if (t_pad == 64)
     hipLaunchKernelGGL(wr_tok_kernel<64>, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
-                       (hipStream_t)stream, (const float4*)stats, Wnorm, lens, dlogits, ld,
+                       (hipStream_t)stream, (const float4*)stats, Wnorm, Rnorm, lens, dlogits, ld,
                        B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 1 : 0, tok_ws);
   else if (t_pad == 32)
     hipLaunchKernelGGL(wr_tok_kernel<32>, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
-                       (hipStream_t)stream, (const float4*)stats, Wnorm, lens, dlogits, ld,
+                       (hipStream_t)stream, (const float4*)stats, Wnorm, Rnorm, lens, dlogits, ld,
                        B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 1 : 0, tok_ws);
   else
     return 1001;
@@ -2502,9 +2623,8 @@ int tgfr_wr_bwd_ws(int B_img, int B_cap, int bounded, int t_pad, int mode, long 
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, int B_img, int B_cap, float gamma1, const float* tok_ws,
                 const uint16_t* Chi, const uint16_t* Clo, float* dR, long long s_b,
-                long long s_r, long long s_d, float* ws, unsigned* counters, int bounded,
-                int t_pad, int mode, void* stream) {
-  (void)counters;
+                long long s_r, long long s_d, float* ws, int bounded, int t_pad, int mode,
+                void* stream) {
   if (B_img <= 0 || B_cap <= 0 || !dR || !ws) return 1001;
   if (mode != MODE_SPLIT && mode != MODE_BF16 && mode != MODE_F16) return 1002;
   auto* s = (hipStream_t)stream;
@@ -2517,19 +2637,21 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
     if (mode == MODE_BF16)
       hipLaunchKernelGGL(wr_bwd_wide2_kernel<MODE_BF16>, dim3(grid), dim3(256),
                          BwdWCfg<MODE_BF16>::LDS, s, Rhi, Whi, B_img, B_cap, n_chunks, gamma1,
-                         tok_ws, Chi, ws);
+                         tok_ws, Chi, dR, s_b, s_r, s_d, (uint16_t*)ws);
     else if (mode == MODE_F16)
       hipLaunchKernelGGL(wr_bwd_wide2_kernel<MODE_F16>, dim3(grid), dim3(256),
                          BwdWCfg<MODE_F16>::LDS, s, Rhi, Whi, B_img, B_cap, n_chunks, gamma1,
-                         tok_ws, Chi, ws);
+                         tok_ws, Chi, dR, s_b, s_r, s_d, (uint16_t*)ws);
     else
       return 1002;
+    return frag_reduce(n_chunks, B_img, (const uint16_t*)ws, dR, s_b, s_r, s_d, s);
   } else if (bounded) {
     if (t_pad != 32) return 1001;
     if (mode != MODE_BF16) return 1002;
     if (const int e = allow_lds(wr_bwd_pipe_kernel, BP_LDS)) return e;
     hipLaunchKernelGGL(wr_bwd_pipe_kernel, dim3(grid), dim3(256), BP_LDS, s, Rhi, Whi, B_img,
-                       B_cap, n_chunks, gamma1, tok_ws, Chi, ws);
+                       B_cap, n_chunks, gamma1, tok_ws, Chi, dR, s_b, s_r, s_d, (uint16_t*)ws);
+    return frag_reduce(n_chunks, B_img, (const uint16_t*)ws, dR, s_b, s_r, s_d, s);
   } else if (mode == MODE_SPLIT && (!Rlo || !Wlo || !Clo)) {
     return 1001;
   } else if (t_pad == 64) {
@@ -2567,8 +2689,8 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   } else {
     return 1001;
   }
-  const long long n = (long long)B_img * NREG * D;
-  const int rgrid = (int)min((n + 255) / 256, 4096LL);
+  const long long n = (long long)B_img * NREG * (D / 4);
+  const int rgrid = (int)min((n + 255) / 256, 8192LL);
   hipLaunchKernelGGL(wr_reduce_kernel, dim3(rgrid), dim3(256), 0, s, ws, n_chunks, B_img, dR, s_b,
                      s_r, s_d, 0);
   return (int)hipGetLastError();
@@ -2578,6 +2700,6 @@ int tgfr_wr_lds_bytes(int which) {
   return which == 0 ? F_LDS : which == 1 ? BwdCfg<MODE_SPLIT>::LDS : FR_LDS;
 }
 
-int tgfr_version(void) { return 200; }
+int tgfr_version(void) { return 300; }
 
 }  // extern "C"

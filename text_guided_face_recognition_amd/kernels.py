@@ -141,14 +141,14 @@ class WordRegionLogits(torch.autograd.Function):
              ptr(logits), b_cap, ptr(stats), ptr(c_hi), ptr(c_lo), ptr(att), att_T,
              int(bool(bounded) and (t_pad == TPAD or m != MODES["fp32"])), t_pad, m,
              _hip.stream())
-        ctx.save_for_backward(r_hi, r_lo, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo)
+        ctx.save_for_backward(r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo)
         ctx.cfg = (gamma1, gamma2, gamma3, eps, m, img_features.shape, fast, t_pad)
         ctx.mark_non_differentiable(*([att] if att is not None else []))
         return (logits, att) if att is not None else logits
 
     @staticmethod
     def backward(ctx, dlogits, *unused):
-        r_hi, r_lo, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo = ctx.saved_tensors
+        r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo = ctx.saved_tensors
         gamma1, gamma2, gamma3, eps, m, shape, fast, t_pad = ctx.cfg
         b_img, b_cap = stats.shape[0], stats.shape[1]
         dev = dlogits.device
@@ -157,15 +157,14 @@ class WordRegionLogits(torch.autograd.Function):
                          device=dev)
         tok = torch.empty(b_img, b_cap, t_pad, 8, dtype=torch.float32, device=dev)
         split = m == MODES["fp32"]
-        call("tgfr_wr_bwd_tok", ptr(stats), ptr(w_norm), ptr(lens), b_img, b_cap, gamma1,
-             gamma2, gamma3, eps, ptr(dlogits), b_cap, int(fast), t_pad, ptr(tok),
+        call("tgfr_wr_bwd_tok", ptr(stats), ptr(w_norm), ptr(r_norm), ptr(lens), b_img, b_cap,
+             gamma1, gamma2, gamma3, eps, ptr(dlogits), b_cap, int(fast), t_pad, ptr(tok),
              _hip.stream())
         d_reg = torch.empty(b_img, NREG, D, dtype=torch.float32, device=dev)
-        assert 2 * b_img <= _hip.N_COUNTERS
         call("tgfr_wr_bwd", ptr(r_hi), ptr(r_lo) if split else None, ptr(w_hi),
              ptr(w_lo) if split else None, b_img, b_cap, gamma1, ptr(tok),
              ptr(c_hi), ptr(c_lo) if split else None, ptr(d_reg), NREG * D, D, 1, ptr(ws),
-             ptr(_hip.counters(dev)), int(fast), t_pad, m, _hip.stream())
+             int(fast), t_pad, m, _hip.stream())
         # same logical shape as img_features, channels-last strides
         d_img = d_reg.transpose(1, 2).reshape(shape)
         return (d_img,) + (None,) * 10

@@ -42,15 +42,14 @@ def main(b=64, nw=30):
            K.ptr(c_hi), None, None, 0, 1, K.TPAD, 0, s)
     dl = torch.randn(b, b, device=dev) * 0.01
     tok = torch.empty(b, b, K.TPAD, 8, device=dev)
-    K.call("tgfr_wr_bwd_tok", K.ptr(stats), K.ptr(w_norm), K.ptr(lens), b, b, 4.0, 5.0, 10.0,
-           1e-8, K.ptr(dl), b, 1, K.TPAD, K.ptr(tok), s)
+    K.call("tgfr_wr_bwd_tok", K.ptr(stats), K.ptr(w_norm), K.ptr(r_norm), K.ptr(lens), b, b,
+           4.0, 5.0, 10.0, 1e-8, K.ptr(dl), b, 1, K.TPAD, K.ptr(tok), s)
     nws = K.wr_bwd_ws_floats(b, b, 1, K.TPAD, 0)
     ws = torch.zeros(nws, device=dev)
     dR = torch.empty(b, 196, 256, device=dev)
-    cnt = H.counters(dev)
     for _ in range(3):
         K.call("tgfr_wr_bwd", K.ptr(r_hi), None, K.ptr(w_hi), None, b, b, 4.0, K.ptr(tok),
-               K.ptr(c_hi), None, K.ptr(dR), 196 * 256, 256, 1, K.ptr(ws), K.ptr(cnt), 1,
+               K.ptr(c_hi), None, K.ptr(dR), 196 * 256, 256, 1, K.ptr(ws), 1,
                K.TPAD, 0, s)
     torch.cuda.synchronize()
     st = ws[-1024 * 16 * 2:].view(torch.int64).view(1024, 16).cpu().numpy().astype(np.float64)

@@ -8,12 +8,14 @@ side, so each rank's contrastive losses see the whole global batch
 (weak scaling: B = 64 images per GPU).
 
 A step is one pass of the hot path over one batch of synthetic frozen-encoder
-outputs already resident in HBM (BASELINE.json configs[1]: iResNet-100 +
-BERT-base features, bs = 64/GPU, 32-token captions -> 30 words): the image
-head (IMIM self-attention), words_loss, sent_loss, global_loss, the two
-ArcMargin/focal identity losses, backward, and both optimiser steps
-(src/train_encoders_bert.py:254-331).  The frozen encoders run under
-torch.no_grad in the reference and are not part of the measured step.
+outputs already resident in HBM (BASELINE.json configs[1]: iResNet-100
+features and BERT-base last hidden states, bs = 64/GPU, 32-token captions ->
+30 words): the frozen text head (TextHeading, under no_grad as in
+utils/dataset_utils.py:38-46), the image head (IMIM self-attention),
+words_loss, sent_loss, global_loss, the two ArcMargin/focal identity losses,
+backward, and both optimiser steps (src/train_encoders_bert.py:254-331).  The
+frozen backbones (iResNet-100, BERT) run under torch.no_grad in the reference
+and are not part of the measured step.
 
 Output: ONE JSON line on rank 0 with the driver's fields plus
   roofline      dominant HIP kernel: algorithmic FLOPs per launch / its average
@@ -51,6 +53,9 @@ def parse():
                    help="also time this precision mode ('' to skip)")
     p.add_argument("--cpu-steps", type=int, default=6)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-text-head", action="store_true",
+                   help="start from ready-made word / sentence features (the round-2 "
+                        "workload) instead of running TextHeading in the step")
     p.add_argument("--eager", action="store_true",
                    help="launch kernels one by one instead of replaying a HIP graph")
     p.add_argument("--simulate-world", type=int, default=0,
@@ -149,6 +154,13 @@ def cpu_baseline(args, n_words):
     words = unit(torch.randn(b, n_words, 256, generator=gen)).transpose(1, 2)
     sent = unit(torch.randn(b, 256, generator=gen))
     cls = torch.randint(0, 10000, (b,), generator=gen)
+    hidden = torch.randn(b, n_words + 1, 768, generator=gen)
+    conv_w, conv_b = [], []
+    for k in (2, 3, 4):                      # Bert_Word_Mapping, models/models.py:177-179
+        conv = torch.nn.Conv2d(1, 256, (k, 768))
+        conv_w.append(conv.weight.detach())
+        conv_b.append(conv.bias.detach())
+    text_head = not args.no_text_head
     p = {}
 
     def lin(o, i):
@@ -182,14 +194,18 @@ def cpu_baseline(args, n_words):
     cls_ids = cls % 4500
 
     def step():
+        w_, s_ = words, sent
+        if text_head:
+            with torch.no_grad():
+                w_, s_ = O.text_heading(hidden, conv_w, conv_b, n_words + 2)
         gp, r = O.image_heading(g, local, hp)
         opt_h.zero_grad()
         opt_c.zero_grad()
-        w0, w1_, _, _ = O.words_loss(r, words, labels, None, n_words, 4.0, 5.0, 10.0)
-        s0, s1, _ = O.sent_loss(gp, sent, labels, cls_np, 10.0)
-        tid = O.focal_loss(O.arc_margin(sent, arc_t, cls_ids, s=35), cls_ids)
+        w0, w1_, _, _ = O.words_loss(r, w_, labels, None, n_words, 4.0, 5.0, 10.0)
+        s0, s1, _ = O.sent_loss(gp, s_, labels, cls_np, 10.0)
+        tid = O.focal_loss(O.arc_margin(s_, arc_t, cls_ids, s=35), cls_ids)
         iid = O.focal_loss(O.arc_margin(gp, arc_i, cls_ids, s=30), cls_ids)
-        cl, _ = O.global_loss(gp, sent)
+        cl, _ = O.global_loss(gp, s_)
         total = w0 + w1_ + s0 + s1 + 100 * (tid + iid) + 2.0 * cl
         total.backward()
         opt_h.step()
@@ -206,7 +222,8 @@ def cpu_baseline(args, n_words):
     return {"value": round(b / med, 3), "unit": "pairs/s", "cores": threads,
             "machine_cpus": machine, "kind": "port",
             "sample": f"{args.cpu_steps} steps (+1 warm-up) of the same bs={b}, T={n_words} "
-                      f"stage-1 step through the fp32 oracle on {threads} torch threads "
+                      f"stage-1 step{' (TextHeading included)' if text_head else ''} "
+                      f"through the fp32 oracle on {threads} torch threads "
                       f"(every core this process may use; the machine has {machine}); "
                       f"median step {med * 1000:.0f} ms"}
 
@@ -251,8 +268,9 @@ def main():
                           num_classes=4500, precision=precision)
         return Train(targs, dev, ctx)
 
-    batch = synthetic_batch(args.batch, n_words, dev, seed=100 + 1000 * ctx.rank)
-    batch = batch[:4] + (batch[4] % 4500,)
+    batch = synthetic_batch(args.batch, n_words, dev, seed=100 + 1000 * ctx.rank,
+                            bert_hidden=not args.no_text_head)
+    batch = batch[:-1] + (batch[-1] % 4500,)
 
     use_graph = not args.eager
 
@@ -317,9 +335,11 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": args.precision, "data": "synthetic",
-        "config": {"workload": "FCAM stage-1 train step (BASELINE configs[1]): IMIM head + "
-                               "words/sent/global losses + identity heads + backward + "
-                               "optimiser, on iResNet-100/BERT-base-shaped frozen features",
+        "config": {"workload": ("FCAM stage-1 train step (BASELINE configs[1]): " +
+                                ("" if args.no_text_head else "frozen TextHeading + ") +
+                                "IMIM head + words/sent/global losses + identity heads + "
+                                "backward + optimiser, on iResNet-100 / BERT-base-shaped "
+                                "frozen-backbone outputs"),
                    "global_batch": args.batch * n, "seq_len": args.words,
                    "words_per_caption": n_words, "parallelism": f"dp{n}",
                    "launch": "hip-graph" if use_graph else "eager"},

@@ -307,7 +307,13 @@ int tgfr_ln_bwd(const float* dy, const float* x, int rows, long long E, const fl
  *     (bf16 weights and their transposes); re-pack after every update.
  *   tail_fwd: R [rows][256] (ld ldr) = normalize(...); saves for the backward
  *     Zb [rows][256], H1b [rows][128], H2b [rows][256] (bf16) and
- *     inv [rows] = 1 / max(|P|, eps).
+ *     inv [rows] = 1 / max(|P|, eps).  Optional (Rrows / Rnorm non-NULL, rows
+ *     a multiple of rows_per_item): R again in the word<->region kernels'
+ *     operand layout, Rrows [rows / rows_per_item][rows_pad][256] bf16 (fp16
+ *     when rows_f16) with rows rows_per_item .. rows_pad - 1 zero, and
+ *     Rnorm [..][rows_pad] = |R_row| -- what tgfr_prep_rows makes of R, so the
+ *     step needs no separate pass over it (models/models.py:399-405 ->
+ *     models/losses.py:96).
  *   tail_bwd: dZ [rows][256] (fp32, ld lddz) from dR; writes dPb [rows][256],
  *     dH2b [rows][256], dH1b [rows][128] (bf16, the ReLU masks applied).
  *   tail_dw: dWp = dP^T H2, dW2 = dH2^T H1, dW1 = dH1^T Z ([out][in], fp32,
@@ -317,7 +323,8 @@ int tgfr_tail_pack(const float* W1, const float* W2, const float* Wp, uint16_t* 
                    void* stream);
 int tgfr_tail_fwd(const float* Z, long long ldz, int rows, const uint16_t* pk, const float* b1,
                   const float* b2, const float* bp, float eps, float* R, long long ldr,
-                  uint16_t* Zb, uint16_t* H1b, uint16_t* H2b, float* inv, void* stream);
+                  uint16_t* Zb, uint16_t* H1b, uint16_t* H2b, float* inv, uint16_t* Rrows,
+                  float* Rnorm, int rows_per_item, int rows_pad, int rows_f16, void* stream);
 int tgfr_tail_bwd(const float* dR, long long lddr, const float* R, long long ldr,
                   const float* inv, int rows, float eps, const uint16_t* pk, const uint16_t* H1b,
                   const uint16_t* H2b, float* dZ, long long lddz, uint16_t* dPb, uint16_t* dH2b,
@@ -485,7 +492,12 @@ int tgfr_optim_step(const tgfr_optim_seg* segs, int n_segs, const tgfr_optim_gro
  *     caption stride s_wb; unit rows, the storage behind the reference's
  *     transposed [B, 256, L-2] view, :231) and sent [B][256] (row stride s_sb;
  *     unit rows, :215-220).  ws: tgfr_text_heading_ws floats (the three relu'd
- *     conv maps).  X, taps and the weights 16-byte aligned.
+ *     conv maps).  X, taps and the weights 16-byte aligned.  Optional (Wrows
+ *     non-NULL): the words again as the word<->region kernels' operand rows,
+ *     Wrows [B][t_pad][256] = bf16 (fp16 when rows_f16) of scale * word with
+ *     rows L1-1 .. t_pad-1 zero, and Wnorm [B][t_pad] = |word| -- what
+ *     tgfr_prep_rows makes of the words (scale log2(e) for the bf16 / fp16
+ *     forward), so the step needs no separate pass over them.
  * Replaces the conv stack and the per-token Python loop of
  * get_each_word_feature / get_word_feature. */
 int tgfr_text_pack_bytes(int mode, long long* bytes);
@@ -493,7 +505,8 @@ int tgfr_text_pack(const float* const* conv_w, uint16_t* taps, int mode, void* s
 int tgfr_text_heading_ws(int B, int L1, long long* floats);
 int tgfr_text_heading(const float* X, int B, int L1, const uint16_t* taps,
                       const float* const* conv_b, float* ws, float* words, long long s_wb,
-                      long long s_wt, float* sent, long long s_sb, int mode, void* stream);
+                      long long s_wt, float* sent, long long s_sb, uint16_t* Wrows, float* Wnorm,
+                      int t_pad, float scale, int rows_f16, int mode, void* stream);
 
 /* ---- FCFM image branch (models/fusion_nets.py:236-237) ----------------------
  * relu(Conv2d(256, 36, 3, padding=0)(x)) -> MaxPool2d(2), fused, and its

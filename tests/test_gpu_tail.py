@@ -42,7 +42,7 @@ def _stagewise(z, w1, b1, w2, b2, wp, bp, dr, eps=1e-12):
     inv = torch.empty(rows, device=dev)
     zb, h1, h2 = (torch.empty(rows, n, **i16) for n in (256, 128, 256))
     call("tgfr_tail_fwd", ptr(z), 256, rows, ptr(pk), ptr(b1), ptr(b2), ptr(bp), eps, ptr(r),
-         256, ptr(zb), ptr(h1), ptr(h2), ptr(inv), _hip.stream())
+         256, ptr(zb), ptr(h1), ptr(h2), ptr(inv), None, None, 0, 0, 0, _hip.stream())
     dz = torch.empty(rows, 256, device=dev)
     dp, dh2, dh1 = (torch.empty(rows, n, **i16) for n in (256, 256, 128))
     call("tgfr_tail_bwd", ptr(dr), 256, ptr(r), 256, ptr(inv), rows, eps, ptr(pk), ptr(h1),
@@ -168,3 +168,31 @@ def test_dw_bf16_generic(rows, n, k, yf32):
     ref = x.float().t() @ yb.float()
     assert _maxrel(dw, ref) <= 1e-2
     assert _maxrel(db, x.float().sum(0)) <= 1e-2
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_imim_operand_rows(gpu, precision):
+    """The IMIM tail kernel writes R a second time in the word<->region
+    operand layout (models/models.py:399-405 -> models/losses.py:96): those
+    rows equal tgfr_prep_rows' hi plane of the returned R bit for bit (zero
+    padding rows included), the norms |R_r| agree to rounding, and the tag is
+    dropped once R changes in place."""
+    from text_guided_face_recognition_amd import kernels as K
+    from text_guided_face_recognition_amd.config import make_args
+    from text_guided_face_recognition_amd.models.models import ImageHeading
+    torch.manual_seed(3)
+    args = make_args(precision=precision)
+    head = ImageHeading(args).to(gpu)
+    g = torch.randn(5, 512, device=gpu)
+    local = torch.randn(5, 256, 14, 14, device=gpu)
+    _, r = head(g, local)
+    f16 = precision == "fp16"
+    rows = K.attached_rows(r, f16)
+    assert rows is not None and K.attached_rows(r, not f16) is None
+    hi, _, nrm = K.prep_rows(K.regions_view(r.detach().float()), 196, 224, want_norms=True,
+                             f16=f16)
+    assert torch.equal(rows[0], hi)
+    torch.testing.assert_close(rows[1], nrm, atol=1e-6, rtol=1e-5)
+    with torch.no_grad():
+        r.mul_(2.0)
+    assert K.attached_rows(r, f16) is None

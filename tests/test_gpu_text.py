@@ -75,3 +75,26 @@ def test_text_heading_contract(gpu):
         net(x)
     with torch.no_grad(), pytest.raises(ValueError):
         net(torch.randn(2, 30, 768, device=gpu))   # token count != bert_words_num - 1
+
+
+@pytest.mark.parametrize("L,precision", [(32, "bf16"), (64, "fp16"), (24, "fp16")])
+def test_text_heading_operand_rows(gpu, L, precision):
+    """In the bf16 / fp16 modes TextHeading's pooling launch also writes the
+    words as the word<->region kernels' log2(e)-scaled operand rows (attached
+    to the returned words): bit-equal to tgfr_prep_rows of the returned words,
+    padding rows zero, norms equal to rounding -- and found through the view
+    words_loss hands the kernels (models/losses.py:83-96)."""
+    from text_guided_face_recognition_amd import kernels as K
+    torch.manual_seed(L)
+    net = _head(L, precision).to(gpu)
+    with torch.no_grad():
+        words, _ = net(torch.randn(9, L - 1, 768, device=gpu))
+    T = L - 2
+    t_pad = 32 if T <= 32 else 64
+    f16 = precision == "fp16"
+    view = K.words_view(words, T)
+    rows = K.attached_rows(view, f16, scale=K.LOG2E)
+    assert rows is not None and K.attached_rows(view, f16) is None
+    hi, _, nrm = K.prep_rows(view.float(), T, t_pad, want_norms=True, scale=K.LOG2E, f16=f16)
+    assert rows[0].shape == hi.shape and torch.equal(rows[0], hi)
+    torch.testing.assert_close(rows[1], nrm, atol=1e-6, rtol=1e-5)

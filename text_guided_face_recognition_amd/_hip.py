@@ -69,7 +69,7 @@ SIGNATURES = {
                                 P, P],
     "tgfr_tail_pack_elems": [],
     "tgfr_tail_pack": [P, P, P, P, P],
-    "tgfr_tail_fwd": [P, L, I, P, P, P, P, F, P, L, P, P, P, P, P],
+    "tgfr_tail_fwd": [P, L, I, P, P, P, P, F, P, L, P, P, P, P, P, P, I, I, I, P],
     "tgfr_tail_bwd": [P, L, P, L, P, I, F, P, P, P, P, L, P, P, P, P],
     "tgfr_tail_dw_ws": [I, P],
     "tgfr_dw_bf16_ws": [I, I, I, P],
@@ -82,7 +82,7 @@ SIGNATURES = {
     "tgfr_text_pack_bytes": [I, P],
     "tgfr_text_pack": [P, P, I, P],
     "tgfr_text_heading_ws": [I, I, P],
-    "tgfr_text_heading": [P, I, I, P, P, P, P, L, L, P, L, I, P],
+    "tgfr_text_heading": [P, I, I, P, P, P, P, L, L, P, L, P, P, I, F, I, I, P],
     "tgfr_sent_global": [P, L, P, L, I, P, F, F, F, P, P, P, P, P],
     "tgfr_sent_global_bwd": [P, P, P, P, L, P, L, I, P, F, F, F, P, P, P, P, L, P],
     "tgfr_focal_ce2": [P, P, I, I, P, F, P, P, P, P, P, P],

@@ -133,7 +133,9 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
     const float* __restrict__ Z, long long ldz, int rows, const uint16_t* __restrict__ pk,
     const float* __restrict__ b1, const float* __restrict__ b2, const float* __restrict__ bp,
     float eps, float* __restrict__ R, long long ldr, uint16_t* __restrict__ Zb,
-    uint16_t* __restrict__ H1b, uint16_t* __restrict__ H2b, float* __restrict__ inv_out) {
+    uint16_t* __restrict__ H1b, uint16_t* __restrict__ H2b, float* __restrict__ inv_out,
+    uint16_t* __restrict__ Rrows, float* __restrict__ Rnorm, int rows_per_item, int rows_pad,
+    int rows_f16) {
   const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE;
   const int lr = lane & 31, h = lane >> 5;
   const int row0 = blockIdx.x * TM;
@@ -269,9 +271,17 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
   if (tid < TM) {
     const float ss = lds_ldf(F_SS + tid * 4) + lds_ldf(F_SS + (TM + tid) * 4) +
                      lds_ldf(F_SS + (2 * TM + tid) * 4) + lds_ldf(F_SS + (3 * TM + tid) * 4);
-    const float iv = 1.f / fmaxf(sqrtf(ss), eps);
+    const float nrm = sqrtf(ss);
+    const float iv = 1.f / fmaxf(nrm, eps);
     lds_stf(F_INV + tid * 4, iv);
-    if (row0 + tid < rows) inv_out[row0 + tid] = iv;
+    if (row0 + tid < rows) {
+      inv_out[row0 + tid] = iv;
+      // |R_row| for the word<->region kernels (tgfr_prep_rows' norms)
+      if (Rnorm) {
+        const int it = (row0 + tid) / rows_per_item, ri = (row0 + tid) % rows_per_item;
+        Rnorm[(long long)it * rows_pad + ri] = nrm * iv;
+      }
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -282,10 +292,31 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
       if (row0 + m < rows) {
         const float iv = lds_ldf(F_INV + m * 4);
         float* o = R + (long long)(row0 + m) * ldr + 64 * w + lr;
-        o[0] = acc[mt][0][q] * iv;
-        o[32] = acc[mt][1][q] * iv;
+        const float v0 = acc[mt][0][q] * iv, v1 = acc[mt][1][q] * iv;
+        o[0] = v0;
+        o[32] = v1;
+        if (Rrows) {
+          // R rows in the contraction's operand layout: [item][rows_pad][256]
+          // bf16 (or fp16) -- what tgfr_prep_rows would make of R
+          const int it = (row0 + m) / rows_per_item, ri = (row0 + m) % rows_per_item;
+          uint16_t* d = Rrows + ((long long)it * rows_pad + ri) * TD + 64 * w + lr;
+          d[0] = rows_f16 ? f16_bits(v0) : bf_bits(v0);
+          d[32] = rows_f16 ? f16_bits(v1) : bf_bits(v1);
+        }
       }
     }
+  if (Rrows) {
+    // the padding rows (rows_per_item .. rows_pad) of every item whose last
+    // row this workgroup holds: zero rows, zero norms
+    for (int m = 0; m < TM; ++m) {
+      const int row = row0 + m;
+      if (row >= rows || row % rows_per_item != rows_per_item - 1) continue;
+      const int it = row / rows_per_item, npad = rows_pad - rows_per_item;
+      uint16_t* d = Rrows + ((long long)it * rows_pad + rows_per_item) * TD;
+      for (int i = tid; i < npad * (TD / 8); i += 256) *(uint4*)(d + 8 * i) = make_uint4(0, 0, 0, 0);
+      if (Rnorm && tid < npad) Rnorm[(long long)it * rows_pad + rows_per_item + tid] = 0.f;
+    }
+  }
 }
 
 // ----------------------------------------------------------- backward ---
@@ -739,13 +770,18 @@ int tgfr_tail_pack(const float* W1, const float* W2, const float* Wp, uint16_t* 
 
 int tgfr_tail_fwd(const float* Z, long long ldz, int rows, const uint16_t* pk, const float* b1,
                   const float* b2, const float* bp, float eps, float* R, long long ldr,
-                  uint16_t* Zb, uint16_t* H1b, uint16_t* H2b, float* inv, void* stream) {
+                  uint16_t* Zb, uint16_t* H1b, uint16_t* H2b, float* inv, uint16_t* Rrows,
+                  float* Rnorm, int rows_per_item, int rows_pad, int rows_f16, void* stream) {
   if (rows <= 0 || ldz < TC || ldr < TD || (ldz & 3) || (ldr & 3)) return 1001;
   if (((uintptr_t)Z & 15) || !pk || !b1 || !b2 || !bp || !R || !Zb || !H1b || !H2b || !inv)
     return 1001;
+  if ((Rrows || Rnorm) && (rows_per_item <= 0 || rows_pad < rows_per_item ||
+                           rows % rows_per_item || ((uintptr_t)Rrows & 15)))
+    return 1001;
   hipLaunchKernelGGL(tail_fwd_kernel, dim3((rows + TM - 1) / TM), dim3(256), F_LDS,
                      (hipStream_t)stream, Z, ldz, rows, pk, b1, b2, bp, eps, R, ldr, Zb, H1b, H2b,
-                     inv);
+                     inv, Rrows, Rnorm, rows_per_item > 0 ? rows_per_item : 1, rows_pad,
+                     rows_f16 ? 1 : 0);
   return (int)hipGetLastError();
 }
 

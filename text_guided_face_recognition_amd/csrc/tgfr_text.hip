@@ -55,7 +55,9 @@ __device__ __forceinline__ float4 div4(float4 a, float d) {
 // 4l .. 4l+3, so every row access is one coalesced 1 KB float4 sweep.
 __global__ __launch_bounds__(64 * TH_NW) void text_pool_kernel(
     const float* __restrict__ Y, long long map_stride, int L1, float* __restrict__ words,
-    long long s_wb, long long s_wt, float* __restrict__ sent, long long s_sb) {
+    long long s_wb, long long s_wt, float* __restrict__ sent, long long s_sb,
+    uint16_t* __restrict__ Wrows, float* __restrict__ Wnorm, int t_pad, float scale,
+    int rows_f16) {
   __shared__ float4 part[TH_NW][3][64];
   const int b = blockIdx.x, w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int T = L1 - 1;                               // words per caption (L - 2)
@@ -78,10 +80,27 @@ __global__ __launch_bounds__(64 * TH_NW) void text_pool_kernel(
       v = max4(v, v4);
     }
     // F.normalize(p=2, dim=2): x / max(|x|, 1e-12)   (models.py:212)
-    const float n = fmaxf(sqrtf(wave_sum(dot4(v))), 1e-12f);
+    const float nraw = sqrtf(wave_sum(dot4(v)));
+    const float n = fmaxf(nraw, 1e-12f);
     float* dst = words + b * s_wb + t * s_wt + 4 * l;
-    *(float4*)dst = div4(v, n);
+    const float4 u = div4(v, n);
+    *(float4*)dst = u;
+    if (Wrows) {
+      // the word<->region kernels' operand row: scale * u in bf16 (fp16), and |u|
+      const float a[4] = {scale * u.x, scale * u.y, scale * u.z, scale * u.w};
+      uint16_t h[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) h[k] = rows_f16 ? f16_bits(a[k]) : bf_bits(a[k]);
+      *(uint2*)(Wrows + ((long long)b * t_pad + t) * TH_D + 4 * l) =
+          make_uint2(pack2(h[0], h[1]), pack2(h[2], h[3]));
+      if (l == 0) Wnorm[(long long)b * t_pad + t] = nraw / n;
+    }
   }
+  if (Wrows)                                          // padding words: zero rows
+    for (int t = T + w; t < t_pad; t += TH_NW) {
+      *(uint2*)(Wrows + ((long long)b * t_pad + t) * TH_D + 4 * l) = make_uint2(0, 0);
+      if (l == 0) Wnorm[(long long)b * t_pad + t] = 0.f;
+    }
   part[w][0][l] = m2;
   part[w][1][l] = m3;
   part[w][2][l] = m4;
@@ -335,8 +354,10 @@ int tgfr_text_heading_ws(int B, int L1, long long* floats) {
 
 int tgfr_text_heading(const float* X, int B, int L1, const uint16_t* taps,
                       const float* const* conv_b, float* ws, float* words, long long s_wb,
-                      long long s_wt, float* sent, long long s_sb, int mode, void* stream) {
+                      long long s_wt, float* sent, long long s_sb, uint16_t* Wrows, float* Wnorm,
+                      int t_pad, float scale, int rows_f16, int mode, void* stream) {
   if (!X || !taps || !conv_b || !ws || !words || !sent || B <= 0 || L1 < 4) return 1001;
+  if (Wrows && (!Wnorm || t_pad < L1 - 1 || ((uintptr_t)Wrows & 7))) return 1001;
   for (int k = 0; k < 3; ++k)
     if (!conv_b[k]) return 1001;
   if (((uintptr_t)X & 15) || ((uintptr_t)taps & 15)) return 1001;
@@ -366,7 +387,7 @@ int tgfr_text_heading(const float* X, int B, int L1, const uint16_t* taps,
                        conv_b[2], ws, map);
   }
   hipLaunchKernelGGL(text_pool_kernel, dim3(B), dim3(64 * TH_NW), 0, s, ws, map, L1, words,
-                     s_wb, s_wt, sent, s_sb);
+                     s_wb, s_wt, sent, s_sb, Wrows, Wnorm, t_pad, scale, rows_f16 ? 1 : 0);
   return (int)hipGetLastError();
 }
 

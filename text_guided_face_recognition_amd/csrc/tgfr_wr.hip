@@ -2176,6 +2176,10 @@ constexpr int BP_TOK = 1024;                   // token table bytes
 constexpr int BP_BUF = B_XIMG + BP_TOK;        // one caption: X image + table
 constexpr int BP_ZERO = BP_NB * BP_BUF;        // a zero token table
 constexpr int BP_LDS = BP_ZERO + BP_TOK;
+// MFMA slot of the stage after which DMA piece j of X(t + 2) is issued (-1: none)
+__device__ __forceinline__ constexpr int bp_dma_slot(int n) {
+  return (n >= 2 && n <= 18 && (n & 1) == 0) ? (n - 2) / 2 : -1;
+}
 
 __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi, int B_img, int B_cap,
@@ -2222,24 +2226,32 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
     dma_off[j] = (j % 4 < 2) ? (uint32_t)((row * D + c * 8) * 2)
                              : (uint32_t)(((c * 32) + (row - 32)) * 8 * 2);
   }
-  auto stage_dma = [&](int k) {     // caption c0 + k -> ring slot k % 4
-    if (k < K) {
-      const uint32_t base = (k % BP_NB) * BP_BUF;
-      const long long pair = (long long)b * B_cap + c0 + k;
-      const uint16_t* wsrc = Whi + (long long)(c0 + k) * TPAD * D;
-      const uint16_t* csrc = Chi + pair * 32 * 32 * 8;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int kk = wid + 4 * j, p = kk % 32;
-        glds16s(j % 4 < 2 ? (const void*)wsrc : (const void*)csrc, dma_off[j],
-                base + (p / 16) * (64 * 256) + 4 * (p % 16) * 256);
-      }
-      // the token table (1 KiB) by one wave, rotating with the caption
-      if (wid == (k & 3)) glds16s(tok + pair * TPAD * 8, lane * 16, base + B_XIMG);
+  // DMA piece j (< 8: X image, 8: token table) of caption c0 + k -> ring slot
+  // k % 4.  Branch-free: past the chunk the last caption is fetched again
+  // (its fill / drain stages read a zero token table, and every slot holds
+  // finite data); the token table is issued by every wave (identical bytes)
+  // rather than by one behind a branch, which would split the unrolled
+  // stage into basic blocks.
+  auto dma_piece = [&](int k, int j) {
+    const int kc = min(k, K - 1);
+    const uint32_t base = (k % BP_NB) * BP_BUF;
+    const long long pair = (long long)b * B_cap + c0 + kc;
+    if (j == 8) {
+      glds16s(tok + pair * TPAD * 8, lane * 16, base + B_XIMG);
+    } else {
+      const int kk = wid + 4 * j, p = kk % 32;
+      const void* src = j % 4 < 2 ? (const void*)(Whi + (long long)(c0 + kc) * TPAD * D)
+                                  : (const void*)(Chi + pair * 32 * 32 * 8);
+      glds16s(src, dma_off[j], base + (p / 16) * (64 * 256) + 4 * (p % 16) * 256);
     }
   };
-  stage_dma(0);
-  stage_dma(1);
+  if (K > 0) {
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      dma_piece(0, j);
+      dma_piece(1, j);
+    }
+  }
 
   // per-lane parts of the swizzled X-image addresses (xoff), as wr_bwd_kernel
   uint32_t g1o[8], g2o[2][4];
@@ -2372,6 +2384,9 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
           Mo[2 + k] = __builtin_bit_cast(bf16x8, make_uint4(mc2[4 * k], mc2[4 * k + 1],
                                                               mc2[4 * k + 2], mc2[4 * k + 3]));
         }
+        // pin phase C here: without a use in this stage the compiler sinks it
+        // past the stage boundary into the next stage's first MFMA gap
+        asm volatile("" ::"v"(Mo[0]), "v"(Mo[1]), "v"(Mo[2]), "v"(Mo[3]));
       }
     }
   };
@@ -2381,7 +2396,6 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
   auto stage = [&](int t, f32x16& A0, f32x16& A1, f32x16& A0n, f32x16& A1n,
                    const bf16x8* Mi, bf16x8* Mo) {
     ring_barrier<0>();                 // X(t+1) landed everywhere; X(t-2) retired
-    stage_dma(t + 2);
     const uint32_t x1 = ((t + 1) % BP_NB) * BP_BUF;          // G1 image
     const uint32_t x3 = ((t + 3) % BP_NB) * BP_BUF;          // G3 image (t-1)
     const uint32_t tbs = t < K ? (t % BP_NB) * BP_BUF + B_XIMG : BP_ZERO;
@@ -2403,11 +2417,30 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
         g1_mfma(n >> 1, op, A0n, A1n, init);
       }
       if (n + PF_BWD < 64) rd[(n + PF_BWD) & 7] = read(n + PF_BWD);
+      // X(t + 2) pieces early in the stage, between MFMAs (a burst at the
+      // stage head issued ~80 cycles per piece with the matrix core idle)
+      if (bp_dma_slot(n) >= 0) dma_piece(t + 2, bp_dma_slot(n));
       sm_chunk(n, tbs, A0, A1, Mo);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
 
+  if (rt >= NRT || K == 0) {
+    // the padding-only tile (and an empty chunk): no MFMA / softmax work, only
+    // this wave's share of the ring traffic, so the other waves' barriers and
+    // DMA pieces stay as they are
+    if (K > 0) {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      const int T2p = (K + 2) & ~1;
+      for (int t = 0; t < T2p; ++t) {
+        ring_barrier<0>();
+#pragma unroll
+        for (int j = 0; j < 9; ++j) dma_piece(t + 2, j);
+      }
+    }
+    if (rt < NRT) store_dr_tile(dR, n_chunks, chunk, b, rt, B_img, lane, out, s_b, s_r, s_d, slab);
+    return;
+  }
   // ---- prologue: G1 of caption 0
   f32x16 Aa0, Aa1, Ab0, Ab1;
   bf16x8 Ma[4], Mb[4];
@@ -2424,7 +2457,6 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
     stage(t, Aa0, Aa1, Ab0, Ab1, Ma, Mb);
     stage(t + 1, Ab0, Ab1, Aa0, Aa1, Mb, Ma);
   }
-  if (rt >= NRT) return;
   store_dr_tile(dR, n_chunks, chunk, b, rt, B_img, lane, out, s_b, s_r, s_d, slab);
 }
 

@@ -25,7 +25,7 @@ def _mode(mode):
     """C-ABI precision of the generic kernels: "fp16" (the word-region
     contraction in fp16, BASELINE config 5) runs everything else in bf16."""
     try:
-        return min(MODES[mode], 1)
+        return MODES["bf16"] if mode == "fp16" else MODES[mode]
     except KeyError:
         raise ValueError(f"precision mode must be one of {sorted(MODES)}") from None
 
@@ -96,7 +96,7 @@ class WordRegionLogits(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, img_features, words, lens, gamma1, gamma2, gamma3, mode,
-                img_offset=0, att_T=0, bounded=False, eps=1e-8):
+                img_offset=0, att_T=0, bounded=False, uniform=False, eps=1e-8):
         dev = img_features.device
         regions = regions_view(img_features.float())
         b_img, b_cap = regions.shape[0], words.shape[0]
@@ -115,13 +115,22 @@ class WordRegionLogits(torch.autograd.Function):
         fast = bool(bounded) and (
             (m == MODES["bf16"] and not att_T and t_pad == TPAD) or
             (m != MODES["fp32"] and t_pad == 2 * TPAD))
-        r_hi, r_lo, r_norm = prep_rows(regions, NREG, RPAD, want_norms=bf16, f16=f16)
+        pre = attached_rows(img_features, f16) if bf16 else None
+        if pre is not None:            # written by the IMIM tail kernel
+            (r_hi, r_norm), r_lo = pre, None
+        else:
+            r_hi, r_lo, r_norm = prep_rows(regions, NREG, RPAD, want_norms=bf16, f16=f16)
         if bf16:
             # the bf16 / fp16 forward takes log2(e)-scaled words (tgfr.h,
             # tgfr_wr_fwd), and so does the pipelined backward; the other
-            # backward the plain ones
-            w_fwd, _, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,
-                                         want_norms=True, scale=LOG2E, f16=f16)
+            # backward the plain ones.  (Written by TextHeading when it made
+            # the words; every caption then has t_words valid words.)
+            pre = attached_rows(words, f16, scale=LOG2E) if uniform else None
+            if pre is not None and pre[0].shape[1] == t_pad:
+                w_fwd, w_norm = pre
+            else:
+                w_fwd, _, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,
+                                             want_norms=True, scale=LOG2E, f16=f16)
             w_hi = w_fwd if fast else prep_rows(words.float(), t_words, t_pad, lens=lens,
                                                 f16=f16)[0]
             w_lo = None
@@ -167,16 +176,19 @@ class WordRegionLogits(torch.autograd.Function):
              int(fast), t_pad, m, _hip.stream())
         # same logical shape as img_features, channels-last strides
         d_img = d_reg.transpose(1, 2).reshape(shape)
-        return (d_img,) + (None,) * 10
+        return (d_img,) + (None,) * 11
 
 
 def word_region_logits(img_features, words, lens, gamma1, gamma2, gamma3,
-                       mode="fp32", img_offset=0, att_T=0, bounded=False):
-    """bounded: the caller guarantees max|W| max|R| < 43 (L2-normalised rows,
-    the BERT path); the bf16 forward then skips the running max."""
+                       mode="fp32", img_offset=0, att_T=0, bounded=False, uniform=False):
+    """bounded: the features are (near) unit rows -- the BERT path -- so the
+    bf16 / fp16 kernels run without a running max (scores shifted by the
+    device-computed bound max|W| max|R| when it reaches 40).  uniform: every
+    caption has all words.shape[1] words (lens is that constant), so operand
+    rows attached to the words by TextHeading (attach_rows) may be used."""
     return WordRegionLogits.apply(img_features, words, lens, float(gamma1),
                                   float(gamma2), float(gamma3), mode, img_offset, att_T,
-                                  bool(bounded))
+                                  bool(bounded), bool(uniform))
 
 
 # -------------------------------------------------------- func_attention ---
@@ -942,7 +954,7 @@ class ImimTail(torch.autograd.Function):
     bf16 (Z, H1, H2), the operands the bf16 GEMMs consume anyway."""
 
     @staticmethod
-    def forward(ctx, z, w1, b1, w2, b2, wp, bp, eps):
+    def forward(ctx, z, w1, b1, w2, b2, wp, bp, eps, rows_spec=None):
         shape = z.shape
         assert shape[-1] == _TAIL_C and tuple(w1.shape[:2]) == (_TAIL_H, _TAIL_C)
         assert tuple(w2.shape[:2]) == (_TAIL_C, _TAIL_H) and tuple(wp.shape) == (_TAIL_D, _TAIL_C)
@@ -957,15 +969,26 @@ class ImimTail(torch.autograd.Function):
         h1 = torch.empty(rows, _TAIL_H, dtype=torch.int16, device=dev)
         h2 = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)
         inv = torch.empty(rows, dtype=torch.float32, device=dev)
+        # rows_spec = (rows per item, padded rows, fp16): R also in the
+        # word<->region operand layout (prep_rows' hi plane and norms)
+        rr = rn = None
+        per, pad, f16 = rows_spec if rows_spec else (0, 0, False)
+        if rows_spec:
+            rr = torch.empty(rows // per, pad, _TAIL_D, dtype=torch.int16, device=dev)
+            rn = torch.empty(rows // per, pad, dtype=torch.float32, device=dev)
         call("tgfr_tail_fwd", ptr(z2), _TAIL_C, rows, ptr(pk), ptr(_aligned(b1)),
              ptr(_aligned(b2)), ptr(_aligned(bp)), float(eps), ptr(r), _TAIL_D, ptr(zb), ptr(h1),
-             ptr(h2), ptr(inv), _hip.stream())
+             ptr(h2), ptr(inv), ptr(rr), ptr(rn), per, pad, int(bool(f16)), _hip.stream())
         ctx.save_for_backward(r, inv, pk, zb, h1, h2)
         ctx.cfg = (float(eps), shape, w1.shape, w2.shape)
-        return r.reshape(*shape[:-1], _TAIL_D)
+        out = r.reshape(*shape[:-1], _TAIL_D)
+        if rows_spec:
+            ctx.mark_non_differentiable(rr, rn)
+            return out, rr, rn
+        return out
 
     @staticmethod
-    def backward(ctx, dr):
+    def backward(ctx, dr, *unused):
         r, inv, pk, zb, h1, h2 = ctx.saved_tensors
         eps, shape, w1shape, w2shape = ctx.cfg
         rows, dev = r.shape[0], r.device
@@ -986,14 +1009,48 @@ class ImimTail(torch.autograd.Function):
         call("tgfr_tail_dw", ptr(dp), ptr(h2), ptr(dh2), ptr(h1), ptr(dh1), ptr(zb), rows,
              ptr(dwp), ptr(dbp), ptr(dw2), ptr(db2), ptr(dw1), ptr(db1), ptr(ws), _hip.stream())
         return (dz.reshape(shape), dw1.reshape(w1shape), db1, dw2.reshape(w2shape), db2, dwp,
-                dbp, None)
+                dbp, None, None)
 
 
-def imim_tail(z, conv1, conv2, proj, eps=1e-12):
+def imim_tail(z, conv1, conv2, proj, eps=1e-12, rows_spec=None):
     """R = normalize(proj(relu(conv2(relu(conv1(z)))))) on channels-last rows
-    z [..., 256] (bf16 operands, fp32 accumulation)."""
-    return ImimTail.apply(z, conv1.weight, conv1.bias, conv2.weight, conv2.bias, proj.weight,
-                          proj.bias, eps)
+    z [..., 256] (bf16 operands, fp32 accumulation).  With rows_spec =
+    (rows per item, padded rows, fp16) also returns (R rows in the
+    word<->region operand layout, their norms) -- see attach_rows."""
+    out = ImimTail.apply(z, conv1.weight, conv1.bias, conv2.weight, conv2.bias, proj.weight,
+                         proj.bias, eps, rows_spec)
+    if rows_spec:
+        return out[0], (out[1], out[2])
+    return out
+
+
+def attach_rows(x, rows, norms, f16, scale=1.0):
+    """Tag a feature tensor with its rows in the word<->region kernels'
+    operand layout (tgfr_prep_rows' hi plane of scale * x, and |x| per row),
+    written by the kernel that produced x: the image regions R by the IMIM
+    tail (tgfr_tail_fwd), the words W by TextHeading (tgfr_text_heading).
+    WordRegionLogits then skips its tgfr_prep_rows pass over x.  The tag
+    holds while x (or a view of it with the same layout) is the same storage
+    at the same version: no in-place change since."""
+    x._tgfr_rows = (rows, norms, bool(f16), float(scale), x._version, x.data_ptr(),
+                    tuple(x.shape), tuple(x.stride()))
+    return x
+
+
+def attached_rows(x, f16, scale=1.0):
+    """(rows, norms) attached to x -- or to the tensor x views with x's own
+    shape and strides -- by attach_rows, if still valid for this operand
+    precision and scale; else None."""
+    for t in (x, getattr(x, "_base", None)):
+        tag = getattr(t, "_tgfr_rows", None) if t is not None else None
+        if tag is None:
+            continue
+        rows, norms, tf16, tscale, version, addr, shape, stride = tag
+        if (tf16 == bool(f16) and tscale == float(scale) and version == t._version and
+                addr == x.data_ptr() and shape == tuple(x.shape) and
+                stride == tuple(x.stride())):
+            return rows, norms
+    return None
 
 
 # ---------------------------------------------------------------- heads ---
@@ -1361,11 +1418,13 @@ def text_pack(conv_w, mode="fp32"):
     return taps
 
 
-def text_heading(words_emb, taps, conv_b, mode="fp32", words=None, sent=None):
+def text_heading(words_emb, taps, conv_b, mode="fp32", words=None, sent=None, rows_spec=None):
     """Bert_Word_Mapping + TextHeading forward: words_emb [B, L1, 768] fp32 (BERT
     last hidden state without [CLS]), taps = text_pack(conv weights, mode),
     conv_b[k] [256] -> (words [B, L1-1, 256] unit rows, sent [B, 256] unit
-    rows).  One launch for the three convs + one pooling launch (tgfr_text.hip)."""
+    rows).  One launch for the three convs + one pooling launch (tgfr_text.hip).
+    rows_spec = (t_pad, scale, fp16): the pooling launch also writes the words
+    as word<->region operand rows, attached to `words` (attach_rows)."""
     assert words_emb.dim() == 3 and words_emb.shape[2] == 768
     assert words_emb.dtype == torch.float32
     b, l1, _ = words_emb.shape
@@ -1382,7 +1441,13 @@ def text_heading(words_emb, taps, conv_b, mode="fp32", words=None, sent=None):
         sent = torch.empty(b, D, dtype=torch.float32, device=dev)
     ws = torch.empty(text_heading_ws_floats(b, l1), dtype=torch.float32, device=dev)
     bp = (ctypes.c_void_p * 3)(*[ptr(v) for v in bs_])
+    t_pad, scale, f16 = rows_spec if rows_spec else (0, 1.0, False)
+    w_rows = torch.empty(b, t_pad, D, dtype=torch.int16, device=dev) if rows_spec else None
+    w_norm = torch.empty(b, t_pad, dtype=torch.float32, device=dev) if rows_spec else None
     call("tgfr_text_heading", ptr(x), b, l1, ptr(taps), ctypes.addressof(bp),
          ptr(ws), ptr(words), words.stride(0), words.stride(1),
-         ptr(sent), sent.stride(0), _mode(mode), _hip.stream())
+         ptr(sent), sent.stride(0), ptr(w_rows), ptr(w_norm), t_pad, float(scale),
+         int(bool(f16)), _mode(mode), _hip.stream())
+    if rows_spec:
+        attach_rows(words, w_rows, w_norm, f16, scale=scale)
     return words, sent

@@ -115,7 +115,8 @@ def words_loss(img_features, words_emb, labels, cap_lens, class_ids, batch_size,
     out = K.word_region_logits(img_features, words, lens, smooth.GAMMA1, smooth.GAMMA2,
                                smooth.GAMMA3, mode=_precision(args), img_offset=row_offset,
                                att_T=n_words if want_maps else 0,
-                               bounded=args.en_type == "BERT")
+                               bounded=args.en_type == "BERT",
+                               uniform=args.en_type == "BERT")
     logits, att = (out if want_maps else (out, None))
     att_maps = []
     if att is not None:

@@ -69,9 +69,17 @@ class IMIM(nn.Module):
         # [HW, C] rows; the [C, H, W] affine maps are read channel-major in place
         z = K.layer_norm_rows(z, self.ln.weight, self.ln.bias, self.ln.eps, ch=c)
         if self.precision in ("bf16", "fp16"):
-            # conv1x1_1 -> ReLU -> conv1x1_2 -> ReLU -> project_local, fused
-            z = K.imim_tail(z, self.conv1x1_1, self.conv1x1_2, self.project_local.projection)
-            return z.reshape(n, h, w, -1).permute(0, 3, 1, 2)
+            # conv1x1_1 -> ReLU -> conv1x1_2 -> ReLU -> project_local, fused; the
+            # kernel also writes R as the word<->region operand rows (:403 ->
+            # losses.py:96), attached to the returned R
+            f16 = self.precision == "fp16"
+            spec = (h * w, K.RPAD, f16) if h * w == K.NREG else None
+            z = K.imim_tail(z, self.conv1x1_1, self.conv1x1_2, self.project_local.projection,
+                            rows_spec=spec)
+            if spec:
+                z, (r_rows, r_norm) = z
+            out = z.reshape(n, h, w, -1).permute(0, 3, 1, 2)
+            return K.attach_rows(out, r_rows, r_norm, f16) if spec else out
         z = K.linear_rows(z, self.conv1x1_1.weight, self.conv1x1_1.bias, relu=True,
                           mode=self.precision)
         z = K.linear_rows(z, self.conv1x1_2.weight, self.conv1x1_2.bias, relu=True,
@@ -149,6 +157,13 @@ class TextHeading(nn.Module):
             raise RuntimeError("TextHeading is forward-only (the reference calls it under "
                                "torch.no_grad(), utils/dataset_utils.py:42); wrap the call "
                                "in torch.no_grad()")
+        # bf16 / fp16: the pooling launch also writes the words as the
+        # word<->region kernels' log2(e)-scaled operand rows (losses.py:96)
+        spec = None
+        if self.precision in ("bf16", "fp16"):
+            n = words_emb.shape[1] - 1
+            spec = (K.TPAD if n <= K.TPAD else 2 * K.TPAD, K.LOG2E, self.precision == "fp16")
         words, sent = K.text_heading(words_emb, self.packed_taps(),
-                                     [c.bias for c in self.bwm.convs1], mode=self.precision)
+                                     [c.bias for c in self.bwm.convs1], mode=self.precision,
+                                     rows_spec=spec)
         return words.transpose(1, 2), sent

@@ -35,7 +35,7 @@ from .dist import DistContext, StepCapture
 from .models.fusion_nets import Working, set_precision
 from .models.losses import ClipLoss, FocalLoss, sent_global_loss, words_loss
 from .models.metrics import ArcMarginProduct
-from .models.models import ImageHeading
+from .models.models import ImageHeading, TextHeading
 from .optim import FusedOptimizer, adam_group, sgd_group
 
 
@@ -43,15 +43,24 @@ def _unit(x, dim=-1):
     return x / x.norm(dim=dim, keepdim=True)
 
 
-def synthetic_batch(b, n_words, device, seed, n_ids=10000):
-    """Frozen-encoder outputs for one batch."""
+def synthetic_batch(b, n_words, device, seed, n_ids=10000, bert_hidden=False):
+    """Frozen-encoder outputs for one batch: (global, local,
+    words [B, 256, T], sent, class ids), or with bert_hidden the BERT-base
+    last hidden states without [CLS] instead of the text features -- (global,
+    local, hidden [B, T + 1, 768], class ids) -- so that the step runs the
+    frozen TextHeading itself, as the reference's does
+    (utils/dataset_utils.py:38-46)."""
     gen = torch.Generator(device="cpu").manual_seed(seed)
     g = torch.randn(b, 512, generator=gen)
     local = torch.randn(b, 256, 14, 14, generator=gen)
+    to = dict(device=device)
+    if bert_hidden:
+        hidden = torch.randn(b, n_words + 1, 768, generator=gen)
+        cls = torch.randint(0, n_ids, (b,), generator=gen)
+        return g.to(**to), local.to(**to), hidden.to(**to), cls.to(**to)
     words = _unit(torch.randn(b, n_words, 256, generator=gen))     # [B, T, 256] storage
     sent = _unit(torch.randn(b, 256, generator=gen))
     cls = torch.randint(0, n_ids, (b,), generator=gen)
-    to = dict(device=device)
     return (g.to(**to), local.to(**to), words.to(**to).transpose(1, 2), sent.to(**to),
             cls.to(**to))
 
@@ -83,6 +92,11 @@ class Train:
         self.image_head = ImageHeading(args).to(device)
         self.image_cls = ArcMarginProduct(args.aux_feat_dim_per_granularity,
                                           args.num_classes, s=30, m=0.5).to(device)
+        # the frozen text head (:212 puts its parameters in the Adam group, but
+        # it runs under no_grad, utils/dataset_utils.py:42-45, so they never
+        # change); used when a batch carries BERT hidden states
+        self.text_head = TextHeading(args).to(device).requires_grad_(False)
+        set_precision(self.text_head, args.precision)
         self.text_cls = ArcMarginProduct(args.aux_feat_dim_per_granularity,
                                          args.num_classes, s=35, m=0.5).to(device)
         for m in (self.image_head, self.image_cls, self.text_cls):
@@ -99,8 +113,16 @@ class Train:
                       lr=0.1, momentum=0.9, weight_decay=5e-5)])
 
     def step(self, batch):
+        """batch: (global, local, words, sent, class ids), or (global, local,
+        BERT hidden states, class ids) -- then the step runs TextHeading under
+        no_grad first (:257, utils/dataset_utils.py:38-46)."""
         args, ctx = self.args, self.ctx
-        g, local, words, sent, class_ids = batch
+        if len(batch) == 4:
+            g, local, hidden, class_ids = batch
+            with torch.no_grad():
+                words, sent = self.text_head(hidden, None)
+        else:
+            g, local, words, sent, class_ids = batch
         b = g.shape[0]
         ctx.set_batch(b)
         args.dist = ctx

@@ -28,7 +28,7 @@ call("tgfr_tail_pack", ptr(w1), ptr(w2), ptr(wp), ptr(pk), _hip.stream())
 R = torch.empty(rows, 256, device="cuda"); zb = torch.empty(rows, 256, dtype=torch.int16, device="cuda")
 H1 = torch.empty(rows, 128, dtype=torch.int16, device="cuda"); H2 = torch.empty(rows, 256, dtype=torch.int16, device="cuda")
 inv = torch.empty(rows, device="cuda")
-call("tgfr_tail_fwd", ptr(z), 256, rows, ptr(pk), ptr(b1), ptr(b2), ptr(bp), 1e-12, ptr(R), 256, ptr(zb), ptr(H1), ptr(H2), ptr(inv), _hip.stream())
+call("tgfr_tail_fwd", ptr(z), 256, rows, ptr(pk), ptr(b1), ptr(b2), ptr(bp), 1e-12, ptr(R), 256, ptr(zb), ptr(H1), ptr(H2), ptr(inv), None, None, 0, 0, 0, _hip.stream())
 print("zb", rel(bf(zb), z), "H1", rel(bf(H1), h1), "H2", rel(bf(H2), h2), "R", rel(R, r), "inv", rel(inv, 1/p.norm(dim=-1)))
 dz = torch.empty(rows, 256, device="cuda"); dP = torch.empty(rows, 256, dtype=torch.int16, device="cuda")
 dH2 = torch.empty(rows, 256, dtype=torch.int16, device="cuda"); dH1 = torch.empty(rows, 128, dtype=torch.int16, device="cuda")

@@ -92,7 +92,7 @@ def build(name):
 def bench(so, rows=12544, reps=20):
     lib = ctypes.CDLL(so)
     P, L, I, F = ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_float
-    lib.tgfr_tail_fwd.argtypes = [P, L, I, P, P, P, P, F, P, L, P, P, P, P, P]
+    lib.tgfr_tail_fwd.argtypes = [P, L, I, P, P, P, P, F, P, L, P, P, P, P, P, P, I, I, I, P]
     lib.tgfr_tail_bwd.argtypes = [P, L, P, L, P, I, F, P, P, P, P, L, P, P, P, P]
     lib.tgfr_tail_pack.argtypes = [P, P, P, P, P]
     d = "cuda"
@@ -112,7 +112,7 @@ def bench(so, rows=12544, reps=20):
     def fwd():
         lib.tgfr_tail_fwd(z.data_ptr(), 256, rows, pk.data_ptr(), b1.data_ptr(), b2.data_ptr(),
                           bp.data_ptr(), 1e-12, r.data_ptr(), 256, zb.data_ptr(), h1.data_ptr(),
-                          h2.data_ptr(), inv.data_ptr(), st)
+                          h2.data_ptr(), inv.data_ptr(), None, None, 0, 0, 0, st)
 
     def bwd():
         lib.tgfr_tail_bwd(dr.data_ptr(), 256, r.data_ptr(), 256, inv.data_ptr(), rows, 1e-12,

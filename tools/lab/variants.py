@@ -18,7 +18,7 @@ from text_guided_face_recognition_amd import build as B  # noqa: E402
 OUT = os.path.join(ROOT, "tools", "lab", "build")
 
 # name -> list of (old, new) substitutions in tgfr_wr.hip
-PAD_SKIP = ("  // ---- prologue: G1 of caption 0\n",
+_OLD_PAD_SKIP = ("  // ---- prologue: G1 of caption 0\n",
             "  if (rt >= NRT) {       // the padding tile: only its share of the DMA\n"
             "    asm volatile(\"s_waitcnt vmcnt(0)\\n\\ts_waitcnt lgkmcnt(0)\\n\\ts_barrier\" ::: \"memory\");\n"
             "    const int T2p = (K + 2) & ~1;\n"
@@ -29,20 +29,24 @@ PAD_SKIP = ("  // ---- prologue: G1 of caption 0\n",
 # round 3: the T <= 32 bounded backward (wr_bwd_pipe_kernel)
 VARIANTS = {
     "base": [],
-    # the padding-only tile (tg 1, wave 3) issues no MFMA / softmax work
-    "padskip": [PAD_SKIP],
-    # ablation (wrong results): no DMA inside the caption loop
-    "nodma": [("    ring_barrier<0>();                 // X(t+1) landed everywhere; X(t-2) retired\n"
-               "    stage_dma(t + 2);\n",
-               "    ring_barrier<0>();                 // X(t+1) landed everywhere; X(t-2) retired\n")],
-    # ablation (wrong results): no softmax VALU
-    "nosm": [("      sm_chunk(n, tbs, A0, A1, Mo);\n", "      if (n == 63) { Mo[0] = Mo[1] = Mo[2] = Mo[3] = "
-              "__builtin_bit_cast(bf16x8, A0[0] > 1e30f ? rd[0] : rd[1]); }\n")],
+    "head": "HEAD",
+    # DMA pieces at the stage head instead of between the first MFMAs
+    "dmahead": [("  return (n >= 2 && n <= 18 && (n & 1) == 0) ? (n - 2) / 2 : -1;",
+                 "  return n < 9 ? n : -1;")],
+    # DMA pieces spread over the first half of the stage
+    "dmaspread": [("  return (n >= 2 && n <= 18 && (n & 1) == 0) ? (n - 2) / 2 : -1;",
+                   "  return (n >= 1 && n <= 33 && (n % 4) == 1) ? (n - 1) / 4 : -1;")],
 }
 
 
+
 def build_variant(name, subs):
-    src = open(os.path.join(B.CSRC, "tgfr_wr.hip")).read()
+    if subs == "HEAD":          # the committed source, for A/B against the work tree
+        src = subprocess.run(["git", "show", "HEAD:text_guided_face_recognition_amd/csrc/tgfr_wr.hip"],
+                             cwd=ROOT, check=True, capture_output=True, text=True).stdout
+        subs = []
+    else:
+        src = open(os.path.join(B.CSRC, "tgfr_wr.hip")).read()
     for old, new in subs:
         if old not in src:
             raise SystemExit(f"{name}: substitution not found: {old[:60]!r}")

@@ -311,7 +311,8 @@ def main():
     pair_count = args.batch * args.batch * n
     flops = {"tgfr_wr_fwd": 4 * R * D * n_words * pair_count,
              "tgfr_wr_bwd": 6 * R * D * n_words * pair_count}
-    dominant = max((k for k in prof if k in flops), key=lambda k: prof[k][1])
+    # the dominant word<->region entry point by its replayed launch time
+    dominant = max((k for k in ktimer.replayed if k in flops), key=lambda k: ktimer.replayed[k])
     # the dominant kernel's launch duration: HIP events around 20 back-to-back
     # re-launches with the step's own arguments (inside the step, while its
     # buffers are alive), on the stream it runs on

@@ -179,6 +179,33 @@ int tgfr_sent_global_bwd(const float* gs0, const float* gs1, const float* ggl, c
                          const float* cosv, const float* stats, const float* nrm, float* dx,
                          long long lddx, void* stream);
 
+/* The same two losses for n_r <= 64 local images (global rows row_offset ..)
+ * against n_c <= 8192 all-gathered captions -- one process per GPU, or one
+ * process with more than 64 rows.  _fwd (grid over 64-column tiles): cosv
+ * [n_r][n_c], row partials, this rank's column partials colpart [2][2][n_c]
+ * (sets sent / global x (max, sum exp)) and norms nrm [n_r + n_c]; the caller
+ * all-gathers colpart rank-major (ONE collective for both losses) and _loss
+ * (one workgroup) forms the column and row log-sum-exps into stats
+ * [2 (n_r + n_c)] and this rank's contributions loss[3] = {sent loss0, sent
+ * loss1, global loss} (each / N_global via inv_n); _bwd: dx [n_r][256] from
+ * the losses' upstream gradients (device scalars, nullable).  Workspace sizes
+ * (floats): tgfr_sent_global_dist_ws. */
+int tgfr_sent_global_dist_ws(int n_r, int n_c, long long* rowpart, long long* colpart,
+                             long long* stats);
+int tgfr_sent_global_dist_fwd(const float* x, long long ldx, int n_r, const float* y,
+                              long long ldy, int n_c, const long long* cls, int row_offset,
+                              float s_sent, float s_glob, float eps, float* cosv, float* rowpart,
+                              float* colpart, float* nrm, void* stream);
+int tgfr_sent_global_dist_loss(const float* cosv, int n_r, int n_c, int row_offset, float s_sent,
+                               float s_glob, const float* rowpart, const float* colparts,
+                               int world, float inv_n, float* stats, float* loss, void* stream);
+int tgfr_sent_global_dist_bwd(const float* gs0, const float* gs1, const float* ggl,
+                              const float* x, long long ldx, int n_r, const float* y,
+                              long long ldy, int n_c, const long long* cls, int row_offset,
+                              float s_sent, float s_glob, float eps, float inv_n,
+                              const float* cosv, const float* stats, const float* nrm, float* dx,
+                              long long lddx, void* stream);
+
 /* loss[0] = inv_n * sum_b (row_lse[b] - L[b][b+off]), loss[1] = inv_n * sum_b
  * (col_lse[b+off] - L[b][b+off]): this rank's share of nn.CrossEntropyLoss on
  * the rows and on the transposed matrix (models/losses.py:52-53, 131-132). */

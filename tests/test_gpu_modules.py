@@ -107,6 +107,56 @@ def test_sent_global_fused(gpu, n):
         assert _relerr(xg.grad, g["d_cnn"]) < 1e-4
 
 
+@pytest.mark.parametrize("n_r,world", [(64, 8), (16, 3), (37, 2), (64, 1)])
+def test_sent_global_dist_ranks(gpu, n_r, world):
+    """The per-rank sent_loss + global_loss kernels (tgfr_sent_global_dist_*,
+    the one-process-per-GPU stage-1 path) with `world` ranks emulated in one
+    process through the C ABI: every rank's forward, the column partials
+    concatenated rank-major (what the all-gather delivers), every rank's loss
+    and backward.  The summed contributions equal the oracle's global-batch
+    losses (1e-4) and the stacked row gradients of s0 + 2 s1 + 3 gl its
+    gradient (1e-4 of max); duplicate class ids exercise the sent mask across
+    ranks (models/losses.py:19-57, :329-351)."""
+    from oracle import tgfr_oracle as O
+    from text_guided_face_recognition_amd import kernels as K
+    from text_guided_face_recognition_amd._hip import call, ptr, stream
+    n = n_r * world
+    gen = torch.Generator().manual_seed(n + world)
+    x = torch.randn(n, 256, generator=gen)
+    y = torch.randn(n, 256, generator=gen)
+    cls = torch.randint(0, max(2, n // 5), (n,), generator=gen)
+    xo = x.clone().requires_grad_()
+    r0, r1, _ = O.sent_loss(xo, y, torch.arange(n), cls.numpy(), 10.0)
+    rg, _ = O.global_loss(xo, y)
+    (r0 + 2 * r1 + 3 * rg).backward()
+    xg, yg, cg = x.to(gpu), y.to(gpu), cls.to(gpu)
+    n_rp, n_cp, n_st = K._sgd_ws(n_r, n)
+    ranks = []
+    for r in range(world):
+        xr = xg[r * n_r:(r + 1) * n_r].contiguous()
+        t_ = dict(cosv=torch.empty(n_r, n, device=gpu), rowpart=torch.empty(n_rp, device=gpu),
+                  colpart=torch.empty(n_cp, device=gpu), nrm=torch.empty(n_r + n, device=gpu),
+                  stats=torch.empty(n_st, device=gpu), loss=torch.empty(3, device=gpu), x=xr)
+        call("tgfr_sent_global_dist_fwd", ptr(xr), 256, n_r, ptr(yg), 256, n, ptr(cg), r * n_r,
+             10.0, 10.0, 1e-8, ptr(t_["cosv"]), ptr(t_["rowpart"]), ptr(t_["colpart"]),
+             ptr(t_["nrm"]), stream())
+        ranks.append(t_)
+    parts = torch.stack([t_["colpart"] for t_ in ranks]).contiguous()
+    gw = [torch.full((), v, device=gpu) for v in (1.0, 2.0, 3.0)]
+    dx = torch.empty(n, 256, device=gpu)
+    for r, t_ in enumerate(ranks):
+        call("tgfr_sent_global_dist_loss", ptr(t_["cosv"]), n_r, n, r * n_r, 10.0, 10.0,
+             ptr(t_["rowpart"]), ptr(parts), world, 1.0 / n, ptr(t_["stats"]), ptr(t_["loss"]),
+             stream())
+        call("tgfr_sent_global_dist_bwd", ptr(gw[0]), ptr(gw[1]), ptr(gw[2]), ptr(t_["x"]), 256,
+             n_r, ptr(yg), 256, n, ptr(cg), r * n_r, 10.0, 10.0, 1e-8, 1.0 / n,
+             ptr(t_["cosv"]), ptr(t_["stats"]), ptr(t_["nrm"]), ptr(dx[r * n_r]), 256, stream())
+    tot = torch.stack([t_["loss"] for t_ in ranks]).sum(0).cpu()
+    for a, b in zip(tot.tolist(), (r0.item(), r1.item(), rg.item())):
+        assert abs(a - b) < 1e-4, (a, b)
+    assert _relerr(dx, xo.grad.numpy()) < 1e-4
+
+
 @pytest.mark.parametrize("tag", ["c256_hw196", "c36_hw36"])
 def test_self_attention(gpu, tag):
     from text_guided_face_recognition_amd.models.fusion_nets import SelfAttention

@@ -247,7 +247,10 @@ def test_train_step_with_text_heading_matches_oracle(gpu, precision, b):
     utils/dataset_utils.py:38-46; the bf16 words reach the word<->region
     kernels as TextHeading's own operand rows).  Against the oracle's
     text_heading + step on the same weights and hidden states.  Tolerances:
-    fp32 as test_train_step_matches_oracle; bf16 as the reduced-precision step,
+    fp32 as test_train_step_matches_oracle, except Adam's first update at 1e-3
+    of scale (its sign decision on |g| ~ 1e-5 elements moves with the ~1e-5
+    word differences TextHeading's own fp32 convs leave: 1.1e-4 measured);
+    bf16 as the reduced-precision step,
     with the sentence-side terms at 1e-2 (TextHeading's bf16 convs: words and
     sentence codes within 2e-2, test_text_heading_vs_oracle)."""
     from text_guided_face_recognition_amd.config import make_args
@@ -277,8 +280,8 @@ def test_train_step_with_text_heading_matches_oracle(gpu, precision, b):
     for k, v in HEAD_KEYS.items():
         gmax = max(gmax, _check_adam(named[k], ref["old"][v], ref["hp"][v].detach(),
                                      ref["grads"][v], args.lr_head, k, g_all,
-                                     **({} if fp32 else dict(gtol=1e-1, utol=1e-3,
-                                                               gfloor=1e-3))))
+                                     **(dict(utol=1e-3) if fp32 else
+                                        dict(gtol=1e-1, utol=1e-3, gfloor=1e-3))))
     print(f"  worst head gradient error {gmax:.3e} of its tensor's scale")
     for new, want in ((tr.image_cls.weight, ref["arc_i"]), (tr.text_cls.weight, ref["arc_t"])):
         scale = want.abs().max().clamp(min=1e-6)

@@ -85,6 +85,11 @@ SIGNATURES = {
     "tgfr_text_heading": [P, I, I, P, P, P, P, L, L, P, L, P, P, I, F, I, I, P],
     "tgfr_sent_global": [P, L, P, L, I, P, F, F, F, P, P, P, P, P],
     "tgfr_sent_global_bwd": [P, P, P, P, L, P, L, I, P, F, F, F, P, P, P, P, L, P],
+    "tgfr_sent_global_dist_ws": [I, I, P, P, P],
+    "tgfr_sent_global_dist_fwd": [P, L, I, P, L, I, P, I, F, F, F, P, P, P, P, P],
+    "tgfr_sent_global_dist_loss": [P, I, I, I, F, F, P, P, I, F, P, P, P],
+    "tgfr_sent_global_dist_bwd": [P, P, P, P, L, I, P, L, I, P, I, F, F, F, F, P, P, P, P, L,
+                                  P],
     "tgfr_focal_ce2": [P, P, I, I, P, F, P, P, P, P, P, P],
     "tgfr_arc_fwd_heads": [P, I, I, I, I, F, I, F, P],
     "tgfr_arc_focal_bwd_heads": [P, I, I, I, I, F, I, F, F, P],

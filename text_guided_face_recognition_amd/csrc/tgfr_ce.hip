@@ -228,34 +228,31 @@ constexpr int SG_LD = D + 4;                 // padded fp32 LDS rows (bank sprea
 constexpr int SG_LDS = 2 * SG_N * SG_LD * 4 + SG_N * (SG_N + 1) * 4;
 constexpr int SG_T = 1024;                   // 16 waves
 
-// 16 waves: staging 8 float4 loads per thread; wave w computes tile w & 3 of
-// the 64 x 64 cosines over k quarter w >> 2 (the quarters summed through LDS);
-// each logit set's LSEs by 4 waves, 4 lanes per row / column.
-__global__ __launch_bounds__(SG_T) void sg_fwd_kernel(
-    const float* __restrict__ x, long long ldx, const float* __restrict__ y, long long ldy, int n,
-    const long long* __restrict__ cls, float s_sent, float s_glob, float eps,
-    float* __restrict__ cosv, float* __restrict__ stats, float* __restrict__ nrm,
-    float* __restrict__ loss) {
+// The cosine tile of up to 64 x rows against up to 64 y rows into LDS
+// cs[r][c] (pitch SG_N + 1), and the squared norms into nxp / nyp [4][64]
+// (k-quarter partials).  1024 threads = 16 waves: staging 4 float4 loads per
+// thread and matrix; wave w computes 32 x 32 tile w & 3 over k quarter w >> 2
+// on split-bf16 MFMAs (~fp32 products), the quarters summed through LDS.
+// Rows past n_x / n_y repeat the last row (their results are never read).
+__device__ __forceinline__ void sg_cos_tile(const float* __restrict__ x, long long ldx, int n_x,
+                                            const float* __restrict__ y, long long ldy, int n_y,
+                                            float eps, float* cs, float (*nxp)[SG_N],
+                                            float (*nyp)[SG_N]) {
   // LDS: x rows | y rows (fp32, padded) | cos [64][65]; the MFMA partials
   // reuse the row area once the products are done
   float* xs = (float*)g_smem;
   float* ys = xs + SG_N * SG_LD;
-  float* cs = ys + SG_N * SG_LD;
   float* part = xs;                            // [16 waves][16][64]
-  __shared__ float nxp[4][SG_N], nyp[4][SG_N];
-  __shared__ long long cl[SG_N];
-  __shared__ float red[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 31, h = lane >> 5;
-  if (tid < n) cl[tid] = cls[tid];
   {
     constexpr int NQ = SG_N * D / 4 / SG_T;    // 4 float4 per thread per matrix
     const uint32_t yoff = SG_N * SG_LD * 4;
     uint4 vx[NQ], vy[NQ];
 #pragma unroll
     for (int u = 0; u < NQ; ++u) {
-      const int i = u * SG_T + tid, r = min(i / (D / 4), n - 1), k = i % (D / 4);
-      vx[u] = *(const uint4*)(x + r * ldx + 4 * k);
-      vy[u] = *(const uint4*)(y + r * ldy + 4 * k);
+      const int i = u * SG_T + tid, k = i % (D / 4);
+      vx[u] = *(const uint4*)(x + min(i / (D / 4), n_x - 1) * ldx + 4 * k);
+      vy[u] = *(const uint4*)(y + min(i / (D / 4), n_y - 1) * ldy + 4 * k);
     }
 #pragma unroll
     for (int u = 0; u < NQ; ++u) {
@@ -299,7 +296,7 @@ __global__ __launch_bounds__(SG_T) void sg_fwd_kernel(
   // cos[r][c] = sum of the 4 quarter partials / max(|x_r||y_c|, eps)
   for (int e = tid; e < SG_N * SG_N; e += SG_T) {
     const int r = e >> 6, c = e & 63;
-    if (r >= n || c >= n) continue;
+    if (r >= n_x || c >= n_y) continue;
     const int tt = (r >> 5) * 2 + (c >> 5), rr = r & 31;
     const int hh = (rr >> 2) & 1, q = (rr & 3) | ((rr >> 3) << 2), ln = (c & 31) + 32 * hh;
     float v = 0.f;
@@ -307,10 +304,24 @@ __global__ __launch_bounds__(SG_T) void sg_fwd_kernel(
     for (int k4 = 0; k4 < 4; ++k4) v += part[((tt + 4 * k4) * 16 + q) * 64 + ln];
     const float nx = nxp[0][r] + nxp[1][r] + nxp[2][r] + nxp[3][r];
     const float ny = nyp[0][c] + nyp[1][c] + nyp[2][c] + nyp[3][c];
-    const float cv = v / fmaxf(sqrtf(nx) * sqrtf(ny), eps);
-    cs[r * (SG_N + 1) + c] = cv;
-    cosv[r * n + c] = cv;
+    cs[r * (SG_N + 1) + c] = v / fmaxf(sqrtf(nx) * sqrtf(ny), eps);
   }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(SG_T) void sg_fwd_kernel(
+    const float* __restrict__ x, long long ldx, const float* __restrict__ y, long long ldy, int n,
+    const long long* __restrict__ cls, float s_sent, float s_glob, float eps,
+    float* __restrict__ cosv, float* __restrict__ stats, float* __restrict__ nrm,
+    float* __restrict__ loss) {
+  float* cs = (float*)g_smem + 2 * SG_N * SG_LD;
+  __shared__ float nxp[4][SG_N], nyp[4][SG_N];
+  __shared__ long long cl[SG_N];
+  __shared__ float red[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid < n) cl[tid] = cls[tid];
+  sg_cos_tile(x, ldx, n, y, ldy, n, eps, cs, nxp, nyp);
+  for (int e = tid; e < n * n; e += SG_T) cosv[e] = cs[(e / n) * (SG_N + 1) + e % n];
   __syncthreads();
   // logit set ls = w >> 2 (0: sent rows, 1: sent columns, 2: global rows,
   // 3: global columns); row / column j = 16 (w & 3) + lane / 4, four lanes
@@ -406,6 +417,181 @@ __global__ __launch_bounds__(256) void sg_bwd_kernel(
   dx[b * lddx + tid] = acc;
 }
 
+// --------------------------- sent_loss + global_loss, rows x global columns ---
+// The same two losses when this rank holds n_r <= 64 images (global rows
+// row_offset ..) against n_c all-gathered captions (DataParallel over
+// processes, or one process with n > 64): three launches and, with a process
+// group, ONE all-gather between the first two.
+//   sgd_fwd   grid = 64-column tiles: the tile's cosines (sg_cos_tile), per
+//             (set, row) the tile's online (max, sum exp) partial and per (set,
+//             column) the column's (max, sum exp) over this rank's rows -- the
+//             column partials are what the ranks exchange
+//   sgd_loss  one workgroup: column LSEs from every rank's partials, row LSEs
+//             from the tiles', this rank's four CE contributions (/ N_global)
+//   sgd_bwd   one workgroup per row: both losses' softmax gradients folded into
+//             one dcos per column, then the cosine backward (as sg_bwd)
+// Sets: 0 = sent (gamma3, same-class off-diagonal entries masked), 1 = global
+// (temp3).  Layouts: rowpart [2][tiles][n_r][2], colpart [2][2][n_c] (max,
+// sum), stats = row LSE [2][n_r] then column LSE [2][n_c].
+__device__ __forceinline__ void lse_push(float& m, float& sum, float L) {
+  if (L > m) {
+    sum = sum * __expf(m - L) + 1.f;
+    m = L;
+  } else {
+    sum += __expf(L - m);
+  }
+}
+__device__ __forceinline__ void lse_merge(float& m, float& sum, float m2, float s2) {
+  const float mm = fmaxf(m, m2);
+  sum = (m == -INFINITY ? 0.f : sum * __expf(m - mm)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mm));
+  m = mm;
+}
+
+__global__ __launch_bounds__(SG_T) void sgd_fwd_kernel(
+    const float* __restrict__ x, long long ldx, int n_r, const float* __restrict__ y,
+    long long ldy, int n_c, const long long* __restrict__ cls, int row_offset, float s_sent,
+    float s_glob, float eps, float* __restrict__ cosv, float* __restrict__ rowpart,
+    float* __restrict__ colpart, float* __restrict__ nrm) {
+  float* cs = (float*)g_smem + 2 * SG_N * SG_LD;
+  __shared__ float nxp[4][SG_N], nyp[4][SG_N];
+  __shared__ long long clr[SG_N], clc[SG_N];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tile = blockIdx.x, tiles = gridDim.x, c0 = tile * SG_N;
+  const int n_y = min(SG_N, n_c - c0);
+  if (tid < n_r) clr[tid] = cls[row_offset + tid];
+  if (tid < n_y) clc[tid] = cls[c0 + tid];
+  sg_cos_tile(x, ldx, n_r, y + (long long)c0 * ldy, ldy, n_y, eps, cs, nxp, nyp);
+  for (int e = tid; e < n_r * n_y; e += SG_T)
+    cosv[(long long)(e / n_y) * n_c + c0 + e % n_y] = cs[(e / n_y) * (SG_N + 1) + e % n_y];
+  // ls = w >> 2: 0 sent rows, 1 sent columns, 2 global rows, 3 global columns;
+  // row / column j = 16 (w & 3) + lane / 4, four lanes each
+  const int ls = w >> 2, j = 16 * (w & 3) + (lane >> 2), sub = lane & 3;
+  const bool glob = ls >= 2, col = ls & 1;
+  const float sc = glob ? s_glob : s_sent;
+  const int nj = col ? n_y : n_r, nk = col ? n_r : n_y;
+  float m = -INFINITY, sum = 0.f;
+  if (j < nj) {
+    for (int k = sub; k < nk; k += 4) {
+      const int b = col ? k : j, i = col ? j : k;
+      if (!glob && clr[b] == clc[i] && row_offset + b != c0 + i) continue;
+      lse_push(m, sum, sc * cs[b * (SG_N + 1) + i]);
+    }
+  }
+#pragma unroll
+  for (int msk = 1; msk <= 2; msk <<= 1) lse_merge(m, sum, __shfl_xor(m, msk), __shfl_xor(sum, msk));
+  if (j < nj && sub == 0) {
+    const int set = glob ? 1 : 0;
+    if (col) {
+      colpart[(set * 2 + 0) * n_c + c0 + j] = m;
+      colpart[(set * 2 + 1) * n_c + c0 + j] = sum;
+    } else {
+      float* rp = rowpart + (((long long)set * tiles + tile) * n_r + j) * 2;
+      rp[0] = m;
+      rp[1] = sum;
+    }
+  }
+  if (tile == 0 && tid < n_r) nrm[tid] = sqrtf(nxp[0][tid] + nxp[1][tid] + nxp[2][tid] + nxp[3][tid]);
+  if (tid < n_y) nrm[n_r + c0 + tid] = sqrtf(nyp[0][tid] + nyp[1][tid] + nyp[2][tid] + nyp[3][tid]);
+}
+
+__global__ __launch_bounds__(SG_T) void sgd_loss_kernel(
+    const float* __restrict__ cosv, int n_r, int n_c, int row_offset, float s_sent, float s_glob,
+    int tiles, const float* __restrict__ rowpart, const float* __restrict__ colparts, int world,
+    float inv_n, float* __restrict__ stats, float* __restrict__ loss) {
+  __shared__ float rl[2][SG_N], cl[2][SG_N];
+  __shared__ float red[SG_T / WAVE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float* row_lse = stats;
+  float* col_lse = stats + 2 * n_r;
+  // column LSEs over every rank's partials (rank-major [world][2 sets][2][n_c])
+  for (int e = tid; e < 2 * n_c; e += SG_T) {
+    const int set = e / n_c, c = e % n_c;
+    float m = -INFINITY, sum = 0.f;
+    for (int r = 0; r < world; ++r) {
+      const float* cp = colparts + (long long)r * 4 * n_c + set * 2 * n_c;
+      lse_merge(m, sum, cp[c], cp[n_c + c]);
+    }
+    const float lse = m + __logf(sum);
+    col_lse[set * n_c + c] = lse;
+    const int b = c - row_offset;
+    if (b >= 0 && b < n_r) cl[set][b] = lse;
+  }
+  // row LSEs over the column tiles' partials
+  if (tid < 2 * n_r) {
+    const int set = tid / n_r, b = tid % n_r;
+    float m = -INFINITY, sum = 0.f;
+    for (int t = 0; t < tiles; ++t) {
+      const float* rp = rowpart + (((long long)set * tiles + t) * n_r + b) * 2;
+      lse_merge(m, sum, rp[0], rp[1]);
+    }
+    const float lse = m + __logf(sum);
+    row_lse[set * n_r + b] = lse;
+    rl[set][b] = lse;
+  }
+  __syncthreads();
+  // this rank's diagonal terms: waves 0-3 sent rows / sent columns / global
+  // rows / global columns
+  float term = 0.f;
+  if (w < 4 && lane < n_r) {
+    const int set = w >> 1;
+    const float d = (set ? s_glob : s_sent) * cosv[(long long)lane * n_c + row_offset + lane];
+    term = ((w & 1) ? cl[set][lane] : rl[set][lane]) - d;
+  }
+  term = wave_sum(term);
+  if (lane == 0) red[w] = term;
+  __syncthreads();
+  if (tid == 0) {
+    loss[0] = red[0] * inv_n;                // sent loss0 (rows)
+    loss[1] = red[1] * inv_n;                // sent loss1 (columns)
+    loss[2] = (red[2] + red[3]) * inv_n;     // global loss0 + loss1
+  }
+}
+
+// grid n_r (row b), 256 threads (thread = feature d); dcos of the n_c columns in LDS
+__global__ __launch_bounds__(256) void sgd_bwd_kernel(
+    const float* __restrict__ gs0, const float* __restrict__ gs1, const float* __restrict__ ggl,
+    const float* __restrict__ x, long long ldx, int n_r, const float* __restrict__ y,
+    long long ldy, int n_c, const long long* __restrict__ cls, int row_offset, float s_sent,
+    float s_glob, float eps, float inv_n, const float* __restrict__ cosv,
+    const float* __restrict__ stats, const float* __restrict__ nrm, float* __restrict__ dx,
+    long long lddx) {
+  extern __shared__ float cf[];                // [n_c]
+  __shared__ float red[4];
+  const int b = blockIdx.x, tid = threadIdx.x, gb = row_offset + b;
+  const float a0 = gs0 ? *gs0 : 0.f, a1 = gs1 ? *gs1 : 0.f, ag = ggl ? *ggl : 0.f;
+  const float* row_lse = stats;
+  const float* col_lse = stats + 2 * n_r;
+  const float nxb = nrm[b], rls = row_lse[b], rlg = row_lse[n_r + b];
+  const long long cb = cls[gb];
+  float xcoef = 0.f;
+  for (int i = tid; i < n_c; i += 256) {
+    const float cv = cosv[(long long)b * n_c + i];
+    const float dg = i == gb ? 1.f : 0.f;
+    float dls = 0.f;
+    if (!(cb == cls[i] && i != gb)) {
+      const float L = s_sent * cv;
+      dls = a0 * (__expf(L - rls) - dg) + a1 * (__expf(L - col_lse[i]) - dg);
+    }
+    const float Lg = s_glob * cv;
+    const float dlg = ag * ((__expf(Lg - rlg) - dg) + (__expf(Lg - col_lse[n_c + i]) - dg));
+    const float dcos = (s_sent * dls + s_glob * dlg) * inv_n;
+    const float den = nxb * nrm[n_r + i];
+    if (den >= eps) {
+      cf[i] = dcos / den;
+      xcoef -= dcos * cv / (nxb * nxb);
+    } else {
+      cf[i] = dcos / eps;
+    }
+  }
+  xcoef = wave_sum(xcoef);
+  if ((tid & 63) == 0) red[tid >> 6] = xcoef;
+  __syncthreads();
+  xcoef = red[0] + red[1] + red[2] + red[3];
+  float acc = xcoef * x[b * ldx + tid];
+  for (int i = 0; i < n_c; ++i) acc = fmaf(cf[i], y[i * ldy + tid], acc);
+  dx[b * lddx + tid] = acc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -464,6 +650,58 @@ int tgfr_sent_global_bwd(const float* gs0, const float* gs1, const float* ggl, c
   if (n <= 0 || n > SG_N || !x || !y || !cls || !cosv || !stats || !nrm || !dx) return 1001;
   hipLaunchKernelGGL(sg_bwd_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, gs0, gs1, ggl, x,
                      ldx, y, ldy, n, cls, s_sent, s_glob, eps, cosv, stats, nrm, dx, lddx);
+  return (int)hipGetLastError();
+}
+
+int tgfr_sent_global_dist_ws(int n_r, int n_c, long long* rowpart, long long* colpart,
+                             long long* stats) {
+  if (n_r <= 0 || n_r > SG_N || n_c <= 0 || n_c > 8192 || !rowpart || !colpart || !stats)
+    return 1001;
+  *rowpart = 2ll * ((n_c + SG_N - 1) / SG_N) * n_r * 2;
+  *colpart = 4ll * n_c;
+  *stats = 2ll * (n_r + n_c);
+  return 0;
+}
+
+int tgfr_sent_global_dist_fwd(const float* x, long long ldx, int n_r, const float* y,
+                              long long ldy, int n_c, const long long* cls, int row_offset,
+                              float s_sent, float s_glob, float eps, float* cosv, float* rowpart,
+                              float* colpart, float* nrm, void* stream) {
+  if (n_r <= 0 || n_r > SG_N || n_c <= 0 || n_c > 8192 || row_offset < 0 ||
+      row_offset + n_r > n_c || !x || !y || !cls || !cosv || !rowpart || !colpart || !nrm ||
+      ldx % 4 || ldy % 4 || ((uintptr_t)x & 15) || ((uintptr_t)y & 15))
+    return 1001;
+  if (const int e = set_max_lds((const void*)sgd_fwd_kernel, SG_LDS)) return e;
+  hipLaunchKernelGGL(sgd_fwd_kernel, dim3((n_c + SG_N - 1) / SG_N), dim3(SG_T), SG_LDS,
+                     (hipStream_t)stream, x, ldx, n_r, y, ldy, n_c, cls, row_offset, s_sent,
+                     s_glob, eps, cosv, rowpart, colpart, nrm);
+  return (int)hipGetLastError();
+}
+
+int tgfr_sent_global_dist_loss(const float* cosv, int n_r, int n_c, int row_offset, float s_sent,
+                               float s_glob, const float* rowpart, const float* colparts,
+                               int world, float inv_n, float* stats, float* loss, void* stream) {
+  if (n_r <= 0 || n_r > SG_N || n_c <= 0 || world <= 0 || !cosv || !rowpart || !colparts ||
+      !stats || !loss)
+    return 1001;
+  hipLaunchKernelGGL(sgd_loss_kernel, dim3(1), dim3(SG_T), 0, (hipStream_t)stream, cosv, n_r, n_c,
+                     row_offset, s_sent, s_glob, (n_c + SG_N - 1) / SG_N, rowpart, colparts,
+                     world, inv_n, stats, loss);
+  return (int)hipGetLastError();
+}
+
+int tgfr_sent_global_dist_bwd(const float* gs0, const float* gs1, const float* ggl,
+                              const float* x, long long ldx, int n_r, const float* y,
+                              long long ldy, int n_c, const long long* cls, int row_offset,
+                              float s_sent, float s_glob, float eps, float inv_n,
+                              const float* cosv, const float* stats, const float* nrm, float* dx,
+                              long long lddx, void* stream) {
+  if (n_r <= 0 || n_r > SG_N || n_c <= 0 || n_c > 8192 || !x || !y || !cls || !cosv || !stats ||
+      !nrm || !dx)
+    return 1001;
+  hipLaunchKernelGGL(sgd_bwd_kernel, dim3(n_r), dim3(256), n_c * sizeof(float),
+                     (hipStream_t)stream, gs0, gs1, ggl, x, ldx, n_r, y, ldy, n_c, cls,
+                     row_offset, s_sent, s_glob, eps, inv_n, cosv, stats, nrm, dx, lddx);
   return (int)hipGetLastError();
 }
 

@@ -292,20 +292,34 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
       if (row0 + m < rows) {
         const float iv = lds_ldf(F_INV + m * 4);
         float* o = R + (long long)(row0 + m) * ldr + 64 * w + lr;
-        const float v0 = acc[mt][0][q] * iv, v1 = acc[mt][1][q] * iv;
-        o[0] = v0;
-        o[32] = v1;
-        if (Rrows) {
-          // R rows in the contraction's operand layout: [item][rows_pad][256]
-          // bf16 (or fp16) -- what tgfr_prep_rows would make of R
-          const int it = (row0 + m) / rows_per_item, ri = (row0 + m) % rows_per_item;
-          uint16_t* d = Rrows + ((long long)it * rows_pad + ri) * TD + 64 * w + lr;
-          d[0] = rows_f16 ? f16_bits(v0) : bf_bits(v0);
-          d[32] = rows_f16 ? f16_bits(v1) : bf_bits(v1);
-        }
+        o[0] = acc[mt][0][q] * iv;
+        o[32] = acc[mt][1][q] * iv;
       }
     }
   if (Rrows) {
+    // R rows in the contraction's operand layout: [item][rows_pad][256] bf16
+    // (or fp16), what tgfr_prep_rows would make of R.  Lanes lr, lr ^ 1 hold
+    // adjacent columns: they swap one value so each stores a 4-byte pair --
+    // the even lane row acc_row(q), the odd lane row acc_row(q + 1)
+    const bool odd = lr & 1;
+    auto bits = [&](float x) { return rows_f16 ? f16_bits(x) : bf_bits(x); };
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 16; q += 2) {
+        const int m0 = 32 * mt + acc_row(q, h), m1 = 32 * mt + acc_row(q + 1, h);
+        const float i0 = lds_ldf(F_INV + m0 * 4), i1 = lds_ldf(F_INV + m1 * 4);
+        const int m = odd ? m1 : m0;
+        const int it = (row0 + m) / rows_per_item, ri = (row0 + m) % rows_per_item;
+        uint16_t* d = Rrows + ((long long)it * rows_pad + ri) * TD + 64 * w + (lr & ~1);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const float a = acc[mt][nt][q] * i0, b = acc[mt][nt][q + 1] * i1;
+          const float y = __shfl_xor(odd ? a : b, 1);
+          const uint32_t pk = odd ? pack2(bits(y), bits(b)) : pack2(bits(a), bits(y));
+          if (row0 + m < rows) *(uint32_t*)(d + 32 * nt) = pk;
+        }
+      }
     // the padding rows (rows_per_item .. rows_pad) of every item whose last
     // row this workgroup holds: zero rows, zero norms
     for (int m = 0; m < TM; ++m) {

@@ -83,11 +83,18 @@ __global__ __launch_bounds__(64 * TH_NW) void text_pool_kernel(
     const float nraw = sqrtf(wave_sum(dot4(v)));
     const float n = fmaxf(nraw, 1e-12f);
     float* dst = words + b * s_wb + t * s_wt + 4 * l;
-    const float4 u = div4(v, n);
+    float4 u = div4(v, n);
+    // pinned: the operand rows below are formed from exactly the stored words
+    // (bit-equal to tgfr_prep_rows of them)
+    asm volatile("" : "+v"(u.x), "+v"(u.y), "+v"(u.z), "+v"(u.w));
     *(float4*)dst = u;
     if (Wrows) {
       // the word<->region kernels' operand row: scale * u in bf16 (fp16), and |u|
-      const float a[4] = {scale * u.x, scale * u.y, scale * u.z, scale * u.w};
+      float a[4] = {scale * u.x, scale * u.y, scale * u.z, scale * u.w};
+      // (pinned fp32 products: the fp16 conversion must not fuse with the
+      // multiply into a singly-rounded mixed FMA -- tgfr_prep_rows rounds
+      // twice, and the rows must be bit-equal to its)
+      asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]));
       uint16_t h[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) h[k] = rows_f16 ? f16_bits(a[k]) : bf_bits(a[k]);

@@ -65,7 +65,9 @@ __global__ __launch_bounds__(256) void prep_rows_kernel(
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (f16) {
-      h[k] = f16_bits(scale * v[k]);
+      float sv = scale * v[k];
+      asm volatile("" : "+v"(sv));      // fp32 product, then fp16 (no mixed FMA)
+      h[k] = f16_bits(sv);
       l[k] = 0;
     } else {
       split2(scale * v[k], h[k], l[k]);
@@ -985,7 +987,7 @@ constexpr int FWD_SLOTS = 16 + 5 * 34 + 18 + 34;
 // LDS operand prefetch distance in MFMA slots (ring of 8; see the wrap
 // argument at the issue site: no live slot is overwritten for 3 <= PF <= 6)
 constexpr int PF_FWD = 3;
-constexpr int PF_BWD = 3;
+constexpr int PF_BWD = 5;      // (3: +0.7 us, 4: +1.4 us at config 2)
 // the caption's slots in issue order
 __device__ __forceinline__ constexpr FwdSlot fwd_slot(int n) {
   if (n < 16) return {0, 1, n, 0, n};
@@ -2176,7 +2178,10 @@ constexpr int BP_TOK = 1024;                   // token table bytes
 constexpr int BP_BUF = B_XIMG + BP_TOK;        // one caption: X image + table
 constexpr int BP_ZERO = BP_NB * BP_BUF;        // a zero token table
 constexpr int BP_LDS = BP_ZERO + BP_TOK;
-// MFMA slot of the stage after which DMA piece j of X(t + 2) is issued (-1: none)
+// MFMA slot of the stage after which DMA piece j of X(t + 2) is issued (-1:
+// none): every other slot from slot 2 (config 2, interleaved A/B rounds,
+// tools/lab/bench_variants.py: 84.8 us against 85.3 with a piece every fourth
+// slot and ~86.5 with all nine at the stage head)
 __device__ __forceinline__ constexpr int bp_dma_slot(int n) {
   return (n >= 2 && n <= 18 && (n & 1) == 0) ? (n - 2) / 2 : -1;
 }

@@ -397,6 +397,75 @@ def sent_global(x, y, cls, s_sent, s_glob, eps=1e-8):
     return SentGlobal.apply(x, y, cls, s_sent, s_glob, eps)
 
 
+def _sgd_ws(n_r, n_c):
+    out = (ctypes.c_longlong * 3)()
+    rc = _hip.lib().tgfr_sent_global_dist_ws(int(n_r), int(n_c), ctypes.addressof(out),
+                                             ctypes.addressof(out) + 8,
+                                             ctypes.addressof(out) + 16)
+    if rc != 0:
+        raise RuntimeError(f"tgfr_sent_global_dist_ws failed with code {rc}")
+    return int(out[0]), int(out[1]), int(out[2])
+
+
+class SentGlobalDist(torch.autograd.Function):
+    """SentGlobal for this rank's n_r <= 64 images (global rows row_offset ..)
+    against n_c gathered captions: cosines and both losses' row / column
+    partials in one launch over column tiles, ONE all-gather of the column
+    partials of both losses (with a process group), one loss launch; backward
+    one launch (tgfr_sent_global_dist_*).  Returns this rank's contributions
+    (sum over ranks = the global-batch losses), as ContrastiveCE does."""
+
+    @staticmethod
+    def forward(ctx, x, y, cls, s_sent, s_glob, eps, row_offset, n_global, group):
+        x = _aligned(x)
+        y = _aligned(y)
+        n_r, n_c = x.shape[0], y.shape[0]
+        dev = x.device
+        cls = cls.to(device=dev, dtype=torch.int64).contiguous()
+        n_rp, n_cp, n_st = _sgd_ws(n_r, n_c)
+        cosv = torch.empty(n_r, n_c, dtype=torch.float32, device=dev)
+        rowpart = torch.empty(n_rp, dtype=torch.float32, device=dev)
+        colpart = torch.empty(n_cp, dtype=torch.float32, device=dev)
+        nrm = torch.empty(n_r + n_c, dtype=torch.float32, device=dev)
+        stats = torch.empty(n_st, dtype=torch.float32, device=dev)
+        loss = torch.empty(3, dtype=torch.float32, device=dev)
+        call("tgfr_sent_global_dist_fwd", ptr(x), x.stride(0), n_r, ptr(y), y.stride(0), n_c,
+             ptr(cls), int(row_offset), float(s_sent), float(s_glob), float(eps), ptr(cosv),
+             ptr(rowpart), ptr(colpart), ptr(nrm), _hip.stream())
+        world = 1
+        parts = colpart
+        if group is not None:
+            from .dist import all_gather_cat
+            parts = all_gather_cat(colpart.unsqueeze(0), group)
+            world = parts.shape[0]
+        inv_n = 1.0 / float(n_global)
+        call("tgfr_sent_global_dist_loss", ptr(cosv), n_r, n_c, int(row_offset), float(s_sent),
+             float(s_glob), ptr(rowpart), ptr(parts), world, inv_n, ptr(stats), ptr(loss),
+             _hip.stream())
+        ctx.save_for_backward(x, y, cls, cosv, stats, nrm)
+        ctx.cfg = (float(s_sent), float(s_glob), float(eps), int(row_offset), inv_n)
+        ctx.set_materialize_grads(False)
+        return loss[0], loss[1], loss[2]
+
+    @staticmethod
+    def backward(ctx, gs0, gs1, ggl):
+        x, y, cls, cosv, stats, nrm = ctx.saved_tensors
+        s_sent, s_glob, eps, row_offset, inv_n = ctx.cfg
+        n_r, n_c = cosv.shape
+        dx = torch.empty_like(x)
+        g = [None if v is None else v.float().contiguous() for v in (gs0, gs1, ggl)]
+        call("tgfr_sent_global_dist_bwd", ptr(g[0]), ptr(g[1]), ptr(g[2]), ptr(x), x.stride(0),
+             n_r, ptr(y), y.stride(0), n_c, ptr(cls), row_offset, s_sent, s_glob, eps, inv_n,
+             ptr(cosv), ptr(stats), ptr(nrm), ptr(dx), dx.stride(0), _hip.stream())
+        return (dx,) + (None,) * 8
+
+
+def sent_global_dist(x, y, cls, s_sent, s_glob, eps=1e-8, row_offset=0, n_global=None,
+                     group=None):
+    return SentGlobalDist.apply(x, y, cls, s_sent, s_glob, eps, row_offset,
+                                n_global or x.shape[0], group)
+
+
 # ------------------------------------------------------------------ bgemm ---
 def bgemm(a, b, out=None, alpha=1.0, accumulate=False, mode="fp32", bias=None,
           relu=False, ksplit=1):
@@ -1196,10 +1265,18 @@ class IdentityHeads(torch.autograd.Function):
     launch, both focal losses in one launch; backward: the focal logit
     gradient formed inside the ArcMargin backward of both heads (one launch),
     then dx of the heads whose input is trained (dcs W GEMM + l2-norm
-    backward, as ArcHead)."""
+    backward, as ArcHead).
+
+    With a process group (one process per GPU, rows = this rank's batch) the
+    focal factor is applied to the GLOBAL mean cross-entropy, as FocalCE does:
+    both heads' local NLL sums go into ONE all-reduce of two floats between
+    the forward launches and the loss formation, and the backward's logit
+    gradient carries f'(CE_global) / N_global -- the same kernels as one
+    process, plus that collective."""
 
     @staticmethod
-    def forward(ctx, x_t, w_t, x_i, w_i, label, s_t, s_i, m, easy, eps, gamma, mode):
+    def forward(ctx, x_t, w_t, x_i, w_i, label, s_t, s_i, m, easy, eps, gamma, mode,
+                group=None, n_global=None):
         xs = [_aligned(x_t), _aligned(x_i)]
         ws_ = [_aligned(w_t), _aligned(w_i)]
         label = label.to(torch.int64).contiguous()
@@ -1225,16 +1302,28 @@ class IdentityHeads(torch.autograd.Function):
         call("tgfr_focal_ce2", ptr(out[0]["logits"]), ptr(out[1]["logits"]), b, c, ptr(label),
              float(gamma), ptr(out[0]["fws"]), ptr(out[1]["fws"]), ptr(_hip.counters(dev)),
              ptr(out[0]["loss"]), ptr(out[1]["loss"]), _hip.stream())
+        losses = [out[0]["loss"][0], out[1]["loss"][0]]
+        if group is not None:
+            from .dist import all_reduce_sum_
+            # fws[b] holds the local mean CE (FocalCE's layout): both heads'
+            # NLL sums in one collective, then the global mean goes back in
+            sums = torch.cat([out[k]["fws"][b:b + 1] * b for k in range(2)])
+            all_reduce_sum_(sums, group)
+            for k in range(2):
+                logp = sums[k:k + 1] / float(n_global)
+                out[k]["fws"][b:b + 1].copy_(logp)
+                losses[k] = ((1.0 - torch.exp(-logp)).pow(float(gamma)) * logp)[0]
         ctx.save_for_backward(ws_[0], ws_[1], label,
                               *[out[k][n] for k in range(2)
                                 for n in ("logits", "cosv", "xn", "inv_nx", "inv_nw", "fws")])
-        ctx.cfg = (float(s_t), float(s_i), float(m), int(easy), float(eps), float(gamma), mode)
-        return out[0]["loss"][0], out[1]["loss"][0]
+        ctx.cfg = (float(s_t), float(s_i), float(m), int(easy), float(eps), float(gamma), mode,
+                   b / float(n_global) if group is not None else 1.0)
+        return losses[0], losses[1]
 
     @staticmethod
     def backward(ctx, g_t, g_i):
         w_t, w_i, label, *rest = ctx.saved_tensors
-        s_t, s_i, m, easy, eps, gamma, mode = ctx.cfg
+        s_t, s_i, m, easy, eps, gamma, mode, gscale = ctx.cfg
         per = [dict(zip(("logits", "cosv", "xn", "inv_nx", "inv_nw", "fws"), rest[6 * k:6 * k + 6]))
                for k in range(2)]
         ws_ = (w_t, w_i)
@@ -1242,7 +1331,10 @@ class IdentityHeads(torch.autograd.Function):
         c = w_t.shape[0]
         dev = w_t.device
         want_dx = (ctx.needs_input_grad[0], ctx.needs_input_grad[2])
-        gs = [g.float().reshape(1).contiguous() for g in (g_t, g_i)]
+        # (the kernel divides by the local row count; under a process group the
+        # global mean's gradient divides by the global one)
+        gs = [(g.float().reshape(1) * gscale if gscale != 1.0 else g.float().reshape(1))
+              .contiguous() for g in (g_t, g_i)]
         dws = [torch.empty_like(w) for w in ws_]
         dcs = [torch.empty(b, c, dtype=torch.float32, device=dev) if want_dx[k] else None
                for k in range(2)]
@@ -1264,14 +1356,17 @@ class IdentityHeads(torch.autograd.Function):
                 dx[k] = torch.empty_like(per[k]["xn"])
                 call("tgfr_l2norm_rows_bwd", ptr(dxn), d, ptr(per[k]["xn"]), d,
                      ptr(per[k]["inv_nx"]), b, d, eps, ptr(dx[k]), d, _hip.stream())
-        return (dx[0], dws[0], dx[1], dws[1]) + (None,) * 8
+        return (dx[0], dws[0], dx[1], dws[1]) + (None,) * 10
 
 
-def identity_heads(x_t, head_t, x_i, head_i, label, gamma, eps=1e-12):
+def identity_heads(x_t, head_t, x_i, head_i, label, gamma, eps=1e-12, group=None,
+                   n_global=None):
     """(focal(head_t(x_t)), focal(head_i(x_i))) for two ArcMarginProduct
-    modules of one (D, C) and margin: kernels.IdentityHeads."""
+    modules of one (D, C) and margin: kernels.IdentityHeads (with a process
+    group: this rank's rows, focal factor of the global-batch mean CE)."""
     return IdentityHeads.apply(x_t, head_t.weight, x_i, head_i.weight, label, head_t.s, head_i.s,
-                               head_t.m, head_t.easy_margin, eps, gamma, head_t.precision)
+                               head_t.m, head_t.easy_margin, eps, gamma, head_t.precision,
+                               group, n_global)
 
 
 class FocalCE(torch.autograd.Function):

@@ -146,13 +146,20 @@ def sent_global_loss(cnn_code, rnn_code, labels, class_ids, batch_size, args, ep
     """(sent loss0, sent loss1, global loss) = sent_loss(...) and
     global_loss(..., temp3) of the trainer (src/train_encoders_bert.py:276-277,
     :310) on the same features.  One process with the whole batch (n <= 64):
-    one fused kernel each way (kernels.SentGlobal); otherwise the two losses
-    as above."""
+    one fused kernel each way (kernels.SentGlobal); this rank's <= 64 images
+    against the gathered captions (one process per GPU, or n > 64 on one):
+    kernels.SentGlobalDist, the same arithmetic over column tiles with ONE
+    column-partial exchange for both losses; otherwise the two losses as
+    above."""
     row_offset, n_global, group = _dist(args)
     n = cnn_code.shape[0]
-    if group is None and n == rnn_code.shape[0] and n <= 64 and labels is not None:
+    if labels is not None and n <= 64:
         cls = _class_tensor(class_ids, cnn_code.device)
-        return K.sent_global(cnn_code, rnn_code, cls, args.TRAIN.SMOOTH.GAMMA3, temp3, eps)
+        if group is None and n == rnn_code.shape[0]:
+            return K.sent_global(cnn_code, rnn_code, cls, args.TRAIN.SMOOTH.GAMMA3, temp3, eps)
+        if rnn_code.shape[0] <= 8192:
+            return K.sent_global_dist(cnn_code, rnn_code, cls, args.TRAIN.SMOOTH.GAMMA3, temp3,
+                                      eps, row_offset, n_global, group)
     s0, s1 = sent_loss(cnn_code, rnn_code, labels, class_ids, batch_size, args, eps)
     return s0, s1, global_loss(cnn_code, rnn_code, eps, temp3, args)
 

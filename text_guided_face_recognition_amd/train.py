@@ -163,12 +163,15 @@ class Train:
 
     def _identity(self, sent, img_features, class_ids, ctx):
         """(focal(text_cls(sent)), focal(image_cls(img))): one launch per
-        direction for both heads on one process (kernels.IdentityHeads),
-        else the per-head path with the global-batch focal factor."""
+        direction for both heads (kernels.IdentityHeads; with a process group
+        one all-reduce of the two NLL sums gives the global-batch focal
+        factor), else the per-head path."""
         tc, ic = self.text_cls, self.image_cls
-        if (not ctx.active and sent.shape[0] <= 64 and tc.weight.shape == ic.weight.shape
+        if (sent.shape[0] <= 64 and tc.weight.shape == ic.weight.shape
                 and tc.m == ic.m and tc.easy_margin == ic.easy_margin):
-            return K.identity_heads(sent, tc, img_features, ic, class_ids, self.ident_loss.gamma)
+            return K.identity_heads(sent, tc, img_features, ic, class_ids, self.ident_loss.gamma,
+                                    group=ctx.group if ctx.active else None,
+                                    n_global=ctx.n_global)
         return K.focal_ce_multi(
             [(tc(sent, class_ids), class_ids), (ic(img_features, class_ids), class_ids)],
             self.ident_loss.gamma, ctx.group if ctx.active else None, ctx.n_global)

@@ -48,20 +48,34 @@ print(f"{name}: fwd {{fwd*1000:.1f}} us ({{4*196*256*nw*b*b/fwd/1e9:.0f}} TF)  "
 
 
 def main():
+    """Each variant runs LAB_ROUNDS times, round-robin (box clocks drift by a
+    few percent over a minute: interleaving keeps that out of the A/B)."""
+    import re
     b = int(os.environ.get("LAB_B", "64"))
+    rounds = int(os.environ.get("LAB_ROUNDS", "3"))
     libs = sorted(glob.glob(os.path.join(ROOT, "tools", "lab", "build", "lib_*.so")))
-    outs = {}
-    for lib in libs:
-        name = os.path.basename(lib)[4:-3]
-        out = f"/tmp/lab_{name}.pt"
-        code = CHILD.format(root=ROOT, lib=lib, b=b, out=out, name=name)
-        res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
-                             timeout=300)
-        sys.stdout.write(res.stdout)
-        if res.returncode != 0:
-            sys.stdout.write(res.stderr[-2000:])
-            continue
-        outs[name] = out
+    outs, times = {}, {}
+    for _ in range(rounds):
+        for lib in libs:
+            name = os.path.basename(lib)[4:-3]
+            out = f"/tmp/lab_{name}.pt"
+            code = CHILD.format(root=ROOT, lib=lib, b=b, out=out, name=name)
+            res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                                 timeout=300)
+            sys.stdout.write(res.stdout)
+            sys.stdout.flush()
+            if res.returncode != 0:
+                sys.stdout.write(res.stderr[-2000:])
+                continue
+            outs[name] = out
+            m = re.search(r"fwd ([\d.]+) us.*bwd ([\d.]+) us", res.stdout)
+            if m:
+                times.setdefault(name, []).append((float(m.group(1)), float(m.group(2))))
+    for name, ts in sorted(times.items()):
+        f = sorted(x[0] for x in ts)
+        bw = sorted(x[1] for x in ts)
+        print(f"SUMMARY {name}: fwd min {f[0]:.1f} med {f[len(f) // 2]:.1f} us | "
+              f"bwd min {bw[0]:.1f} med {bw[len(bw) // 2]:.1f} us")
     import torch
     if "base" in outs:
         lg0, g0 = torch.load(outs["base"])

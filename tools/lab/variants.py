@@ -30,12 +30,9 @@ _OLD_PAD_SKIP = ("  // ---- prologue: G1 of caption 0\n",
 VARIANTS = {
     "base": [],
     "head": "HEAD",
-    # DMA pieces at the stage head instead of between the first MFMAs
-    "dmahead": [("  return (n >= 2 && n <= 18 && (n & 1) == 0) ? (n - 2) / 2 : -1;",
-                 "  return n < 9 ? n : -1;")],
-    # DMA pieces spread over the first half of the stage
-    "dmaspread": [("  return (n >= 2 && n <= 18 && (n & 1) == 0) ? (n - 2) / 2 : -1;",
-                   "  return (n >= 1 && n <= 33 && (n % 4) == 1) ? (n - 1) / 4 : -1;")],
+    # LDS operand reads 4 / 5 MFMA slots ahead instead of 3
+    "pf4": [("constexpr int PF_BWD = 3;", "constexpr int PF_BWD = 4;")],
+    "pf5": [("constexpr int PF_BWD = 3;", "constexpr int PF_BWD = 5;")],
 }
 
 

@@ -8,6 +8,7 @@ import subprocess
 import sys
 
 import pytest
+import torch
 
 from conftest import ROOT
 
@@ -54,7 +55,42 @@ def test_dp_graphed_train_step(gpu, tmp_path, precision):
     for rank in range(2):
         r = json.load(open(f"{out}.{rank}"))
         # text gather, 2 column exchanges (word<->region; sentence + global
-        # together), the focal NLL-sum all-reduce, the gradient all-reduce
-        # -> 6 graphs
-        assert r["segments"] == 6, r
+        # together), the focal NLL-sum all-reduce, the classifiers' gradient
+        # all-reduce (overlapped on NCCL; in place over gloo), the head's
+        # gradient all-reduce -> 7 graphs
+        assert r["segments"] == 7, r
         assert r["err_out"] < 1e-4 and r["err_par"] < 1e-5 and r["err_rank"] == 0.0, r
+
+
+@pytest.mark.parametrize("precision", ["bf16"])
+def test_overlapped_grad_reduce_graphed(gpu, precision):
+    """The classifiers' gradient all-reduce runs on a side stream overlapping
+    the word<->region branch (dist.reduce_grads_async; StepCapture.cut_async /
+    join).  One process as rank 0 of 4 replicas (dist.ReplicaGroup: the
+    collectives are local, their stream ordering is the real one): the graph
+    replay, which records the side stream and the join, must give exactly the
+    eager step's losses and parameters (the tolerances of the 2-rank test)."""
+    from text_guided_face_recognition_amd.config import make_args
+    from text_guided_face_recognition_amd.dist import DistContext, ReplicaGroup
+    from text_guided_face_recognition_amd.train import GraphedStep, Train, synthetic_batch
+
+    def build():
+        torch.manual_seed(5)
+        args = make_args(batch_size=16, num_classes=300, precision=precision,
+                         bert_words_num=32)
+        return Train(args, gpu, DistContext(ReplicaGroup(4)))
+
+    batch = synthetic_batch(16, 30, gpu, seed=9, n_ids=300, bert_hidden=True)
+    eager, graphed = build(), build()
+    outs_e = [eager.step(batch) for _ in range(5)]
+    gs = GraphedStep(graphed, tuple(t.clone() for t in batch), warmup=3)
+    gs.step()
+    out_g = {k: v.clone() for k, v in gs.step().items()}
+    torch.cuda.synchronize()
+    # text gather, 2 column exchanges, focal NLL sums, classifier gradients
+    # (async) and their join, head gradients -> 8 graphs
+    assert len(gs.capture.graphs) == 8
+    for k in out_g:
+        assert (out_g[k] - outs_e[-1][k]).abs().max().item() < 1e-4, k
+    for a, b in zip(graphed.params, eager.params):
+        assert (a - b).abs().max().item() < 1e-5

@@ -48,6 +48,7 @@ class StepCapture:
         self.collectives = []
         self.pool = torch.cuda.graph_pool_handle()
         self.stream = torch.cuda.Stream()
+        self.side = torch.cuda.Stream()       # overlapped collectives (cut_async)
 
     def _begin(self):
         g = torch.cuda.CUDAGraph()
@@ -60,6 +61,35 @@ class StepCapture:
         self.graphs[-1].capture_end()
         fn()
         self.collectives.append(fn)
+        self._begin()
+
+    def cut_async(self, fn):
+        """Close the current graph; run collective `fn` on the side stream
+        (after everything captured so far) now and at every replay, so that
+        the next graphs overlap it; returns the event that join() waits on."""
+        self.graphs[-1].capture_end()
+        ev = torch.cuda.Event()
+
+        def launch():
+            cur = torch.cuda.current_stream()
+            self.side.wait_stream(cur)
+            with torch.cuda.stream(self.side):
+                fn()
+            ev.record(self.side)
+        launch()
+        self.collectives.append(launch)
+        self._begin()
+        return ev
+
+    def join(self, ev):
+        """Close the current graph; the next graphs start after `ev` (an
+        overlapped collective of cut_async) completes."""
+        self.graphs[-1].capture_end()
+
+        def wait():
+            torch.cuda.current_stream().wait_event(ev)
+        wait()
+        self.collectives.append(wait)
         self._begin()
 
     def capture(self, step, *args):
@@ -160,6 +190,30 @@ class DistContext:
             c += w
         return tuple(outs)
 
+    def reduce_grads_async(self, params):
+        """reduce_grads of `params` started now and overlapped with the work
+        that follows (a side stream; a cut of its own under StepCapture);
+        returns a handle for wait_grads.  For gradients that are final early
+        in the step (the identity heads' classifiers, after their branch's
+        backward) while the word<->region branch still runs."""
+        if not self.active:
+            return None
+        ps = [p for p in params if p.grad is not None]
+        if not ps:
+            return None
+        flat = torch.cat([p.grad.reshape(-1) for p in ps])
+        off = 0
+        for p in ps:
+            n = p.numel()
+            p.grad = flat[off:off + n].view_as(p)
+            off += n
+        return all_reduce_sum_async_(flat, self.group)
+
+    def wait_grads(self, handle):
+        """Order the current stream after a reduce_grads_async."""
+        if handle is not None:
+            _join(handle)
+
     def reduce_grads(self, params):
         """Sum the gradients of `params` over ranks in one all-reduce of a flat
         buffer (the DDP replacement: losses are pre-weighted so that the SUM is
@@ -244,6 +298,45 @@ def all_reduce_sum_(t, group=None):
             dist.all_reduce(t, group=group)
     _run_or_cut(run)
     return t
+
+
+_SIDE = {}
+
+
+def all_reduce_sum_async_(t, group=None):
+    """In-place SUM all-reduce started on a side stream after the current
+    stream's work (capture-aware: StepCapture.cut_async); returns the event
+    to join.  gloo (CPU tests) stages through host memory synchronously."""
+    replica = isinstance(group, ReplicaGroup)
+    if not replica and dist.get_backend(group) == "gloo":
+        all_reduce_sum_(t, group)
+        return None
+
+    def run():
+        if replica:
+            t.mul_(group.world)
+        else:
+            dist.all_reduce(t, group=group)
+    if _CAPTURE is not None:
+        return _CAPTURE.cut_async(run)
+    dev = torch.cuda.current_device()
+    side = _SIDE.setdefault(dev, torch.cuda.Stream())
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        run()
+    ev = torch.cuda.Event()
+    ev.record(side)
+    t.record_stream(side)
+    return ev
+
+
+def _join(ev):
+    if ev is None:
+        return
+    if _CAPTURE is not None:
+        _CAPTURE.join(ev)
+    else:
+        torch.cuda.current_stream().wait_event(ev)
 
 
 def init_from_env(backend=None):

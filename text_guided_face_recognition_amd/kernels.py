@@ -22,10 +22,12 @@ MODES = {"bf16": 0, "fp32": 1, "fp16": 2}
 
 
 def _mode(mode):
-    """C-ABI precision of the generic kernels: "fp16" (the word-region
-    contraction in fp16, BASELINE config 5) runs everything else in bf16."""
+    """C-ABI precision of the generic kernels: "fp16" (BASELINE config 5's
+    "fp16 with fp32 contrastive accumulate": the word-region contraction on
+    fp16 MFMAs) runs the generic GEMMs in the fp32 split mode; the fused IMIM
+    and TextHeading kernels run bf16 (models/models.py)."""
     try:
-        return MODES["bf16"] if mode == "fp16" else MODES[mode]
+        return min(MODES[mode], MODES["fp32"])
     except KeyError:
         raise ValueError(f"precision mode must be one of {sorted(MODES)}") from None
 

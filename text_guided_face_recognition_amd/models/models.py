@@ -138,13 +138,17 @@ class TextHeading(nn.Module):
         self.precision = getattr(args, "precision", "fp32")
         self._taps = None          # (key, packed tap planes)
 
+    def _conv_mode(self):
+        # fp16 mode: bf16 convs (the words are normalised, then rounded to fp16)
+        return "bf16" if self.precision == "fp16" else self.precision
+
     def packed_taps(self):
         """The conv weights as tap-major bf16 planes, re-packed only when a
         weight tensor is replaced or modified in place (its version moves)."""
         ws = [c.weight for c in self.bwm.convs1]
-        key = (self.precision,) + tuple((w.data_ptr(), w._version) for w in ws)
+        key = (self._conv_mode(),) + tuple((w.data_ptr(), w._version) for w in ws)
         if self._taps is None or self._taps[0] != key:
-            self._taps = (key, K.text_pack(ws, mode=self.precision))
+            self._taps = (key, K.text_pack(ws, mode=self._conv_mode()))
         return self._taps[1]
 
     def forward(self, words_emb, sent_emb=None):
@@ -164,6 +168,6 @@ class TextHeading(nn.Module):
             n = words_emb.shape[1] - 1
             spec = (K.TPAD if n <= K.TPAD else 2 * K.TPAD, K.LOG2E, self.precision == "fp16")
         words, sent = K.text_heading(words_emb, self.packed_taps(),
-                                     [c.bias for c in self.bwm.convs1], mode=self.precision,
+                                     [c.bias for c in self.bwm.convs1], mode=self._conv_mode(),
                                      rows_spec=spec)
         return words.transpose(1, 2), sent

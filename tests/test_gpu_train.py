@@ -46,3 +46,41 @@ def test_fusion_step(gpu):
         last = tr.step(batch)["loss"].item()
     assert torch.isfinite(torch.tensor([first, last])).all()
     assert last < first        # the FCFM head learns the fixed batch
+
+
+def test_plain_torch_graph_capture(gpu):
+    """The standard PyTorch recipe -- torch.cuda.graph on its own capture
+    stream, no dist.StepCapture -- captures kernels that use the in-launch
+    counters (the single-rank contrastive CE's last-arriver loss block): the
+    counter buffer is made inside the capture and re-zeroed by the graph, and
+    replays reproduce eager losses and gradients."""
+    import torch.nn.functional as F  # noqa: F401
+    from text_guided_face_recognition_amd import kernels as K
+    torch.manual_seed(2)
+    unit = lambda x: x / x.norm(dim=-1, keepdim=True)  # noqa: E731
+    r = unit(torch.randn(12, 14, 14, 256, device=gpu)).permute(0, 3, 1, 2).requires_grad_()
+    w = unit(torch.randn(12, 30, 256, device=gpu))
+    lens = torch.full((12,), 30, dtype=torch.int32, device=gpu)
+
+    def step():
+        r.grad = None
+        logits = K.word_region_logits(r, w, lens, 4.0, 5.0, 10.0, mode="bf16", bounded=True)
+        l0, l1 = K.contrastive_ce(logits)
+        (l0 + l1).backward()
+        return (l0 + l1).detach()
+    ref = step()
+    ref_g = r.grad.clone()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    r.grad = None
+    with torch.cuda.graph(g):
+        out = step()
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert torch.equal(r.grad, ref_g)

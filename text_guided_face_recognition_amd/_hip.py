@@ -197,16 +197,17 @@ def counters(device):
     and every kernel leaves the words it used at zero again, so the calls of a
     stream share its buffer, while kernels of different streams never share
     a word.
-    A stream's buffer is made eagerly on first use; a stream that is being
-    captured into a HIP graph must have been given its buffer before the
-    capture began (dist.StepCapture does this for its capture stream)."""
+    A stream's buffer is made on first use.  First used inside a HIP graph
+    capture (e.g. plain torch.cuda.graph, whose capture stream is its own),
+    the buffer comes from that graph's memory pool and its zeroing is a node
+    of the graph, so every replay starts from zeroed words; it then belongs to
+    that capture (dist.StepCapture makes its stream's buffer before capturing,
+    so its graphs carry no such node)."""
     dev = torch.device(device)
     stream = torch.cuda.current_stream(dev)
     key = (dev.index, stream.cuda_stream)
     buf = _counters.get(key)
     if buf is None:
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("tgfr counters for a stream first used inside a graph capture")
         buf = torch.zeros(N_COUNTERS, dtype=torch.int32, device=dev)
         _counters[key] = buf
     return buf

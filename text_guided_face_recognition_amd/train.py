@@ -161,8 +161,8 @@ class Train:
                  (1, 1, 1, 1, 0, 0, 0),                               # damsm
                  (0, 0, 0, 0, 1, 0, 0),                               # clip
                  (0, 0, 0, 0, 0, wi, wi)])                            # ident
-        ctx.reduce_grads(self.head_params)
         ctx.wait_grads(pending)
+        ctx.reduce_grads(self.head_params)
         self.optimizer.step()
         return {"damsm": report[0], "clip": report[1], "ident": report[2]}
 

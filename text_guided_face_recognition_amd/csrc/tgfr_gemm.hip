@@ -527,18 +527,23 @@ __global__ __launch_bounds__(64 * WR_NW) void bgemm_wres_kernel(
     wres_load_b<K, false>(B, sBk, sBn, n0, N, tid);
 
   constexpr int NJ = WR_TN / 32 / (WR_NW / 2);          // 32-col tiles per wave
+  // The products are formed transposed, C^T = B^T A^T (the weights as the
+  // MFMA's A operand): a lane then holds, per accumulator quad, 4 consecutive
+  // output columns of ONE row, so the epilogue stores 8-byte (bf16) or 16-byte
+  // (fp32) row pieces instead of one 2- / 4-byte element per register.
   f32x16 acc[NJ];
-  // the epilogue's bias values, loaded once: no plain global load may sit in
-  // the loop beside the DMA ring (hipcc would drain the ring with vmcnt(0)
-  // before every use of it)
-  float bcol[NJ];
+  // the epilogue's bias values (column n = 8 g + 4 h + i of the wave's tile
+  // j), loaded once: no plain global load may sit in the loop beside the DMA
+  // ring (hipcc would drain the ring with vmcnt(0) before every use of it)
+  float bcol[NJ][16];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int n = n0 + wn * 32 * NJ + 32 * j + (lane & 31);
-    bcol[j] = bias && n < N ? bias[n] : 0.f;
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
-  }
+    for (int q = 0; q < 16; ++q) {
+      const int n = n0 + wn * 32 * NJ + 32 * j + acc_row(q, lane >> 5);
+      bcol[j][q] = bias && n < N ? bias[n] : 0.f;
+      acc[j][q] = 0.f;
+    }
 
   for (int t = 0; t < T; ++t) {
     // stage t has landed once at most NS-2 younger stages (and the stores of
@@ -559,25 +564,41 @@ __global__ __launch_bounds__(64 * WR_NW) void bgemm_wres_kernel(
       for (int j = 0; j < NJ; ++j) {
         const int nl = wn * 32 * NJ + 32 * j + (lane & 31);
         const bf16x8 bh = as_bf8(lds_ld16(wres_off(nl, c, K)));
-        mma<MODE_BF16>(acc[j], ah, al, bh, bh);
+        mma<MODE_BF16>(acc[j], bh, bh, ah, al);          // C^T tile (see above)
       }
     }
     if (kt == NK - 1) {
       const int m0 = (g + (t / NK) * per_slice) * WR_TM;
+      const int m = m0 + wm * 32 + (lane & 31);
+      // 4-column pieces as one store when rows are 16-B aligned
+      const bool vec = sCn == 1 && (sCm & 3) == 0 && (((uintptr_t)Cm & 15) == 0);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int n = n0 + wn * 32 * NJ + 32 * j + (lane & 31);
-        if (n < N) {
 #pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const int m = m0 + wm * 32 + acc_row(q, lane >> 5);
-            float v = alpha * acc[j][q] + bcol[j];
-            v = relu ? fmaxf(v, 0.f) : v;
-            if (m < M) {
+        for (int gq = 0; gq < 4; ++gq) {
+          const int nb = n0 + wn * 32 * NJ + 32 * j + 8 * gq + 4 * (lane >> 5);
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[i] = alpha * acc[j][4 * gq + i] + bcol[j][4 * gq + i];
+            v[i] = relu ? fmaxf(v[i], 0.f) : v[i];
+          }
+          if (m < M) {
+            if (vec && nb + 3 < N) {
               if constexpr (OBF)
-                ((uint16_t*)Cm)[m * sCm + n * sCn] = bf_bits(v);   // bf16 output image
+                *(uint2*)((uint16_t*)Cm + m * sCm + nb) =
+                    make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
               else
-                Cm[m * sCm + n * sCn] = v;
+                *(float4*)(Cm + m * sCm + nb) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                if (nb + i >= N) continue;
+                if constexpr (OBF)
+                  ((uint16_t*)Cm)[m * sCm + (nb + i) * sCn] = bf_bits(v[i]);
+                else
+                  Cm[m * sCm + (nb + i) * sCn] = v[i];
+              }
             }
           }
         }

@@ -140,20 +140,28 @@ __device__ __forceinline__ void dma_tile(const uint16_t* X, long long ld, int ro
   }
 }
 
-// Forward: one 2-wave workgroup per (sample, pair of query tiles), online
-// softmax over the key tiles in a ROLLED loop (a fully unrolled run-once
-// kernel of ~40 KB spent its time on instruction-cache misses).  The Kr and
-// V tiles stream, interleaved, through a DMA ring shared by both waves.
+// Forward: one 4-wave workgroup per (sample, pair of query tiles); wave w
+// takes query tile 2 j + (w & 1) over key half w >> 1 (tiles [0, nh) or
+// [nh, nt), nh = ceil(nt / 2)), so every SIMD of the CU holds a wave (the
+// 2-wave version left half of them idle: 448 waves on 1024 SIMDs at B = 64)
+// and each wave's serial chain of key tiles is half as long.  Online softmax
+// over the wave's key tiles in a ROLLED loop (a fully unrolled run-once kernel
+// of ~40 KB spent its time on instruction-cache misses); at the end the key
+// half 1 waves hand (m, l, O) to their half-0 partners through LDS, which
+// combine the two partial softmaxes and write O and the row LSE.
 // Per key tile: S^T = Kr Qr^T (lane = query, so the running max / sum are
 // per lane plus one cross-half combine), then O^T += V^T P^T with P^T the
 // accumulator as it stands (k axis in the accumulator's key order, V read
 // transposed in the same order) -- O^T keeps the query on the lane too, so the
 // online-softmax rescale is one scalar per lane.
-// LDS: [0, 2 IMG) the waves' Qr tiles, then the ring.
-constexpr int FWD_NS = 7;
-constexpr int FWD_LDS = (2 + FWD_NS) * IMG;
+// LDS: [0, 2 IMG) the query tiles, then a 2-deep ring of stages; stage i =
+// Kr, V of key tile i (half 0) and of key tile nh + i (half 1), each wave
+// DMA-ing a quarter of every tile.
+constexpr int FWD_STAGE = 4 * IMG;
+constexpr int FWD_LDS = 2 * IMG + 2 * FWD_STAGE;       // 160 KiB
+constexpr int FWD_XCH = 8 * 16 + 2;                    // floats per lane handed over
 
-__global__ __launch_bounds__(128) void attn_fwd_kernel(const uint16_t* __restrict__ Qp,
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ Qp,
                                                        const uint16_t* __restrict__ Kp,
                                                        const uint16_t* __restrict__ Vp,
                                                        long long ld, long long sb, int hw,
@@ -161,23 +169,31 @@ __global__ __launch_bounds__(128) void attn_fwd_kernel(const uint16_t* __restric
                                                        long long ldo, long long sbo,
                                                        float* __restrict__ lse) {
   const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE, lr = lane & 31, h = lane >> 5;
-  const int nt = (hw + 31) / 32, np = (nt + 1) / 2;
+  const int qsel = w & 1, half = w >> 1;
+  const int nt = (hw + 31) / 32, np = (nt + 1) / 2, nh = (nt + 1) / 2;
   // the workgroups of one sample run on one XCD (its Kr / V stay in that L2)
   const int wid = xcd_remap(blockIdx.x, gridDim.x);
-  const int b = wid / np, qt = 2 * (wid % np) + w;
+  const int b = wid / np, qt = 2 * (wid % np) + qsel;
   const bool active = qt < nt;                       // uniform per wave
-  const uint32_t qimg = w * IMG, ring = 2 * IMG;
-  const int n_st = 2 * nt;                           // stages: Kr 0, V 0, Kr 1, V 1, ...
-  auto issue = [&](int st) {
-    const uint16_t* X = ((st & 1) ? Vp : Kp) + b * sb;
-    dma_tile(X, ld, 32 * (st >> 1), hw, ring + (st % FWD_NS) * IMG, w, 2, lane);
+  const uint32_t qimg = qsel * IMG, ring = 2 * IMG;
+  const int iters = nh;                              // half 0 has nh tiles, half 1 nt - nh
+  auto issue = [&](int i) {                          // stage i -> ring slot i % 2
+    const uint32_t base = ring + (i & 1) * FWD_STAGE;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int kt = u ? nh + i : i;
+      const int n = kt < nt ? hw : 0;                // a missing half-1 tile: zeros
+      dma_tile(Kp + b * sb, ld, 32 * kt, n, base + (2 * u) * IMG, w, 4, lane);
+      dma_tile(Vp + b * sb, ld, 32 * kt, n, base + (2 * u + 1) * IMG, w, 4, lane);
+    }
   };
-  // stage st has landed (this wave's pieces) and every wave got here
-  auto wait = [&](int st) { ring_wait8(min(FWD_NS - 2, n_st - 1 - st)); };
-  dma_tile(Qp + b * sb, ld, 32 * qt, active ? hw : 0, qimg, 0, 1, lane);
-  for (int st = 0; st < FWD_NS - 1 && st < n_st; ++st) issue(st);
-  wait(0);                                           // also covers the Qr tile
-  if (FWD_NS - 1 < n_st) issue(FWD_NS - 1);
+  // the query tiles (this wave's quarter of both), then stage 0
+  dma_tile(Qp + b * sb, ld, 32 * (2 * (wid % np)), hw, 0, w, 4, lane);
+  dma_tile(Qp + b * sb, ld, 32 * (2 * (wid % np) + 1), 2 * (wid % np) + 1 < nt ? hw : 0, IMG, w,
+           4, lane);
+  issue(0);
+  ring_barrier<0>();
+  if (iters > 1) issue(1);
   bf16x8 qf[AD / 16];
 #pragma unroll
   for (int s = 0; s < AD / 16; ++s) qf[s] = frag(qimg, s, lane);
@@ -189,13 +205,19 @@ __global__ __launch_bounds__(128) void attn_fwd_kernel(const uint16_t* __restric
   for (int t = 0; t < AD / 32; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[t][r] = 0.f;
-  for (int kt = 0; kt < nt; ++kt) {
-    const int sk = 2 * kt;
-    if (kt > 0) {
-      wait(sk);
-      if (sk + FWD_NS - 1 < n_st) issue(sk + FWD_NS - 1);
+  for (int i = 0; i < iters; ++i) {
+    if (i > 0) {
+      // stage i landed (16 pieces per wave per stage: stage i+1 may still fly)
+      if (i + 1 < iters) {
+        ring_barrier<0>();
+        issue(i + 1);
+      } else {
+        ring_barrier<0>();
+      }
     }
-    const uint32_t kbuf = ring + (sk % FWD_NS) * IMG;
+    const int kt = half ? nh + i : i;
+    if (kt >= nt) continue;                          // uniform per wave (half 1, odd nt)
+    const uint32_t kbuf = ring + (i & 1) * FWD_STAGE + (2 * half) * IMG, vbuf = kbuf + IMG;
     f32x16 sc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) sc[r] = 0.f;
@@ -216,7 +238,7 @@ __global__ __launch_bounds__(128) void attn_fwd_kernel(const uint16_t* __restric
     // max exceeds it by more than 8 / c (P then stays <= 2^8, exact in the
     // fp32 sums and fine in bf16); otherwise O and l keep their scale and the
     // 128-register rescale of O is skipped
-    if (kt == 0) {
+    if (i == 0) {
       m = tmax;
     } else if (__builtin_amdgcn_ballot_w64((tmax - m) * c > 8.f)) {
       const float mn = fmaxf(m, tmax);
@@ -242,9 +264,6 @@ __global__ __launch_bounds__(128) void attn_fwd_kernel(const uint16_t* __restric
                                  pk_bf16(sc[8 * s2 + 2], sc[8 * s2 + 3]),
                                  pk_bf16(sc[8 * s2 + 4], sc[8 * s2 + 5]),
                                  pk_bf16(sc[8 * s2 + 6], sc[8 * s2 + 7])));
-    wait(sk + 1);
-    if (sk + FWD_NS < n_st) issue(sk + FWD_NS);
-    const uint32_t vbuf = ring + ((sk + 1) % FWD_NS) * IMG;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -254,20 +273,40 @@ __global__ __launch_bounds__(128) void attn_fwd_kernel(const uint16_t* __restric
       }
   }
   l = xhalf_sum(l);
-  if (!active) return;
+  // key half 1 -> its half-0 partner (same query tile) through the ring area
+  __syncthreads();                                   // every wave is done with the ring
+  const uint32_t xch = ring + (uint32_t)(qsel * 64 + lane) * FWD_XCH * 4;
+  if (half == 1) {
+#pragma unroll
+    for (int t = 0; t < AD / 32; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) lds_stf(xch + (16 * t + r) * 4, oacc[t][r]);
+    lds_stf(xch + 128 * 4, m);
+    lds_stf(xch + 129 * 4, l);
+  }
+  __syncthreads();
+  if (half == 1 || !active) return;
+  const float m1 = lds_ldf(xch + 128 * 4), l1 = lds_ldf(xch + 129 * 4);
+  const float mm = fmaxf(m, m1);
+  const float a0 = __builtin_amdgcn_exp2f((m - mm) * c);
+  const float a1 = m1 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m1 - mm) * c);
+  const float lt = l * a0 + l1 * a1;
   const int q = 32 * qt + lr;
   if (q >= hw) return;
-  if (h == 0) lse[(long long)b * hw + q] = m * scale + __logf(l);
-  const float inv = 1.f / l;
+  if (h == 0) lse[(long long)b * hw + q] = mm * scale + __logf(lt);
+  const float i0 = a0 / lt, i1 = a1 / lt;
   // lane: query q; register r of tile t: column 32 t + acc_row(r, h)
   float* orow = O + b * sbo + (long long)q * ldo;
 #pragma unroll
   for (int t = 0; t < AD / 32; ++t)
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
-      *(float4*)(orow + 32 * t + 8 * g + 4 * h) =
-          make_float4(oacc[t][4 * g] * inv, oacc[t][4 * g + 1] * inv, oacc[t][4 * g + 2] * inv,
-                      oacc[t][4 * g + 3] * inv);
+    for (int g = 0; g < 4; ++g) {
+      float v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        v[k] = oacc[t][4 * g + k] * i0 + lds_ldf(xch + (16 * t + 4 * g + k) * 4) * i1;
+      *(float4*)(orow + 32 * t + 8 * g + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
+    }
 }
 
 // D[row] = sum_c dO[row][c] O[row][c] and dO in bf16 (the backward's operand);
@@ -405,62 +444,83 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(
     }
 }
 
-// dQr = dS Kr: one 2-wave workgroup per (sample, pair of query tiles), the Kr
-// tiles through a DMA ring (rolled loop); each wave's dS rows are staged in
-// LDS first (464-B rows: conflict-free ds_read_b128).
+// dQr = dS Kr: one 4-wave workgroup per (sample, pair of query tiles); wave w
+// computes query tile 2 j + (w & 1), output columns [128 (w >> 1), +128) -- all
+// four SIMDs busy (the 2-wave version, one query tile per wave, left two idle)
+// and half the MFMA chain per wave.  The Kr tiles stream through a DMA ring
+// (rolled loop); each query tile's dS rows are staged in LDS first by its two
+// waves (464-B rows: conflict-free ds_read_b128).
 constexpr int Q_NS = 7;
 constexpr int DS_PITCH = 464;
 constexpr int Q_LDS = Q_NS * IMG + 2 * 32 * DS_PITCH;
 
-__global__ __launch_bounds__(128) void attn_bwd_q_kernel(const uint16_t* __restrict__ Kp,
+// ring_wait8 for rings of 4 pieces per wave per stage
+__device__ __forceinline__ void ring_wait4(int younger) {
+  switch (younger) {
+    case 0: ring_barrier<0>(); break;
+    case 1: ring_barrier<4>(); break;
+    case 2: ring_barrier<8>(); break;
+    case 3: ring_barrier<12>(); break;
+    case 4: ring_barrier<16>(); break;
+    case 5: ring_barrier<20>(); break;
+    default: ring_barrier<24>(); break;
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_q_kernel(const uint16_t* __restrict__ Kp,
                                                          long long ld, long long sb, int hw,
                                                          const uint16_t* __restrict__ dS,
                                                          uint16_t* __restrict__ dQ, long long ldg,
                                                          long long sbg) {
   const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE, lr = lane & 31, h = lane >> 5;
+  const int qsel = w & 1, dh = w >> 1;
   const int nt = (hw + 31) / 32, kp = 32 * nt, np = (nt + 1) / 2;
   const int wid = xcd_remap(blockIdx.x, gridDim.x);
-  const int b = wid / np, qt = 2 * (wid % np) + w;
+  const int b = wid / np, qt = 2 * (wid % np) + qsel;
   const uint16_t* Kb = Kp + b * sb;
-  const uint32_t dsimg = Q_NS * IMG + w * 32 * DS_PITCH;
-  // this wave's 32 dS rows (kp bf16 each) -> LDS; plain loads, drained before
-  // the ring starts so its counted waits see only DMA
-  for (int i = lane; i < 32 * (kp / 8); i += 64) {
+  const uint32_t dsimg = Q_NS * IMG + qsel * 32 * DS_PITCH;
+  // the query tile's 32 dS rows (kp bf16 each) -> LDS, half by each of its
+  // two waves; plain loads, drained before the ring starts so its counted
+  // waits see only DMA (the first ring wait publishes the rows)
+  for (int i = lane + 64 * dh; i < 32 * (kp / 8); i += 128) {
     const int r = i / (kp / 8), c8 = i % (kp / 8), q = 32 * qt + r;
     const uint4 v = q < hw ? *(const uint4*)(dS + ((long long)b * hw + q) * kp + 8 * c8)
                            : make_uint4(0, 0, 0, 0);
     lds_st16(dsimg + r * DS_PITCH + 16 * c8, v);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  f32x16 acc[AD / 32];
+  constexpr int NTD = AD / 32 / 2;                   // d tiles per wave
+  f32x16 acc[NTD];
 #pragma unroll
-  for (int t = 0; t < AD / 32; ++t)
+  for (int t = 0; t < NTD; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   for (int st = 0; st < Q_NS - 1 && st < nt; ++st)
-    dma_tile(Kb, ld, 32 * st, hw, st * IMG, w, 2, lane);
+    dma_tile(Kb, ld, 32 * st, hw, st * IMG, w, 4, lane);
   for (int kt = 0; kt < nt; ++kt) {
-    ring_wait8(min(Q_NS - 2, nt - 1 - kt));
+    ring_wait4(min(Q_NS - 2, nt - 1 - kt));
     if (kt + Q_NS - 1 < nt)
-      dma_tile(Kb, ld, 32 * (kt + Q_NS - 1), hw, ((kt + Q_NS - 1) % Q_NS) * IMG, w, 2, lane);
+      dma_tile(Kb, ld, 32 * (kt + Q_NS - 1), hw, ((kt + Q_NS - 1) % Q_NS) * IMG, w, 4, lane);
     const uint32_t buf = (kt % Q_NS) * IMG;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 a = as_bf8(lds_ld16(dsimg + lr * DS_PITCH + 2 * (32 * kt + 16 * s2 + 8 * h)));
 #pragma unroll
-      for (int t = 0; t < AD / 32; ++t) {
-        const bf16x8 kb = trf(buf, 16 * s2 + 8 * h, 16 * s2 + 8 * h + 4, 32 * t, lane);
+      for (int t = 0; t < NTD; ++t) {
+        const bf16x8 kb =
+            trf(buf, 16 * s2 + 8 * h, 16 * s2 + 8 * h + 4, 32 * (NTD * dh + t), lane);
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, kb, acc[t], 0, 0, 0);
       }
     }
   }
   if (qt >= nt) return;
 #pragma unroll
-  for (int t = 0; t < AD / 32; ++t)
+  for (int t = 0; t < NTD; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qq = 32 * qt + acc_row(r, h);
-      if (qq < hw) dQ[b * sbg + (long long)qq * ldg + 32 * t + lr] = bf_bits(acc[t][r]);
+      if (qq < hw)
+        dQ[b * sbg + (long long)qq * ldg + 32 * (NTD * dh + t) + lr] = bf_bits(acc[t][r]);
     }
 }
 
@@ -495,7 +555,7 @@ int tgfr_attn_fwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long 
   if (((uintptr_t)Q | (uintptr_t)K | (uintptr_t)V | (uintptr_t)O) & 15) return 1001;
   const int np = ((hw + 31) / 32 + 1) / 2;
   if (const int e = set_max_lds((const void*)attn_fwd_kernel, FWD_LDS)) return e;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * np), dim3(128), FWD_LDS, (hipStream_t)stream, Q, K,
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * np), dim3(256), FWD_LDS, (hipStream_t)stream, Q, K,
                      V, ld, sb, hw, scale, O, ldo, sbo, lse);
   return (int)hipGetLastError();
 }
@@ -533,7 +593,7 @@ int tgfr_attn_bwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long 
   hipLaunchKernelGGL(attn_bwd_kv_kernel, dim3(B * np), dim3(256), KV_LDS, s, Q, K, V, ld, sb, hw,
                      scale, dOb, lse, D, dK, dV, ldg, sbg, dS);
   if (const int e = set_max_lds((const void*)attn_bwd_q_kernel, Q_LDS)) return e;
-  hipLaunchKernelGGL(attn_bwd_q_kernel, dim3(B * np), dim3(128), Q_LDS, s, K, ld, sb, hw, dS, dQ,
+  hipLaunchKernelGGL(attn_bwd_q_kernel, dim3(B * np), dim3(256), Q_LDS, s, K, ld, sb, hw, dS, dQ,
                      ldg, sbg);
   return (int)hipGetLastError();
 }

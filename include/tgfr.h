@@ -406,7 +406,7 @@ int tgfr_bn_fold(const float* W, const float* b, int O, int C, const float* gamm
                  const float* beta, float* Wf, float* bf, void* stream);
 /* From G = dY^T xhat [O][C] and s = colsum(dY) [O]: dW = G diag(gamma) +
  * s beta^T, dgamma = sum_o W .* G, dbeta = sum_o W .* s (fixed-order sums).
- * ws: 2 * ceil(O / 64) * C floats; counters: ceil(C / 64) zeroed words. */
+ * ws: 2 * ceil(O / 16) * C floats; counters: ceil(C / 64) zeroed words. */
 int tgfr_bn_unfold(const float* G, const float* s, const float* W, int O, int C,
                    const float* gamma, const float* beta, float* dW, float* dgamma, float* dbeta,
                    float* ws, unsigned* counters, void* stream);

@@ -171,10 +171,12 @@ __global__ __launch_bounds__(256) void bn_fold_kernel(Parts P, int O, int C,
   if (lane == 0) bf[o] = P.bias(o) + acc;
 }
 
-// grid (ceil(C / 64), ceil(O / 64)); block = 64 columns x 4 row lanes over a
-// 64-row chunk.  dW is elementwise; the dgamma / dbeta column partials of the
-// chunks are combined by the last chunk of each column group (chunk order).
-constexpr int UF_ROWS = 64;
+// grid (ceil(C / 64), ceil(O / 16)); block = 64 columns x 4 row lanes over a
+// 16-row chunk (192 workgroups at O = 768: the 64-row chunks of round 2 put 48
+// on the chip, latency-bound at 13 us for 0.8 MB).  dW is elementwise; the
+// dgamma / dbeta column partials of the chunks are combined by the last chunk
+// of each column group (chunk order, loads of 8 chunks in flight).
+constexpr int UF_ROWS = 16;
 __global__ __launch_bounds__(256) void bn_unfold_kernel(
     const float* __restrict__ G, const float* __restrict__ s, Parts W, int O,
     int C, const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dW,
@@ -207,6 +209,7 @@ __global__ __launch_bounds__(256) void bn_unfold_kernel(
   if (!last_arrival(counters + blockIdx.x, gridDim.y, (int*)&red[512])) return;
   if (ry == 0 && c < C) {
     float a = 0.f, b = 0.f;
+#pragma unroll 8
     for (int k = 0; k < (int)gridDim.y; ++k) {
       a += part[((long long)k * C + c) * 2];
       b += part[((long long)k * C + c) * 2 + 1];
@@ -262,7 +265,7 @@ int tgfr_bn_fold3(const float* const* W, const float* const* b, int rows, int C,
   return (int)hipGetLastError();
 }
 
-// ws: 2 * ceil(O / 64) * C floats; counters: ceil(C / 64) zeroed words.
+// ws: 2 * ceil(O / 16) * C floats; counters: ceil(C / 64) zeroed words.
 static int bn_unfold_launch(const float* G, const float* s, const Parts& W, int O, int C,
                             const float* gamma, const float* beta, float* dW, float* dgamma,
                             float* dbeta, float* ws, unsigned* counters, void* stream) {

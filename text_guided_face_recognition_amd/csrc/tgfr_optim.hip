@@ -112,9 +112,36 @@ __global__ __launch_bounds__(THREADS) void optim_step_kernel(Args a, const float
   const bool adam = G.kind == TGFR_OPTIM_ADAM;
   const bool has_s0 = adam || G.momentum != 0.f;
   const long long base = (long long)(b - a.bstart[s]) * VEC_PER_BLOCK * 4;
+  constexpr int J = VEC_PER_BLOCK / THREADS;
+  if (sg.vec && base + 4LL * VEC_PER_BLOCK <= sg.n) {
+    // a whole block of float4 items: every load first (the stores to p could
+    // alias the next item's loads as far as the compiler knows, which
+    // serialised four HBM round trips per block), then update and store
+    float4 p[J], g[J], m[J], v[J];
 #pragma unroll
-  for (int j = 0; j < VEC_PER_BLOCK / THREADS; ++j)
-    update_vec(sg, base + 4LL * (j * THREADS + threadIdx.x), adam, has_s0, G, c);
+    for (int j = 0; j < J; ++j) {
+      const long long e0 = base + 4LL * (j * THREADS + threadIdx.x);
+      p[j] = *(const float4*)(sg.p + e0);
+      g[j] = *(const float4*)(sg.g + e0);
+      m[j] = has_s0 ? *(const float4*)(sg.s0 + e0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[j] = adam ? *(const float4*)(sg.s1 + e0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const long long e0 = base + 4LL * (j * THREADS + threadIdx.x);
+      update(p[j].x, g[j].x, m[j].x, v[j].x, G, c);
+      update(p[j].y, g[j].y, m[j].y, v[j].y, G, c);
+      update(p[j].z, g[j].z, m[j].z, v[j].z, G, c);
+      update(p[j].w, g[j].w, m[j].w, v[j].w, G, c);
+      *(float4*)(sg.p + e0) = p[j];
+      if (has_s0) *(float4*)(sg.s0 + e0) = m[j];
+      if (adam) *(float4*)(sg.s1 + e0) = v[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      update_vec(sg, base + 4LL * (j * THREADS + threadIdx.x), adam, has_s0, G, c);
+  }
   // The last block to arrive advances the step count.  Every block read it
   // at its start; nothing else is published, so the arrival needs no release
   // fence (an agent-scope release per block would write back L2 each time).

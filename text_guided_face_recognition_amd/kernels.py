@@ -841,7 +841,7 @@ def _bn_unfold(ctx, gm, s):
     dw = torch.empty(o, c, dtype=torch.float32, device=dev)
     dgamma = torch.empty(c, dtype=torch.float32, device=dev)
     dbeta = torch.empty_like(dgamma)
-    uws = torch.empty(2 * -(-o // 64) * c, dtype=torch.float32, device=dev)
+    uws = torch.empty(2 * -(-o // 16) * c, dtype=torch.float32, device=dev)
     if isinstance(w2, tuple):
         rows = w2[0].shape[0]
         wp = (ctypes.c_void_p * 3)(*[ptr(t) for t in w2])

@@ -1054,12 +1054,17 @@ class ImimTail(torch.autograd.Function):
         ctx.cfg = (float(eps), shape, w1.shape, w2.shape)
         out = r.reshape(*shape[:-1], _TAIL_D)
         if rows_spec:
+            # (no zero-filled gradients for the operand rows: that was a 7 MB
+            # fill kernel per step)
             ctx.mark_non_differentiable(rr, rn)
+            ctx.set_materialize_grads(False)
             return out, rr, rn
         return out
 
     @staticmethod
     def backward(ctx, dr, *unused):
+        if dr is None:                       # (grads not materialised: nothing flows)
+            return (None,) * 9
         r, inv, pk, zb, h1, h2 = ctx.saved_tensors
         eps, shape, w1shape, w2shape = ctx.cfg
         rows, dev = r.shape[0], r.device

@@ -270,6 +270,27 @@ int tgfr_attn_bwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long 
                   long long ldo, long long sbo, const float* lse, uint16_t* dQ, uint16_t* dK,
                   uint16_t* dV, long long ldg, long long sbg, void* ws, void* stream);
 
+/* Fused small attention for FCFM's cross-attention (fusion_nets.py:93-118 as
+ * called at :248 with SelfAttention(36, scale=1): HW = C' = C = 36), one
+ * workgroup per sample, exact fp32.  Replaces the composed QK^T / softmax /
+ * PV (tgfr_bgemm + tgfr_attn_softmax) for HW <= 64.
+ * X [B][hw][*] fp32 rows (sample stride sxn, row stride sxr) hold Qr at
+ * columns [0, cq) and V at [cv, cv + c); Y (NULL = X) holds Kr at
+ * [ck, ck + cq).  O [B][hw][c] (son, sor) = softmax(scale Qr Kr^T) V;
+ * P [B][hw][hw] dense, saved for the backward.
+ * The backward overwrites dQr / dV in dX's columns [0, cq) / [cv, cv + c)
+ * and dKr in dY's [ck, ck + cq) (dY NULL = dX; the three ranges must then
+ * be disjoint).  1001 on a shape that does not fit. */
+int tgfr_attn_small_fwd(const float* X, long long sxn, long long sxr, const float* Y,
+                        long long syn, long long syr, int B, int hw, int cq, int ck, int cv,
+                        int c, float scale, float* O, long long son, long long sor, float* P,
+                        void* stream);
+int tgfr_attn_small_bwd(const float* X, long long sxn, long long sxr, const float* Y,
+                        long long syn, long long syr, int B, int hw, int cq, int ck, int cv,
+                        int c, float scale, const float* P, const float* dO, long long sdn,
+                        long long sdr, float* dX, long long sgn, long long sgr, float* dY,
+                        long long skn, long long skr, void* stream);
+
 /* y = x / max(|x|, eps) per row (F.normalize; ProjectionHead models/models.py:119,
  * ArcMarginProduct models/metrics.py:44); inv_norm[row] = 1 / max(|x|, eps). */
 int tgfr_l2norm_rows(const float* x, long long ldx, int rows, int d, float eps, float* y,

@@ -132,3 +132,61 @@ def test_func_attention_attn_grad(gpu):
         outs.append((w.detach(), a.detach(), qq.grad, cc.grad))
     for x, y in zip(*outs):
         assert float((x - y).abs().max() / y.abs().max()) < 1e-4
+
+
+@pytest.mark.parametrize("nb,hw,cq,c,cross", [
+    (256, 36, 36, 36, True), (3, 36, 36, 36, False), (2, 49, 8, 20, True), (5, 64, 64, 64, False),
+    (4, 5, 3, 7, True), (1, 1, 1, 1, False), (2, 65, 16, 16, True)])
+def test_small_attention(nb, hw, cq, c, cross):
+    """kernels.attention_core at FCFM sizes (HW <= 64: the fused
+    tgfr_attn_small_fwd / _bwd, exact fp32; HW = 65 takes the composed path)
+    against fp32 autograd on the GPU: 1e-5 of max on O and on each gradient
+    slice; packed gradients must leave no column unwritten."""
+    torch.backends.cuda.matmul.allow_tf32 = False
+    g = torch.Generator(device="cuda").manual_seed(hw * 100 + cq)
+    if cross:
+        px = torch.randn(nb, hw, cq + c, generator=g, device="cuda")
+        py = torch.randn(nb, hw, cq, generator=g, device="cuda")
+        ck, cv = 0, cq
+    else:
+        px = torch.randn(nb, hw, 2 * cq + c, generator=g, device="cuda")
+        py = None
+        ck, cv = cq, 2 * cq
+    do = torch.randn(nb, hw, c, generator=g, device="cuda")
+    scale = 1.0 / float(cq) ** 0.5
+    xr = px.clone().requires_grad_()
+    yr = py.clone().requires_grad_() if cross else None
+    mode = "fp32" if hw > 64 else "bf16"       # the fused path is fp32 in every mode
+    o = K.attention_core(xr, yr, cq, ck, cv, scale, mode)
+    dx, *dy = torch.autograd.grad(o, [xr] + ([yr] if cross else []), do)
+
+    xe = px.clone().requires_grad_()
+    ye = py.clone().requires_grad_() if cross else None
+    ky = ye if cross else xe
+    ref = torch.softmax(scale * xe[..., :cq] @ ky[..., ck:ck + cq].transpose(1, 2), -1) @ \
+        xe[..., cv:]
+    dxe, *dye = torch.autograd.grad(ref, [xe] + ([ye] if cross else []), do)
+    tol = 1e-5 if hw <= 64 else 1e-4
+
+    def rel(a, b):
+        return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+    assert rel(o, ref) < tol
+    assert rel(dx, dxe) < tol
+    if cross:
+        assert rel(dy[0], dye[0]) < tol
+
+
+def test_small_attention_abi_rejects():
+    """tgfr_attn_small_* refuse shapes they cannot hold (HW > 64) and, for
+    self-attention, overlapping gradient column ranges."""
+    from text_guided_face_recognition_amd import _hip
+    x = torch.zeros(1, 65, 8, device="cuda")
+    o = torch.zeros(1, 65, 4, device="cuda")
+    p = torch.zeros(1, 65 * 65, device="cuda")
+    args = (x.data_ptr(), 65 * 8, 8, None, 0, 0, 1, 65, 2, 2, 4, 4, 1.0, o.data_ptr(), 65 * 4,
+            4, p.data_ptr(), _hip.stream())
+    assert _hip.lib().tgfr_attn_small_fwd(*args) == 1001
+    bad = (x.data_ptr(), 64 * 8, 8, None, 0, 0, 1, 64, 4, 2, 4, 4, 1.0, p.data_ptr(),
+           o.data_ptr(), 64 * 4, 4, x.data_ptr(), 64 * 8, 8, None, 0, 0, _hip.stream())
+    assert _hip.lib().tgfr_attn_small_bwd(*bad) == 1001      # dK [2, 6) overlaps dQ [0, 4)

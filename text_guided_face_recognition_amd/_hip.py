@@ -53,6 +53,9 @@ SIGNATURES = {
     "tgfr_attn_fwd": [P, P, P, L, L, I, I, F, P, L, L, P, P],
     "tgfr_linear_bf16out": [P, L, I, I, P, L, P, I, P, L, P],
     "tgfr_attn_bwd_ws": [I, I, P],
+    "tgfr_attn_small_fwd": [P, L, L, P, L, L, I, I, I, I, I, I, F, P, L, L, P, P],
+    "tgfr_attn_small_bwd": [P, L, L, P, L, L, I, I, I, I, I, I, F, P, P, L, L, P, L, L, P, L, L,
+                            P],
     "tgfr_attn_bwd": [P, P, P, L, L, I, I, F, P, P, L, L, P, P, P, P, L, L, P, P],
     "tgfr_ln_ws_floats": [I, L, I, I, P],
     "tgfr_loss_mix": [I, P, I, P, P, P],

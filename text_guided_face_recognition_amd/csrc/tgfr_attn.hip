@@ -30,6 +30,9 @@
 //                 per key tile in LDS.
 // No HW x HW fp32 matrix is ever written; D = rowsum(dO * O) comes from
 // attn_bwd_prep.
+//
+// Fused small attention (FCFM: HW = C' = C = 36): attn_small_fwd / _bwd, one
+// workgroup per sample with the whole problem in LDS, exact fp32.
 #include "tgfr_common.h"
 
 using namespace tgfr;
@@ -524,6 +527,121 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const uint16_t* __restr
     }
 }
 
+// ------------------------------------------- fused small (FCFM, HW <= 64) ---
+// One workgroup per sample holds the whole problem in LDS (fp32, row pitch
+// width + 1): FCFM's cross-attention is HW = 36 positions x C' = C = 36
+// channels (fusion_nets.py:217-258 -> SelfAttention(36, scale=1)), a few
+// tens of KB per sample, so QK^T, the softmax, PV and the five backward
+// products run back to back in one launch each way, in exact fp32 FMA (the
+// products are 36-deep: latency, not the matrix core, bounds them).
+// P [B][hw][hw] is saved for the backward.
+constexpr int SM_MAX_HW = 64;
+
+// out(m, n) = sum_k A(m, k) B(n, k) over LDS operands addressed with
+// (row, k) strides, every thread taking outputs idx = t, t + 256, ...
+template <typename Store>
+__device__ __forceinline__ void small_product(const float* A, int am, int ak, const float* Bm,
+                                              int bn, int bk, int M, int N, int K, Store st) {
+  for (int idx = threadIdx.x; idx < M * N; idx += 256) {
+    const int m = idx / N, n = idx - m * N;
+    const float* a = A + m * am;
+    const float* b = Bm + n * bn;
+    float acc = 0.f;
+    for (int k = 0; k < K; ++k) acc = fmaf(a[k * ak], b[k * bk], acc);
+    st(m, n, acc);
+  }
+}
+
+__device__ __forceinline__ void small_load(float* dst, int ld, const float* src, long long sr,
+                                           int rows, int cols) {
+  for (int idx = threadIdx.x; idx < rows * cols; idx += 256) {
+    const int r = idx / cols, k = idx - r * cols;
+    dst[r * ld + k] = src[r * sr + k];
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_small_fwd_kernel(
+    const float* __restrict__ X, long long sxn, long long sxr, const float* __restrict__ Y,
+    long long syn, long long syr, int hw, int cq, int ck, int cv, int c, float scale,
+    float* __restrict__ O, long long son, long long sor, float* __restrict__ P) {
+  extern __shared__ float sm[];
+  const int lq = cq + 1, lv = c + 1, lp = hw + 1;
+  float* sQ = sm;
+  float* sK = sQ + hw * lq;
+  float* sV = sK + hw * lq;
+  float* sP = sV + hw * lv;
+  const long long n = blockIdx.x;
+  const float* x = X + n * sxn;
+  small_load(sQ, lq, x, sxr, hw, cq);
+  small_load(sK, lq, Y + n * syn + ck, syr, hw, cq);
+  small_load(sV, lv, x + cv, sxr, hw, c);
+  __syncthreads();
+  small_product(sQ, lq, 1, sK, lq, 1, hw, hw, cq,
+                [&](int i, int j, float v) { sP[i * lp + j] = v * scale; });
+  __syncthreads();
+  const int w = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
+  float* pg = P + n * hw * hw;
+  for (int i = w; i < hw; i += 4) {
+    const float v = lane < hw ? sP[i * lp + lane] : -INFINITY;
+    const float m = wave_max(v);
+    const float e = lane < hw ? __expf(v - m) : 0.f;
+    const float inv = 1.f / wave_sum(e);
+    if (lane < hw) {
+      sP[i * lp + lane] = e * inv;
+      pg[i * hw + lane] = e * inv;
+    }
+  }
+  __syncthreads();
+  float* o = O + n * son;
+  small_product(sP, lp, 1, sV, 1, lv, hw, c, hw,
+                [&](int i, int cc, float v) { o[i * sor + cc] = v; });
+}
+
+// dP = dO V^T, dS = scale P (dP - rowsum(P dP)), dQ = dS K, dK = dS^T Q,
+// dV = P^T dO; dQ / dV into dX's columns [0, cq) / [cv, cv + c), dK into dY's
+// [ck, ck + cq) (dY = dX for self-attention).
+__global__ __launch_bounds__(256) void attn_small_bwd_kernel(
+    const float* __restrict__ X, long long sxn, long long sxr, const float* __restrict__ Y,
+    long long syn, long long syr, int hw, int cq, int ck, int cv, int c, float scale,
+    const float* __restrict__ P, const float* __restrict__ dO, long long sdn, long long sdr,
+    float* dX, long long sgn, long long sgr, float* dY, long long skn, long long skr) {
+  extern __shared__ float sm[];
+  const int lq = cq + 1, lv = c + 1, lp = hw + 1;
+  float* sQ = sm;
+  float* sK = sQ + hw * lq;
+  float* sV = sK + hw * lq;
+  float* sO = sV + hw * lv;
+  float* sP = sO + hw * lv;
+  float* sS = sP + hw * lp;
+  const long long n = blockIdx.x;
+  const float* x = X + n * sxn;
+  small_load(sQ, lq, x, sxr, hw, cq);
+  small_load(sK, lq, Y + n * syn + ck, syr, hw, cq);
+  small_load(sV, lv, x + cv, sxr, hw, c);
+  small_load(sO, lv, dO + n * sdn, sdr, hw, c);
+  small_load(sP, lp, P + n * hw * hw, hw, hw, hw);
+  __syncthreads();
+  small_product(sO, lv, 1, sV, lv, 1, hw, hw, c,
+                [&](int i, int j, float v) { sS[i * lp + j] = v; });
+  __syncthreads();
+  const int w = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
+  for (int i = w; i < hw; i += 4) {
+    const float p = lane < hw ? sP[i * lp + lane] : 0.f;
+    const float dp = lane < hw ? sS[i * lp + lane] : 0.f;
+    const float dot = wave_sum(p * dp);
+    if (lane < hw) sS[i * lp + lane] = scale * p * (dp - dot);
+  }
+  __syncthreads();
+  float* gx = dX + n * sgn;
+  float* gy = dY + n * skn + ck;
+  small_product(sS, lp, 1, sK, 1, lq, hw, cq, hw,
+                [&](int i, int k, float v) { gx[i * sgr + k] = v; });
+  small_product(sS, 1, lp, sQ, 1, lq, hw, cq, hw,
+                [&](int j, int k, float v) { gy[j * skr + k] = v; });
+  small_product(sP, 1, lp, sO, 1, lv, hw, c, hw,
+                [&](int j, int cc, float v) { gx[j * sgr + cv + cc] = v; });
+}
+
 }  // namespace
 
 extern "C" {
@@ -595,6 +713,68 @@ int tgfr_attn_bwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long 
   if (const int e = set_max_lds((const void*)attn_bwd_q_kernel, Q_LDS)) return e;
   hipLaunchKernelGGL(attn_bwd_q_kernel, dim3(B * np), dim3(256), Q_LDS, s, K, ld, sb, hw, dS, dQ,
                      ldg, sbg);
+  return (int)hipGetLastError();
+}
+
+static int small_check(int B, int hw, int cq, int ck, int cv, int c) {
+  if (B <= 0 || hw <= 0 || hw > SM_MAX_HW || cq <= 0 || c <= 0 || ck < 0 || cv < 0) return 1001;
+  return 0;
+}
+
+// FCFM-sized fused attention (HW <= 64): X [B][hw][*] fp32 rows holding Qr
+// at columns [0, cq) and V at [cv, cv + c); Y (NULL = X) holding Kr at
+// [ck, ck + cq).  O [B][hw][c] (son, sor); P [B][hw][hw] dense, written.
+int tgfr_attn_small_fwd(const float* X, long long sxn, long long sxr, const float* Y,
+                        long long syn, long long syr, int B, int hw, int cq, int ck, int cv,
+                        int c, float scale, float* O, long long son, long long sor, float* P,
+                        void* stream) {
+  if (const int e = small_check(B, hw, cq, ck, cv, c)) return e;
+  if (!X || !O || !P) return 1001;
+  if (!Y) {
+    Y = X;
+    syn = sxn;
+    syr = sxr;
+  }
+  const int lds = 4 * (2 * hw * (cq + 1) + hw * (c + 1) + hw * (hw + 1));
+  if (lds > 160 * 1024) return 1001;
+  if (const int e = set_max_lds((const void*)attn_small_fwd_kernel, lds)) return e;
+  hipLaunchKernelGGL(attn_small_fwd_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, X, sxn,
+                     sxr, Y, syn, syr, hw, cq, ck, cv, c, scale, O, son, sor, P);
+  return (int)hipGetLastError();
+}
+
+// Its backward: dO [B][hw][c] (sdn, sdr); dQr / dV overwrite dX's columns
+// [0, cq) / [cv, cv + c), dKr overwrites dY's [ck, ck + cq) (dY NULL = dX:
+// the three column ranges must then be disjoint).
+int tgfr_attn_small_bwd(const float* X, long long sxn, long long sxr, const float* Y,
+                        long long syn, long long syr, int B, int hw, int cq, int ck, int cv,
+                        int c, float scale, const float* P, const float* dO, long long sdn,
+                        long long sdr, float* dX, long long sgn, long long sgr, float* dY,
+                        long long skn, long long skr, void* stream) {
+  if (const int e = small_check(B, hw, cq, ck, cv, c)) return e;
+  if (!X || !P || !dO || !dX) return 1001;
+  if (!Y) {
+    Y = X;
+    syn = sxn;
+    syr = sxr;
+  }
+  if (!dY) {
+    const bool qk = ck < cq;                                    // [0,cq) vs [ck,ck+cq)
+    const bool qv = cv < cq;                                    // [0,cq) vs [cv,cv+c)
+    const bool kv = ck < cv + c && cv < ck + cq;                // [ck,..) vs [cv,..)
+    if (qk || qv || kv) return 1001;
+    dY = dX;
+    skn = sgn;
+    skr = sgr;
+  } else if (cv < cq) {
+    return 1001;
+  }
+  const int lds = 4 * (2 * hw * (cq + 1) + 2 * hw * (c + 1) + 2 * hw * (hw + 1));
+  if (lds > 160 * 1024) return 1001;
+  if (const int e = set_max_lds((const void*)attn_small_bwd_kernel, lds)) return e;
+  hipLaunchKernelGGL(attn_small_bwd_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, X, sxn,
+                     sxr, Y, syn, syr, hw, cq, ck, cv, c, scale, P, dO, sdn, sdr, dX, sgn, sgr,
+                     dY, skn, skr);
   return (int)hipGetLastError();
 }
 

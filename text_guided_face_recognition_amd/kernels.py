@@ -701,10 +701,22 @@ class AttentionCore(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, px, py, cq, ck, cv, scale, mode):
-        px = px.float()
-        ky = px if py is None else py.float()
+        px = _rows(px.float())
+        ky = px if py is None else _rows(py.float())
         qr, kr, v = px[..., :cq], ky[..., ck:ck + cq], px[..., cv:]
         nb, hw, _ = qr.shape
+        c = v.shape[-1]
+        ctx.small = _attn_small_fits(hw, cq, ck, cv, c, py is None)
+        if ctx.small:
+            # FCFM-sized: one fused launch (tgfr_attn_small_fwd), exact fp32
+            o = torch.empty(nb, hw, c, dtype=torch.float32, device=px.device)
+            p = torch.empty(nb, hw, hw, dtype=torch.float32, device=px.device)
+            call("tgfr_attn_small_fwd", ptr(px), px.stride(0), px.stride(1),
+                 None if py is None else ptr(ky), ky.stride(0), ky.stride(1), nb, hw, cq, ck,
+                 cv, c, float(scale), ptr(o), o.stride(0), o.stride(1), ptr(p), _hip.stream())
+            ctx.save_for_backward(px, None if py is None else ky, p)
+            ctx.cfg = (float(scale), mode, cq, ck, cv)
+            return o
         s = bgemm(qr, kr.transpose(1, 2), mode=mode)
         p = torch.empty_like(s)
         call("tgfr_attn_softmax", ptr(s), ptr(p), None, nb * hw, hw, hw, float(scale),
@@ -720,8 +732,26 @@ class AttentionCore(torch.autograd.Function):
         scale, mode, cq, ck, cv = ctx.cfg
         ky = px if py is None else py
         qr, kr, v = px[..., :cq], ky[..., ck:ck + cq], px[..., cv:]
-        do = do.float()
+        do = _rows(do.float())
         nb, hw, _ = qr.shape
+        if ctx.small:
+            dpx = torch.empty_like(px)
+            dky = None if py is None else torch.empty_like(py)
+            if py is None:
+                if ck != cq or cv != 2 * cq or px.shape[-1] != cv + v.shape[-1]:
+                    dpx.zero_()
+            else:
+                if cv != cq:
+                    dpx.zero_()
+                if ck != 0 or cq != py.shape[-1]:
+                    dky.zero_()
+            g = dpx if dky is None else dky
+            call("tgfr_attn_small_bwd", ptr(px), px.stride(0), px.stride(1),
+                 None if py is None else ptr(ky), ky.stride(0), ky.stride(1), nb, hw, cq, ck,
+                 cv, v.shape[-1], scale, ptr(p), ptr(do), do.stride(0), do.stride(1), ptr(dpx),
+                 dpx.stride(0), dpx.stride(1), None if dky is None else ptr(dky), g.stride(0),
+                 g.stride(1), _hip.stream())
+            return dpx, dky, None, None, None, None, None
         dp = bgemm(do, v.transpose(1, 2), mode=mode)
         ds = torch.empty_like(dp)
         call("tgfr_attn_softmax_bwd", ptr(p), ptr(dp), ptr(ds), nb * hw, hw, hw, scale,
@@ -740,6 +770,23 @@ class AttentionCore(torch.autograd.Function):
         bgemm(ds.transpose(1, 2), qr, out=dky[..., ck:ck + cq], mode=mode)
         bgemm(p.transpose(1, 2), do, out=dpx[..., cv:], mode=mode)
         return dpx, (None if py is None else dky), None, None, None, None, None
+
+
+def _rows(t):
+    """t with unit element stride (a copy only when it has not)."""
+    return t if t.stride(-1) == 1 else t.contiguous()
+
+
+def _attn_small_fits(hw, cq, ck, cv, c, self_attn):
+    """Whether tgfr_attn_small_fwd/_bwd take this shape: HW <= 64, the
+    backward's six LDS operands within 160 KB, and gradient column ranges
+    that do not overlap (the kernel overwrites them)."""
+    lds = 4 * 2 * hw * ((cq + 1) + (c + 1) + (hw + 1))
+    if hw > 64 or lds > 160 * 1024:
+        return False
+    if self_attn:
+        return ck >= cq and cv >= cq and not (ck < cv + c and cv < ck + cq)
+    return cv >= cq
 
 
 def attention_core(px, py, cq, ck, cv, scale, mode="fp32"):

@@ -273,7 +273,7 @@ int tgfr_attn_bwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long 
 /* Fused small attention for FCFM's cross-attention (fusion_nets.py:93-118 as
  * called at :248 with SelfAttention(36, scale=1): HW = C' = C = 36), one
  * workgroup per sample, exact fp32.  Replaces the composed QK^T / softmax /
- * PV (tgfr_bgemm + tgfr_attn_softmax) for HW <= 64.
+ * PV (tgfr_bgemm + tgfr_attn_softmax) for HW, C', C <= 64.
  * X [B][hw][*] fp32 rows (sample stride sxn, row stride sxr) hold Qr at
  * columns [0, cq) and V at [cv, cv + c); Y (NULL = X) holds Kr at
  * [ck, ck + cq).  O [B][hw][c] (son, sor) = softmax(scale Qr Kr^T) V;

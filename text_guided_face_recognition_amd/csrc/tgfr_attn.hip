@@ -32,7 +32,7 @@
 // attn_bwd_prep.
 //
 // Fused small attention (FCFM: HW = C' = C = 36): attn_small_fwd / _bwd, one
-// workgroup per sample with the whole problem in LDS, exact fp32.
+// workgroup per sample with the whole problem in LDS, fp32 MFMA (exact fp32).
 #include "tgfr_common.h"
 
 using namespace tgfr;
@@ -528,39 +528,139 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const uint16_t* __restr
 }
 
 // ------------------------------------------- fused small (FCFM, HW <= 64) ---
-// One workgroup per sample holds the whole problem in LDS (fp32, row pitch
-// width + 1): FCFM's cross-attention is HW = 36 positions x C' = C = 36
+// One 8-wave workgroup per sample holds the whole problem in LDS (fp32, row
+// pitch width + 1): FCFM's cross-attention is HW = 36 positions x C' = C = 36
 // channels (fusion_nets.py:217-258 -> SelfAttention(36, scale=1)), a few
 // tens of KB per sample, so QK^T, the softmax, PV and the five backward
-// products run back to back in one launch each way, in exact fp32 FMA (the
-// products are 36-deep: latency, not the matrix core, bounds them).
-// P [B][hw][hw] is saved for the backward.
+// products run back to back in one launch each way.  The products run on
+// v_mfma_f32_16x16x4_f32 (fp32 operands: exact fp32 products and sums, the
+// same as an fmaf chain), one 16x16 output tile per wave at a time, operands
+// read straight from LDS with (row, k) strides (so transposed operands need
+// no copy).  Every operand is loaded from HBM in one batch per thread (all
+// loads in flight before the first LDS store).  P [B][hw][hw] is saved for
+// the backward.
 constexpr int SM_MAX_HW = 64;
+constexpr int SNT = 576;                 // threads per workgroup: 9 waves, one per
+                                         // 16x16 tile of a 36 x 36 product
+constexpr int SLD = (64 * 64 + SNT - 1) / SNT;   // max elements per thread per operand
 
-// out(m, n) = sum_k A(m, k) B(n, k) over LDS operands addressed with
-// (row, k) strides, every thread taking outputs idx = t, t + 256, ...
+// max / sum over the 16 lanes of a DPP row, in every lane: mirror (i <->
+// 15 - i), half mirror (i <-> 7 - i), then quad xor 1 and xor 2.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp<0x140>(v));
+  v = fmaxf(v, dpp<0x141>(v));
+  v = fmaxf(v, dpp<0xB1>(v));
+  return fmaxf(v, dpp<0x4E>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp<0x140>(v);
+  v += dpp<0x141>(v);
+  v += dpp<0xB1>(v);
+  return v + dpp<0x4E>(v);
+}
+
+// out(m, n) = sum_k A(m, k) B(n, k), A(m, k) = A[m am + k ak], B likewise;
+// 16x16 tiles dealt to the waves round robin starting at wave w0.
 template <typename Store>
 __device__ __forceinline__ void small_product(const float* A, int am, int ak, const float* Bm,
-                                              int bn, int bk, int M, int N, int K, Store st) {
-  for (int idx = threadIdx.x; idx < M * N; idx += 256) {
-    const int m = idx / N, n = idx - m * N;
-    const float* a = A + m * am;
-    const float* b = Bm + n * bn;
-    float acc = 0.f;
-    for (int k = 0; k < K; ++k) acc = fmaf(a[k * ak], b[k * bk], acc);
-    st(m, n, acc);
+                                              int bn, int bk, int M, int N, int K, int w0,
+                                              Store st) {
+  const int w = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
+  const int li = lane & 15, lk = lane >> 4;
+  const int mt = (M + 15) / 16, nt = (N + 15) / 16;
+  for (int t = (w - w0 + SNT / WAVE) % (SNT / WAVE); t < mt * nt; t += SNT / WAVE) {
+    const int m = 16 * (t / nt) + li, n = 16 * (t % nt) + li;
+    const float* a = A + m * am + lk * ak;
+    const float* b = Bm + n * bn + lk * bk;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 3
+    for (int k = 0; k < K; k += 4) {
+      const bool kin = k + lk < K;
+      const float av = kin && m < M ? a[k * ak] : 0.f;
+      const float bv = kin && n < N ? b[k * bk] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+    }
+    const int col = 16 * (t % nt) + li;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * (t / nt) + 4 * lk + r;
+      if (row < M && col < N) st(row, col, acc[r]);
+    }
   }
 }
 
-__device__ __forceinline__ void small_load(float* dst, int ld, const float* src, long long sr,
-                                           int rows, int cols) {
-  for (int idx = threadIdx.x; idx < rows * cols; idx += 256) {
-    const int r = idx / cols, k = idx - r * cols;
-    dst[r * ld + k] = src[r * sr + k];
+struct SmallOp {
+  float* dst;
+  int ld;
+  const float* src;
+  long long sr;
+  int rows, cols;
+};
+
+// dst[r ld + k] = src[r sr + k] for every operand, all HBM loads issued
+// before the first LDS store
+template <int NOP>
+__device__ __forceinline__ void small_load(const SmallOp (&op)[NOP]) {
+  float v[NOP][SLD];
+  int r0[NOP], c0[NOP];
+#pragma unroll
+  for (int o = 0; o < NOP; ++o) {
+    const int cols = op[o].cols, total = op[o].rows * cols;
+    const int dr = SNT / cols, dc = SNT - dr * cols;
+    int r = threadIdx.x / cols, c = threadIdx.x - r * cols;
+    r0[o] = r;
+    c0[o] = c;
+#pragma unroll
+    for (int u = 0; u < SLD; ++u) {
+      v[o][u] = (int)threadIdx.x + u * SNT < total ? op[o].src[r * op[o].sr + c] : 0.f;
+      r += dr;
+      c += dc;
+      if (c >= cols) {
+        c -= cols;
+        ++r;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < NOP; ++o) {
+    const int cols = op[o].cols, total = op[o].rows * cols;
+    const int dr = SNT / cols, dc = SNT - dr * cols;
+    int r = r0[o], c = c0[o];
+#pragma unroll
+    for (int u = 0; u < SLD; ++u) {
+      if ((int)threadIdx.x + u * SNT < total) op[o].dst[r * op[o].ld + c] = v[o][u];
+      r += dr;
+      c += dc;
+      if (c >= cols) {
+        c -= cols;
+        ++r;
+      }
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void attn_small_fwd_kernel(
+// dst[r sd + k] = src[r ld + k] (LDS -> HBM, coalesced over the whole group)
+__device__ __forceinline__ void small_store(float* dst, long long sd, const float* src, int ld,
+                                            int rows, int cols) {
+  const int total = rows * cols, dr = SNT / cols, dc = SNT - dr * cols;
+  int r = threadIdx.x / cols, c = threadIdx.x - r * cols;
+  for (int idx = threadIdx.x; idx < total; idx += SNT) {
+    dst[r * sd + c] = src[r * ld + c];
+    r += dr;
+    c += dc;
+    if (c >= cols) {
+      c -= cols;
+      ++r;
+    }
+  }
+}
+
+__global__ __launch_bounds__(SNT) void attn_small_fwd_kernel(
     const float* __restrict__ X, long long sxn, long long sxr, const float* __restrict__ Y,
     long long syn, long long syr, int hw, int cq, int ck, int cv, int c, float scale,
     float* __restrict__ O, long long son, long long sor, float* __restrict__ P) {
@@ -572,35 +672,48 @@ __global__ __launch_bounds__(256) void attn_small_fwd_kernel(
   float* sP = sV + hw * lv;
   const long long n = blockIdx.x;
   const float* x = X + n * sxn;
-  small_load(sQ, lq, x, sxr, hw, cq);
-  small_load(sK, lq, Y + n * syn + ck, syr, hw, cq);
-  small_load(sV, lv, x + cv, sxr, hw, c);
+  const SmallOp ops[3] = {{sQ, lq, x, sxr, hw, cq},
+                          {sK, lq, Y + n * syn + ck, syr, hw, cq},
+                          {sV, lv, x + cv, sxr, hw, c}};
+  small_load(ops);
   __syncthreads();
-  small_product(sQ, lq, 1, sK, lq, 1, hw, hw, cq,
+  small_product(sQ, lq, 1, sK, lq, 1, hw, hw, cq, 0,
                 [&](int i, int j, float v) { sP[i * lp + j] = v * scale; });
   __syncthreads();
-  const int w = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
-  float* pg = P + n * hw * hw;
-  for (int i = w; i < hw; i += 4) {
-    const float v = lane < hw ? sP[i * lp + lane] : -INFINITY;
-    const float m = wave_max(v);
-    const float e = lane < hw ? __expf(v - m) : 0.f;
-    const float inv = 1.f / wave_sum(e);
-    if (lane < hw) {
-      sP[i * lp + lane] = e * inv;
-      pg[i * hw + lane] = e * inv;
+  // softmax: 16 lanes per row (one DPP row), up to 4 keys per lane
+  for (int i = threadIdx.x / 16; i < hw; i += SNT / 16) {
+    float* row = sP + i * lp;
+    const int j0 = threadIdx.x % 16;
+    float v[SM_MAX_HW / 16];
+    float m = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < SM_MAX_HW / 16; ++u) {
+      v[u] = j0 + 16 * u < hw ? row[j0 + 16 * u] : -INFINITY;
+      m = fmaxf(m, v[u]);
     }
+    m = row16_max(m);
+    float sum = 0.f;
+#pragma unroll
+    for (int u = 0; u < SM_MAX_HW / 16; ++u) {
+      v[u] = __expf(v[u] - m);
+      sum += v[u];
+    }
+    const float inv = 1.f / row16_sum(sum);
+#pragma unroll
+    for (int u = 0; u < SM_MAX_HW / 16; ++u)
+      if (j0 + 16 * u < hw) row[j0 + 16 * u] = v[u] * inv;
   }
   __syncthreads();
+  small_store(P + n * hw * hw, hw, sP, lp, hw, hw);
   float* o = O + n * son;
-  small_product(sP, lp, 1, sV, 1, lv, hw, c, hw,
+  small_product(sP, lp, 1, sV, 1, lv, hw, c, hw, 0,
                 [&](int i, int cc, float v) { o[i * sor + cc] = v; });
 }
 
 // dP = dO V^T, dS = scale P (dP - rowsum(P dP)), dQ = dS K, dK = dS^T Q,
 // dV = P^T dO; dQ / dV into dX's columns [0, cq) / [cv, cv + c), dK into dY's
 // [ck, ck + cq) (dY = dX for self-attention).
-__global__ __launch_bounds__(256) void attn_small_bwd_kernel(
+__global__ __launch_bounds__(SNT) void attn_small_bwd_kernel(
     const float* __restrict__ X, long long sxn, long long sxr, const float* __restrict__ Y,
     long long syn, long long syr, int hw, int cq, int ck, int cv, int c, float scale,
     const float* __restrict__ P, const float* __restrict__ dO, long long sdn, long long sdr,
@@ -615,30 +728,44 @@ __global__ __launch_bounds__(256) void attn_small_bwd_kernel(
   float* sS = sP + hw * lp;
   const long long n = blockIdx.x;
   const float* x = X + n * sxn;
-  small_load(sQ, lq, x, sxr, hw, cq);
-  small_load(sK, lq, Y + n * syn + ck, syr, hw, cq);
-  small_load(sV, lv, x + cv, sxr, hw, c);
-  small_load(sO, lv, dO + n * sdn, sdr, hw, c);
-  small_load(sP, lp, P + n * hw * hw, hw, hw, hw);
+  const SmallOp ops[5] = {{sQ, lq, x, sxr, hw, cq},
+                          {sK, lq, Y + n * syn + ck, syr, hw, cq},
+                          {sV, lv, x + cv, sxr, hw, c},
+                          {sO, lv, dO + n * sdn, sdr, hw, c},
+                          {sP, lp, P + n * hw * hw, hw, hw, hw}};
+  small_load(ops);
   __syncthreads();
-  small_product(sO, lv, 1, sV, lv, 1, hw, hw, c,
+  small_product(sO, lv, 1, sV, lv, 1, hw, hw, c, 0,
                 [&](int i, int j, float v) { sS[i * lp + j] = v; });
   __syncthreads();
-  const int w = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
-  for (int i = w; i < hw; i += 4) {
-    const float p = lane < hw ? sP[i * lp + lane] : 0.f;
-    const float dp = lane < hw ? sS[i * lp + lane] : 0.f;
-    const float dot = wave_sum(p * dp);
-    if (lane < hw) sS[i * lp + lane] = scale * p * (dp - dot);
+  for (int i = threadIdx.x / 16; i < hw; i += SNT / 16) {   // 16 lanes per row
+    const float* pr = sP + i * lp;
+    float* sr = sS + i * lp;
+    const int j0 = threadIdx.x % 16;
+    float p[SM_MAX_HW / 16], dp[SM_MAX_HW / 16];
+    float dot = 0.f;
+#pragma unroll
+    for (int u = 0; u < SM_MAX_HW / 16; ++u) {
+      const bool in = j0 + 16 * u < hw;
+      p[u] = in ? pr[j0 + 16 * u] : 0.f;
+      dp[u] = in ? sr[j0 + 16 * u] : 0.f;
+      dot = fmaf(p[u], dp[u], dot);
+    }
+    dot = row16_sum(dot);
+#pragma unroll
+    for (int u = 0; u < SM_MAX_HW / 16; ++u)
+      if (j0 + 16 * u < hw) sr[j0 + 16 * u] = scale * p[u] * (dp[u] - dot);
   }
   __syncthreads();
   float* gx = dX + n * sgn;
   float* gy = dY + n * skn + ck;
-  small_product(sS, lp, 1, sK, 1, lq, hw, cq, hw,
+  // the three products' tiles continue each other's round robin over the waves
+  const int tq = ((hw + 15) / 16) * ((cq + 15) / 16);
+  small_product(sS, lp, 1, sK, 1, lq, hw, cq, hw, 0,
                 [&](int i, int k, float v) { gx[i * sgr + k] = v; });
-  small_product(sS, 1, lp, sQ, 1, lq, hw, cq, hw,
+  small_product(sS, 1, lp, sQ, 1, lq, hw, cq, hw, tq % (SNT / WAVE),
                 [&](int j, int k, float v) { gy[j * skr + k] = v; });
-  small_product(sP, 1, lp, sO, 1, lv, hw, c, hw,
+  small_product(sP, 1, lp, sO, 1, lv, hw, c, hw, (2 * tq) % (SNT / WAVE),
                 [&](int j, int cc, float v) { gx[j * sgr + cv + cc] = v; });
 }
 
@@ -717,7 +844,9 @@ int tgfr_attn_bwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long 
 }
 
 static int small_check(int B, int hw, int cq, int ck, int cv, int c) {
-  if (B <= 0 || hw <= 0 || hw > SM_MAX_HW || cq <= 0 || c <= 0 || ck < 0 || cv < 0) return 1001;
+  if (B <= 0 || hw <= 0 || hw > SM_MAX_HW || cq <= 0 || cq > SM_MAX_HW || c <= 0 ||
+      c > SM_MAX_HW || ck < 0 || cv < 0)
+    return 1001;
   return 0;
 }
 
@@ -738,7 +867,7 @@ int tgfr_attn_small_fwd(const float* X, long long sxn, long long sxr, const floa
   const int lds = 4 * (2 * hw * (cq + 1) + hw * (c + 1) + hw * (hw + 1));
   if (lds > 160 * 1024) return 1001;
   if (const int e = set_max_lds((const void*)attn_small_fwd_kernel, lds)) return e;
-  hipLaunchKernelGGL(attn_small_fwd_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, X, sxn,
+  hipLaunchKernelGGL(attn_small_fwd_kernel, dim3(B), dim3(SNT), lds, (hipStream_t)stream, X, sxn,
                      sxr, Y, syn, syr, hw, cq, ck, cv, c, scale, O, son, sor, P);
   return (int)hipGetLastError();
 }
@@ -772,7 +901,7 @@ int tgfr_attn_small_bwd(const float* X, long long sxn, long long sxr, const floa
   const int lds = 4 * (2 * hw * (cq + 1) + 2 * hw * (c + 1) + 2 * hw * (hw + 1));
   if (lds > 160 * 1024) return 1001;
   if (const int e = set_max_lds((const void*)attn_small_bwd_kernel, lds)) return e;
-  hipLaunchKernelGGL(attn_small_bwd_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, X, sxn,
+  hipLaunchKernelGGL(attn_small_bwd_kernel, dim3(B), dim3(SNT), lds, (hipStream_t)stream, X, sxn,
                      sxr, Y, syn, syr, hw, cq, ck, cv, c, scale, P, dO, sdn, sdr, dX, sgn, sgr,
                      dY, skn, skr);
   return (int)hipGetLastError();

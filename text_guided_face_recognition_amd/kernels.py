@@ -778,11 +778,10 @@ def _rows(t):
 
 
 def _attn_small_fits(hw, cq, ck, cv, c, self_attn):
-    """Whether tgfr_attn_small_fwd/_bwd take this shape: HW <= 64, the
-    backward's six LDS operands within 160 KB, and gradient column ranges
-    that do not overlap (the kernel overwrites them)."""
-    lds = 4 * 2 * hw * ((cq + 1) + (c + 1) + (hw + 1))
-    if hw > 64 or lds > 160 * 1024:
+    """Whether tgfr_attn_small_fwd/_bwd take this shape: HW, C', C <= 64,
+    and gradient column ranges that do not overlap (the kernel overwrites
+    them)."""
+    if max(hw, cq, c) > 64:
         return False
     if self_attn:
         return ck >= cq and cv >= cq and not (ck < cv + c and cv < ck + cq)

@@ -27,11 +27,7 @@ namespace {
 constexpr int CB = 16;          // classes per block
 constexpr int NT = 256;
 
-__device__ __forceinline__ float group16_sum(float v) {
-#pragma unroll
-  for (int m = 8; m >= 1; m >>= 1) v += __shfl_xor(v, m);
-  return v;
-}
+__device__ __forceinline__ float group16_sum(float v) { return row16_sum(v); }
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *(const float4*)p; }
 __device__ __forceinline__ float4 lds4(uint32_t off) {
@@ -63,6 +59,36 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, long l
         const int r = i / q, k = i % q;
         lds_st16(off + (uint32_t)((r * (D + 4) + 4 * k) * 4), __builtin_bit_cast(uint4, v[u]));
       }
+    }
+  }
+}
+
+// Split form of stage_rows for tiles that fit one pass (n D / 4 <= U NT):
+// load_rows issues the thread's U float4 loads into registers, store_rows
+// writes them to LDS later, so several tiles' loads (and a next chunk's) are
+// in flight together.
+template <int U>
+__device__ __forceinline__ void load_rows(float4 (&v)[U], const float* __restrict__ src,
+                                          long long ld, int r0, int n, int rows, int D) {
+  const int q = D / 4, total = n * q;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = min((int)threadIdx.x + u * NT, total - 1);
+    const int r = i / q, k = i % q;
+    const int row = min(r0 + r, rows - 1);
+    v[u] = ld4(src + (long long)row * ld + 4 * k);
+    if (r0 + r >= rows) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+template <int U>
+__device__ __forceinline__ void store_rows(const float4 (&v)[U], int n, int D, uint32_t off) {
+  const int q = D / 4, total = n * q;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = threadIdx.x + u * NT;
+    if (i < total) {
+      const int r = i / q, k = i % q;
+      lds_st16(off + (uint32_t)((r * (D + 4) + 4 * k) * 4), __builtin_bit_cast(uint4, v[u]));
     }
   }
 }
@@ -166,22 +192,37 @@ __global__ __launch_bounds__(NT) void arc_fwd_kernel(
 #pragma unroll
   for (int q = 0; q < 16; ++q) acc[q] = 0.f;
   float sw[2] = {0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
+  // both operands' chunk loads in one batch; chunk j + 1's loads are issued
+  // right after chunk j is in LDS, so they fly during chunk j's MFMAs
+  constexpr int UW = CBF * FK / 4 / NT, UX = FRB * FK / 4 / NT;
+  float4 vw[UW], vx[UX];
+  load_rows(vw, W, ldw, c0, CBF, C, min(FK, D));
+  load_rows(vx, x, ldx, b0, FRB, B, min(FK, D));
   for (int k0 = 0; k0 < D; k0 += FK) {
     const int kc = min(FK, D - k0);      // multiple of 8 (D % 8 == 0)
     __syncthreads();                     // previous chunk's readers are done
-    stage_rows(W + k0, ldw, c0, CBF, C, kc, w_off);
-    stage_rows(x + k0, ldx, b0, FRB, B, kc, x_off);
+    store_rows(vw, CBF, kc, w_off);
+    store_rows(vx, FRB, kc, x_off);
     __syncthreads();
+    if (k0 + FK < D) {
+      const int kn = min(FK, D - k0 - FK);
+      load_rows(vw, W + k0 + FK, ldw, c0, CBF, C, kn);
+      load_rows(vx, x + k0 + FK, ldx, b0, FRB, B, kn);
+    }
     // running sums of squares: 16 lanes per row, rows tid / 16 + 16 i
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = (tid >> 4) + 16 * i;
-      for (int k = g; k < kc / 4; k += 16) {
-        const float4 v = lds4(x_off + (uint32_t)((r * (kc + 4) + 4 * k) * 4));
-        sx[i] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-        if (i < 2) {
-          const float4 u = lds4(w_off + (uint32_t)((r * (kc + 4) + 4 * k) * 4));
-          sw[i] += u.x * u.x + u.y * u.y + u.z * u.z + u.w * u.w;
+#pragma unroll
+      for (int j = 0; j < FK / 64; ++j) {
+        const int k = g + 16 * j;
+        if (k < kc / 4) {
+          const float4 v = lds4(x_off + (uint32_t)((r * (kc + 4) + 4 * k) * 4));
+          sx[i] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+          if (i < 2) {
+            const float4 u = lds4(w_off + (uint32_t)((r * (kc + 4) + 4 * k) * 4));
+            sw[i] += u.x * u.x + u.y * u.y + u.z * u.z + u.w * u.w;
+          }
         }
       }
     }
@@ -402,9 +443,12 @@ __global__ __launch_bounds__(NT) void arc_bwd_kernel(
 // transposes); wave w owns d tiles w NTW .. w NTW + NTW - 1 (D = 128 NTW).
 // The l2-norm backward's per-class dot is reduced across lanes and waves
 // through LDS.  LDS: dcos [rows_per + RB][33] (rows past the slice zero) |
-// xn chunk [RB][D + 4].
+// xn chunk [RB][D + 4]; for slices of <= 64 rows at D <= 256, the whole
+// slice: dcos [rows_per][33] | xn [rows_per][D + 4], with every HBM load of
+// the block (xn rows, then logits / cos / labels) in flight at once.
 constexpr int CBM = 32;
 constexpr int RBM = 16;         // xn rows per staged chunk
+constexpr int ARC_WHOLE = 64;   // slices of at most this many rows are staged whole
 template <int NTW>
 __global__ __launch_bounds__(NT) void arc_bwd_mma_kernel(
     const float* __restrict__ dlogits, const float* __restrict__ cosv,
@@ -431,13 +475,21 @@ __global__ __launch_bounds__(NT) void arc_bwd_mma_kernel(
   }
   constexpr int LDC = CBM + 1;
   const int rb0 = blockIdx.y * rows_per, rb1 = min(B, rb0 + rows_per), nbs = rb1 - rb0;
+  // whole: the slice's xn rows (<= ARC_WHOLE) staged at once, their loads
+  // issued before the dcos loads so both are in flight together; else RBM-row
+  // chunks
+  const bool whole = NTW <= 2 && rows_per <= ARC_WHOLE;
+  const int dc_rows = whole ? (rows_per + 1) & ~1 : rows_per + RBM;
   float* dc = (float*)g_smem;
-  const uint32_t x_off = (uint32_t)(((rows_per + RBM) * LDC * 4 + 15) & ~15);
+  const uint32_t x_off = (uint32_t)((dc_rows * LDC * 4 + 15) & ~15);
   const float* xs = (const float*)(g_smem + x_off);
   const int c0 = blockIdx.x * CBM, tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6, lr = lane & 31, h = lane >> 5;
+  constexpr int UXN = NTW <= 2 ? ARC_WHOLE * 32 * NTW / NT : 1;   // float4 per thread (D = 128 NTW)
+  float4 vx[UXN];
+  if (whole) load_rows(vx, xn, D, rb0, dc_rows, B, D);
   // dcos of the block's columns; rows past the slice (up to one chunk) zero
-  for (int base = tid; base < (rows_per + RBM) * CBM; base += NT * 4) {
+  for (int base = tid; base < dc_rows * CBM; base += NT * 4) {
     float gl[4], cv[4], iw[4];
     bool tg[4];
 #pragma unroll
@@ -445,16 +497,17 @@ __global__ __launch_bounds__(NT) void arc_bwd_mma_kernel(
       const int i = min(base + u * NT, max(nbs * CBM - 1, 0));
       const int b = rb0 + i / CBM, col = min(c0 + i % CBM, C - 1);
       const long long e = (long long)b * C + col;
+      const long long lb = label[b];
       gl[u] = dlogits ? dlogits[e]
-                      : fscale * (__expf(F.L[e] - F.ws[b]) - (label[b] == col ? 1.f : 0.f));
+                      : fscale * (__expf(F.L[e] - F.ws[b]) - (lb == col ? 1.f : 0.f));
       cv[u] = cosv[e];
       iw[u] = inv_nw[col];
-      tg[u] = label[b] == col;
+      tg[u] = lb == col;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int i = base + u * NT;
-      if (i < (rows_per + RBM) * CBM) {
+      if (i < dc_rows * CBM) {
         const int r = i / CBM, cc = i % CBM, col = c0 + cc;
         float d = 0.f;
         if (r < nbs && col < C) {
@@ -471,17 +524,38 @@ __global__ __launch_bounds__(NT) void arc_bwd_mma_kernel(
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
   const int dbase = 32 * NTW * w + lr;
-  for (int b0 = rb0; b0 < rb1; b0 += RBM) {
-    const int nb = min(RBM, rb1 - b0);
+  // the epilogue's W values (lane: classes acc_row(q, h), its d columns),
+  // loaded now so they arrive during the MFMAs
+  float wv[16][NTW];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const float* wr = W + (long long)min(c0 + acc_row(q, h), C - 1) * ldw + dbase;
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) wv[q][t] = wr[32 * t];
+  }
+  if (whole) {
+    store_rows(vx, dc_rows, D, x_off);   // rows past B are zeros
     __syncthreads();
-    stage_rows(xn, D, b0, RBM, B, D, x_off);   // rows past B staged as zeros
-    __syncthreads();
-    for (int k = 0; k < nb; k += 2) {
-      const float a = dc[(b0 - rb0 + k + h) * LDC + lr];
+    for (int k = 0; k < nbs; k += 2) {
+      const float a = dc[(k + h) * LDC + lr];
       const float* xr = xs + (k + h) * (D + 4) + dbase;
 #pragma unroll
       for (int t = 0; t < NTW; ++t)
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xr[32 * t], acc[t], 0, 0, 0);
+    }
+  } else {
+    for (int b0 = rb0; b0 < rb1; b0 += RBM) {
+      const int nb = min(RBM, rb1 - b0);
+      __syncthreads();
+      stage_rows(xn, D, b0, RBM, B, D, x_off);   // rows past B staged as zeros
+      __syncthreads();
+      for (int k = 0; k < nb; k += 2) {
+        const float a = dc[(b0 - rb0 + k + h) * LDC + lr];
+        const float* xr = xs + (k + h) * (D + 4) + dbase;
+#pragma unroll
+        for (int t = 0; t < NTW; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xr[32 * t], acc[t], 0, 0, 0);
+      }
     }
   }
   if (gridDim.y > 1) {                       // raw dWn partials: part[y][C][D]
@@ -502,14 +576,10 @@ __global__ __launch_bounds__(NT) void arc_bwd_mma_kernel(
   float part_dot[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
-    const int col = min(c0 + acc_row(q, h), C - 1);
-    const float* wr = W + (long long)col * ldw + dbase;
     float sdot = 0.f;
 #pragma unroll
-    for (int t = 0; t < NTW; ++t) sdot = fmaf(wr[32 * t], acc[t][q], sdot);
-#pragma unroll
-    for (int m = 16; m >= 1; m >>= 1) sdot += __shfl_xor(sdot, m);
-    part_dot[q] = sdot;
+    for (int t = 0; t < NTW; ++t) sdot = fmaf(wv[q][t], acc[t][q], sdot);
+    part_dot[q] = x16_sum(row16_sum(sdot));  // over the 32 d columns of the half
   }
   if (lr == 0) {
 #pragma unroll
@@ -524,10 +594,9 @@ __global__ __launch_bounds__(NT) void arc_bwd_mma_kernel(
     const bool clamped = inv >= 1.f / eps;   // |W_c| <= eps: y = W / eps, no projection
     const float dot = clamped ? 0.f
                               : inv * (red[cc] + red[CBM + cc] + red[2 * CBM + cc] + red[3 * CBM + cc]);
-    const float* wr = W + (long long)col * ldw + dbase;
     float* o = dW + (long long)col * lddw + dbase;
 #pragma unroll
-    for (int t = 0; t < NTW; ++t) o[32 * t] = (acc[t][q] - wr[32 * t] * inv * dot) * inv;
+    for (int t = 0; t < NTW; ++t) o[32 * t] = (acc[t][q] - wv[q][t] * inv * dot) * inv;
   }
 }
 
@@ -589,7 +658,9 @@ int launch_arc_bwd_mma(const float* dlogits, const float* cosv, const long long*
   Fn fn = D == 128 ? &arc_bwd_mma_kernel<1> : D == 256 ? &arc_bwd_mma_kernel<2>
         : D == 512 ? &arc_bwd_mma_kernel<4> : D == 640 ? &arc_bwd_mma_kernel<5> : nullptr;
   if (!fn || ldw % 4 || lddw % 4) return -1;
-  const int lds = (((rows_per + RBM) * (CBM + 1) * 4 + 15) & ~15) + RBM * (D + 4) * 4;
+  const bool whole = D <= 256 && rows_per <= ARC_WHOLE;
+  const int dc_rows = whole ? (rows_per + 1) & ~1 : rows_per + RBM;
+  const int lds = ((dc_rows * (CBM + 1) * 4 + 15) & ~15) + (whole ? dc_rows : RBM) * (D + 4) * 4;
   if (lds > 160 * 1024) return -1;
   if (const int e = set_max_lds((const void*)fn, lds)) return e;
   hipLaunchKernelGGL(fn, dim3((C + CBM - 1) / CBM, S, n_heads), dim3(NT), lds,

@@ -544,26 +544,6 @@ constexpr int SNT = 576;                 // threads per workgroup: 9 waves, one 
                                          // 16x16 tile of a 36 x 36 product
 constexpr int SLD = (64 * 64 + SNT - 1) / SNT;   // max elements per thread per operand
 
-// max / sum over the 16 lanes of a DPP row, in every lane: mirror (i <->
-// 15 - i), half mirror (i <-> 7 - i), then quad xor 1 and xor 2.
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-  return __builtin_bit_cast(
-      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float row16_max(float v) {
-  v = fmaxf(v, dpp<0x140>(v));
-  v = fmaxf(v, dpp<0x141>(v));
-  v = fmaxf(v, dpp<0xB1>(v));
-  return fmaxf(v, dpp<0x4E>(v));
-}
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dpp<0x140>(v);
-  v += dpp<0x141>(v);
-  v += dpp<0xB1>(v);
-  return v + dpp<0x4E>(v);
-}
-
 // out(m, n) = sum_k A(m, k) B(n, k), A(m, k) = A[m am + k ak], B likewise;
 // 16x16 tiles dealt to the waves round robin starting at wave w0.
 template <typename Store>

@@ -227,6 +227,34 @@ __device__ __forceinline__ float xhalf_max(float v) {
   return __builtin_fmaxf(__int_as_float(r[0]), __int_as_float(r[1]));
 }
 
+// max / sum over the 16 lanes of a DPP row, in every lane: mirror (i <->
+// 15 - i), half mirror (i <-> 7 - i), then quad xor 1 and xor 2.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp<0x140>(v));
+  v = fmaxf(v, dpp<0x141>(v));
+  v = fmaxf(v, dpp<0xB1>(v));
+  return fmaxf(v, dpp<0x4E>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp<0x140>(v);
+  v += dpp<0x141>(v);
+  v += dpp<0xB1>(v);
+  return v + dpp<0x4E>(v);
+}
+
+// v summed with lane l ^ 16 by v_permlane16_swap (VALU, no LDS round trip);
+// with row16_sum first: the sum over each 32-lane half, in every lane
+__device__ __forceinline__ float x16_sum(float v) {
+  const int u = __float_as_int(v);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __int_as_float(r[0]) + __int_as_float(r[1]);
+}
+
 __device__ __forceinline__ float half_max(float v) {
 #pragma unroll
   for (int m = 16; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));

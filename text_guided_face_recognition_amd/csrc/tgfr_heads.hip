@@ -126,20 +126,43 @@ __global__ __launch_bounds__(256) void focal_ce_kernel(const float* __restrict__
   }
   const int b = blockIdx.x, wid = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
   const float* r = L + (long long)b * cols;
-  float m = -INFINITY;
-  for (int c = threadIdx.x; c < cols; c += 256) m = fmaxf(m, r[c]);
-  m = wave_max(m);
-  if (lane == 0) red[wid] = m;
-  __syncthreads();
-  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  __syncthreads();
-  float sum = 0.f;
-  for (int c = threadIdx.x; c < cols; c += 256) sum += __expf(r[c] - m);
-  sum = wave_sum(sum);
-  if (lane == 0) red[wid] = sum;
+  // one pass, online log-sum-exp: 4 loads in flight per thread per step
+  float m = -INFINITY, sum = 0.f;
+  for (int c0 = threadIdx.x; c0 < cols; c0 += 4 * 256) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = c0 + 256 * u < cols ? r[c0 + 256 * u] : -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (v[u] > m) {
+        sum = sum * __expf(m - v[u]) + 1.f;
+        m = v[u];
+      } else if (v[u] != -INFINITY) {
+        sum += __expf(v[u] - m);
+      }
+    }
+  }
+  // combine (m, sum) over the wave, then over the 4 waves
+#pragma unroll
+  for (int k = 32; k >= 1; k >>= 1) {
+    const float m2 = __shfl_xor(m, k), s2 = __shfl_xor(sum, k);
+    const float mm = fmaxf(m, m2);
+    sum = (m == -INFINITY ? 0.f : sum * __expf(m - mm)) +
+          (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mm));
+    m = mm;
+  }
+  __shared__ float rm[4];
+  if (lane == 0) {
+    rm[wid] = m;
+    red[wid] = sum;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float lse = m + __logf(red[0] + red[1] + red[2] + red[3]);
+    const float mm = fmaxf(fmaxf(rm[0], rm[1]), fmaxf(rm[2], rm[3]));
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tot += rm[k] == -INFINITY ? 0.f : red[k] * __expf(rm[k] - mm);
+    const float lse = mm + __logf(tot);
     ws[b] = lse;
     ws[rows + 1 + b] = lse - r[label[b]];
   }

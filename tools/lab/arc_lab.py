@@ -17,7 +17,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "lab", "build")
-NAME = "tgfr_arc.hip"
+NAME = os.environ.get("LAB_FILE", "tgfr_arc.hip")
 
 ALL_VARIANTS = {
     "base": [],
@@ -64,10 +64,12 @@ def step():
 for _ in range(3):
     step()
 torch.cuda.synchronize()
-with H.KernelTimer(replay=("tgfr_arc_fwd_heads", "tgfr_arc_focal_bwd_heads"), reps=100) as kt:
+with H.KernelTimer(replay=("tgfr_arc_fwd_heads", "tgfr_arc_focal_bwd_heads", "tgfr_focal_ce2"),
+                  reps=100) as kt:
     step()
 f, g = kt.replayed["tgfr_arc_fwd_heads"], kt.replayed["tgfr_arc_focal_bwd_heads"]
-print(f"{name}: fwd {{f*1000:.1f}} us  bwd {{g*1000:.1f}} us", flush=True)
+fc = kt.replayed.get("tgfr_focal_ce2", 0.0)
+print(f"{name}: fwd {{f*1000:.1f}} us  bwd {{g*1000:.1f}} us  focal {{fc*1000:.1f}} us", flush=True)
 '''
 
 
@@ -112,11 +114,11 @@ def run():
             if res.returncode:
                 sys.stdout.write(res.stderr[-1500:])
                 continue
-            m = re.search(r"fwd ([\d.]+) us  bwd ([\d.]+) us", res.stdout)
-            times.setdefault(name, []).append((float(m.group(1)), float(m.group(2))))
+            m = re.search(r"fwd ([\d.]+) us  bwd ([\d.]+) us  focal ([\d.]+) us", res.stdout)
+            times.setdefault(name, []).append(tuple(float(m.group(k)) for k in (1, 2, 3)))
     for name, ts in times.items():
         print(f"SUMMARY {name:10s} fwd min {min(t[0] for t in ts):6.1f}  "
-              f"bwd min {min(t[1] for t in ts):6.1f} us")
+              f"bwd min {min(t[1] for t in ts):6.1f}  focal min {min(t[2] for t in ts):6.1f} us")
 
 
 if __name__ == "__main__":

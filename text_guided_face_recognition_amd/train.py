@@ -141,7 +141,9 @@ class Train:
         # forward (no loss-mix backward launch, no join).  One stream: on
         # MI355X the step replays faster as a linear graph than with the
         # branches forked onto side streams (0.665 vs 0.694 ms at config 2,
-        # tools/lab/branch_ab.py) -- the word<->region kernels fill the chip.
+        # round 2) -- the word<->region kernels fill the chip.  Forking only
+        # the frozen TextHeading off the image head's forward loses too
+        # (0.596 vs 0.573 ms, round 3).
         wi, lc = float(args.lambda_id), float(args.lambda_clip)
         s0, s1, cl = sent_global_loss(img_features, sent_g, labels, cls_g, b, args)  # :276, :310
         # :293-306, both focal losses from the global-batch mean CE

@@ -331,11 +331,15 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const float* __restr
 
 // dK / dV: one 4-wave workgroup per (sample, pair of key tiles); wave
 // (kk, half) = (w >> 1, w & 1) owns columns [128 half, +128) of dKr and dV
-// for key tile 2 j + kk; all four recompute S and dP of their key tile in
-// full.  The Qr and dO tiles of each query tile are DMA-staged once for the
-// four waves (double buffer).  LDS: Kr and V images of both key tiles
-// [0, 4 IMG), then 2 stages x (Qr, dO) [4 IMG, 8 IMG), then lse / D.
-constexpr int KV_LDS = 8 * IMG + 2 * 32 * AT * 4;
+// for key tile 2 j + kk.  Per query tile the pair splits the recompute: wave
+// half 0 forms S = Qr Kr^T, half 1 dP = dO V^T (16 MFMAs each instead of 32,
+// and each holds only its own key tile's fragments), and they swap the
+// 32 x 32 results through LDS.  The Qr and dO tiles of each query tile are
+// DMA-staged once for the four waves (double buffer).  LDS: Kr and V images
+// of both key tiles [0, 4 IMG), then 2 stages x (Qr, dO) [4 IMG, 8 IMG),
+// then lse / D, then the S / dP exchange [4 waves][16][64] fp32.
+constexpr int KV_XCH = 8 * IMG + 2 * 32 * AT * 4;
+constexpr int KV_LDS = KV_XCH + 4 * 16 * 64 * 4;
 
 __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(
     const uint16_t* __restrict__ Qp, const uint16_t* __restrict__ Kp,
@@ -371,28 +375,46 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dk[t][r] = dv[t][r] = 0.f;
-  // the key tile's Kr / V operand fragments, held for the whole loop
-  bf16x8 kf[AD / 16], vf[AD / 16];
+  // this wave's operand fragments (Kr for half 0, V for half 1), held for
+  // the whole loop
+  bf16x8 kf[AD / 16];
 
   for (int qt = 0; qt < nt; ++qt) {
     // every outstanding op of this wave is this stage's DMA or older
     ring_barrier<0>();
     if (qt == 0) {
 #pragma unroll
-      for (int s = 0; s < AD / 16; ++s) {
-        kf[s] = frag(KI, s, lane);
-        vf[s] = frag(VI, s, lane);
-      }
+      for (int s = 0; s < AD / 16; ++s) kf[s] = frag(half ? VI : KI, s, lane);
     }
     if (qt + 1 < nt) issue(qt + 1);
     const uint32_t QI = ST + (qt & 1) * 2 * IMG, OI = QI + IMG;
+    // half 0: S = Qr Kr^T; half 1: dP = dO V^T; then swap with the partner
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+    const uint32_t AI = half ? OI : QI;
+#pragma unroll
+    for (int s = 0; s < AD / 16; s += 2) {     // two chains: half the dependent latency
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(AI, s, lane), kf[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(AI, s + 1, lane), kf[s + 1], acc1, 0,
+                                                     0, 0);
+    }
     f32x16 sacc, pacc;
+    {
+      const uint32_t mine = KV_XCH + (uint32_t)(w * 16 * 64 + lane) * 4;
+      const uint32_t other = KV_XCH + (uint32_t)((w ^ 1) * 16 * 64 + lane) * 4;
+      f32x16 own;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) sacc[r] = pacc[r] = 0.f;
+      for (int r = 0; r < 16; ++r) {
+        own[r] = acc0[r] + acc1[r];
+        lds_stf(mine + r * 64 * 4, own[r]);
+      }
+      __syncthreads();
+      f32x16 par;
 #pragma unroll
-    for (int s = 0; s < AD / 16; ++s) {
-      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(QI, s, lane), kf[s], sacc, 0, 0, 0);
-      pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(OI, s, lane), vf[s], pacc, 0, 0, 0);
+      for (int r = 0; r < 16; ++r) par[r] = lds_ldf(other + r * 64 * 4);
+      sacc = half ? par : own;
+      pacc = half ? own : par;
     }
     // lane: key column; register r: query 32 qt + acc_row(r, h)
     float pv[16], ds[16];

@@ -39,6 +39,31 @@ ALL_VARIANTS = {
 VARIANTS = {k: v for k, v in ALL_VARIANTS.items()
             if k in os.environ.get("LAB_ONLY", ",".join(ALL_VARIANTS)).split(",")}
 
+ATTN_CHILD = r'''
+import ctypes, sys, torch
+sys.path.insert(0, {root!r})
+sys.path.insert(0, {root!r} + "/tests")
+from text_guided_face_recognition_amd import _hip as H
+lib = ctypes.CDLL({lib!r}, mode=ctypes.RTLD_GLOBAL)
+for n, a in H.SIGNATURES.items():
+    f = getattr(lib, n, None)
+    if f is not None:
+        f.argtypes = a; f.restype = ctypes.c_int
+H._lib = lib
+from test_gpu_attn import _attn
+nb, hw = int({b!r}), 196
+g = torch.Generator(device="cuda").manual_seed(0)
+pxb = torch.randn(nb, hw, 768, generator=g, device="cuda").to(torch.bfloat16)
+do = torch.randn(nb, hw, 256, generator=g, device="cuda")
+for _ in range(3):
+    _attn(pxb, do, 1 / 16)
+torch.cuda.synchronize()
+with H.KernelTimer(replay=("tgfr_attn_fwd", "tgfr_attn_bwd"), reps=100) as kt:
+    _attn(pxb, do, 1 / 16)
+f, g = kt.replayed["tgfr_attn_fwd"], kt.replayed["tgfr_attn_bwd"]
+print(f"{name}: fwd {{f*1000:.1f}} us  bwd {{g*1000:.1f}} us  focal 0.0 us", flush=True)
+'''
+
 CHILD = r'''
 import ctypes, sys, torch
 sys.path.insert(0, {root!r})
@@ -107,7 +132,11 @@ def run():
     for _ in range(rounds):
         for name in VARIANTS:
             lib = os.path.join(OUT, f"arc_{name}.so")
-            code = CHILD.format(root=ROOT, lib=lib, name=name)
+            if os.environ.get("LAB_CASE") == "attn":
+                code = ATTN_CHILD.format(root=ROOT, lib=lib, name=name,
+                                         b=os.environ.get("LAB_B", "64"))
+            else:
+                code = CHILD.format(root=ROOT, lib=lib, name=name)
             res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
                                  timeout=300)
             sys.stdout.write(res.stdout)

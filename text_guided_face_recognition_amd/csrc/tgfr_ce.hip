@@ -237,7 +237,7 @@ constexpr int SG_T = 1024;                   // 16 waves
 __device__ __forceinline__ void sg_cos_tile(const float* __restrict__ x, long long ldx, int n_x,
                                             const float* __restrict__ y, long long ldy, int n_y,
                                             float eps, float* cs, float (*nxp)[SG_N],
-                                            float (*nyp)[SG_N]) {
+                                            float (*nyp)[SG_N], float* gcos = nullptr) {
   // LDS: x rows | y rows (fp32, padded) | cos [64][65]; the MFMA partials
   // reuse the row area once the products are done
   float* xs = (float*)g_smem;
@@ -304,7 +304,9 @@ __device__ __forceinline__ void sg_cos_tile(const float* __restrict__ x, long lo
     for (int k4 = 0; k4 < 4; ++k4) v += part[((tt + 4 * k4) * 16 + q) * 64 + ln];
     const float nx = nxp[0][r] + nxp[1][r] + nxp[2][r] + nxp[3][r];
     const float ny = nyp[0][c] + nyp[1][c] + nyp[2][c] + nyp[3][c];
-    cs[r * (SG_N + 1) + c] = v / fmaxf(sqrtf(nx) * sqrtf(ny), eps);
+    const float cv = v / fmaxf(sqrtf(nx) * sqrtf(ny), eps);
+    cs[r * (SG_N + 1) + c] = cv;
+    if (gcos) gcos[r * n_y + c] = cv;          // dense [n_x][n_y] copy (nullable)
   }
   __syncthreads();
 }
@@ -317,47 +319,42 @@ __global__ __launch_bounds__(SG_T) void sg_fwd_kernel(
   float* cs = (float*)g_smem + 2 * SG_N * SG_LD;
   __shared__ float nxp[4][SG_N], nyp[4][SG_N];
   __shared__ long long cl[SG_N];
-  __shared__ float red[16];
+  __shared__ float red[4 * 16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (tid < n) cl[tid] = cls[tid];
-  sg_cos_tile(x, ldx, n, y, ldy, n, eps, cs, nxp, nyp);
-  for (int e = tid; e < n * n; e += SG_T) cosv[e] = cs[(e / n) * (SG_N + 1) + e % n];
-  __syncthreads();
-  // logit set ls = w >> 2 (0: sent rows, 1: sent columns, 2: global rows,
-  // 3: global columns); row / column j = 16 (w & 3) + lane / 4, four lanes
-  // per row each taking every fourth element (online log-sum-exp, combined)
-  const int ls = w >> 2, j = 16 * (w & 3) + (lane >> 2), sub = lane & 3;
-  const bool glob = ls >= 2, col = ls & 1;
-  const float sc = glob ? s_glob : s_sent;
-  float m = -INFINITY, sum = 0.f;
-  if (j < n) {
-    for (int k = sub; k < n; k += 4) {
-      const int b = col ? k : j, i = col ? j : k;
-      if (!glob && cl[b] == cl[i] && b != i) continue;
-      const float L = sc * cs[b * (SG_N + 1) + i];
-      if (L > m) {
-        sum = sum * __expf(m - L) + 1.f;
-        m = L;
-      } else {
-        sum += __expf(L - m);
-      }
-    }
-  }
+  sg_cos_tile(x, ldx, n, y, ldy, n, eps, cs, nxp, nyp, cosv);
+  // logit sets ls = 0..3 (sent rows, sent columns, global rows, global
+  // columns) in turn; row / column j = 4 w + lane / 16 of the set, 16 lanes
+  // (one DPP row) per row, each taking every 16th element
+  const int j = 4 * w + (lane >> 4), sub = lane & 15;
 #pragma unroll
-  for (int msk = 1; msk <= 2; msk <<= 1) {
-    const float m2 = __shfl_xor(m, msk), s2 = __shfl_xor(sum, msk);
-    const float mm = fmaxf(m, m2);
-    sum = (m == -INFINITY ? 0.f : sum * __expf(m - mm)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mm));
-    m = mm;
+  for (int ls = 0; ls < 4; ++ls) {
+    const bool glob = ls >= 2, col = ls & 1;
+    const float sc = glob ? s_glob : s_sent;
+    float L[SG_N / 16];
+    float m = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < SG_N / 16; ++u) {
+      const int k = sub + 16 * u;
+      const int b = col ? k : j, i = col ? j : k;
+      const bool ok = j < n && k < n && (glob || cl[b] != cl[i] || b == i);
+      L[u] = ok ? sc * cs[b * (SG_N + 1) + i] : -INFINITY;
+      m = fmaxf(m, L[u]);
+    }
+    m = row16_max(m);
+    float sum = 0.f;
+#pragma unroll
+    for (int u = 0; u < SG_N / 16; ++u) sum += L[u] == -INFINITY ? 0.f : __expf(L[u] - m);
+    sum = row16_sum(sum);
+    float term = 0.f;
+    if (j < n && sub == 0) {
+      const float lse = m + __logf(sum);
+      stats[ls * n + j] = lse;
+      term = lse - sc * cs[j * (SG_N + 1) + j];
+    }
+    term = wave_sum(term);
+    if (lane == 0) red[ls * 16 + w] = term;
   }
-  float term = 0.f;
-  if (j < n && sub == 0) {
-    const float lse = m + __logf(sum);
-    stats[ls * n + j] = lse;
-    term = lse - sc * cs[j * (SG_N + 1) + j];
-  }
-  term = wave_sum(term);
-  if (lane == 0) red[w] = term;
   if (tid < n) {
     nrm[tid] = sqrtf(nxp[0][tid] + nxp[1][tid] + nxp[2][tid] + nxp[3][tid]);
     nrm[n + tid] = sqrtf(nyp[0][tid] + nyp[1][tid] + nyp[2][tid] + nyp[3][tid]);
@@ -366,7 +363,11 @@ __global__ __launch_bounds__(SG_T) void sg_fwd_kernel(
   if (tid == 0) {
     float l4[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) l4[k] = (red[4 * k] + red[4 * k + 1]) + (red[4 * k + 2] + red[4 * k + 3]);
+    for (int k = 0; k < 4; ++k) {
+      l4[k] = 0.f;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) l4[k] += red[16 * k + v];
+    }
     const float inv = 1.f / (float)n;
     loss[0] = l4[0] * inv;                   // sent loss0 (rows)
     loss[1] = l4[1] * inv;                   // sent loss1 (columns)

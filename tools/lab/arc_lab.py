@@ -32,12 +32,45 @@ ALL_VARIANTS = {
     "bwd_nodcs": [("          if (dcs) dcs[", "          if (false) dcs[")],
     "bwd_nodot": [("    for (int t = 0; t < NTW; ++t) sdot = fmaf(wr[32 * t], acc[t][q], sdot);\n",
                    "    for (int t = 0; t < 0; ++t) sdot = fmaf(wr[32 * t], acc[t][q], sdot);\n")],
+    "sg_nolse": [("    for (int k = sub; k < n; k += 4) {\n      const int b = col ? k : j, i = col ? j : k;",
+                  "    for (int k = sub; k < 0; k += 4) {\n      const int b = col ? k : j, i = col ? j : k;")],
+    "sg_nocosv": [("  for (int e = tid; e < n * n; e += SG_T) cosv[e] = cs[(e / n) * (SG_N + 1) + e % n];",
+                   "")],
+    "sg_nocosasm": [("    cs[r * (SG_N + 1) + c] = v / fmaxf(sqrtf(nx) * sqrtf(ny), eps);",
+                     "    cs[r * (SG_N + 1) + c] = v;")],
     "bwd_noepi": [("    for (int t = 0; t < NTW; ++t) o[32 * t] = (acc[t][q] - wr[32 * t] * inv * dot) * inv;",
                    "    for (int t = 0; t < NTW; ++t) o[32 * t] = acc[t][q];")],
 }
 
 VARIANTS = {k: v for k, v in ALL_VARIANTS.items()
             if k in os.environ.get("LAB_ONLY", ",".join(ALL_VARIANTS)).split(",")}
+
+SG_CHILD = r'''
+import ctypes, sys, torch
+sys.path.insert(0, {root!r})
+from text_guided_face_recognition_amd import _hip as H
+lib = ctypes.CDLL({lib!r}, mode=ctypes.RTLD_GLOBAL)
+for n, a in H.SIGNATURES.items():
+    f = getattr(lib, n, None)
+    if f is not None:
+        f.argtypes = a; f.restype = ctypes.c_int
+H._lib = lib
+from text_guided_face_recognition_amd import kernels as K
+torch.manual_seed(0)
+x = torch.randn(64, 256, device="cuda", requires_grad=True)
+y = torch.randn(64, 256, device="cuda")
+cls = torch.randint(0, 40, (64,), device="cuda")
+def step():
+    a, b_, c = K.sent_global(x, y, cls, 10.0, 10.0)
+    (a + b_ + 2 * c).backward()
+for _ in range(3):
+    step()
+torch.cuda.synchronize()
+with H.KernelTimer(replay=("tgfr_sent_global", "tgfr_sent_global_bwd"), reps=100) as kt:
+    step()
+f, g = kt.replayed["tgfr_sent_global"], kt.replayed["tgfr_sent_global_bwd"]
+print(f"{name}: fwd {{f*1000:.1f}} us  bwd {{g*1000:.1f}} us  focal 0.0 us", flush=True)
+'''
 
 ATTN_CHILD = r'''
 import ctypes, sys, torch
@@ -132,7 +165,9 @@ def run():
     for _ in range(rounds):
         for name in VARIANTS:
             lib = os.path.join(OUT, f"arc_{name}.so")
-            if os.environ.get("LAB_CASE") == "attn":
+            if os.environ.get("LAB_CASE") == "sg":
+                code = SG_CHILD.format(root=ROOT, lib=lib, name=name)
+            elif os.environ.get("LAB_CASE") == "attn":
                 code = ATTN_CHILD.format(root=ROOT, lib=lib, name=name,
                                          b=os.environ.get("LAB_B", "64"))
             else:

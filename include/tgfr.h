@@ -331,12 +331,10 @@ int tgfr_focal_ce_bwd(const float* L, int rows, int cols, const long long* label
  * x [rows][E] (row-contiguous, E % 4 == 0, 16-B aligned), affine w, b of E
  * elements: indexed like a row (ch == 0), or stored channel-major [ch][E/ch]
  * for rows laid out [E/ch][ch] (ch > 0, ch % 4 == 0): LayerNorm([C, H, W])
- * weights applied to channels-last rows (the forward transposes w, b once
- * into ws).
+ * weights applied to channels-last rows (read in place, no transposed copy).
  * y = (x - mean_r) / sqrt(var_r + eps) * w + b with biased var_r, as
  * nn.LayerNorm.  ws: tgfr_ln_ws_floats(rows, E, ch, 1) floats; the forward
- * leaves mean/rstd (and, ch > 0, channels-last copies of w and b) in it for
- * the backward (pass the same ws). */
+ * leaves mean/rstd in it for the backward (pass the same ws). */
 int tgfr_ln_ws_floats(int rows, long long E, int ch, int backward, long long* out);
 int tgfr_ln_fwd(const float* x, int rows, long long E, const float* w, const float* b, float eps,
                 int ch, float* y, float* ws, void* stream);

@@ -42,30 +42,15 @@ __device__ __forceinline__ long long aidx(long long e, int ch, long long E) {
   return ch ? (e % ch) * (E / ch) + e / ch : e;
 }
 
-// wt[p * ch + c] = w[c * n + p] (n = E / ch), same for b: 32 x 32 LDS tiles.
-__global__ __launch_bounds__(NT) void ln_aff_t_kernel(const float* __restrict__ w,
-                                                      const float* __restrict__ b, int ch, int n,
-                                                      float* __restrict__ wt,
-                                                      float* __restrict__ bt) {
-  __shared__ float tile[2][32][33];
-  const int c0 = blockIdx.y * 32, p0 = blockIdx.x * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 8 rows per pass
-#pragma unroll
-  for (int k = 0; k < 32; k += 8) {
-    const int c = c0 + ty + k, p = p0 + tx;
-    const bool ok = c < ch && p < n;
-    tile[0][ty + k][tx] = ok ? w[(long long)c * n + p] : 0.f;
-    tile[1][ty + k][tx] = ok ? b[(long long)c * n + p] : 0.f;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 32; k += 8) {
-    const int p = p0 + ty + k, c = c0 + tx;
-    if (p < n && c < ch) {
-      wt[(long long)p * ch + c] = tile[0][tx][ty + k];
-      bt[(long long)p * ch + c] = tile[1][tx][ty + k];
-    }
-  }
+// The affine values of channels-last elements 4 i4 .. 4 i4 + 3 (one position
+// p, channels c .. c + 3) read from the reference's channel-major [ch][n]
+// map in place (ch = 0: the map is row-indexed like x).  No per-step
+// transposed copy of the map.
+__device__ __forceinline__ float4 aff4(const float* __restrict__ a, long long i4, int ch, int n) {
+  if (!ch) return ((const float4*)a)[i4];
+  const int e = (int)(4 * i4), p = e / ch, c = e - p * ch;
+  const float* q = a + (long long)c * n + p;
+  return make_float4(q[0], q[n], q[2 * n], q[3 * n]);
 }
 
 struct Slice {
@@ -129,8 +114,8 @@ constexpr int LN_GROUP = 8;   // samples per ln_apply / ln_bwd_dx block
 // grid (ceil(E/4 / NT), ceil(rows / LN_GROUP)); w, b row-indexed ([E]).
 __global__ __launch_bounds__(NT) void ln_apply_kernel(const float* __restrict__ x, long long E,
                                                       int S, const float* __restrict__ w,
-                                                      const float* __restrict__ bias, float eps,
-                                                      const float* __restrict__ part,
+                                                      const float* __restrict__ bias, int ch,
+                                                      float eps, const float* __restrict__ part,
                                                       float* __restrict__ stats, int rows,
                                                       float* __restrict__ y) {
   __shared__ float ms[2][LN_GROUP];
@@ -149,7 +134,8 @@ __global__ __launch_bounds__(NT) void ln_apply_kernel(const float* __restrict__ 
   __syncthreads();
   const long long i = blockIdx.x * (long long)NT + threadIdx.x;
   if (i >= E / 4) return;
-  const float4 ww = ((const float4*)w)[i], bb = ((const float4*)bias)[i];
+  const int n = ch ? (int)(E / ch) : 0;
+  const float4 ww = aff4(w, i, ch, n), bb = aff4(bias, i, ch, n);
   float4 v[LN_GROUP];
 #pragma unroll
   for (int k = 0; k < LN_GROUP; ++k)
@@ -168,18 +154,18 @@ __global__ __launch_bounds__(NT) void ln_apply_kernel(const float* __restrict__ 
 __global__ __launch_bounds__(NT) void ln_bwd_part_kernel(const float* __restrict__ dy,
                                                          const float* __restrict__ x, long long E,
                                                          int S, const float* __restrict__ w,
-                                                         const float* __restrict__ stats, int rows,
-                                                         float* __restrict__ part) {
+                                                         int ch, const float* __restrict__ stats,
+                                                         int rows, float* __restrict__ part) {
   __shared__ float red[4];
   const int b = blockIdx.y, s = blockIdx.x;
   const Slice sl = slice_of(E, S, s);
   const float mean = stats[b], rstd = stats[rows + b];
   const float4* xr = (const float4*)(x + (long long)b * E);
   const float4* gr = (const float4*)(dy + (long long)b * E);
-  const float4* w4 = (const float4*)w;
+  const int n = ch ? (int)(E / ch) : 0;
   float sg = 0.f, sgx = 0.f;
   for (long long i = sl.lo / 4 + threadIdx.x; i < sl.hi / 4; i += NT) {
-    const float4 d = gr[i], ww = w4[i], v = xr[i];
+    const float4 d = gr[i], ww = aff4(w, i, ch, n), v = xr[i];
     const float ga = d.x * ww.x, gb = d.y * ww.y, gc = d.z * ww.z, gd = d.w * ww.w;
     sg += (ga + gb) + (gc + gd);
     sgx += (ga * (v.x - mean) + gb * (v.y - mean)) + (gc * (v.z - mean) + gd * (v.w - mean));
@@ -197,7 +183,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_part_kernel(const float* __restrict
 // loops over the samples of its group; dwp/dbp [n_groups][E] partials.
 __global__ __launch_bounds__(NT) void ln_bwd_dx_kernel(
     const float* __restrict__ dy, const float* __restrict__ x, long long E, int S,
-    const float* __restrict__ w, const float* __restrict__ stats, int rows,
+    const float* __restrict__ w, int ch, const float* __restrict__ stats, int rows,
     const float* __restrict__ part, int per_group, float* __restrict__ dx,
     float* __restrict__ dwp, float* __restrict__ dbp) {
   __shared__ float coef[3][64];
@@ -216,7 +202,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_dx_kernel(
   __syncthreads();
   const long long i = blockIdx.x * (long long)NT + threadIdx.x;
   if (i >= E / 4) return;
-  const float4 ww = ((const float4*)w)[i];
+  const float4 ww = aff4(w, i, ch, ch ? (int)(E / ch) : 0);
   float4 dw = make_float4(0.f, 0.f, 0.f, 0.f), db = dw;
   for (int b = g0; b < g1; ++b) {
     const float mean = stats[b], rstd = coef[0][b - g0];
@@ -257,10 +243,10 @@ int slices_for(int rows, long long E) {
   return (int)std::max<long long>(1, s);
 }
 
-// Workspace floats: part [rows][S][2] | mean [rows] | rstd [rows] | (ch > 0)
-// channels-last w, b [2][E] -- all written by the forward and read by the
-// backward -- then (backward) dw, db group partials [2][G][E], G =
-// ceil(rows / LN_GROUP).
+// Workspace floats: part [rows][S][2] | mean [rows] | rstd [rows] -- written
+// by the forward and read by the backward -- then (backward) dw, db group
+// partials [2][G][E], G = ceil(rows / LN_GROUP).  (The channel-major affine
+// maps are read in place, aff4.)
 struct LnWs {
   long long stats, aff, bwd, total_fwd, total_bwd;
 };
@@ -269,7 +255,7 @@ LnWs ln_ws(int rows, long long E, int ch) {
   LnWs o;
   o.stats = rows * S * 2;
   o.aff = o.stats + 2LL * rows;
-  o.bwd = o.aff + (ch ? 2 * E : 0);
+  o.bwd = o.aff;
   o.total_fwd = o.bwd;
   o.total_bwd = o.bwd + 2LL * ((rows + LN_GROUP - 1) / LN_GROUP) * E;
   return o;
@@ -299,20 +285,10 @@ int tgfr_ln_fwd(const float* x, int rows, long long E, const float* w, const flo
   float* part = ws;
   float* stats = ws + o.stats;
   auto* st = (hipStream_t)stream;
-  const float* wr = w;
-  const float* br = b;
-  if (ch) {
-    float* wt = ws + o.aff;
-    const int n = (int)(E / ch);
-    hipLaunchKernelGGL(ln_aff_t_kernel, dim3((n + 31) / 32, (ch + 31) / 32), dim3(NT), 0, st, w,
-                       b, ch, n, wt, wt + E);
-    wr = wt;
-    br = wt + E;
-  }
   hipLaunchKernelGGL(ln_part_kernel, dim3(S, rows), dim3(NT), 0, st, x, E, S, part);
   hipLaunchKernelGGL(ln_apply_kernel,
                      dim3((unsigned)((E / 4 + NT - 1) / NT), (rows + LN_GROUP - 1) / LN_GROUP),
-                     dim3(NT), 0, st, x, E, S, wr, br, eps, part, stats, rows, y);
+                     dim3(NT), 0, st, x, E, S, w, b, ch, eps, part, stats, rows, y);
   return (int)hipGetLastError();
 }
 
@@ -326,15 +302,15 @@ int tgfr_ln_bwd(const float* dy, const float* x, int rows, long long E, const fl
   const int groups = (rows + LN_GROUP - 1) / LN_GROUP;
   float* part = ws;
   const float* stats = ws + o.stats;
-  const float* wr = ch ? ws + o.aff : w;
   float* dwp = ws + o.bwd;
   float* dbp = dwp + (long long)groups * E;
   auto* st = (hipStream_t)stream;
   // the forward's slice moments are no longer needed: reuse their slots
-  hipLaunchKernelGGL(ln_bwd_part_kernel, dim3(S, rows), dim3(NT), 0, st, dy, x, E, S, wr, stats,
-                     rows, part);
+  hipLaunchKernelGGL(ln_bwd_part_kernel, dim3(S, rows), dim3(NT), 0, st, dy, x, E, S, w, ch,
+                     stats, rows, part);
   hipLaunchKernelGGL(ln_bwd_dx_kernel, dim3((unsigned)((E / 4 + NT - 1) / NT), groups),
-                     dim3(NT), 0, st, dy, x, E, S, wr, stats, rows, part, LN_GROUP, dx, dwp, dbp);
+                     dim3(NT), 0, st, dy, x, E, S, w, ch, stats, rows, part, LN_GROUP, dx, dwp,
+                     dbp);
   hipLaunchKernelGGL(ln_bwd_dw_kernel, dim3((unsigned)((E + NT - 1) / NT)), dim3(NT), 0, st,
                      dwp, dbp, E, groups, ch, dw, db);
   return (int)hipGetLastError();

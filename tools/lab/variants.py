@@ -26,15 +26,13 @@ _OLD_PAD_SKIP = ("  // ---- prologue: G1 of caption 0\n",
             "    return;\n  }\n"
             "  // ---- prologue: G1 of caption 0\n")
 
-# round 3: the T <= 32 bounded backward (wr_bwd_pipe_kernel)
+# round 3: LDS operand prefetch distance of the bounded forward (wr_fwd_pipe_kernel)
 VARIANTS = {
     "base": [],
-    "head": "HEAD",
-    # LDS operand reads 4 / 5 MFMA slots ahead instead of 3
-    "pf4": [("constexpr int PF_BWD = 3;", "constexpr int PF_BWD = 4;")],
-    "pf5": [("constexpr int PF_BWD = 3;", "constexpr int PF_BWD = 5;")],
+    "fpf4": [("constexpr int PF_FWD = 3;", "constexpr int PF_FWD = 4;")],
+    "fpf5": [("constexpr int PF_FWD = 3;", "constexpr int PF_FWD = 5;")],
+    "fpf6": [("constexpr int PF_FWD = 3;", "constexpr int PF_FWD = 6;")],
 }
-
 
 
 def build_variant(name, subs):

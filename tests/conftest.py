@@ -44,3 +44,16 @@ def text_heading_golden(name):
     assert np.array_equal(words, g["words_emb"])
     g["conv_w"], g["conv_b"] = ws, bs
     return g
+
+
+def words_seeded_golden(name):
+    """A full-shape words_loss fixture with its inputs regenerated from the
+    stored seed (tests/golden/make_golden.py:words_seeded_inputs), checked
+    against the stored input checksums: (fixture, R [B,256,14,14], W [B,256,T])."""
+    from tests.golden.make_golden import words_seeded_inputs
+    g = load_golden(name)
+    b, L = int(g["batch"]), int(g["bert_words_num"])
+    r, w = words_seeded_inputs(int(g["seed"]), b, L - 2)
+    assert abs(r.double().sum().item() - float(g["r_sum"])) < 1e-9
+    assert abs(w.double().sum().item() - float(g["w_sum"])) < 1e-9
+    return g, r, w

@@ -33,7 +33,8 @@ def main():
                          bert_words_num=24)
         return Train(args, dev, ctx)
 
-    batch = synthetic_batch(8, 22, dev, seed=40 + ctx.rank, n_ids=200)
+    bert = os.environ.get("TGFR_DP_BERT", "0") == "1"
+    batch = synthetic_batch(8, 22, dev, seed=40 + ctx.rank, n_ids=200, bert_hidden=bert)
     eager, graphed = build(), build()
     outs_e = [eager.step(batch) for _ in range(5)]
     gs = GraphedStep(graphed, tuple(t.clone() for t in batch), warmup=3)
@@ -44,7 +45,8 @@ def main():
     err_par = max((a - b).abs().max().item()
                   for a, b in zip(graphed.params, eager.params))
     # replicas identical across ranks
-    flat = torch.cat([p.detach().reshape(-1) for p in graphed.params]).unsqueeze(0)
+    flat = torch.cat([p.detach().reshape(-1) for p in graphed.params +
+                      list(graphed.text_head.parameters())]).unsqueeze(0)
     allp = all_gather_cat(flat, ctx.group)
     err_rank = (allp[0] - allp[1]).abs().max().item()
     res = {"rank": ctx.rank, "segments": len(gs.capture.graphs), "err_out": err_out,

@@ -98,15 +98,53 @@ def main():
     oerr_loss = (tot.cpu() - oref.detach()).abs().max().item()
     oerr_r = ((rl.grad.cpu() - ro.grad[orows]).abs().max() / ro.grad.abs().max()).item()
     oerr_i = ((il.grad.cpu() - io.grad[orows]).abs().max() / io.grad.abs().max()).item()
+    # bf16 with the text side gathered as the word<->region operand rows
+    # (Train._gather_text: bf16 rows + norms, half the fp32 words' bytes):
+    # each rank prepares its own captions' rows (as TextHeading attaches them),
+    # one all-gather, rows-only words; the DP losses and this rank's region
+    # gradient equal the single-process bf16 global batch on the same rows,
+    # and the oracle within the bf16 mode's tolerance
+    bargs = make_args(bert_words_num=24, precision="bf16", return_att_maps=False)
+    wb = words.transpose(1, 2).contiguous()                       # [n, 22, 256]
+    rows_all, _, norms_all = K.prep_rows(wb, 22, 32, want_norms=True, scale=K.LOG2E)
+    K.attach_rows(wb, rows_all, norms_all, False, K.LOG2E)
+    labels = torch.arange(n, device=dev)
+    rgb = r_all.clone().requires_grad_()
+    bref = torch.stack(L.words_loss(rgb, wb.transpose(1, 2), labels, None, cls, n, bargs)[:2])
+    bref.sum().backward()
+    rows_l, _, norms_l = K.prep_rows(wb[rows], 22, 32, want_norms=True, scale=K.LOG2E)
+    rows_g, norms_g = ctx.gather_text(rows_l, norms_l)
+    wro = K.rows_only_words(rows_g, norms_g, 22, False)
+    bargs.dist = ctx
+    rlb = r_all[rows].clone().requires_grad_()
+    bmine = torch.stack(L.words_loss(rlb, wro, labels, None, cls, b_l, bargs)[:2])
+    bmine.sum().backward()
+    btot = ctx.sum(bmine.detach())
+    torch.cuda.synchronize()
+    rows_err_loss = (btot - bref.detach()).abs().max().item()
+    rows_err_r = ((rlb.grad - rgb.grad[rows]).abs().max() / rgb.grad.abs().max()).item()
+    rows_oerr_loss = (btot.cpu() - oref[:2].detach()).abs().max().item()
+    rows_oerr_r = ((rlb.grad.cpu() - ro.grad[orows]).abs().max() / ro.grad.abs().max()).item()
+    # (the oracle gradient above is of all five losses; compare the word terms' own)
+    ro2 = r_all.cpu().clone().requires_grad_()
+    w0o, w1o, _, _ = O.words_loss(ro2, words.cpu(), torch.arange(n), None, 22, 4.0, 5.0, 10.0)
+    (w0o + w1o).backward()
+    rows_oerr_r = ((rlb.grad.cpu() - ro2.grad[orows]).abs().max() / ro2.grad.abs().max()).item()
     res = {"rank": ctx.rank, "err_loss": err_loss, "err_r": err_r, "err_i": err_i,
            "oracle_err_loss": oerr_loss, "oracle_err_r": oerr_r, "oracle_err_i": oerr_i,
-           "focal_err": ferr, "focal_grad_err": fgerr}
+           "focal_err": ferr, "focal_grad_err": fgerr, "rows_err_loss": rows_err_loss,
+           "rows_err_r": rows_err_r, "rows_oracle_err_loss": rows_oerr_loss,
+           "rows_oracle_err_r": rows_oerr_r,
+           "rows_bytes_per_caption": rows_l[0].numel() * 2 + norms_l[0].numel() * 4,
+           "words_bytes_per_caption": 22 * 256 * 4}
     out = os.environ.get("TGFR_DP_OUT")
     if out:
         with open(f"{out}.{ctx.rank}", "w") as f:
             json.dump(res, f)
     ok = err_loss < 1e-4 and err_r < 1e-4 and err_i < 1e-4 and oerr_loss < 1e-3 and \
-        oerr_r < 2e-3 and oerr_i < 2e-3 and ferr < 1e-5 and fgerr < 1e-5
+        oerr_r < 2e-3 and oerr_i < 2e-3 and ferr < 1e-5 and fgerr < 1e-5 and \
+        rows_err_loss < 1e-4 and rows_err_r < 1e-4 and rows_oerr_loss < 5e-2 and \
+        rows_oerr_r < 3e-2
     sys.exit(0 if ok else 3)
 
 

@@ -29,6 +29,7 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 
 
 def _import_reference(root):
+    sys.dont_write_bytecode = True          # the reference tree stays untouched
     sys.path.insert(0, root)
     sys.modules.setdefault("torchsummary", types.SimpleNamespace(summary=None))
     import transformers  # noqa: F401  (models.models imports these names first)
@@ -273,6 +274,49 @@ def gen_text_heading(ref_models):
               words_emb=words, words_out=w_out.contiguous(), sent_out=s_out)
 
 
+def words_seeded_inputs(seed, b, t, noise=0.02):
+    """Inputs of the full-shape words_loss fixtures, regenerated from the seed
+    instead of stored (the B = 64 region map alone is 12.8 MB): unit regions
+    R [B, 14, 14, 256] (returned as the channels-last [B, 256, 14, 14] view
+    IMIM produces) and captions whose words are noisy copies of regions of
+    their own image, W [B, 256, T] (a view of [B, T, 256] storage), so every
+    matching pair leads its row and column by >= 1 logit -- a margin the
+    reduced-precision kernels must resolve (argmax identity).  CPU generator:
+    bit-identical on any host with this torch build."""
+    gen = torch.Generator().manual_seed(seed)
+    r = _unit_rows(torch.randn(b, 196, 256, generator=gen), -1)
+    idx = torch.randint(0, 196, (b, t), generator=gen)
+    w = _unit_rows(r[torch.arange(b)[:, None], idx] +
+                   noise * torch.randn(b, t, 256, generator=gen), -1)
+    return r.reshape(b, 14, 14, 256).permute(0, 3, 1, 2), w.transpose(1, 2)
+
+
+SEEDED_WORDS = {"bert_b64_l32": (900, 64, 32), "bert_b16_l64": (901, 16, 64)}
+
+
+def gen_words_loss_seeded(ref_loss):
+    """words_loss at the headline batch (B = 64, bert_words_num = 32, T = 30)
+    and at configs[4]'s caption length (bert_words_num = 64, T = 62,
+    models/losses.py:83): the reference's logits and losses, and its region
+    gradient sampled at 4096 seeded positions plus its max and norm (the
+    inputs are regenerated from the seed, words_seeded_inputs)."""
+    seen = _record_ce(ref_loss)
+    for tag, (seed, b, L) in SEEDED_WORDS.items():
+        r, w = words_seeded_inputs(seed, b, L - 2)
+        r = r.detach().requires_grad_()
+        args = _Args("BERT", L)
+        labels = torch.arange(b)
+        seen.clear()
+        l0, l1, _ = ref_loss.words_loss(r, w, labels, None, None, b, args)
+        (l0 + l1).backward()
+        g = r.grad.detach()
+        pick = torch.randperm(g.numel(), generator=torch.Generator().manual_seed(seed))[:4096]
+        _save(f"words_loss_{tag}_seeded", seed=seed, batch=b, bert_words_num=L,
+              r_sum=r.detach().double().sum(), w_sum=w.double().sum(),
+              logits=seen[0], loss0=l0, loss1=l1, d_img_idx=pick,
+              d_img_val=g.reshape(-1)[pick], d_img_absmax=g.abs().max(), d_img_norm=g.norm())
+
+
 def _cpu_torch_proxy():
     """A ``torch`` module proxy whose ``zeros`` ignores ``device=``: the one
     CUDA-only call of ArcMarginProduct.forward is its one-hot buffer
@@ -332,6 +376,7 @@ def main():
     gen_image_heading(ref_models)
     gen_text_heading(ref_models)
     gen_arc_margin(ref_metrics)
+    gen_words_loss_seeded(ref_loss)
 
 
 if __name__ == "__main__":

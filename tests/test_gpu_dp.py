@@ -43,15 +43,23 @@ def test_dp_world2_matches_global(gpu, tmp_path):
         assert r["oracle_err_loss"] < 1e-3 and r["oracle_err_r"] < 2e-3 and \
             r["oracle_err_i"] < 2e-3, r
         assert r["focal_err"] < 1e-5 and r["focal_grad_err"] < 1e-5, r
+        # bf16, text side gathered as operand rows (rows-only words)
+        assert r["rows_err_loss"] < 1e-4 and r["rows_err_r"] < 1e-4, r
+        assert r["rows_oracle_err_loss"] < 5e-2 and r["rows_oracle_err_r"] < 3e-2, r
+        # (T = 22 here: 16.1 KiB against 22 KiB; at T = 30, configs[2], 16.1 against 30)
+        assert r["rows_bytes_per_caption"] * 1.3 < r["words_bytes_per_caption"], r
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_dp_graphed_train_step(gpu, tmp_path, precision):
+@pytest.mark.parametrize("precision,bert", [("fp32", 0), ("bf16", 0), ("bf16", 1)])
+def test_dp_graphed_train_step(gpu, tmp_path, precision, bert):
     """2 ranks: the stage-1 step replayed as graphs cut at its collectives
-    equals eager stepping, and the replicas stay identical."""
+    equals eager stepping, and the replicas stay identical.  bert = 1: the
+    batches carry BERT hidden states, so each rank runs the frozen TextHeading
+    (its weights broadcast from rank 0: the ranks are seeded differently) and
+    the text side is gathered as operand rows (rows-only words)."""
     import json
     out = str(tmp_path / "dpt")
-    _run("dp_train_worker.py", out, TGFR_DP_PRECISION=precision)
+    _run("dp_train_worker.py", out, TGFR_DP_PRECISION=precision, TGFR_DP_BERT=str(bert))
     for rank in range(2):
         r = json.load(open(f"{out}.{rank}"))
         # text gather, 2 column exchanges (word<->region; sentence + global

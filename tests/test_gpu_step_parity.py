@@ -164,9 +164,10 @@ def test_train_step_matches_oracle(gpu, b, nw, n_ids):
 
 # Reduced-precision steps (the benchmarked configuration and BASELINE configs[4]'s
 # precision).  Tolerances (measured on MI355X, round 3, in brackets):
-#   word-region terms w0, w1: 1e-2 each -- the bf16 operands carry 2^-9
-#     relative rounding that gamma2 * gamma3 = 50 amplifies in the logits
-#     (DESIGN.md 2); fp16 2^-11  [damsm group 1.8e-4 bf16, 2.0e-4 fp16]
+#   word-region terms w0, w1: 1e-3 each (the north star's bar on losses),
+#     although the bf16 operands carry 2^-9 relative rounding that gamma2 *
+#     gamma3 = 50 amplifies in each logit: the CE averages it
+#     out  [damsm group 1.8e-4 bf16, 2.0e-4 fp16, round 3]
 #   sentence / global / identity terms: 1e-3 (north star): they run on fp32
 #     features (g' by the split-mode projection, the fp32-MFMA ArcMargin)
 #     [<= 1e-6; ident group 1.2e-4 / 9.8e-4 = 100 x focal errors of ~1e-5]
@@ -178,8 +179,8 @@ def test_train_step_matches_oracle(gpu, b, nw, n_ids):
 #     step), the update's sign wherever the reference gradient exceeds 4x that
 #     error  [worst 1.1e-2 of scale, bf16]
 REDUCED = {
-    "bf16": dict(wtol=1e-2, otol=1e-3, gtol=1e-1),
-    "fp16": dict(wtol=1e-2, otol=1e-3, gtol=1e-1),
+    "bf16": dict(wtol=1e-3, otol=1e-3, gtol=1e-1),
+    "fp16": dict(wtol=1e-3, otol=1e-3, gtol=1e-1),
 }
 
 
@@ -216,13 +217,20 @@ def test_train_step_reduced_precision_matches_oracle(gpu, precision, b, nw):
     print(f"{precision} step B={b} T={nw}: word-region logit error {lerr:.3e}, "
           f"rows with a resolvable top-2 gap {int(sure.sum())}/{b}")
     assert (wl.argmax(1) == wref.argmax(1))[sure].all()
+    # each word-region term from the trainer's own logits (CE rows / columns)
+    w0 = torch.nn.functional.cross_entropy(wl, torch.arange(b)).item()
+    w1 = torch.nn.functional.cross_entropy(wl.t(), torch.arange(b)).item()
+    for k, v in (("w0", w0), ("w1", w1)):
+        err = abs(v - ref["terms"][k])
+        print(f"  {k}: error {err:.3e}")
+        assert err < tol["wtol"], (k, v, ref["terms"][k])
     for k in ("s0", "s1", "global"):
         err = abs(mine[k] - ref["terms"][k])
         print(f"  {k}: error {err:.3e}")
         assert err < tol["otol"], (k, mine[k], ref["terms"][k])
     errs = {k: abs(out[k].item() - v) for k, v in ref["groups"].items()}
     print("  groups:", {k: f"{v:.3e}" for k, v in errs.items()})
-    assert errs["damsm"] < 2 * tol["wtol"] + 2 * tol["otol"], errs
+    assert errs["damsm"] < tol["wtol"], errs
     assert errs["clip"] < tol["otol"], errs
     assert errs["ident"] < 2 * args.lambda_id * 1e-3, errs
     named = dict(tr.image_head.named_parameters())
@@ -398,16 +406,26 @@ def test_lstm_graphed_step(gpu):
         torch.testing.assert_close(out[k], outs[-1][k], rtol=1e-5, atol=1e-5)
 
 
-def test_fusion_step_matches_oracle(gpu):
+@pytest.mark.parametrize("precision,b,n_ids", [("fp32", 6, 11), ("bf16", 256, 4500)])
+def test_fusion_step_matches_oracle(gpu, precision, b, n_ids):
     """Stage-2 FCFM step: image head -> Working -> ArcMargin(640) -> focal,
-    SGD(lr 0.1, wd 5e-4) on the classifier, Adam(wd 5e-5) on head + fusion."""
+    SGD(lr 0.1, wd 5e-4) on the classifier, Adam(wd 5e-5) on head + fusion.
+    fp32 mode at B = 6: the tolerances of the stage-1 step.  bf16 at the
+    benchmarked configs[3] step (B = 256, T = 22, 4500 classes): the loss
+    within 1e-2 (relative), the SGD update within 1e-3 of the tensor's scale,
+    every Adam update's sign equal where the reference gradient is resolvable
+    (4x the measured gradient error) and its value within 1e-3 of scale there,
+    gradients within 2.5e-1 of each tensor's max (a bf16 near-tie in a 2x2
+    pooling window sends one element's gradient elsewhere, test_working_oracle_b256)."""
     from text_guided_face_recognition_amd.config import make_args
     from text_guided_face_recognition_amd.train import Fusion, synthetic_batch
-    b, nw = 6, 22
+    nw = 22
+    fp32 = precision == "fp32"
     torch.manual_seed(21)
-    args = make_args(batch_size=b, bert_words_num=24, num_classes=11, precision="fp32")
+    args = make_args(batch_size=b, bert_words_num=nw + 2, num_classes=n_ids,
+                     precision=precision)
     tr = Fusion(args, gpu)
-    batch = synthetic_batch(b, nw, gpu, seed=22, n_ids=11)
+    batch = synthetic_batch(b, nw, gpu, seed=22, n_ids=n_ids)
     hp = _cpu_params(tr.image_head, HEAD_KEYS)
     wp = _cpu_params(tr.fusion_net, WORKING_KEYS)
     arc = tr.metric_fc.weight.detach().cpu().clone().requires_grad_()
@@ -426,14 +444,26 @@ def test_fusion_step_matches_oracle(gpu):
 
     got = tr.step(batch)["loss"].item()
     torch.cuda.synchronize()
-    assert abs(got - loss.item()) < 1e-3, (got, loss.item())
-    _check_sgd(tr.metric_fc.weight.detach().cpu(), arc.detach())
+    lerr = abs(got - loss.item())
+    scale = arc.detach().abs().max().clamp(min=1e-6)
+    serr = ((tr.metric_fc.weight.detach().cpu() - arc.detach()).abs().max() / scale).item()
+    print(f"fusion {precision} B={b}: loss {got:.5f} vs {loss.item():.5f} (error {lerr:.3e}), "
+          f"SGD update error {serr:.3e} of scale")
+    if fp32:
+        assert lerr < 1e-3, (got, loss.item())
+        _check_sgd(tr.metric_fc.weight.detach().cpu(), arc.detach())
+    else:
+        assert lerr < 1e-2 * abs(loss.item()), (got, loss.item())
+        assert serr < 1e-3, serr
     g_all = max(x.abs().max().item() for x in grads.values())
+    kw = dict(wd=5e-5) if fp32 else dict(wd=5e-5, gtol=2.5e-1, utol=1e-3, gfloor=1e-3)
+    gmax = 0.0
     named_h = dict(tr.image_head.named_parameters())
     for k, v in HEAD_KEYS.items():
-        _check_adam(named_h[k], old[("h", v)], hp[v].detach(), grads[("h", v)], args.lr_head,
-                    k, g_all, wd=5e-5)
+        gmax = max(gmax, _check_adam(named_h[k], old[("h", v)], hp[v].detach(),
+                                     grads[("h", v)], args.lr_head, k, g_all, **kw))
     named_w = dict(tr.fusion_net.named_parameters())
     for k, v in WORKING_KEYS.items():
-        _check_adam(named_w[k], old[("w", v)], wp[v].detach(), grads[("w", v)], args.lr_head,
-                    k, g_all, wd=5e-5)
+        gmax = max(gmax, _check_adam(named_w[k], old[("w", v)], wp[v].detach(),
+                                     grads[("w", v)], args.lr_head, k, g_all, **kw))
+    print(f"  worst gradient error {gmax:.3e} of its tensor's scale")

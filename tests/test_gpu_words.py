@@ -343,21 +343,25 @@ def test_words_config5_rank_shape(gpu, mode, ltol, gtol):
     assert (got.argmax(0) == refd.argmax(0))[surec].all()
 
 
-@pytest.mark.parametrize("mode,nw,ltol,gtol", [("bf16", 30, 2e-1, 6e-2), ("bf16", 62, 3e-2, 4e-2),
-                                               ("fp16", 62, 5e-3, 1e-2)])
-def test_words_bounded_past_unit_norm(gpu, mode, nw, ltol, gtol):
+@pytest.mark.parametrize("mode,nw,wn,rn,ltol,gtol", [
+    ("bf16", 30, 6.0, 8.0, 2e-1, 6e-2), ("bf16", 62, 6.0, 8.0, 3e-2, 4e-2),
+    ("fp16", 62, 6.0, 8.0, 5e-3, 1e-2), ("fp16", 30, 8.0, 10.0, 5e-2, 5e-2),
+    ("fp16", 62, 8.0, 10.0, 5e-2, 5e-2), ("fp16", 30, 12.0, 12.0, 1e-1, 1e-1)])
+def test_words_bounded_past_unit_norm(gpu, mode, nw, wn, rn, ltol, gtol):
     """The max-free (bounded) kernels fed features far from the unit-norm
-    contract (|W| = 6, |R| = 8, so the score bound c = 48 > 40): forward and
-    backward both shift the scores by the device-computed bound, so logits and
-    gradients stay finite and match the oracle (models/losses.py:83-109 on
-    unnormalised BERT-path features).  Measured (MI355X): bf16 T=30 logits
-    1.0e-1 (the t_pad = 32 forward's shift cancels c Z in N),
-    gradients 3.6e-2 of max; bf16 T=62 7.5e-3 / 1.8e-2; fp16 8.7e-4 / 2.7e-3."""
+    contract through the drop-in path (kernels.word_region_logits with
+    bounded=True, as words_loss does for en_type BERT): |W| = 6, |R| = 8 (score
+    bound c = 48) and |W| = 8, |R| = 10 (c = 80): exact, no shift (the window
+    of csrc/tgfr_wr.hip bound_shift, c <= 84.5); |W| = |R| = 12 (c = 144):
+    past WR_BOUND_MAX, so the host takes the exact running-max kernels.
+    Logits and gradients finite and matching the oracle (models/losses.py:83-109
+    on unnormalised BERT-path features); the tolerance grows with c because
+    the operands' relative rounding scales every score by |W| |R|."""
     K = _kernels()
     torch.manual_seed(23 + nw)
     b_img, b_cap = 7, 11
-    r = 8.0 * _unit(torch.randn(b_img, 14, 14, 256)).permute(0, 3, 1, 2)
-    w = 6.0 * _unit(torch.randn(b_cap, nw, 256)).transpose(1, 2)
+    r = rn * _unit(torch.randn(b_img, 14, 14, 256)).permute(0, 3, 1, 2)
+    w = wn * _unit(torch.randn(b_cap, nw, 256)).transpose(1, 2)
     ro = r.clone().requires_grad_()
     _, _, _, ref = O.words_loss(ro, w, None, None, nw, 4.0, 5.0, 10.0, batch_size=b_cap)
     probe = torch.randn(b_img, b_cap)
@@ -371,6 +375,70 @@ def test_words_bounded_past_unit_norm(gpu, mode, nw, ltol, gtol):
     assert torch.isfinite(got).all() and torch.isfinite(rg.grad).all()
     lerr = (got - ref.detach()).abs().max().item()
     gerr = (rg.grad.cpu() - ro.grad).abs().max().item() / ro.grad.abs().max().item()
-    print(f"{mode} T={nw}: logit err {lerr:.3e}, grad err {gerr:.3e}")
+    print(f"{mode} T={nw} c={wn * rn:.0f}: logit err {lerr:.3e}, grad err {gerr:.3e}")
     assert lerr < ltol, lerr
+    assert gerr < gtol, gerr
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_words_loss_bert_c80_drop_in(gpu, precision):
+    """words_loss (the drop-in, en_type BERT) on features with |W| |R| = 80,
+    models/losses.py:61-135 vs the oracle: finite losses that match (the
+    reference's torch softmaxes never overflow, attention.py:28-36)."""
+    from text_guided_face_recognition_amd.config import make_args
+    from text_guided_face_recognition_amd.models import losses as L
+    torch.manual_seed(80)
+    b, nw = 6, 30
+    r = 10.0 * _unit(torch.randn(b, 14, 14, 256)).permute(0, 3, 1, 2)
+    w = 8.0 * _unit(torch.randn(b, nw + 2, 256)).transpose(1, 2)
+    args = make_args(bert_words_num=nw + 2, precision=precision)
+    args.return_att_maps = False
+    labels = torch.arange(b)
+    ro = r.clone().requires_grad_()
+    l0, l1, _, _ = O.words_loss(ro, w, labels, None, nw, 4.0, 5.0, 10.0)
+    (l0 + l1).backward()
+    rg = r.to(gpu).requires_grad_()
+    g0, g1, _ = L.words_loss(rg, w.to(gpu), labels.to(gpu), None, None, b, args)
+    (g0 + g1).backward()
+    assert torch.isfinite(g0) and torch.isfinite(g1) and torch.isfinite(rg.grad).all()
+    err = max(abs(g0.item() - l0.item()), abs(g1.item() - l1.item()))
+    gerr = ((rg.grad.cpu() - ro.grad).abs().max() / ro.grad.abs().max()).item()
+    print(f"{precision} c=80: loss err {err:.3e}, grad err {gerr:.3e}")
+    assert err < 5e-2 and gerr < 5e-2
+
+
+@pytest.mark.parametrize("tag", ["bert_b64_l32", "bert_b16_l64"])
+@pytest.mark.parametrize("mode,ltol,gtol", [("fp32", 1e-3, 2e-3), ("bf16", 5e-2, 3e-2),
+                                            ("fp16", 1e-2, 1e-2)])
+def test_words_seeded_full_shape_vs_reference(gpu, tag, mode, ltol, gtol):
+    """The benchmarked (bounded) kernels at the headline batch (B = 64,
+    bert_words_num = 32) and at configs[4]'s caption length (bert_words_num =
+    64, T = 62) against the REFERENCE's outputs on the same inputs
+    (tests/golden/make_golden.py:gen_words_loss_seeded): logits, both losses
+    and the reference's region gradient at 4096 sampled positions, with
+    identical row and column argmax in every mode (matching pairs lead by
+    >= 1 logit in these inputs)."""
+    from conftest import words_seeded_golden
+    K = _kernels()
+    g, r, w = words_seeded_golden(f"words_loss_{tag}_seeded")
+    b, nw = r.shape[0], int(g["bert_words_num"]) - 2
+    rg = r.to(gpu).requires_grad_()
+    logits = K.word_region_logits(rg, K.words_view(w.to(gpu), nw),
+                                  torch.full((b,), nw, dtype=torch.int32), 4.0, 5.0, 10.0,
+                                  mode=mode, bounded=True)
+    labels = torch.arange(b, device=gpu)
+    l0 = F.cross_entropy(logits, labels)
+    l1 = F.cross_entropy(logits.t(), labels)
+    (l0 + l1).backward()
+    got = logits.detach().cpu()
+    ref = torch.from_numpy(g["logits"])
+    lerr = (got - ref).abs().max().item()
+    d = rg.grad.cpu().reshape(-1)[torch.from_numpy(g["d_img_idx"])]
+    gerr = (d - torch.from_numpy(g["d_img_val"])).abs().max().item() / float(g["d_img_absmax"])
+    print(f"{tag} {mode}: logit err {lerr:.3e}, loss err "
+          f"{max(abs(l0.item() - float(g['loss0'])), abs(l1.item() - float(g['loss1']))):.3e}, "
+          f"sampled grad err {gerr:.3e} of max")
+    assert lerr < ltol, lerr
+    assert abs(l0.item() - float(g["loss0"])) < ltol and abs(l1.item() - float(g["loss1"])) < ltol
+    assert (got.argmax(1) == ref.argmax(1)).all() and (got.argmax(0) == ref.argmax(0)).all()
     assert gerr < gtol, gerr

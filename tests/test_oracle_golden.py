@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import load_golden, t
+from conftest import load_golden, t, words_seeded_golden
 from oracle import tgfr_oracle as O
 
 torch.set_num_threads(4)
@@ -46,6 +46,28 @@ def test_words_loss(tag):
         close(a[0], g["att_diag"][i, :a.shape[1]], atol=1e-6)
     (l0 + l1).backward()
     close(r.grad, g["d_img"], atol=1e-6, rtol=1e-4)
+
+
+@pytest.mark.parametrize("tag", ["bert_b64_l32", "bert_b16_l64"])
+def test_words_loss_seeded_full_shape(tag):
+    """The oracle at the headline batch (B = 64, T = 30) and at configs[4]'s
+    caption length (T = 62) against the reference's own outputs there: logits,
+    losses and the sampled region gradient (inputs regenerated from the seed)."""
+    g, r, w = words_seeded_golden(f"words_loss_{tag}_seeded")
+    r = r.contiguous().requires_grad_()
+    b, nw = r.shape[0], int(g["bert_words_num"]) - 2
+    l0, l1, _, logits = O.words_loss(r, w, torch.arange(b), None, nw, 4.0, 5.0, 10.0)
+    close(logits, g["logits"], atol=2e-4)
+    assert (logits.argmax(1).numpy() == g["logits"].argmax(1)).all()
+    assert (logits.argmax(0).numpy() == g["logits"].argmax(0)).all()
+    close(l0, g["loss0"], atol=1e-5)
+    close(l1, g["loss1"], atol=1e-5)
+    (l0 + l1).backward()
+    got = r.grad.reshape(-1)[torch.from_numpy(g["d_img_idx"])]
+    scale = float(g["d_img_absmax"])
+    assert (got - t(g["d_img_val"])).abs().max().item() < 1e-4 * scale
+    assert abs(r.grad.abs().max().item() - scale) < 1e-4 * scale
+    assert abs(r.grad.norm().item() - float(g["d_img_norm"])) < 1e-4 * float(g["d_img_norm"])
 
 
 def test_sent_global_clip_focal():

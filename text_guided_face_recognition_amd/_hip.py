@@ -192,6 +192,23 @@ class KernelTimer:
 
 _counters = {}
 N_COUNTERS = 1 << 20
+_hiprt = None
+
+
+def _capture_id(stream_handle):
+    """The HIP graph capture id of a stream, or None when it is not capturing
+    (hipStreamGetCaptureInfo of the runtime torch mapped)."""
+    global _hiprt
+    if not torch.cuda.is_current_stream_capturing():
+        return None
+    if _hiprt is None:
+        _hiprt = lib()        # dlsym through the library reaches its HIP runtime
+        _hiprt.hipStreamGetCaptureInfo.argtypes = [P, C.POINTER(I), C.POINTER(C.c_ulonglong)]
+    st, cid = I(0), C.c_ulonglong(0)
+    rc = _hiprt.hipStreamGetCaptureInfo(P(stream_handle), C.byref(st), C.byref(cid))
+    if rc != 0:
+        raise RuntimeError(f"hipStreamGetCaptureInfo failed with code {rc}")
+    return int(cid.value) if st.value == 1 else None
 
 
 def counters(device):
@@ -200,19 +217,26 @@ def counters(device):
     and every kernel leaves the words it used at zero again, so the calls of a
     stream share its buffer, while kernels of different streams never share
     a word.
-    A stream's buffer is made on first use.  First used inside a HIP graph
-    capture (e.g. plain torch.cuda.graph, whose capture stream is its own),
-    the buffer comes from that graph's memory pool and its zeroing is a node
-    of the graph, so every replay starts from zeroed words; it then belongs to
-    that capture (dist.StepCapture makes its stream's buffer before capturing,
-    so its graphs carry no such node)."""
+    A stream's buffer is made on first use.  Made inside a HIP graph capture
+    (e.g. plain torch.cuda.graph, whose capture stream is its own), the buffer
+    comes from that graph's memory pool and its zeroing is a node of that
+    graph, so it is cached for that capture only (keyed by the capture id):
+    another capture on the same stream, or eager use of it, makes its own
+    zeroed buffer instead of reading words only that graph ever zeroes.
+    (dist.StepCapture makes its stream's buffer before capturing, so its
+    graphs carry no such node.)"""
     dev = torch.device(device)
     stream = torch.cuda.current_stream(dev)
     key = (dev.index, stream.cuda_stream)
     buf = _counters.get(key)
     if buf is None:
-        buf = torch.zeros(N_COUNTERS, dtype=torch.int32, device=dev)
-        _counters[key] = buf
+        cid = _capture_id(stream.cuda_stream)
+        if cid is not None:
+            key = key + (cid,)
+            buf = _counters.get(key)
+        if buf is None:
+            buf = torch.zeros(N_COUNTERS, dtype=torch.int32, device=dev)
+            _counters[key] = buf
     return buf
 
 

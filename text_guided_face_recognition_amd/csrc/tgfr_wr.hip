@@ -41,6 +41,19 @@ constexpr int NREG = 196;
 constexpr int TPAD = 32;       // words per caption padded to one tile
 constexpr int NRT = 7;         // region tiles
 
+// Score shift of the bounded (max-free) kernels, in units of the pair's score
+// bound c = max_t |W_t| max_r |R_r| (U = log2(e) c >= |every S'|): unshifted
+// while U <= 122 (c <= 84.5): no term, and no 64-term sum, overflows, and a
+// region's best term is >= 2^-122 (normal), so p = exp2(S') is exact for any
+// such input.  Past that the scores are shifted by log2(e) (c - 84.5), which
+// keeps every sum finite and every row's best term normal while c <= 85.9
+// (WR_BOUND_MAX, kernels.py); beyond it the row sums are clamped at 2^-126
+// (finite, not exact) and the host routes such inputs to the exact
+// running-max kernels.  (Round 3 shifted from c = 40 on, which underflowed
+// rows whose best word sits near -c from c ~ 44.)
+__device__ __forceinline__ float bound_shift(float c) { return fmaxf(c - 84.5f, 0.f); }
+__device__ __forceinline__ float sum_floor(float s) { return fmaxf(s, 0x1p-126f); }
+
 // ----------------------------------------------------------------- prep ---
 __global__ __launch_bounds__(256) void prep_rows_kernel(
     const float* __restrict__ x, long long s_item, long long s_row, long long s_col,
@@ -743,12 +756,12 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
     // (accumulators start at the word bias: 0, or -1e30 for padding words,
     // whose E = exp(0) = 1 then only feeds their own unused statistics and
     // C-hat rows, as in wr_fwd_pipe_kernel)
-    // (BOUNDED: valid words start at -log2(e) c, c = max|W| max|R| of the
-    // caption when >= 40, else 0; both token tiles' waves form the same c)
+    // (BOUNDED: valid words start at -log2(e) bound_shift(c), c = max|W|
+    // max|R| of the caption; both token tiles' waves form the same c)
     float cb = 0.f;
     if (BOUNDED) {
       cb = wave_max(Wnorm[(long long)ic * TP + lane]) * rmax;
-      if (cb < 40.f) cb = 0.f;
+      cb = bound_shift(cb);
     }
     const float sh = -L2E * cb;
     f32x16 S[NRT];
@@ -773,7 +786,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
     }
     // ---- softmax over the caption's words, per region: max and sum over
     // both token tiles (partner wave = wid ^ 1)
-    // (BOUNDED: the caller guarantees |S| < 43, so p = exp2(S') needs no max)
+    // (BOUNDED: p = exp2(S' - log2(e) bound_shift(c)) needs no max)
     float mj[NRT];
 #pragma unroll
     for (int j = 0; j < NRT; ++j) mj[j] = 0.f;
@@ -823,7 +836,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
 #pragma unroll
     for (int j = 0; j < NRT; ++j) {
       const float rb = j * 32 + lr < NREG ? 0.f : -1e30f;   // padding regions
-      const float kj = g1 * L2E * __builtin_amdgcn_rcpf(sj[j]);
+      const float kj = g1 * L2E * __builtin_amdgcn_rcpf(sum_floor(sj[j]));
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const float p = __builtin_amdgcn_exp2f(S[j][q] - mj[j]);
@@ -942,11 +955,11 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
 // With c = max_t |W_t| * max_r |R_r| >= |every score of the caption|, the
 // softmax over words is p = exp2(S'^T) directly -- no max, no subtraction:
 // exact in real arithmetic (any shift cancels in the normalisation), and no
-// term overflows and no region's sum underflows while c < 40 (c = 1 for the
-// L2-normalised BERT-path features, models/models.py:212,403; <= 16 for the
-// LSTM's tanh outputs against unit regions).  GEMM1's accumulator starts at
-// the word bias (0, or -1e30 for padding words).  For 40 <= c < 43 it also
-// carries the shift -log2(e) c (p <= 1); the shift is added back in the
+// term overflows and no region's sum underflows while c <= 84.5 (c = 1 for
+// the L2-normalised BERT-path features, models/models.py:212,403; <= 16 for
+// the LSTM's tanh outputs against unit regions).  GEMM1's accumulator starts
+// at the word bias (0, or -1e30 for padding words).  Past c = 84.5 it also
+// carries the shift -log2(e) bound_shift(c); the shift is added back in the
 // statistics.  The shift is applied only where needed: N = sum_r E S then
 // cancels c Z, which costs ~1e-4 of N when Z is formed from the bf16 E of
 // GEMM2 -- visible as ~0.05 logit error through cos = N / (|W| |C|) with
@@ -1049,7 +1062,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
   auto caption_init = [&](int ii, float wn, float& c) {
     const int len = lens[ii];
     c = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(half_max(wn) * rmax)));
-    if (c < 40.f) c = 0.f;             // no shift needed (see above)
+    c = bound_shift(c);             // no shift below c = 84.5 (bound_shift)
     const float sh = -L2E * c;
     f32x16 init;
 #pragma unroll
@@ -1136,7 +1149,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
       ma[2] += p[6] + p[14];
       ma[3] += p[7] + p[15];
     } else if (c == 15) {
-      kk = kg * __builtin_amdgcn_rcpf(xhalf_sum((ma[0] + ma[1]) + (ma[2] + ma[3])));
+      kk = kg * __builtin_amdgcn_rcpf(sum_floor(xhalf_sum((ma[0] + ma[1]) + (ma[2] + ma[3]))));
     } else {
       const int q = c - 16;
       const float e = __builtin_amdgcn_exp2f(j == 6 ? fmaf(p[q], kk, rb6) : p[q] * kk);
@@ -1282,8 +1295,8 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
   const bool valid = t < len;
   const float4 st = valid ? stats[pair * TP + t] : make_float4(1.f, 0.f, 0.f, 0.f);
   // layout 1: the pair's score bound c = max_t |W_t| max_r |R_r| (as the
-  // bounded forwards form it); past 40 the max-free backwards shift S' by
-  // -log2(e) c through the G1 initial row, and sigma absorbs alpha c
+  // bounded forwards form it); the max-free backwards shift S' by -log2(e)
+  // bound_shift(c) through the G1 initial row, and sigma absorbs alpha times it
   float cb = 0.f;
   if (layout != 0 && Rnorm) {
     const float* rn = Rnorm + (long long)b * RPAD;
@@ -1292,7 +1305,7 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
     rmax = wave_max(rmax);
     const float wn = Wnorm[(long long)i * TP + t];
     cb = (TP == 64 ? wave_max(wn) : half_max(wn)) * rmax;
-    if (cb < 40.f) cb = 0.f;
+    cb = bound_shift(cb);
   }
   const float ex = valid ? __expf(g2 * st.w) : 0.f;
   const float tot = TP == 64 ? wave_sum(ex) : half_sum(ex);
@@ -1865,6 +1878,7 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide_kernel(
 // chunk's partial, well inside the bf16 mode's gradient error.)
 constexpr long long FRAG_TILE = 8 * 64 * 16;     // bf16 elements per (image, region tile)
 
+template <bool F32P = false>
 __device__ __forceinline__ void store_dr_tile(const f32x16 (&dR)[8], int n_chunks, int chunk,
                                               int b, int rt, int B_img, int lane,
                                               float* __restrict__ out, long long s_b,
@@ -1882,7 +1896,21 @@ __device__ __forceinline__ void store_dr_tile(const f32x16 (&dR)[8], int n_chunk
     }
     return;
   }
-  uint16_t* dst = slab + (((long long)chunk * B_img + b) * NRT + rt) * FRAG_TILE + lane * 16;
+  const long long at = (((long long)chunk * B_img + b) * NRT + rt) * FRAG_TILE + lane * 16;
+  if constexpr (F32P) {
+    // fp32 partials (fp16 mode: bf16 rounding would be coarser than its operands)
+    float* dst = (float*)slab + at;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      const f32x16& a = dR[dt];
+      float4* d4 = (float4*)(dst + dt * 64 * 16);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        d4[k] = make_float4(a[4 * k], a[4 * k + 1], a[4 * k + 2], a[4 * k + 3]);
+    }
+    return;
+  }
+  uint16_t* dst = slab + at;
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) {
     const f32x16& a = dR[dt];
@@ -1894,9 +1922,10 @@ __device__ __forceinline__ void store_dr_tile(const f32x16 (&dR)[8], int n_chunk
   }
 }
 
-// dR[b][r][d] = sum over chunks of the fragment-order bf16 partials; thread =
-// one (image, region tile, d tile, lane): 32 B per chunk in, 16 rows of one
-// column out (a wave's stores are 128-B row segments)
+// dR[b][r][d] = sum over chunks of the fragment-order partials (bf16, or fp32
+// with F32P); thread = one (image, region tile, d tile, lane): 32 (64) B per
+// chunk in, 16 rows of one column out (a wave's stores are 128-B row segments)
+template <bool F32P>
 __global__ __launch_bounds__(256) void wr_reduce_frag_kernel(const uint16_t* __restrict__ slab,
                                                              int n_chunks, int B_img,
                                                              float* __restrict__ out,
@@ -1911,15 +1940,28 @@ __global__ __launch_bounds__(256) void wr_reduce_frag_kernel(const uint16_t* __r
 #pragma unroll
   for (int q = 0; q < 16; ++q) acc[q] = 0.f;
   const long long cstride = (long long)B_img * NRT * FRAG_TILE;
-  const uint16_t* src = slab + (long long)tile * FRAG_TILE + (dt * 64 + lane) * 16;
+  const long long at = (long long)tile * FRAG_TILE + (dt * 64 + lane) * 16;
   for (int c = 0; c < n_chunks; ++c) {
-    const uint4 v0 = *(const uint4*)(src + c * cstride);
-    const uint4 v1 = *(const uint4*)(src + c * cstride + 8);
-    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    if constexpr (F32P) {
+      const float4* src = (const float4*)((const float*)slab + at + c * cstride);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      acc[2 * k] += __uint_as_float(w[k] << 16);
-      acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+      for (int k = 0; k < 4; ++k) {
+        const float4 v = src[k];
+        acc[4 * k] += v.x;
+        acc[4 * k + 1] += v.y;
+        acc[4 * k + 2] += v.z;
+        acc[4 * k + 3] += v.w;
+      }
+    } else {
+      const uint16_t* src = slab + at + c * cstride;
+      const uint4 v0 = *(const uint4*)src;
+      const uint4 v1 = *(const uint4*)(src + 8);
+      const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        acc[2 * k] += __uint_as_float(w[k] << 16);
+        acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+      }
     }
   }
   float* o = out + (long long)b * s_b + (dt * 32 + lr) * s_d;
@@ -2049,7 +2091,7 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
         a1[u][q] = __builtin_amdgcn_exp2f(A0[u][q]);
         sum += a1[u][q];
       }
-    const float inv = __builtin_amdgcn_rcpf(xhalf_sum(sum));
+    const float inv = __builtin_amdgcn_rcpf(sum_floor(xhalf_sum(sum)));
     const float kq = gL * inv;
     float rho = 0.f;
 #pragma unroll
@@ -2146,7 +2188,8 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
     }
   }
   if (rt >= NRT) return;
-  store_dr_tile(dR, n_chunks, chunk, b, rt, B_img, lane, out, s_b, s_r, s_d, slab);
+  store_dr_tile<MODE == MODE_F16>(dR, n_chunks, chunk, b, rt, B_img, lane, out, s_b, s_r, s_d,
+                                  slab);
 }
 
 // -------------------------------------------- bwd, bf16, bounded, pipelined ---
@@ -2354,7 +2397,7 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
     } else if (c == 11) {
       inv = xhalf_sum((s8[0] + s8[1]) + (s8[2] + s8[3]));
     } else if (c == 12) {
-      inv = __builtin_amdgcn_rcpf(inv);
+      inv = __builtin_amdgcn_rcpf(sum_floor(inv));
       kq = gL * inv;
       rho = 0.f;
     } else if (c < 45) {          // phase B, two chunks per token q
@@ -2465,6 +2508,316 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
   store_dr_tile(dR, n_chunks, chunk, b, rt, B_img, lane, out, s_b, s_r, s_d, slab);
 }
 
+// ------------------------------- bwd, bf16, bounded, two roles per SIMD ---
+// The same arithmetic as wr_bwd_pipe_kernel, with each region tile's work
+// split between two waves that share one SIMD (512-thread workgroup, waves w
+// and w + 4 on one SIMD):
+//   S wave (waves 0-3): G1 [S'^T ; Q-hat^T] = [W' ; C-hat] R_tile^T of
+//       caption t + 1 (32 MFMAs) in the issue gaps of the softmax recompute
+//       and both softmax backwards of caption t (the VALU-heavy half); hands
+//       the caption's M fragments [M_w | M_c] (4 KB per tile) to its partner
+//       through LDS.
+//   M wave (waves 4-7): G3 dR_tile += [M_w | M_c] [W' ; C-hat] of caption
+//       t - 1 (32 MFMAs, operands read transposed from the X image) and the
+//       X-image DMA of caption t + 2.
+// One wave per SIMD could hide only ~5 issue slots per MFMA gap and none of
+// its own waits; two waves with complementary mixes let the SIMD overlap one
+// wave's softmax VALU and LDS waits with the other's MFMAs.
+// Per stage t: barrier B1 (X(t+1) landed, M(t-1) written); S: G1(t+1) + SM(t);
+// M: reads M(t-1), G3(t-1), DMA X(t+2); barrier B2 (M(t-1) consumed); S
+// writes M(t).  Captions past the chunk read a zero token table (their M
+// fragments are zero), so the fill / drain stages need no branches.
+constexpr int BD_NB = 4;                        // X ring depth
+constexpr int BD_BUF = B_XIMG + BP_TOK;         // one caption: X image + token table
+constexpr int BD_MS = BD_NB * BD_BUF;           // M hand-off: 4 tiles x 4 KB
+constexpr int BD_ZERO = BD_MS + 4 * 4096;       // a zero token table
+constexpr int BD_LDS = BD_ZERO + BP_TOK;
+constexpr int BD_PF1 = 3;                       // G1 operand prefetch distance (slots)
+constexpr int BD_PF3 = 4;                       // G3 operand prefetch distance (slots)
+
+// MFMA slot of the M wave's stage after which DMA piece j of X(t + 2) is
+// issued (-1: none): every other slot from slot 1
+__device__ __forceinline__ constexpr int bd_dma_slot(int n) {
+  return (n >= 1 && n <= 17 && (n & 1) == 1) ? (n - 1) / 2 : -1;
+}
+
+__global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
+    const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi, int B_img, int B_cap,
+    int n_chunks, float g1, const float* __restrict__ tok, const uint16_t* __restrict__ Chi,
+    float* __restrict__ out, long long s_b, long long s_r, long long s_d,
+    uint16_t* __restrict__ slab) {
+  const int total = n_chunks * 2 * B_img;
+  const int work = xcd_remap(blockIdx.x, total);
+  const int b = work / (2 * n_chunks);
+  const int rem = work % (2 * n_chunks);
+  const int tg = rem / n_chunks, chunk = rem % n_chunks;
+  const int per = (B_cap + n_chunks - 1) / n_chunks;
+  const int c0 = chunk * per, c1 = min(B_cap, c0 + per);
+  const int K = max(0, c1 - c0);
+  const int tid = threadIdx.x, lane = tid % WAVE;
+  const int wv = __builtin_amdgcn_readfirstlane(tid / WAVE);
+  const int role = wv >> 2;                    // 0: S wave, 1: M wave
+  const int wid = wv & 3;
+  const int lr = lane & 31, h = lane >> 5;
+  const int rt = tg * 4 + wid;                 // region tile (7: padding only)
+  const bool live = rt < NRT && K > 0;
+  const int T2 = (K + 2) & ~1;                 // stages 0..K, padded to even
+  const uint32_t ms = BD_MS + wid * 4096 + lane * 16;   // this tile's M slot (lane-linear)
+
+  // zero the ring (the first G3 reads an empty image), the M slots and the
+  // zero table
+  for (int o = tid * 16; o < BD_LDS; o += 512 * 16) lds_st16(o, make_uint4(0, 0, 0, 0));
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  if (role == 1) {
+    // ================================================================ M wave
+    // DMA pieces of one caption (bwd_stage's layout): M wave wid issues
+    // pieces k = wid + 4 j (j < 8) of the X image and (every M wave, the
+    // same bytes) the token table
+    uint32_t dma_off[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = wid + 4 * j, p = k % 32, half = p / 16;
+      const int row = 4 * (p % 16) + lane / 16, pc = lane % 16;
+      const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
+      const int c = half * 16 + (pc ^ sw);
+      dma_off[j] = (j % 4 < 2) ? (uint32_t)((row * D + c * 8) * 2)
+                               : (uint32_t)(((c * 32) + (row - 32)) * 8 * 2);
+    }
+    auto dma_piece = [&](int k, int j) {
+      const int kc = min(k, K - 1);
+      const uint32_t base = (k % BD_NB) * BD_BUF;
+      const long long pair = (long long)b * B_cap + c0 + kc;
+      if (j == 8) {
+        glds16s(tok + pair * TPAD * 8, lane * 16, base + B_XIMG);
+      } else {
+        const int kk = wid + 4 * j, p = kk % 32;
+        const void* src = j % 4 < 2 ? (const void*)(Whi + (long long)(c0 + kc) * TPAD * D)
+                                    : (const void*)(Chi + pair * 32 * 32 * 8);
+        glds16s(src, dma_off[j], base + (p / 16) * (64 * 256) + 4 * (p % 16) * 256);
+      }
+    };
+    if (K > 0) {
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        dma_piece(0, j);
+        dma_piece(1, j);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");     // X(0), X(1) landed
+    asm volatile("s_barrier" ::: "memory");                           // S: G1(0) done
+
+    uint32_t g2o[2][4];
+    {
+      const int g16 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd)
+          g2o[bb][dd] = (4 * h + q4 + 8 * bb) * 256 + ((dd ^ q4) << 6) +
+                        (((2 * (g16 & 1) + (p4 >> 1)) ^ ((h + 2 * bb) & 3)) << 4) + (p4 & 1) * 8;
+    }
+    // G3 operand read u: d tile dt = u >> 2, k block ks = u & 3
+    auto g3_read = [&](int u, uint32_t xb) {
+      const int dt = u >> 2, ks = u & 3;
+      const uint32_t kb = xb + (dt >> 2) * (64 * 256) + ((ks >> 1) * 32 + (ks & 1) * 16) * 256;
+      return join_tr(lds_tr4(kb + g2o[0][dt & 3]), lds_tr4(kb + g2o[1][dt & 3]));
+    };
+    f32x16 dR[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dR[j][q] = 0.f;
+
+    for (int t = 0; t < T2; ++t) {
+      ring_barrier<0>();                       // B1: X(t+1) landed; M(t-1) written
+      const uint32_t x3 = ((t + 3) % BD_NB) * BD_BUF;        // X(t-1)
+      if (live) {
+        bf16x8 Mi[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) Mi[k] = as_bf8(lds_ld16(ms + k * 1024));
+        bf16x8 rd[8];
+#pragma unroll
+        for (int n = 0; n < BD_PF3; ++n) rd[n] = g3_read(n, x3);
+#pragma clang loop unroll(full)
+        for (int n = 0; n < 32; ++n) {
+          dR[n >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Mi[n & 3], rd[n & 7], dR[n >> 2],
+                                                              0, 0, 0);
+          if (n + BD_PF3 < 32) rd[(n + BD_PF3) & 7] = g3_read(n + BD_PF3, x3);
+          if (bd_dma_slot(n) >= 0) dma_piece(t + 2, bd_dma_slot(n));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else if (K > 0) {
+#pragma unroll
+        for (int j = 0; j < 9; ++j) dma_piece(t + 2, j);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B2
+    }
+    if (rt < NRT) store_dr_tile(dR, n_chunks, chunk, b, rt, B_img, lane, out, s_b, s_r, s_d, slab);
+    return;
+  }
+
+  // ================================================================== S wave
+  const float gL = g1 * 1.4426950408889634f;
+  // R tile as B fragments: lane (r, h), k-step s -> d = 16 s + 8 h .. + 7
+  bf16x8 Rf[16];
+  {
+    const long long roff = ((long long)b * RPAD + min(rt, NRT - 1) * 32 + lr) * D;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) Rf[s] = as_bf8(*(const uint4*)(Rhi + roff + s * 16 + h * 8));
+  }
+  uint32_t g1o[8];
+  {
+    const int sw1 = ((lr & 3) << 2) | ((lr >> 2) & 3);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g1o[k] = lr * 256 + (((2 * k + h) ^ sw1) << 4);
+  }
+  // G1 operand read u (0..15 W' rows, 16..31 C-hat rows) of the image at xb
+  auto g1_read = [&](int u, uint32_t xb) {
+    const int s = u & 15;
+    return __builtin_bit_cast(
+        u32x4, lds_ld16(xb + g1o[s & 7] + (s >> 3) * (64 * 256) + (u >= 16 ? 32 * 256 : 0)));
+  };
+  auto g1_mfma = [&](int u, const u32x4& op, f32x16& A0, f32x16& A1, const f32x16& init) {
+    const bf16x8 x = __builtin_bit_cast(bf16x8, op);
+    const int s = u & 15;
+    if (u < 16)
+      A0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, Rf[s], s == 0 ? init : A0, 0, 0, 0);
+    else
+      A1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, Rf[s], s == 0 ? (f32x16){} : A1, 0, 0,
+                                                   0);
+  };
+  // token scalar k for the lane's tokens 8g + 4h + 0..3 (q = 4g .. 4g+3)
+  auto scal = [&](uint32_t tb, int k, int g) {
+    return __builtin_bit_cast(u32x4, lds_ld16(tb + k * 128 + g * 32 + h * 16));
+  };
+  auto init_of = [&](uint32_t tb) {   // the token-bias row (scalar 6) as G1's init
+    f32x16 r;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const u32x4 x = scal(tb, 6, g);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[4 * g + k] = __uint_as_float(x[k]);
+    }
+    return r;
+  };
+  auto fl = [](const u32x4& x, int q) { return __uint_as_float(x[q & 3]); };
+
+  // softmax state of the caption in SM (a1 overwrites p in place)
+  float a1[16], ax[16], v[16];
+  float s8[8], inv = 0.f, kq = 0.f, rho = 0.f;
+  u32x4 fb[2][4], fc[2][2];     // scalars f0..f3 (phase B) / f4, f5 (phase C), by group parity
+  uint32_t mw2[8], mc2[8];
+  // SM chunk c (0..63) of the caption with token table tb and G1 results A0, A1
+  auto sm_chunk = [&](int c, uint32_t tb, const f32x16& A0, const f32x16& A1, bf16x8* Mo) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (c == 9 + 8 * g)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) fb[g & 1][k] = scal(tb, k, g);
+      if (c == 43 + 4 * g) {
+        fc[g & 1][0] = scal(tb, 4, g);
+        fc[g & 1][1] = scal(tb, 5, g);
+      }
+    }
+    if (c < 8) {                  // phase A: p = exp2(S') (bias rows: 0)
+      a1[2 * c] = __builtin_amdgcn_exp2f(A0[2 * c]);
+      a1[2 * c + 1] = __builtin_amdgcn_exp2f(A0[2 * c + 1]);
+    } else if (c == 8) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s8[k] = a1[k] + a1[k + 8];
+    } else if (c == 9) {
+#pragma unroll
+      for (int k = 4; k < 8; ++k) s8[k] = a1[k] + a1[k + 8];
+    } else if (c == 10) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s8[k] += s8[k + 4];
+    } else if (c == 11) {
+      inv = xhalf_sum((s8[0] + s8[1]) + (s8[2] + s8[3]));
+    } else if (c == 12) {
+      inv = __builtin_amdgcn_rcpf(sum_floor(inv));
+      kq = gL * inv;
+      rho = 0.f;
+    } else if (c < 45) {          // phase B, two chunks per token q
+      const int q = (c - 13) >> 1;
+      const u32x4* fb_ = fb[(q >> 2) & 1];
+      if (((c - 13) & 1) == 0) {
+        ax[q] = __builtin_amdgcn_exp2f(fmaf(a1[q], kq, fl(fb_[0], q)));   // g1 A2 / log2e
+        a1[q] = a1[q] * inv;                                              // A1
+      } else {
+        // (dA2 - sigma) = (alpha / log2e) S' + (beta / Z) Q-hat - sigma
+        const float du = fmaf(fl(fb_[1], q), A0[q], fmaf(fl(fb_[2], q), A1[q], -fl(fb_[3], q)));
+        v[q] = a1[q] * (ax[q] * du);                         // A1 dA1 / log2e
+        rho += v[q];
+      }
+    } else if (c == 45) {
+      rho = xhalf_sum(rho);
+    } else if (c < 62) {          // phase C, one chunk per token q
+      const int q = c - 46;
+      const u32x4* fc_ = fc[(q >> 2) & 1];
+      const float dsx = fmaf(-a1[q], rho, v[q]);              // dS / log2e
+      v[q] = fmaf(fl(fc_[0], q), ax[q], dsx);                  // M_w (scaled for W')
+      ax[q] = fl(fc_[1], q) * ax[q];                           // M_c (for C-hat)
+      if (q & 1) {
+        mw2[q >> 1] = pk_bf16(v[q - 1], v[q]);
+        mc2[q >> 1] = pk_bf16(ax[q - 1], ax[q]);
+      }
+      if (q == 15) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          Mo[k] = __builtin_bit_cast(bf16x8, make_uint4(mw2[4 * k], mw2[4 * k + 1],
+                                                          mw2[4 * k + 2], mw2[4 * k + 3]));
+          Mo[2 + k] = __builtin_bit_cast(bf16x8, make_uint4(mc2[4 * k], mc2[4 * k + 1],
+                                                              mc2[4 * k + 2], mc2[4 * k + 3]));
+        }
+        asm volatile("" ::"v"(Mo[0]), "v"(Mo[1]), "v"(Mo[2]), "v"(Mo[3]));
+      }
+    }
+  };
+
+  // one stage t: G1(t+1) -> (A0n, A1n) in the gaps of SM(t) on (A0, A1)
+  auto stage = [&](int t, f32x16& A0, f32x16& A1, f32x16& A0n, f32x16& A1n) {
+    ring_barrier<0>();                 // B1: X(t+1) landed everywhere
+    const uint32_t x1 = ((t + 1) % BD_NB) * BD_BUF;          // G1 image
+    const uint32_t tbs = t < K ? (t % BD_NB) * BD_BUF + B_XIMG : BD_ZERO;
+    const f32x16 init = init_of(x1 + B_XIMG);
+    bf16x8 Mo[4];
+    u32x4 rd[4];
+#pragma unroll
+    for (int n = 0; n < BD_PF1; ++n) rd[n] = g1_read(n, x1);
+#pragma clang loop unroll(full)
+    for (int n = 0; n < 32; ++n) {
+      g1_mfma(n, rd[n & 3], A0n, A1n, init);
+      if (n + BD_PF1 < 32) rd[(n + BD_PF1) & 3] = g1_read(n + BD_PF1, x1);
+      sm_chunk(2 * n, tbs, A0, A1, Mo);
+      sm_chunk(2 * n + 1, tbs, A0, A1, Mo);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B2: M(t-1) consumed
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lds_st16(ms + k * 1024, __builtin_bit_cast(uint4, Mo[k]));
+  };
+
+  asm volatile("s_barrier" ::: "memory");                             // X(0), X(1) landed
+  f32x16 Aa0, Aa1, Ab0, Ab1;
+  if (live) {
+    const f32x16 init = init_of(B_XIMG);
+#pragma unroll
+    for (int u = 0; u < 32; ++u) g1_mfma(u, g1_read(u, 0), Aa0, Aa1, init);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");     // G1(0) done
+  if (!live) {
+    // the padding tile (and an empty chunk): only the barriers
+    for (int t = 0; t < T2; ++t)
+      asm volatile("s_barrier\n\ts_barrier" ::: "memory");
+    return;
+  }
+  for (int t = 0; t < T2; t += 2) {
+    stage(t, Aa0, Aa1, Ab0, Ab1);
+    stage(t + 1, Ab0, Ab1, Aa0, Aa1);
+  }
+}
+
 __global__ __launch_bounds__(256) void wr_reduce_kernel(const float* __restrict__ slab,
                                                         int n_chunks, int B_img,
                                                         float* __restrict__ out, long long s_b,
@@ -2516,11 +2869,15 @@ static int slab_chunks(int B_img, int B_cap) {
 // the bounded kernels' dR: written in place by the kernel (one chunk), else
 // the chunks' fragment-order bf16 partials summed by wr_reduce_frag_kernel
 static int frag_reduce(int n_chunks, int B_img, const uint16_t* slab, float* dR, long long s_b,
-                       long long s_r, long long s_d, hipStream_t s) {
+                       long long s_r, long long s_d, hipStream_t s, bool f32_partials = false) {
   if (n_chunks > 1) {
     const int threads = B_img * NRT * 8 * 64;
-    hipLaunchKernelGGL(wr_reduce_frag_kernel, dim3((threads + 255) / 256), dim3(256), 0, s, slab,
-                       n_chunks, B_img, dR, s_b, s_r, s_d);
+    if (f32_partials)
+      hipLaunchKernelGGL(wr_reduce_frag_kernel<true>, dim3((threads + 255) / 256), dim3(256), 0, s,
+                         slab, n_chunks, B_img, dR, s_b, s_r, s_d);
+    else
+      hipLaunchKernelGGL(wr_reduce_frag_kernel<false>, dim3((threads + 255) / 256), dim3(256), 0,
+                         s, slab, n_chunks, B_img, dR, s_b, s_r, s_d);
   }
   return (int)hipGetLastError();
 }
@@ -2681,12 +3038,13 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                          tok_ws, Chi, dR, s_b, s_r, s_d, (uint16_t*)ws);
     else
       return 1002;
-    return frag_reduce(n_chunks, B_img, (const uint16_t*)ws, dR, s_b, s_r, s_d, s);
+    return frag_reduce(n_chunks, B_img, (const uint16_t*)ws, dR, s_b, s_r, s_d, s,
+                       mode == MODE_F16);
   } else if (bounded) {
     if (t_pad != 32) return 1001;
     if (mode != MODE_BF16) return 1002;
-    if (const int e = allow_lds(wr_bwd_pipe_kernel, BP_LDS)) return e;
-    hipLaunchKernelGGL(wr_bwd_pipe_kernel, dim3(grid), dim3(256), BP_LDS, s, Rhi, Whi, B_img,
+    if (const int e = allow_lds(wr_bwd_duo_kernel, BD_LDS)) return e;
+    hipLaunchKernelGGL(wr_bwd_duo_kernel, dim3(grid), dim3(512), BD_LDS, s, Rhi, Whi, B_img,
                        B_cap, n_chunks, gamma1, tok_ws, Chi, dR, s_b, s_r, s_d, (uint16_t*)ws);
     return frag_reduce(n_chunks, B_img, (const uint16_t*)ws, dR, s_b, s_r, s_d, s);
   } else if (mode == MODE_SPLIT && (!Rlo || !Wlo || !Clo)) {

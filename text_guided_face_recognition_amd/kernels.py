@@ -41,6 +41,9 @@ def _wr_mode(mode):
 
 
 LOG2E = 1.4426950408889634
+# largest score bound max|W| max|R| the max-free word<->region kernels handle
+# exactly (csrc/tgfr_wr.hip, bound_shift)
+WR_BOUND_MAX = 85.9
 
 
 def prep_rows(x, n_rows, rows_pad, lens=None, want_norms=False, scale=1.0, f16=False):
@@ -118,6 +121,7 @@ class WordRegionLogits(torch.autograd.Function):
             (m == MODES["bf16"] and not att_T and t_pad == TPAD) or
             (m != MODES["fp32"] and t_pad == 2 * TPAD))
         pre = attached_rows(img_features, f16) if bf16 else None
+        own_rows = pre is not None
         if pre is not None:            # written by the IMIM tail kernel
             (r_hi, r_norm), r_lo = pre, None
         else:
@@ -128,15 +132,35 @@ class WordRegionLogits(torch.autograd.Function):
             # backward the plain ones.  (Written by TextHeading when it made
             # the words; every caption then has t_words valid words.)
             pre = attached_rows(words, f16, scale=LOG2E) if uniform else None
-            if pre is not None and pre[0].shape[1] == t_pad:
+            w_attached = pre is not None and pre[0].shape[1] == t_pad
+            if w_attached:
                 w_fwd, w_norm = pre
             else:
+                if _rows_only(words):
+                    raise RuntimeError("words carry only their operand rows "
+                                       "(rows_only_words), which this call cannot use")
+                own_rows = False
                 w_fwd, _, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,
                                              want_norms=True, scale=LOG2E, f16=f16)
+            # The max-free kernels are exact while the score bound max|W|
+            # max|R| <= WR_BOUND_MAX (csrc/tgfr_wr.hip, bound_shift).  Rows
+            # made by this package's heads are L2-normalised (bound ~1); other
+            # inputs are checked here (one host read, skipped under graph
+            # capture) and past the bound take the exact running-max kernels,
+            # as the reference's softmax never overflows (models/attention.py:28-36)
+            if bounded and not own_rows and not torch.cuda.is_current_stream_capturing():
+                if not float((w_norm.max() * r_norm.max()).item()) <= WR_BOUND_MAX:
+                    bounded = fast = False
+            if _rows_only(words) and not fast:
+                raise RuntimeError("words carry only their bounded-kernel operand rows "
+                                   "(rows_only_words): this path needs the feature values")
             w_hi = w_fwd if fast else prep_rows(words.float(), t_words, t_pad, lens=lens,
                                                 f16=f16)[0]
             w_lo = None
         else:
+            if _rows_only(words):
+                raise RuntimeError("words carry only their bf16 / fp16 operand rows "
+                                   "(rows_only_words): fp32 mode needs the feature values")
             w_hi, w_lo, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,
                                            want_norms=True)
             w_fwd = w_hi
@@ -1157,6 +1181,25 @@ def attach_rows(x, rows, norms, f16, scale=1.0):
     x._tgfr_rows = (rows, norms, bool(f16), float(scale), x._version, x.data_ptr(),
                     tuple(x.shape), tuple(x.stride()))
     return x
+
+
+def rows_only_words(rows, norms, n_words, f16, scale=LOG2E):
+    """A words tensor [B, 256, n_words] that carries ONLY its operand rows
+    (rows [B, t_pad, 256], norms [B, t_pad], attach_rows) -- no feature
+    values: the text side of a data-parallel step, all-gathered as the
+    word<->region kernels' bf16 / fp16 rows (half the bytes of the fp32
+    words).  Any path that would read its values raises
+    (WordRegionLogits)."""
+    b = rows.shape[0]
+    base = torch.empty_strided((b, n_words, D), (0, 0, 0), dtype=torch.float32,
+                               device=rows.device)
+    base._tgfr_rows_only = True
+    attach_rows(base, rows, norms, f16, scale)
+    return base.transpose(1, 2)
+
+
+def _rows_only(x):
+    return any(getattr(t, "_tgfr_rows_only", False) for t in (x, getattr(x, "_base", None)))
 
 
 def attached_rows(x, f16, scale=1.0):

@@ -153,7 +153,10 @@ def sent_global_loss(cnn_code, rnn_code, labels, class_ids, batch_size, args, ep
     above."""
     row_offset, n_global, group = _dist(args)
     n = cnn_code.shape[0]
-    if labels is not None and n <= 64:
+    # the fused kernels return no gradient for the sentence codes (the
+    # reference's text side is detached, utils/dataset_utils.py:42); a caller
+    # whose codes require grad takes the per-loss path, which computes it
+    if labels is not None and n <= 64 and not rnn_code.requires_grad:
         cls = _class_tensor(class_ids, cnn_code.device)
         if group is None and n == rnn_code.shape[0]:
             return K.sent_global(cnn_code, rnn_code, cls, args.TRAIN.SMOOTH.GAMMA3, temp3, eps)

@@ -163,9 +163,11 @@ class TextHeading(nn.Module):
                                "in torch.no_grad()")
         # bf16 / fp16: the pooling launch also writes the words as the
         # word<->region kernels' log2(e)-scaled operand rows (losses.py:96)
+        # (captions past 64 words have no operand layout: the word<->region
+        # kernels then prepare their rows themselves)
         spec = None
-        if self.precision in ("bf16", "fp16"):
-            n = words_emb.shape[1] - 1
+        n = words_emb.shape[1] - 1
+        if self.precision in ("bf16", "fp16") and n <= 2 * K.TPAD:
             spec = (K.TPAD if n <= K.TPAD else 2 * K.TPAD, K.LOG2E, self.precision == "fp16")
         words, sent = K.text_heading(words_emb, self.packed_taps(),
                                      [c.bias for c in self.bwm.convs1], mode=self._conv_mode(),

@@ -104,7 +104,9 @@ class Train:
         self.head_params = list(self.image_head.parameters())
         self.cls_params = list(self.image_cls.parameters()) + list(self.text_cls.parameters())
         self.params = self.head_params + self.cls_params
-        self.ctx.broadcast_params(self.params)
+        # the frozen text head too: every rank must make its captions with the
+        # same weights, or the gathered words mix different text heads
+        self.ctx.broadcast_params(self.params + list(self.text_head.parameters()))
         self.ident_loss = FocalLoss(gamma=2)
         # :212 (text_head params would join here; the text side is frozen input)
         # :212 Adam for the head, :219-222 SGD for both classifiers: one launch
@@ -128,8 +130,7 @@ class Train:
         ctx.set_batch(b)
         args.dist = ctx
         # text side: all-gathered global batch (detached, as in the reference)
-        words_g, sent_g, cls_g = ctx.gather_text(words.transpose(1, 2), sent, class_ids)
-        words_g = words_g.transpose(1, 2)
+        words_g, sent_g, cls_g = self._gather_text(words, sent, class_ids)
         labels = self._labels(ctx.n_global, g.device)
 
         img_features, words_features = self.image_head(g, local)   # :265
@@ -167,6 +168,25 @@ class Train:
         ctx.reduce_grads(self.head_params)
         self.optimizer.step()
         return {"damsm": report[0], "clip": report[1], "ident": report[2]}
+
+    def _gather_text(self, words, sent, class_ids):
+        """(words, sent, class ids) of the global batch in one all-gather.
+        Words that carry the word<->region kernels' operand rows (TextHeading
+        in bf16 / fp16 mode) travel as those rows + norms -- bf16 / fp16
+        [t_pad, 256] per caption, about half the fp32 words' bytes -- and the
+        gathered words are rows-only (kernels.rows_only_words): the DP step
+        then re-prepares nothing.  Otherwise the fp32 words themselves."""
+        ctx = self.ctx
+        words_bt = words.transpose(1, 2)               # [B, T, 256] storage
+        f16 = self.args.precision == "fp16"
+        pre = K.attached_rows(words_bt, f16, scale=K.LOG2E) \
+            if ctx.active and self.args.precision in ("bf16", "fp16") else None
+        if pre is not None:
+            rows, norms = pre
+            rows_g, norms_g, sent_g, cls_g = ctx.gather_text(rows, norms, sent, class_ids)
+            return K.rows_only_words(rows_g, norms_g, words.shape[2], f16), sent_g, cls_g
+        words_g, sent_g, cls_g = ctx.gather_text(words_bt, sent, class_ids)
+        return words_g.transpose(1, 2), sent_g, cls_g
 
     def _identity(self, sent, img_features, class_ids, ctx):
         """(focal(text_cls(sent)), focal(image_cls(img))): one launch per

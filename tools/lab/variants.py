@@ -26,12 +26,15 @@ _OLD_PAD_SKIP = ("  // ---- prologue: G1 of caption 0\n",
             "    return;\n  }\n"
             "  // ---- prologue: G1 of caption 0\n")
 
-# round 3: LDS operand prefetch distance of the bounded forward (wr_fwd_pipe_kernel)
+# round 4: the two-role backward (wr_bwd_duo_kernel) against round 3's
+# one-wave-per-SIMD pipe kernel
+_DUO = ("""    if (const int e = allow_lds(wr_bwd_duo_kernel, BD_LDS)) return e;
+    hipLaunchKernelGGL(wr_bwd_duo_kernel, dim3(grid), dim3(512), BD_LDS, s, Rhi, Whi, B_img,""")
+_PIPE = ("""    if (const int e = allow_lds(wr_bwd_pipe_kernel, BP_LDS)) return e;
+    hipLaunchKernelGGL(wr_bwd_pipe_kernel, dim3(grid), dim3(256), BP_LDS, s, Rhi, Whi, B_img,""")
 VARIANTS = {
     "base": [],
-    "fpf4": [("constexpr int PF_FWD = 3;", "constexpr int PF_FWD = 4;")],
-    "fpf5": [("constexpr int PF_FWD = 3;", "constexpr int PF_FWD = 5;")],
-    "fpf6": [("constexpr int PF_FWD = 3;", "constexpr int PF_FWD = 6;")],
+    "pipe": [(_DUO, _PIPE)],
 }
 
 

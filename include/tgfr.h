@@ -68,10 +68,11 @@ int tgfr_prep_rows_f16(const float* x, long long s_item, long long s_row, long l
  * [B_cap][32].  Mode 0 keeps the image's R resident in LDS (Rlo/Wlo unused, may
  * be NULL) and takes the words scaled by log2(e) (Whi = bf16(log2(e) W),
  * tgfr_prep_rows scale).  bounded = 1 (with Rnorm = |R_r| [B_img][224]) lets
- * the mode-0 forward shift every caption's scores by max|W| max|R| instead of
- * a running max (exact while that product is < 43, e.g. the unit-norm
- * BERT-path features); otherwise the exact-max kernel runs.  C is stored
- * unnormalised (C-hat = Z C); tgfr_wr_bwd_tok folds the 1/Z back in. */
+ * the mode-0 forward run without a running max (max-free kernels: exact for
+ * any input whose score bound max|W| max|R| is <= 85.9 -- unshifted up to
+ * 84.5, shifted by the bound beyond; the unit-norm BERT-path features have
+ * ~1); otherwise the exact-max kernel runs.  C is stored unnormalised
+ * (C-hat = Z C); tgfr_wr_bwd_tok folds the 1/Z back in. */
 int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, const float* Wnorm, const float* Rnorm, const int* lens,
                 int B_img, int B_cap,
@@ -87,15 +88,14 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
  * accumulated.  ws: tgfr_wr_bwd_ws floats of workspace: caption-chunk partial
  * slabs, added in chunk order into dR by a reduction launch inside the call.
  * Rnorm (bounded only; the forward's |R_r| [B_img][224]): the pair's score
- * bound c = max|W| max|R| is formed again here, and from c >= 40 on the
- * max-free backwards shift the recomputed scores by it exactly as the
- * bounded forward does, so the bounded kernels stay finite past the unit-norm
- * contract (fp32 range: c < ~58 for any input).  The text side is detached in the
- * reference (utils/dataset_utils.py:42).  bounded = 1 (mode 0 with t_pad 32
- * after a bounded forward, or modes 0 / 2 with t_pad 64; scores bounded as
- * for tgfr_wr_fwd): both calls must pass it, Whi is the forward's
- * log2(e)-scaled words, and the max-free kernels run (t_pad 32: the
- * software-pipelined one). */
+ * bound c = max|W| max|R| is formed again here and the recomputed scores are
+ * shifted exactly as the bounded forward shifted them (none below c = 84.5).
+ * The text side is detached in the reference (utils/dataset_utils.py:42).
+ * bounded = 1 (mode 0 with t_pad 32 after a bounded forward, or modes 0 / 2
+ * with t_pad 64; scores bounded as for tgfr_wr_fwd): both calls must pass
+ * it, Whi is the forward's
+ * log2(e)-scaled words, and the max-free kernels run (t_pad 32: the two-role
+ * one, wr_bwd_duo_kernel). */
 int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const float* Rnorm, const int* lens,
                     int B_img, int B_cap, float gamma1, float gamma2, float gamma3, float eps,
                     const float* dlogits, int ld, int bounded, int t_pad, float* tok_ws,

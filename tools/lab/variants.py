@@ -18,23 +18,75 @@ from text_guided_face_recognition_amd import build as B  # noqa: E402
 OUT = os.path.join(ROOT, "tools", "lab", "build")
 
 # name -> list of (old, new) substitutions in tgfr_wr.hip
-_OLD_PAD_SKIP = ("  // ---- prologue: G1 of caption 0\n",
-            "  if (rt >= NRT) {       // the padding tile: only its share of the DMA\n"
-            "    asm volatile(\"s_waitcnt vmcnt(0)\\n\\ts_waitcnt lgkmcnt(0)\\n\\ts_barrier\" ::: \"memory\");\n"
-            "    const int T2p = (K + 2) & ~1;\n"
-            "    for (int t = 0; t < T2p; ++t) { ring_barrier<0>(); stage_dma(t + 2); }\n"
-            "    return;\n  }\n"
-            "  // ---- prologue: G1 of caption 0\n")
-
 # round 4: the two-role backward (wr_bwd_duo_kernel) against round 3's
 # one-wave-per-SIMD pipe kernel
 _DUO = ("""    if (const int e = allow_lds(wr_bwd_duo_kernel, BD_LDS)) return e;
     hipLaunchKernelGGL(wr_bwd_duo_kernel, dim3(grid), dim3(512), BD_LDS, s, Rhi, Whi, B_img,""")
 _PIPE = ("""    if (const int e = allow_lds(wr_bwd_pipe_kernel, BP_LDS)) return e;
     hipLaunchKernelGGL(wr_bwd_pipe_kernel, dim3(grid), dim3(256), BP_LDS, s, Rhi, Whi, B_img,""")
+# ablations of the two-role backward (timing only: results are wrong)
+_SM = ("""      sm_chunk(2 * n, tbs, A0, A1, Mo);
+      sm_chunk(2 * n + 1, tbs, A0, A1, Mo);""")
+_G3 = ("""          dR[n >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Mi[n & 3], rd[n & 7], dR[n >> 2],
+                                                              0, 0, 0);""")
+_DMA = ("""          if (bd_dma_slot(n) >= 0) dma_piece(t + 2, bd_dma_slot(n));""")
+_SWAVE = ("""  // ================================================================== S wave
+  const float gL = g1 * 1.4426950408889634f;""")
+_MWAVE = ("""    // ================================================================ M wave
+    // DMA pieces of one caption (bwd_stage's layout): M wave wid issues""")
+# in-kernel stamps of the two-role backward (s_memtime at B1 done, work done,
+# B2 done for stages 8..23 of every wave) into a device array of the variant's
+# own code object, read back by tools/lab/stamps_duo.py (tgfr_lab_stamps)
+_STAMP_DEF = ("""constexpr int BD_PF3 = 4;                       // G3 operand prefetch distance (slots)""",
+              """constexpr int BD_PF3 = 4;                       // G3 operand prefetch distance (slots)
+__device__ unsigned long long g_lab_stamps[512 * 8 * 16 * 4];
+#define LAB_STAMP(t, k) do { if ((t) >= 8 && (t) < 24 && lane == 0) \\
+  g_lab_stamps[((blockIdx.x * 8 + wv) * 16 + ((t) - 8)) * 4 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)""")
+_STAMPS = [
+    _STAMP_DEF,
+    ("""    ring_barrier<0>();                 // B1: X(t+1) landed everywhere""",
+     """    ring_barrier<0>();                 // B1: X(t+1) landed everywhere
+    LAB_STAMP(t, 0);"""),
+    (r"""      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B2: M(t-1) consumed""",
+     r"""      __builtin_amdgcn_sched_barrier(0);
+    }
+    LAB_STAMP(t, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B2: M(t-1) consumed
+    LAB_STAMP(t, 2);"""),
+    ("""      ring_barrier<0>();                       // B1: X(t+1) landed; M(t-1) written""",
+     """      ring_barrier<0>();                       // B1: X(t+1) landed; M(t-1) written
+      LAB_STAMP(t, 0);"""),
+    (r"""      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B2
+    }""",
+     r"""      LAB_STAMP(t, 1);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B2
+      LAB_STAMP(t, 2);
+    }"""),
+    ("""int tgfr_version(void) { return 300; }""",
+     """int tgfr_version(void) { return 300; }
+int tgfr_lab_stamps(void* dst, long long bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_lab_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}"""),
+]
 VARIANTS = {
     "base": [],
-    "pipe": [(_DUO, _PIPE)],
+    "head": "HEAD",
+    "nosm": [(_SM, """      asm volatile("" ::"v"(A0), "v"(A1));""")],
+    "nog3": [(_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));""")],
+    "nodma": [(_DMA, "")],
+    "prio_s": [(_SWAVE, _SWAVE + "\n  __builtin_amdgcn_s_setprio(1);")],
+    "stamps": _STAMPS,
+    "pf1_5": [("constexpr int BD_PF1 = 3;", "constexpr int BD_PF1 = 5;")],
+    "pf3_6": [("constexpr int BD_PF3 = 4;", "constexpr int BD_PF3 = 6;")],
+    "pf56": [("constexpr int BD_PF1 = 3;", "constexpr int BD_PF1 = 5;"),
+             ("constexpr int BD_PF3 = 4;", "constexpr int BD_PF3 = 6;")],
+    "dma_early": [("return (n >= 1 && n <= 17 && (n & 1) == 1) ? (n - 1) / 2 : -1;",
+                   "return n < 9 ? n : -1;")],
+    "prio_s2": [(_SWAVE, _SWAVE + "\n  __builtin_amdgcn_s_setprio(2);"),
+                (_MWAVE, _MWAVE.replace("    // DMA", "    __builtin_amdgcn_s_setprio(0);\n    // DMA"))],
+    "prio_m": [(_MWAVE, _MWAVE.replace("    // DMA", "    __builtin_amdgcn_s_setprio(1);\n    // DMA"))],
 }
 
 

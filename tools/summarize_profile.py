@@ -20,13 +20,16 @@ import sys
 
 # ABI entry point -> alternative kernel sets (the first set fully present wins);
 # one ABI call launches every kernel of its set once
-ABI_KERNELS = {"tgfr_wr_bwd": (("wr_bwd_pipe_kernel", "wr_reduce_frag_kernel"),
+ABI_KERNELS = {"tgfr_wr_bwd": (("wr_bwd_duo_kernel", "wr_reduce_frag_kernel"),
+                               ("wr_bwd_duo_kernel",),
+                               ("wr_bwd_pipe_kernel", "wr_reduce_frag_kernel"),
                                ("wr_bwd_wide2_kernel", "wr_reduce_frag_kernel"),
                                ("wr_bwd_wide2_kernel",),
                                ("wr_bwd_pipe_kernel", "wr_reduce_kernel"),
                                ("wr_bwd_wide_kernel", "wr_reduce_kernel"),
                                ("wr_bwd_kernel", "wr_reduce_kernel")),
-               "tgfr_wr_fwd": (("wr_fwd_pipe_kernel",), ("wr_fwd_res2_kernel",),
+               "tgfr_wr_fwd": (("wr_fwd_duo_kernel",), ("wr_fwd_pipe_kernel",),
+                               ("wr_fwd_res2_kernel",),
                                ("wr_fwd_res_kernel",),
                                ("wr_fwd_kernel",))}
 

@@ -11,8 +11,10 @@ import json
 import os
 import sys
 
-KERNELS = ("wr_bwd_pipe_kernel", "wr_fwd_pipe_kernel", "wr_bwd_wide2_kernel",
-           "wr_fwd_res2_kernel", "wr_reduce_frag_kernel")
+KERNELS = ("wr_bwd_duo_kernel", "wr_fwd_duo_kernel", "wr_bwd_pipe_kernel", "wr_fwd_pipe_kernel",
+           "wr_bwd_wide2_kernel", "wr_fwd_res2_kernel", "wr_reduce_frag_kernel")
+# waves that share one SIMD for the kernel's whole life (its workgroup size / 256)
+WAVES_PER_SIMD = {"wr_bwd_duo_kernel": 2, "wr_fwd_duo_kernel": 2}
 
 
 def main(out, note, *dirs):
@@ -33,6 +35,8 @@ def main(out, note, *dirs):
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
         res[k] = avg
     flops = {"wr_bwd_pipe_kernel": 6 * 196 * 256 * 30 * 64 * 64,
+             "wr_bwd_duo_kernel": 6 * 196 * 256 * 30 * 64 * 64,
+             "wr_fwd_duo_kernel": 4 * 196 * 256 * 30 * 64 * 64,
              "wr_fwd_pipe_kernel": 4 * 196 * 256 * 30 * 64 * 64}
     derived = {}
     for k, avg in res.items():
@@ -46,10 +50,12 @@ def main(out, note, *dirs):
             # (SQ_INSTS_VALU counts the MFMAs too)
             d["valu_insts_per_mfma"] = (avg["SQ_INSTS_VALU"] - avg["SQ_INSTS_MFMA"]) / avg["SQ_INSTS_MFMA"]
         if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "SQ_WAVE_CYCLES" in avg:
-            # one wave per SIMD: the matrix core's busy cycles (32 per
-            # 32x32x16 MFMA) over the waves' resident cycles (quad-cycles x 4)
-            d["mfma_busy_over_wave_cycles"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (
-                4 * avg["SQ_WAVE_CYCLES"])
+            # the matrix core's busy cycles (32 per 32x32x16 MFMA) over the
+            # SIMDs' resident cycles: the waves' (quad-cycles x 4) divided by
+            # the waves that share a SIMD (co-resident for the whole kernel)
+            w = WAVES_PER_SIMD.get(k, 1)
+            d["mfma_busy_over_simd_cycles"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (
+                4 * avg["SQ_WAVE_CYCLES"] / w)
         if "SQ_WAIT_ANY" in avg and "SQ_WAVE_CYCLES" in avg:
             d["wait_any_over_wave_cycles"] = avg["SQ_WAIT_ANY"] / avg["SQ_WAVE_CYCLES"]
         derived[k] = d

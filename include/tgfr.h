@@ -236,6 +236,12 @@ int tgfr_ce_grad(const float* L, long long ld, int n_r, int n_c, int row_offset,
 int tgfr_linear_bf16out(const float* A, long long sAm, int M, int K, const float* W,
                         long long sWn, const float* bias, int N, uint16_t* C, long long sCm,
                         void* stream);
+/* The same with a bf16 A (rows 16-B aligned, sAm % 8 == 0): the BatchNorm'd
+ * map of tgfr_bn_fwd_cl_bf16; identical products (the fp32 path rounds A to
+ * bf16 at fragment read). */
+int tgfr_linear_bf16io(const uint16_t* A, long long sAm, int M, int K, const float* W,
+                       long long sWn, const float* bias, int N, uint16_t* C, long long sCm,
+                       void* stream);
 
 int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, const float* B,
                long long sBb, long long sBk, long long sBn, float* C, long long sCb,
@@ -376,6 +382,55 @@ int tgfr_tail_bwd(const float* dR, long long lddr, const float* R, long long ldr
                   const uint16_t* H2b, float* dZ, long long lddz, uint16_t* dPb, uint16_t* dH2b,
                   uint16_t* dH1b, void* stream);
 int tgfr_tail_dw_ws(int rows, long long* floats);
+/* The tail with IMIM's LayerNorm([C, H, W]) (models/models.py:401) fused in,
+ * on the attention output X [rows][256] (channels-last, rows = n * hw, hw >=
+ * 32): Z = LayerNorm(X) is formed on the tail's load and never stored, and the
+ * LayerNorm backward's per-sample sums run in the tail backward's epilogue.
+ * Replaces tgfr_ln_fwd + tgfr_tail_pack + tgfr_tail_fwd (forward) and
+ * tgfr_tail_bwd + tgfr_ln_bwd (backward): 3 + 3 launches instead of 4 + 4.
+ *   ws: tgfr_ln_tail_ws floats, one buffer for the pair (LayerNorm moments and
+ *     statistics, the backward's partial sums, the affine maps as
+ *     channels-last rows); the forward's contents are read by the backward.
+ *   tail_pack_ln: tail_pack plus the affine maps lnw, lnb ([256][hw], as the
+ *     reference stores them) transposed into ws.
+ *   ln_tail_fwd: LayerNorm slice moments of X, then tail_fwd on the
+ *     normalised rows (ln_eps: nn.LayerNorm eps); outputs as tgfr_tail_fwd.
+ *   ln_tail_bwd: tail_bwd (dZ [rows][256] fp32, dPb, dH2b, dH1b) plus the
+ *     LayerNorm backward: dX [rows][256], dlnw / dlnb [256][hw] (reference
+ *     layout, overwritten).  tgfr_tail_dw then takes the same saved operands. */
+int tgfr_ln_tail_ws(int rows, int hw, long long* floats);
+int tgfr_tail_pack_ln(const float* W1, const float* W2, const float* Wp, const float* lnw,
+                      const float* lnb, int rows, int hw, uint16_t* pk, float* ws, void* stream);
+int tgfr_ln_tail_fwd(const float* X, int rows, int hw, float ln_eps, float* ws,
+                     const uint16_t* pk, const float* b1, const float* b2, const float* bp,
+                     float eps, float* R, long long ldr, uint16_t* Zb, uint16_t* H1b,
+                     uint16_t* H2b, float* inv, uint16_t* Rrows, float* Rnorm,
+                     int rows_per_item, int rows_pad, int rows_f16, void* stream);
+int tgfr_ln_tail_bwd(const float* dR, const float* R, const float* inv, int rows, float eps,
+                     const uint16_t* pk, const uint16_t* H1b, const uint16_t* H2b,
+                     const float* X, int hw, float* ws, float* dZ, uint16_t* dPb,
+                     uint16_t* dH2b, uint16_t* dH1b, float* dX, float* dlnw, float* dlnb,
+                     void* stream);
+/* IMIM as one node (kernels.ImimFused): tgfr_imim_pack = tgfr_bn_fold3 (the
+ * q/k/v weights Wqkv[3] / biases bqkv[3] (nullable), rows_qkv rows of C each,
+ * folded with gamma / beta into Wf, bf) + tgfr_tail_pack_ln, one launch;
+ * tgfr_ln_tail_bwd_att = tgfr_ln_tail_bwd writing, instead of dX, the
+ * attention backward's operands into att_ws (tgfr_attn_bwd's workspace: D
+ * [rows] = rowsum(dX * X), then dX [rows][256] in bf16); tgfr_attn_bwd_prepped
+ * = tgfr_attn_bwd without its prep pass, reading them from ws. */
+int tgfr_imim_pack(const float* const* Wqkv, const float* const* bqkv, int rows_qkv, int C,
+                   const float* gamma, const float* beta, float* Wf, float* bf, const float* W1,
+                   const float* W2, const float* Wp, const float* lnw, const float* lnb,
+                   int rows, int hw, uint16_t* pk, float* ws, void* stream);
+int tgfr_ln_tail_bwd_att(const float* dR, const float* R, const float* inv, int rows, float eps,
+                         const uint16_t* pk, const uint16_t* H1b, const uint16_t* H2b,
+                         const float* X, int hw, float* ws, float* dZ, uint16_t* dPb,
+                         uint16_t* dH2b, uint16_t* dH1b, void* att_ws, float* dlnw, float* dlnb,
+                         void* stream);
+int tgfr_attn_bwd_prepped(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long long ld,
+                          long long sb, int B, int hw, float scale, const float* lse,
+                          uint16_t* dQ, uint16_t* dK, uint16_t* dV, long long ldg, long long sbg,
+                          void* ws, void* stream);
 /* Generic bf16 weight gradient of a row-wise linear map: dW [N][K] = X^T Y,
  * db [N] = column sums of X, for dense X [rows][N] bf16 and Y [rows][K]
  * (bf16, or fp32 when y_f32); N, K multiples of 128; fp32 outputs
@@ -415,6 +470,11 @@ int tgfr_loss_mix_bwd(const float* g, int n, const float* W, float* dloss, void*
 int tgfr_bn_fwd_cl(const float* x, int N, int C, int HW, float eps, float momentum,
                    int training, float* running_mean, float* running_var, long long* nbt,
                    float* mean, float* rstd, float* xhat, void* stream);
+/* tgfr_bn_fwd_cl with xhat written in bf16 (bf16 mode without a BN input
+ * gradient: its consumers, tgfr_linear_bf16io and tgfr_dw_bf16, read bf16). */
+int tgfr_bn_fwd_cl_bf16(const float* x, int N, int C, int HW, float eps, float momentum,
+                        int training, float* running_mean, float* running_var, long long* nbt,
+                        float* mean, float* rstd, uint16_t* xhat, void* stream);
 /* BatchNorm2d input gradient: dx [N][C][HW] from the channels-last gradient
  * of xhat, dxh [N][HW][C], xhat and rstd of tgfr_bn_fwd_cl; training = batch
  * statistics (rstd (dxh - mean dxh - xhat mean(dxh xhat))), else rstd dxh. */
@@ -488,6 +548,38 @@ int tgfr_arc_fwd_heads(const tgfr_arc_head* heads, int n_heads, int B, int D, in
                        int easy, float eps, void* stream);
 int tgfr_arc_focal_bwd_heads(const tgfr_arc_head* heads, int n_heads, int B, int D, int C,
                              float m, int easy, float eps, float gamma, void* stream);
+
+/* ---- small-batch fp32 heads (csrc/tgfr_proj.hip) ---------------------------
+ * tgfr_proj_l2norm_fwd: g = normalize(x W^T + b) per row, F.normalize(dim = 1,
+ * eps) after nn.Linear -- ImageHeading.project_global (models/models.py:98-120,
+ * :336) -- in one launch, exact fp32 (VALU FMA).  x [B][K] (ldx), W [N][K]
+ * (ldw), bias [N] (nullable); g [B][N] (ldg), inv_norm [B] = 1 / max(|y|, eps)
+ * for the backward.  N % 32 == 0, N <= 1024, K % 4 == 0, K <= 612, 16-B
+ * aligned x / W.
+ * ws: tgfr_proj_l2norm_ws floats.  counters: zeroed words (ceil(B / 8) used,
+ * left zero).  Replaces tgfr_bgemm + tgfr_l2norm_rows.
+ * tgfr_proj_dw: the Linear's weight gradient from dy (the l2-norm backward's
+ * output, tgfr_l2norm_rows_bwd): dW = dy^T x [N][K] (lddw), db = colsum dy
+ * (nullable); B <= 64.  Replaces tgfr_bias_grad + tgfr_bgemm.  Both: fixed
+ * summation order (deterministic). */
+int tgfr_proj_l2norm_ws(int B, int N, long long* floats);
+int tgfr_proj_l2norm_fwd(const float* x, long long ldx, int B, int K, const float* W,
+                         long long ldw, const float* bias, int N, float eps, float* ws,
+                         float* g, long long ldg, float* inv_norm, unsigned* counters,
+                         void* stream);
+int tgfr_proj_dw(const float* dy, long long lddy, const float* x, long long ldx, int B, int K,
+                 int N, float* dW, long long lddw, float* db, void* stream);
+/* tgfr_arc_dx: an ArcMarginProduct head's input gradient from the dcs its
+ * backward wrote (tgfr_arc_bwd / tgfr_arc_focal_bwd_heads): dxn = dcs W over
+ * class chunks (partials in ws, tgfr_arc_dx_ws floats), summed in chunk order,
+ * then dx = (dxn - xn (xn . dxn)) inv_nx (models/metrics.py:43, F.normalize
+ * backward).  dcs [B][C], W [C][D] (16-B aligned, ldw % 4 == 0), xn [B][D],
+ * D % 4 == 0, D <= 768.
+ * Replaces tgfr_bgemm (+ its k-split reduce) + tgfr_l2norm_rows_bwd. */
+int tgfr_arc_dx_ws(int B, int C, int D, long long* floats);
+int tgfr_arc_dx(const float* dcs, const float* W, long long ldw, int B, int C, int D,
+                const float* xn, const float* inv_nx, float eps, float* ws, float* dx,
+                void* stream);
 
 /* ---- optimiser step ------------------------------------------------------
  * Every trainable tensor of a trainer in one launch (replaces the two torch

@@ -196,3 +196,77 @@ def test_imim_operand_rows(gpu, precision):
     with torch.no_grad():
         r.mul_(2.0)
     assert K.attached_rows(r, f16) is None
+
+
+@pytest.mark.parametrize("n,hw", [(64, 196), (3, 49), (2, 32)])
+def test_ln_tail_fused(n, hw):
+    """IMIM's LayerNorm fused into the tail (kernels.ImimLnTail: the
+    normalisation applied on the tail's load, the LayerNorm backward's sums in
+    the tail backward's epilogue) against the two-Function composition
+    LayerNormRows(ch = 256) -> ImimTail on the same inputs: R and every
+    gradient (x, LN w / b, tail weights / biases).  The normalised values are
+    the same fp32 expression, so the bf16 operands agree except where a
+    rounding boundary is crossed: 2e-3 of the max on R, 1e-2 on gradients;
+    odd hw makes 32-row workgroups straddle samples."""
+    torch.backends.cuda.matmul.allow_tf32 = False
+    z, w1, b1, w2, b2, wp, bp, dr = _inputs(n * hw, n + hw)
+    g = torch.Generator(device="cuda").manual_seed(hw)
+    x = (z * 2.0 + 0.5).reshape(n, hw, 256)
+    lnw = torch.randn(256, hw, generator=g, device="cuda") * 0.3 + 1.0
+    lnb = torch.randn(256, hw, generator=g, device="cuda") * 0.1
+    dr = dr.reshape(n, hw, 256)
+
+    def leaves():
+        return [t.clone().requires_grad_() for t in (x, lnw, lnb, w1.reshape(128, 256, 1, 1),
+                                                     b1, w2.reshape(256, 128, 1, 1), b2, wp, bp)]
+
+    a = leaves()
+    ra = K.ImimLnTail.apply(*a, 1e-5, 1e-12)
+    ga = torch.autograd.grad(ra, a, dr)
+    b = leaves()
+    zb = K.layer_norm_rows(b[0], b[1], b[2], 1e-5, ch=256)
+    rb = K.ImimTail.apply(zb.reshape(-1, 256), *b[3:], 1e-12).reshape(n, hw, 256)
+    gb = torch.autograd.grad(rb, b, dr)
+    assert _maxrel(ra, rb) <= 2e-3
+    for i, (p, q) in enumerate(zip(ga, gb)):
+        assert _maxrel(p, q) <= 1e-2, (i, _maxrel(p, q))
+
+
+@pytest.mark.parametrize("n,precision", [(64, "bf16"), (3, "fp16")])
+def test_imim_fused_node(gpu, n, precision):
+    """The whole IMIM head as one autograd node (kernels.ImimFused: one weight
+    preparation launch, the LayerNorm backward writing the attention
+    backward's bf16 dO and D itself) against the two-node chain ImimAttention
+    -> ImimLnTail on the same module: R, the attached operand rows and every
+    parameter gradient agree to 1e-5 of their max (the same kernels and
+    operand roundings), and BN's running statistics are updated once."""
+    import copy
+    from text_guided_face_recognition_amd.config import make_args
+    from text_guided_face_recognition_amd.models.models import IMIM
+    torch.manual_seed(11)
+    args = make_args(precision=precision)
+    a = IMIM(args, 256).to(gpu)
+    for p_ in a.parameters():
+        p_.data.add_(torch.randn_like(p_) * 0.05)
+    b = copy.deepcopy(a)
+    x = torch.randn(n, 256, 14, 14, device=gpu) * 1.5 + 0.3
+    probe = torch.randn(n, 256, 14, 14, device=gpu)
+    ra = a(x)
+    assert K.attached_rows(ra, precision == "fp16") is not None
+    (ra * probe).sum().backward()
+    f16 = precision == "fp16"
+    z = K.imim_attention(x, b.bn_img, b.sa, 1.0 / float(b.sa.sqrt_dim))
+    zb, (rows_b, _) = K.imim_ln_tail(z, b.ln, b.conv1x1_1, b.conv1x1_2,
+                                     b.project_local.projection,
+                                     rows_spec=(196, K.RPAD, f16))
+    rb = zb.reshape(n, 14, 14, -1).permute(0, 3, 1, 2)
+    (rb * probe).sum().backward()
+    assert _maxrel(ra.detach(), rb.detach()) <= 1e-5
+    assert torch.equal(K.attached_rows(ra, f16)[0], rows_b)
+    for (na, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        if pb.grad is None:
+            assert pa.grad is None, na
+            continue
+        assert _maxrel(pa.grad, pb.grad) <= 1e-5, (na, _maxrel(pa.grad, pb.grad))
+    torch.testing.assert_close(a.bn_img.running_mean, b.bn_img.running_mean)
+    torch.testing.assert_close(a.bn_img.running_var, b.bn_img.running_var)

@@ -107,6 +107,20 @@ SIGNATURES = {
     "tgfr_fcfm_conv_dx": [P, P, I, P, P, L, L, I, P],
     "tgfr_fcfm_conv_dw_ws": [I, P],
     "tgfr_fcfm_conv_dw": [P, L, L, P, P, I, P, P, P, I, P],
+    "tgfr_ln_tail_ws": [I, I, P],
+    "tgfr_ln_tail_bwd_att": [P, P, P, I, F, P, P, P, P, I, P, P, P, P, P, P, P, P, P],
+    "tgfr_attn_bwd_prepped": [P, P, P, L, L, I, I, F, P, P, P, P, L, L, P, P],
+    "tgfr_imim_pack": [P, P, I, I, P, P, P, P, P, P, P, P, P, I, I, P, P, P],
+    "tgfr_bn_fwd_cl_bf16": [P, I, I, I, F, F, I, P, P, P, P, P, P, P],
+    "tgfr_linear_bf16io": [P, L, I, I, P, L, P, I, P, L, P],
+    "tgfr_tail_pack_ln": [P, P, P, P, P, I, I, P, P, P],
+    "tgfr_ln_tail_fwd": [P, I, I, F, P, P, P, P, P, F, P, L, P, P, P, P, P, P, I, I, I, P],
+    "tgfr_ln_tail_bwd": [P, P, P, I, F, P, P, P, P, I, P, P, P, P, P, P, P, P, P],
+    "tgfr_proj_l2norm_ws": [I, I, P],
+    "tgfr_proj_l2norm_fwd": [P, L, I, I, P, L, P, I, F, P, P, L, P, P, P],
+    "tgfr_proj_dw": [P, L, P, L, I, I, I, P, L, P, P],
+    "tgfr_arc_dx_ws": [I, I, I, P],
+    "tgfr_arc_dx": [P, P, L, I, I, I, P, P, F, P, P, P],
 }
 
 

@@ -845,6 +845,30 @@ int tgfr_attn_bwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long 
   return (int)hipGetLastError();
 }
 
+// tgfr_attn_bwd with its prep pass already done by the caller: ws holds D
+// [rows] and dO [rows][256] bf16 in tgfr_attn_bwd's layout (the IMIM LayerNorm
+// backward writes them, tgfr_ln_tail_bwd_att).
+int tgfr_attn_bwd_prepped(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long long ld,
+                          long long sb, int B, int hw, float scale, const float* lse,
+                          uint16_t* dQ, uint16_t* dK, uint16_t* dV, long long ldg, long long sbg,
+                          void* ws, void* stream) {
+  if (B <= 0 || hw <= 0 || hw > 32 * AT || (ld & 7) || (sb & 7) || !ws) return 1001;
+  if (((uintptr_t)Q | (uintptr_t)K | (uintptr_t)V | (uintptr_t)ws) & 15) return 1001;
+  const int nt = (hw + 31) / 32, np = (nt + 1) / 2;
+  auto* s = (hipStream_t)stream;
+  const long long rows = (long long)B * hw;
+  const float* D = (const float*)ws;
+  auto* dOb = (const uint16_t*)((char*)ws + (rows * 4 + 15) / 16 * 16);
+  uint16_t* dS = (uint16_t*)dOb + rows * AD;
+  if (const int e = set_max_lds((const void*)attn_bwd_kv_kernel, KV_LDS)) return e;
+  hipLaunchKernelGGL(attn_bwd_kv_kernel, dim3(B * np), dim3(256), KV_LDS, s, Q, K, V, ld, sb, hw,
+                     scale, dOb, lse, D, dK, dV, ldg, sbg, dS);
+  if (const int e = set_max_lds((const void*)attn_bwd_q_kernel, Q_LDS)) return e;
+  hipLaunchKernelGGL(attn_bwd_q_kernel, dim3(B * np), dim3(256), Q_LDS, s, K, ld, sb, hw, dS, dQ,
+                     ldg, sbg);
+  return (int)hipGetLastError();
+}
+
 static int small_check(int B, int hw, int cq, int ck, int cv, int c) {
   if (B <= 0 || hw <= 0 || hw > SM_MAX_HW || cq <= 0 || cq > SM_MAX_HW || c <= 0 ||
       c > SM_MAX_HW || ck < 0 || cv < 0)

@@ -18,14 +18,16 @@
 //                 NCHW -> channels-last transpose
 //   bn_fold       W' = W diag(gamma), b' = b + W beta
 //   bn_unfold     dW, dgamma, dbeta from G and s (fixed-order column sums)
-#include "tgfr_common.h"
+#include "tgfr_fold.h"
 
 using namespace tgfr;
 
 namespace {
 
-// grid C; 256 threads.  x[n][c][hw]: thread t owns positions hw = t, t+256,
-// ... of every sample, so each load instruction reads HW-contiguous floats.
+// grid C; 256 threads.  Up to 256 * BN_REG values per channel (B = 64 at
+// 14 x 14: 49 per thread) are loaded once into registers; larger maps take the
+// two-pass loop (thread t owns positions hw = t, t+256, ... of every sample).
+constexpr int BN_REG = 64;
 __global__ __launch_bounds__(256) void bn_stats_kernel(
     const float* __restrict__ x, int N, int C, int HW, float eps, float momentum, int training,
     float* __restrict__ running_mean, float* __restrict__ running_var,
@@ -42,22 +44,44 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(
   const long long cnt = (long long)N * HW;
   const float* xc = x + (long long)c * HW;
   const long long sn = (long long)C * HW;
-  float s = 0.f;
-  for (int hw = tid; hw < HW; hw += 256) {
-#pragma unroll 8
-    for (int n = 0; n < N; ++n) s += xc[n * sn + hw];
-  }
-  s = wave_sum(s);
-  if (lane == 0) red[wid] = s;
-  __syncthreads();
-  const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)cnt;
-  __syncthreads();
-  float m2 = 0.f;
-  for (int hw = tid; hw < HW; hw += 256) {
-#pragma unroll 8
-    for (int n = 0; n < N; ++n) {
-      const float d = xc[n * sn + hw] - mean;
+  float s = 0.f, m2 = 0.f, mean;
+  if (cnt <= 256 * BN_REG) {
+    // the channel's N x HW values, flattened over all 256 threads, loaded once
+    // with every load in flight (one HBM round trip), both moments from registers
+    float v[BN_REG];
+#pragma unroll
+    for (int u = 0; u < BN_REG; ++u) {
+      const int e = tid + 256 * u, n = e / HW, hw = e - n * HW;
+      v[u] = e < cnt ? xc[n * sn + hw] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < BN_REG; ++u) s += v[u];
+    s = wave_sum(s);
+    if (lane == 0) red[wid] = s;
+    __syncthreads();
+    mean = (red[0] + red[1] + red[2] + red[3]) / (float)cnt;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < BN_REG; ++u) {
+      const float d = tid + 256 * u < cnt ? v[u] - mean : 0.f;
       m2 += d * d;
+    }
+  } else {
+    for (int hw = tid; hw < HW; hw += 256) {
+#pragma unroll 8
+      for (int n = 0; n < N; ++n) s += xc[n * sn + hw];
+    }
+    s = wave_sum(s);
+    if (lane == 0) red[wid] = s;
+    __syncthreads();
+    mean = (red[0] + red[1] + red[2] + red[3]) / (float)cnt;
+    __syncthreads();
+    for (int hw = tid; hw < HW; hw += 256) {
+#pragma unroll 8
+      for (int n = 0; n < N; ++n) {
+        const float d = xc[n * sn + hw] - mean;
+        m2 += d * d;
+      }
     }
   }
   m2 = wave_sum(m2);
@@ -76,24 +100,53 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(
   }
 }
 
-// grid (ceil(C / 64), N); 256 threads; LDS [64][HW + 1] floats.
+// grid (ceil(C / 64), N); 256 threads; LDS [64][HW + 1] floats.  OBF: y is
+// bf16 (the bf16-mode consumers -- the q/k/v projection GEMM and its weight
+// gradient -- round their xhat operand to bf16 anyway: same values, half the
+// bytes written and read).
+template <bool OBF>
 __global__ __launch_bounds__(256) void bn_norm_cl_kernel(const float* __restrict__ x, int C,
                                                          int HW, const float* __restrict__ mean,
                                                          const float* __restrict__ rstd,
-                                                         float* __restrict__ y) {
+                                                         void* __restrict__ yv) {
   extern __shared__ float tile[];
   const int c0 = blockIdx.x * 64, n = blockIdx.y, tid = threadIdx.x;
   const int cn = min(64, C - c0), ld = HW + 1;
   const float* xs = x + ((long long)n * C + c0) * HW;
-  for (int i = tid; i < cn * HW; i += 256) {
-    const int cc = i / HW, hw = i % HW;
-    tile[cc * ld + hw] = (xs[i] - mean[c0 + cc]) * rstd[c0 + cc];
+  // loads in batches of 16 per thread, all in flight before their LDS stores
+  for (int i0 = 0; i0 < cn * HW; i0 += 256 * 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = i0 + 256 * u + tid;
+      v[u] = i < cn * HW ? xs[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = i0 + 256 * u + tid;
+      if (i < cn * HW) {
+        const int cc = i / HW, hw = i % HW;
+        tile[cc * ld + hw] = (v[u] - mean[c0 + cc]) * rstd[c0 + cc];
+      }
+    }
   }
   __syncthreads();
-  float* ys = y + (long long)n * HW * C + c0;
-  for (int i = tid; i < cn * HW; i += 256) {
-    const int hw = i / cn, cc = i % cn;
-    ys[(long long)hw * C + cc] = tile[cc * ld + hw];
+  if constexpr (OBF) {
+    // 4 channels per 8-byte store (cn % 4 == 0: C % 4 == 0)
+    uint16_t* ys = (uint16_t*)yv + (long long)n * HW * C + c0;
+    const int cq = cn / 4;
+    for (int i = tid; i < cq * HW; i += 256) {
+      const int hw = i / cq, c4 = 4 * (i % cq);
+      *(uint2*)(ys + (long long)hw * C + c4) =
+          make_uint2(pk_bf16(tile[c4 * ld + hw], tile[(c4 + 1) * ld + hw]),
+                     pk_bf16(tile[(c4 + 2) * ld + hw], tile[(c4 + 3) * ld + hw]));
+    }
+  } else {
+    float* ys = (float*)yv + (long long)n * HW * C + c0;
+    for (int i = tid; i < cn * HW; i += 256) {
+      const int hw = i / cn, cc = i % cn;
+      ys[(long long)hw * C + cc] = tile[cc * ld + hw];
+    }
   }
 }
 
@@ -134,41 +187,14 @@ __global__ __launch_bounds__(256) void bn_bwd_cl_kernel(const float* __restrict_
   }
 }
 
-// one wave per output row o
-// A weight [O][C] given as up to 3 row blocks of `rows` rows each (the
-// three 1x1 projections of a self-attention, read in place: no concatenated
-// copy), and their biases (each nullable).
-struct Parts {
-  const float* w[3];
-  const float* b[3];
-  int rows;
-  __device__ __forceinline__ const float* row(int o, int C) const {
-    const int p = o / rows;
-    return (p == 0 ? w[0] : p == 1 ? w[1] : w[2]) + (long long)(o - p * rows) * C;
-  }
-  __device__ __forceinline__ float bias(int o) const {
-    const int p = o / rows;
-    const float* bp = p == 0 ? b[0] : p == 1 ? b[1] : b[2];
-    return bp ? bp[o - p * rows] : 0.f;
-  }
-};
-
+// one wave per output row o (bn_fold_row, tgfr_fold.h)
 __global__ __launch_bounds__(256) void bn_fold_kernel(Parts P, int O, int C,
                                                       const float* __restrict__ gamma,
                                                       const float* __restrict__ beta,
                                                       float* __restrict__ Wf,
                                                       float* __restrict__ bf) {
-  const int o = blockIdx.x * 4 + threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
-  if (o >= O) return;
-  const float* wr = P.row(o, C);
-  float acc = 0.f;
-  for (int c = lane; c < C; c += WAVE) {
-    const float w = wr[c];
-    Wf[(long long)o * C + c] = w * gamma[c];
-    acc += w * beta[c];
-  }
-  acc = wave_sum(acc);
-  if (lane == 0) bf[o] = P.bias(o) + acc;
+  const int o = blockIdx.x * 4 + threadIdx.x / WAVE;
+  if (o < O) bn_fold_row(P, o, C, gamma, beta, Wf, bf, threadIdx.x % WAVE);
 }
 
 // grid (ceil(C / 64), ceil(O / 16)); block = 64 columns x 4 row lanes over a
@@ -231,20 +257,39 @@ int tgfr_bn_bwd_cl(const float* dxh, const float* xhat, const float* rstd, int N
   return (int)hipGetLastError();
 }
 
-int tgfr_bn_fwd_cl(const float* x, int N, int C, int HW, float eps, float momentum,
-                   int training, float* running_mean, float* running_var, long long* nbt,
-                   float* mean, float* rstd, float* xhat, void* stream) {
+static int bn_fwd_cl(const float* x, int N, int C, int HW, float eps, float momentum,
+                     int training, float* running_mean, float* running_var, long long* nbt,
+                     float* mean, float* rstd, void* xhat, bool obf, hipStream_t st) {
   if (N <= 0 || C <= 0 || HW <= 0 || (64 * (HW + 1) * 4 > 160 * 1024)) return 1001;
   if (!training && (!running_mean || !running_var)) return 1001;
-  auto* st = (hipStream_t)stream;
   hipLaunchKernelGGL(bn_stats_kernel, dim3(C), dim3(256), 0, st, x, N, C, HW, eps, momentum,
                      training, running_mean, running_var, nbt, mean, rstd);
   const int lds = 64 * (HW + 1) * 4;
+  const void* fn = obf ? (const void*)bn_norm_cl_kernel<true> : (const void*)bn_norm_cl_kernel<false>;
   if (lds > 64 * 1024)
-    if (const int e = set_max_lds((const void*)bn_norm_cl_kernel, lds)) return e;
-  hipLaunchKernelGGL(bn_norm_cl_kernel, dim3((C + 63) / 64, N), dim3(256), lds, st, x, C, HW,
-                     mean, rstd, xhat);
+    if (const int e = set_max_lds(fn, lds)) return e;
+  if (obf)
+    hipLaunchKernelGGL(bn_norm_cl_kernel<true>, dim3((C + 63) / 64, N), dim3(256), lds, st, x, C,
+                       HW, mean, rstd, xhat);
+  else
+    hipLaunchKernelGGL(bn_norm_cl_kernel<false>, dim3((C + 63) / 64, N), dim3(256), lds, st, x,
+                       C, HW, mean, rstd, xhat);
   return (int)hipGetLastError();
+}
+
+int tgfr_bn_fwd_cl(const float* x, int N, int C, int HW, float eps, float momentum,
+                   int training, float* running_mean, float* running_var, long long* nbt,
+                   float* mean, float* rstd, float* xhat, void* stream) {
+  return bn_fwd_cl(x, N, C, HW, eps, momentum, training, running_mean, running_var, nbt, mean,
+                   rstd, xhat, false, (hipStream_t)stream);
+}
+
+int tgfr_bn_fwd_cl_bf16(const float* x, int N, int C, int HW, float eps, float momentum,
+                        int training, float* running_mean, float* running_var, long long* nbt,
+                        float* mean, float* rstd, uint16_t* xhat, void* stream) {
+  if (C % 4 || ((uintptr_t)xhat & 7)) return 1001;
+  return bn_fwd_cl(x, N, C, HW, eps, momentum, training, running_mean, running_var, nbt, mean,
+                   rstd, xhat, true, (hipStream_t)stream);
 }
 
 int tgfr_bn_fold(const float* W, const float* b, int O, int C, const float* gamma,

@@ -1,0 +1,46 @@
+// BatchNorm folded into the 1x1 projection that follows it (W' = W diag(gamma),
+// b' = b + W beta), shared by the BN kernels (tgfr_bn.hip) and the IMIM weight
+// preparation launch (tgfr_imim_pack, tgfr_tail.hip).
+#pragma once
+#include "tgfr_common.h"
+
+namespace {
+
+using namespace tgfr;
+
+// A weight [O][C] given as up to 3 row blocks of `rows` rows each (the
+// three 1x1 projections of a self-attention, read in place: no concatenated
+// copy), and their biases (each nullable).
+struct Parts {
+  const float* w[3];
+  const float* b[3];
+  int rows;
+  __device__ __forceinline__ const float* row(int o, int C) const {
+    const int p = o / rows;
+    return (p == 0 ? w[0] : p == 1 ? w[1] : w[2]) + (long long)(o - p * rows) * C;
+  }
+  __device__ __forceinline__ float bias(int o) const {
+    const int p = o / rows;
+    const float* bp = p == 0 ? b[0] : p == 1 ? b[1] : b[2];
+    return bp ? bp[o - p * rows] : 0.f;
+  }
+};
+
+// Row o of the folded weight and its bias, one wave.
+__device__ __forceinline__ void bn_fold_row(const Parts& P, int o, int C,
+                                            const float* __restrict__ gamma,
+                                            const float* __restrict__ beta,
+                                            float* __restrict__ Wf, float* __restrict__ bf,
+                                            int lane) {
+  const float* wr = P.row(o, C);
+  float acc = 0.f;
+  for (int c = lane; c < C; c += WAVE) {
+    const float w = wr[c];
+    Wf[(long long)o * C + c] = w * gamma[c];
+    acc += w * beta[c];
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) bf[o] = P.bias(o) + acc;
+}
+
+}  // namespace

@@ -489,13 +489,18 @@ __device__ __forceinline__ void wres_load_b(const float* __restrict__ B, long lo
   }
 }
 
-template <int K, bool OBF = false>
+// ABF: A is bf16 (e.g. BatchNorm's xhat in bf16 mode): a ring stage then
+// holds 64 k instead of 32 in the same 128-B-per-row swizzled image (8-bf16
+// chunks where the fp32 image has 4-float quads), and a fragment is one
+// ds_read_b128 with no conversion.
+template <int K, bool OBF = false, bool ABF = false>
 __global__ __launch_bounds__(64 * WR_NW) void bgemm_wres_kernel(
     const float* __restrict__ A, long long sAm, const float* __restrict__ B, long long sBk,
     long long sBn, float* __restrict__ Cm, long long sCm, long long sCn, int M, int N,
     float alpha, const float* __restrict__ bias, int relu, int n_slices, int per_slice) {
   constexpr int WB = WR_TN * K * 2;                     // B image bytes
-  constexpr int NK = K / BK;
+  constexpr int KS = ABF ? 2 * BK : BK;                 // k per ring stage
+  constexpr int NK = K / KS;
   const int tid = threadIdx.x, wid = tid / WAVE, lane = tid % WAVE;
   const int wm = wid >> 2, wn = wid & 3;              // 2 x 4 waves of 32 x 32
   // block -> (slice, g): consecutive remapped ids = the slices of one A tile
@@ -511,9 +516,13 @@ __global__ __launch_bounds__(64 * WR_NW) void bgemm_wres_kernel(
   auto issue = [&](int t) {
     const int j = t / NK, kt = t % NK;
     const int m0 = (g + j * per_slice) * WR_TM;
-    issue_tile<LAY_K, WR_TM, WR_NW>(A + (long long)m0 * sAm + kt * BK, sAm, 1, M - m0,
-                                    K - kt * BK,
-                             WB + (t % WR_NS) * WR_STG, wid, lane);
+    if constexpr (ABF)   // bf16 rows seen as float pairs: same piece geometry
+      issue_tile<LAY_K, WR_TM, WR_NW>(
+          (const float*)((const uint16_t*)A + (long long)m0 * sAm + kt * KS), sAm / 2, 1,
+          M - m0, (K - kt * KS) / 2, WB + (t % WR_NS) * WR_STG, wid, lane);
+    else
+      issue_tile<LAY_K, WR_TM, WR_NW>(A + (long long)m0 * sAm + kt * BK, sAm, 1, M - m0,
+                                      K - kt * BK, WB + (t % WR_NS) * WR_STG, wid, lane);
   };
 #pragma unroll
   for (int t = 0; t < WR_NS - 1; ++t)
@@ -554,12 +563,17 @@ __global__ __launch_bounds__(64 * WR_NW) void bgemm_wres_kernel(
     const uint32_t o = WB + (t % WR_NS) * WR_STG;
     const int kt = t % NK;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      Frag8 f;
+    for (int s = 0; s < KS / 16; ++s) {
       bf16x8 ah, al;
-      read_frag<LAY_K, WR_TM>(f, o, wm * 32, s, lane);
-      frag8<MODE_BF16>(f.v, ah, al);
-      const int c = (kt * BK + 16 * s) / 8 + (lane >> 5);
+      if constexpr (ABF) {
+        const int row = wm * 32 + (lane & 31), q = 2 * s + (lane >> 5);
+        ah = al = as_bf8(lds_ld16(o + row * 128 + (kswz(row, q) << 4)));
+      } else {
+        Frag8 f;
+        read_frag<LAY_K, WR_TM>(f, o, wm * 32, s, lane);
+        frag8<MODE_BF16>(f.v, ah, al);
+      }
+      const int c = (kt * KS + 16 * s) / 8 + (lane >> 5);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int nl = wn * 32 * NJ + 32 * j + (lane & 31);
@@ -729,6 +743,24 @@ int tgfr_bgemm(const float* A, long long sAb, long long sAm, long long sAk, cons
 // IMIM in bf16 mode, read by tgfr_attn_fwd / _bwd as bf16): A [M][K] fp32
 // rows (K = 128 or 256, 16-B aligned, sAm % 4 == 0), W [N][K] fp32
 // (row stride sWn), C [M][N] bf16 (row stride sCm).
+int tgfr_linear_bf16io(const uint16_t* A, long long sAm, int M, int K, const float* W,
+                       long long sWn, const float* bias, int N, uint16_t* C, long long sCm,
+                       void* stream) {
+  if (M <= 0 || N <= 0 || (K != 128 && K != 256) || !al16(A) || (sAm & 7) || !al16(W) ||
+      (sWn & 3))
+    return 1001;
+  const int n_slices = (N + WR_TN - 1) / WR_TN;
+  const int m_tiles = (M + WR_TM - 1) / WR_TM;
+  const int per_slice = std::max(1, std::min(m_tiles, 256 / n_slices));
+  const int lds = WR_TN * K * 2 + WR_NS * WR_STG;
+  auto fn = K == 256 ? &bgemm_wres_kernel<256, true, true> : &bgemm_wres_kernel<128, true, true>;
+  if (const int e = set_max_lds((const void*)fn, lds)) return e;
+  hipLaunchKernelGGL(fn, dim3(n_slices * per_slice), dim3(64 * WR_NW), lds, (hipStream_t)stream,
+                     (const float*)A, sAm, W, (long long)1, sWn, (float*)C, sCm, (long long)1, M,
+                     N, 1.f, bias, 0, n_slices, per_slice);
+  return (int)hipGetLastError();
+}
+
 int tgfr_linear_bf16out(const float* A, long long sAm, int M, int K, const float* W,
                         long long sWn, const float* bias, int N, uint16_t* C, long long sCm,
                         void* stream) {

@@ -5,9 +5,6 @@
 // PyTorch launches one block per sample (64 blocks on a 256-CU part, ~100 us
 // for the backward).  Here every sample is cut into S slices so the launch has
 // >= ~1024 blocks:
-//   ln_aff_t    (ch > 0 only) w, b [ch][E / ch] -> channels-last copies in
-//               the workspace, so every later access to them is a coalesced
-//               float4 (the backward reuses the copies)
 //   ln_part     per (sample, slice): count-free (mean_i, M2_i) of the slice
 //   ln_apply    per (element block, group of samples): combine the S slice
 //               moments (Chan, fixed order) -> mean, rstd of the group's
@@ -18,22 +15,11 @@
 //               block also sums dy xhat and dy over its group of samples
 //   ln_bwd_dw   dw[e] = sum of the group partials, db likewise (fixed order)
 // Every reduction has a fixed order, so results are run-to-run identical.
-#include "tgfr_common.h"
+#include "tgfr_ln.h"
 
 using namespace tgfr;
 
 namespace {
-
-constexpr int NT = 256;
-
-__device__ __forceinline__ float block_sum(float v, float* red) {
-  v = wave_sum(v);
-  const int wid = threadIdx.x / WAVE;
-  __syncthreads();
-  if (threadIdx.x % WAVE == 0) red[wid] = v;
-  __syncthreads();
-  return red[0] + red[1] + red[2] + red[3];
-}
 
 // dw, db scatter back to the reference layout: the affine map is stored
 // channel-major [ch][E / ch] while x's rows are [E / ch][ch] (IMIM's
@@ -52,64 +38,6 @@ __device__ __forceinline__ float4 aff4(const float* __restrict__ a, long long i4
   const float* q = a + (long long)c * n + p;
   return make_float4(q[0], q[n], q[2 * n], q[3 * n]);
 }
-
-struct Slice {
-  long long lo, hi;
-};
-__device__ __forceinline__ Slice slice_of(long long E, int S, int s) {
-  const long long len = ((E + S - 1) / S + 3) / 4 * 4;
-  const long long lo = min(E, s * len);
-  return {lo, min(E, lo + len)};
-}
-
-// ws layout: part [rows][S][2] | mean [rows] | rstd [rows]
-__global__ __launch_bounds__(NT) void ln_part_kernel(const float* __restrict__ x, long long E,
-                                                     int S, float* __restrict__ part) {
-  __shared__ float red[4];
-  const int b = blockIdx.y, s = blockIdx.x;
-  const Slice sl = slice_of(E, S, s);
-  // slices are whole float4s (slice_of rounds the length to 4, E % 4 == 0)
-  const float4* xr = (const float4*)(x + (long long)b * E);
-  const long long lo = sl.lo / 4, hi = sl.hi / 4;
-  float sum = 0.f;
-  for (long long i = lo + threadIdx.x; i < hi; i += NT) {
-    const float4 v = xr[i];
-    sum += (v.x + v.y) + (v.z + v.w);
-  }
-  const float n = (float)(sl.hi - sl.lo);
-  const float mean = n > 0.f ? block_sum(sum, red) / n : 0.f;
-  float m2 = 0.f;
-  for (long long i = lo + threadIdx.x; i < hi; i += NT) {
-    const float4 v = xr[i];
-    const float a = v.x - mean, c = v.y - mean, d = v.z - mean, e = v.w - mean;
-    m2 += (a * a + c * c) + (d * d + e * e);
-  }
-  m2 = block_sum(m2, red);
-  if (threadIdx.x == 0) {
-    part[((long long)b * S + s) * 2] = mean;
-    part[((long long)b * S + s) * 2 + 1] = m2;
-  }
-}
-
-// Chan's parallel combine of the S slice moments of row b.
-__device__ __forceinline__ void ln_stats(const float* part, long long E, int S, int b,
-                                         float eps, float& mean, float& rstd) {
-  float n = 0.f, mu = 0.f, m2 = 0.f;
-  for (int s = 0; s < S; ++s) {
-    const Slice sl = slice_of(E, S, s);
-    const float nb = (float)(sl.hi - sl.lo);
-    if (nb <= 0.f) continue;
-    const float mb = part[((long long)b * S + s) * 2], m2b = part[((long long)b * S + s) * 2 + 1];
-    const float nn = n + nb, d = mb - mu;
-    mu += d * nb / nn;
-    m2 += m2b + d * d * n * nb / nn;
-    n = nn;
-  }
-  mean = mu;
-  rstd = rsqrtf(m2 / n + eps);   // biased variance, as nn.LayerNorm
-}
-
-constexpr int LN_GROUP = 8;   // samples per ln_apply / ln_bwd_dx block
 
 // grid (ceil(E/4 / NT), ceil(rows / LN_GROUP)); w, b row-indexed ([E]).
 __global__ __launch_bounds__(NT) void ln_apply_kernel(const float* __restrict__ x, long long E,
@@ -181,20 +109,22 @@ __global__ __launch_bounds__(NT) void ln_bwd_part_kernel(const float* __restrict
 
 // grid (ceil(E/4 / NT), n_groups): thread owns 4 consecutive elements e and
 // loops over the samples of its group; dwp/dbp [n_groups][E] partials.
+// ATT (the IMIM LayerNorm, whose input is the attention output O = x with
+// 256 channels): instead of dx in fp32, the attention backward's operands --
+// dOb = bf16(dx) and D[row] = sum_c dx[row][c] O[row][c] (one wave = one row
+// of 256 channels) -- so the attention backward needs no prep pass.
+template <bool ATT>
 __global__ __launch_bounds__(NT) void ln_bwd_dx_kernel(
-    const float* __restrict__ dy, const float* __restrict__ x, long long E, int S,
+    const float* __restrict__ dy, const float* __restrict__ x, long long E, PartSrc src,
     const float* __restrict__ w, int ch, const float* __restrict__ stats, int rows,
-    const float* __restrict__ part, int per_group, float* __restrict__ dx,
-    float* __restrict__ dwp, float* __restrict__ dbp) {
+    int per_group, float* __restrict__ dx, float* __restrict__ dwp, float* __restrict__ dbp,
+    float* __restrict__ Dout, uint16_t* __restrict__ dOb) {
   __shared__ float coef[3][64];
   const int g0 = blockIdx.y * per_group, g1 = min(rows, g0 + per_group);
   // per-sample coefficients: rstd, mean(g), mean(g xhat)
   for (int b = g0 + threadIdx.x; b < g1; b += NT) {
-    float sg = 0.f, sgx = 0.f;
-    for (int s = 0; s < S; ++s) {
-      sg += part[((long long)b * S + s) * 2];
-      sgx += part[((long long)b * S + s) * 2 + 1];
-    }
+    float sg, sgx;
+    src.sums(b, sg, sgx);
     coef[0][b - g0] = stats[rows + b];
     coef[1][b - g0] = sg / (float)E;
     coef[2][b - g0] = sgx / (float)E;
@@ -204,16 +134,36 @@ __global__ __launch_bounds__(NT) void ln_bwd_dx_kernel(
   if (i >= E / 4) return;
   const float4 ww = aff4(w, i, ch, ch ? (int)(E / ch) : 0);
   float4 dw = make_float4(0.f, 0.f, 0.f, 0.f), db = dw;
-  for (int b = g0; b < g1; ++b) {
-    const float mean = stats[b], rstd = coef[0][b - g0];
-    const float mg = coef[1][b - g0], mgx = coef[2][b - g0];
-    const float4 v = ((const float4*)(x + (long long)b * E))[i];
-    const float4 d = ((const float4*)(dy + (long long)b * E))[i];
+  // the group's loads all in flight before the arithmetic (per_group <= LN_GROUP)
+  float4 vv[LN_GROUP], dd[LN_GROUP];
+#pragma unroll
+  for (int k = 0; k < LN_GROUP; ++k) {
+    const int b = g0 + k;
+    if (b < g1) {
+      vv[k] = ((const float4*)(x + (long long)b * E))[i];
+      dd[k] = ((const float4*)(dy + (long long)b * E))[i];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < LN_GROUP; ++k) {
+    const int b = g0 + k;
+    if (b >= g1) break;
+    const float mean = stats[b], rstd = coef[0][k];
+    const float mg = coef[1][k], mgx = coef[2][k];
+    const float4 v = vv[k], d = dd[k];
     const float4 xh = make_float4((v.x - mean) * rstd, (v.y - mean) * rstd,
                                   (v.z - mean) * rstd, (v.w - mean) * rstd);
-    ((float4*)(dx + (long long)b * E))[i] =
+    const float4 o =
         make_float4(rstd * (d.x * ww.x - mg - xh.x * mgx), rstd * (d.y * ww.y - mg - xh.y * mgx),
                     rstd * (d.z * ww.z - mg - xh.z * mgx), rstd * (d.w * ww.w - mg - xh.w * mgx));
+    if constexpr (ATT) {
+      *(uint2*)(dOb + (long long)b * E + 4 * i) =
+          make_uint2(pk_bf16(o.x, o.y), pk_bf16(o.z, o.w));
+      const float dsum = wave_sum(o.x * v.x + o.y * v.y + o.z * v.z + o.w * v.w);
+      if ((threadIdx.x & 63) == 0) Dout[(long long)b * (E / 256) + (4 * i) / 256] = dsum;
+    } else {
+      ((float4*)(dx + (long long)b * E))[i] = o;
+    }
     dw.x += d.x * xh.x; dw.y += d.y * xh.y; dw.z += d.z * xh.z; dw.w += d.w * xh.w;
     db.x += d.x; db.y += d.y; db.z += d.z; db.w += d.w;
   }
@@ -235,30 +185,6 @@ __global__ __launch_bounds__(NT) void ln_bwd_dw_kernel(const float* __restrict__
   const long long t = aidx(e, ch, E);
   dw[t] = a;
   db[t] = c;
-}
-
-int slices_for(int rows, long long E) {
-  long long s = (1024 + rows - 1) / rows;
-  s = std::min<long long>(s, std::max<long long>(1, E / 1024));
-  return (int)std::max<long long>(1, s);
-}
-
-// Workspace floats: part [rows][S][2] | mean [rows] | rstd [rows] -- written
-// by the forward and read by the backward -- then (backward) dw, db group
-// partials [2][G][E], G = ceil(rows / LN_GROUP).  (The channel-major affine
-// maps are read in place, aff4.)
-struct LnWs {
-  long long stats, aff, bwd, total_fwd, total_bwd;
-};
-LnWs ln_ws(int rows, long long E, int ch) {
-  const long long S = slices_for(rows, E);
-  LnWs o;
-  o.stats = rows * S * 2;
-  o.aff = o.stats + 2LL * rows;
-  o.bwd = o.aff;
-  o.total_fwd = o.bwd;
-  o.total_bwd = o.bwd + 2LL * ((rows + LN_GROUP - 1) / LN_GROUP) * E;
-  return o;
 }
 
 bool ln_args_ok(int rows, long long E, int ch) {
@@ -308,12 +234,46 @@ int tgfr_ln_bwd(const float* dy, const float* x, int rows, long long E, const fl
   // the forward's slice moments are no longer needed: reuse their slots
   hipLaunchKernelGGL(ln_bwd_part_kernel, dim3(S, rows), dim3(NT), 0, st, dy, x, E, S, w, ch,
                      stats, rows, part);
-  hipLaunchKernelGGL(ln_bwd_dx_kernel, dim3((unsigned)((E / 4 + NT - 1) / NT), groups),
-                     dim3(NT), 0, st, dy, x, E, S, w, ch, stats, rows, part, LN_GROUP, dx, dwp,
-                     dbp);
+  hipLaunchKernelGGL(ln_bwd_dx_kernel<false>, dim3((unsigned)((E / 4 + NT - 1) / NT), groups),
+                     dim3(NT), 0, st, dy, x, E, PartSrc{part, S, 0, 0, 1}, w, ch, stats, rows,
+                     LN_GROUP, dx, dwp, dbp, nullptr, nullptr);
   hipLaunchKernelGGL(ln_bwd_dw_kernel, dim3((unsigned)((E + NT - 1) / NT)), dim3(NT), 0, st,
                      dwp, dbp, E, groups, ch, dw, db);
   return (int)hipGetLastError();
 }
 
 }  // extern "C"
+
+namespace tgfr {
+
+int ln_part_launch(const float* x, int rows, long long E, float* ws, hipStream_t s) {
+  if (!ln_args_ok(rows, E, 0)) return 1001;
+  const int S = slices_for(rows, E);
+  hipLaunchKernelGGL(ln_part_kernel, dim3(S, rows), dim3(NT), 0, s, x, E, S, ws);
+  return (int)hipGetLastError();
+}
+
+int ln_bwd_tail_launch(const float* dy, const float* x, int rows, long long E, const float* w_cl,
+                       int ch, float* ws, const float* tail_part, int hw, int tm, float* dx,
+                       float* D, uint16_t* dOb, float* dw, float* db, hipStream_t s) {
+  if (!ln_args_ok(rows, E, ch) || hw < tm || tm <= 0) return 1001;
+  if (dOb && (ch != 256 || !D)) return 1001;
+  const LnWs o = ln_ws(rows, E, ch);
+  const int groups = (rows + LN_GROUP - 1) / LN_GROUP;
+  const float* stats = ws + o.stats;
+  float* dwp = ws + o.bwd;
+  float* dbp = dwp + (long long)groups * E;
+  const dim3 grid((unsigned)((E / 4 + NT - 1) / NT), groups);
+  const PartSrc src{tail_part, 0, 1, hw, tm};
+  if (dOb)
+    hipLaunchKernelGGL(ln_bwd_dx_kernel<true>, grid, dim3(NT), 0, s, dy, x, E, src, w_cl, 0,
+                       stats, rows, LN_GROUP, nullptr, dwp, dbp, D, dOb);
+  else
+    hipLaunchKernelGGL(ln_bwd_dx_kernel<false>, grid, dim3(NT), 0, s, dy, x, E, src, w_cl, 0,
+                       stats, rows, LN_GROUP, dx, dwp, dbp, nullptr, nullptr);
+  hipLaunchKernelGGL(ln_bwd_dw_kernel, dim3((unsigned)((E + NT - 1) / NT)), dim3(NT), 0, s,
+                     dwp, dbp, E, groups, ch, dw, db);
+  return (int)hipGetLastError();
+}
+
+}  // namespace tgfr

@@ -31,7 +31,8 @@
 // in one launch: row slices per workgroup, operands transposed at LDS read
 // time by ds_read_b64_tr_b16, slice partials summed in slice order by
 // tail_dw_reduce (deterministic).
-#include "tgfr_common.h"
+#include "tgfr_fold.h"
+#include "tgfr_ln.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -101,13 +102,11 @@ __device__ __forceinline__ const uint16_t* frag_ptr(const uint16_t* pk, int off,
   return pk + off + ((rt * (K / 16) + s) * 64 + lane) * 8;
 }
 
-__global__ __launch_bounds__(256) void tail_pack_kernel(const float* __restrict__ W1,
-                                                        const float* __restrict__ W2,
-                                                        const float* __restrict__ Wp,
-                                                        uint16_t* __restrict__ pk) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= PACK_ELEMS) return;
-  // segment: (source, source row length, transposed?, K of M, offset)
+// element e of the fragment-order pack
+__device__ __forceinline__ void pack_elem(const float* __restrict__ W1,
+                                          const float* __restrict__ W2,
+                                          const float* __restrict__ Wp, uint16_t* __restrict__ pk,
+                                          int e) {
   const float* W;
   int off, K, ld, tr;
   if (e < OFF_W2) { W = W1; off = OFF_W1; K = TC; ld = TC; tr = 0; }
@@ -122,6 +121,60 @@ __global__ __launch_bounds__(256) void tail_pack_kernel(const float* __restrict_
   pk[e] = bf_bits(tr ? W[k * ld + r] : W[r * ld + k]);
 }
 
+// (aff != NULL: also the IMIM LayerNorm's affine maps, stored [C][H W] by the
+// reference, as channels-last rows aff[0 | 1][p][c] = (w | b)[c][p] for the
+// LayerNorm fused into tail_fwd / tail_bwd: coalesced loads there)
+__global__ __launch_bounds__(256) void tail_pack_kernel(const float* __restrict__ W1,
+                                                        const float* __restrict__ W2,
+                                                        const float* __restrict__ Wp,
+                                                        uint16_t* __restrict__ pk,
+                                                        const float* __restrict__ lnw,
+                                                        const float* __restrict__ lnb, int hw,
+                                                        float* __restrict__ aff) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= PACK_ELEMS) {
+    const int f = e - PACK_ELEMS, n = hw * TC;
+    if (!aff || f >= 2 * n) return;
+    const int j = f / n, r = f % n, p = r / TC, c = r % TC;
+    aff[f] = (j ? lnb : lnw)[(long long)c * hw + p];
+    return;
+  }
+  // segment: (source, source row length, transposed?, K of M, offset)
+  pack_elem(W1, W2, Wp, pk, e);
+}
+
+// IMIM's whole per-step weight preparation in one launch: blocks [0, nf)
+// fold bn_img into the packed q/k/v projection (one wave per row, as
+// bn_fold_kernel), the rest run tail_pack_kernel's elements (weights and the
+// LayerNorm affine maps).
+__global__ __launch_bounds__(256) void imim_pack_kernel(Parts P, int O, int C,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta,
+                                                        float* __restrict__ Wf,
+                                                        float* __restrict__ bf, int nf,
+                                                        const float* __restrict__ W1,
+                                                        const float* __restrict__ W2,
+                                                        const float* __restrict__ Wp,
+                                                        uint16_t* __restrict__ pk,
+                                                        const float* __restrict__ lnw,
+                                                        const float* __restrict__ lnb, int hw,
+                                                        float* __restrict__ aff) {
+  if ((int)blockIdx.x < nf) {
+    const int o = blockIdx.x * 4 + threadIdx.x / WAVE;
+    if (o < O) bn_fold_row(P, o, C, gamma, beta, Wf, bf, threadIdx.x % WAVE);
+    return;
+  }
+  const int e = (blockIdx.x - nf) * 256 + threadIdx.x;
+  if (e >= PACK_ELEMS) {
+    const int f = e - PACK_ELEMS, n = hw * TC;
+    if (f >= 2 * n) return;
+    const int j = f / n, r = f % n, p = r / TC, c = r % TC;
+    aff[f] = (j ? lnb : lnw)[(long long)c * hw + p];
+    return;
+  }
+  pack_elem(W1, W2, Wp, pk, e);
+}
+
 // ------------------------------------------------------------ forward ---
 // LDS: [0, 32K) Z image (later the H2 image), [32K, 48K) H1 image,
 //      [48K, 49K) row sum-of-squares partials [4 waves][64], [49K, 49.25K) 1/norm
@@ -129,25 +182,107 @@ constexpr int F_Z = 0, F_H2 = 0, F_H1 = TM * TC * 2, F_SS = F_H1 + TM * TH * 2,
               F_INV = F_SS + 4 * TM * 4;
 constexpr int F_LDS = F_INV + TM * 4;
 
+// The IMIM LayerNorm fused into the tail (LN = true): Z = (X - mean_b) rstd_b
+// w + b for sample b = row / hw of the attention output X (models/models.py
+// :401), from ln_part's slice moments (combined here, Chan, fixed order) and
+// the channels-last affine rows of tail_pack; the first workgroup of each
+// sample stores its (mean, rstd) for the backward.
+struct LnFwd {
+  const float* part;      // ln_part moments [n][S][2]
+  float* stats;           // mean [n] | rstd [n]
+  const float* aff;       // w rows [hw][TC] | b rows [hw][TC]
+  long long E;            // hw * TC
+  int S, hw, n;
+  float eps;
+};
+constexpr int F_LN = F_LDS;                 // LN: mean, rstd of the two samples
+constexpr int F_MOM = F_LDS + 16;           // LN: their slice moments [2][S][2], S <= 64
+constexpr int F_LDS_LN = F_MOM + 2 * 64 * 2 * 4;
+
+template <bool LN>
 __global__ __launch_bounds__(256) void tail_fwd_kernel(
     const float* __restrict__ Z, long long ldz, int rows, const uint16_t* __restrict__ pk,
     const float* __restrict__ b1, const float* __restrict__ b2, const float* __restrict__ bp,
     float eps, float* __restrict__ R, long long ldr, uint16_t* __restrict__ Zb,
     uint16_t* __restrict__ H1b, uint16_t* __restrict__ H2b, float* __restrict__ inv_out,
     uint16_t* __restrict__ Rrows, float* __restrict__ Rnorm, int rows_per_item, int rows_pad,
-    int rows_f16) {
+    int rows_f16, LnFwd L) {
   const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE;
   const int lr = lane & 31, h = lane >> 5;
   const int row0 = blockIdx.x * TM;
 
   // Z rows -> bf16 image (and the bf16 copy for dW1); rows past the end are 0
+  constexpr int NI = TM * (TC / 8) / 256;
+  float4 va[NI], vb[NI];
 #pragma unroll
-  for (int i = tid; i < TM * (TC / 8); i += 256) {
-    const int m = i / (TC / 8), c = i % (TC / 8);
-    uint4 v = make_uint4(0, 0, 0, 0);
+  for (int u = 0; u < NI; ++u) {
+    const int i = tid + 256 * u, m = i / (TC / 8), c = i % (TC / 8);
+    va[u] = vb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (row0 + m < rows) {
       const float* src = Z + (long long)(row0 + m) * ldz + 8 * c;
-      const float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
+      va[u] = *(const float4*)src;
+      vb[u] = *(const float4*)(src + 4);
+    }
+  }
+  if constexpr (LN) {
+    // affine values of the same elements (loads in flight with X's), then
+    // the two samples' statistics
+    float4 wa[NI], wb[NI], ba[NI], bb[NI];
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int i = tid + 256 * u, m = i / (TC / 8), c = i % (TC / 8);
+      const int p = min(row0 + m, rows - 1) % L.hw;
+      const float* wr = L.aff + (long long)p * TC + 8 * c;
+      wa[u] = *(const float4*)wr;
+      wb[u] = *(const float4*)(wr + 4);
+      ba[u] = *(const float4*)(wr + L.E);
+      bb[u] = *(const float4*)(wr + L.E + 4);
+    }
+    // the two samples' slice moments: one load per thread (all in flight),
+    // staged in LDS, then combined (Chan, slice order) by two threads
+    const int s0 = row0 / L.hw;
+    float* mom = (float*)(g_smem + F_MOM);          // [2][S][2]
+    if (tid < 4 * L.S) {
+      const int sl = tid / (2 * L.S), r = tid % (2 * L.S), b = s0 + sl;
+      mom[tid] = b < L.n ? L.part[(long long)b * L.S * 2 + r] : 0.f;
+    }
+    __syncthreads();
+    if (tid < 2) {
+      const int b = s0 + tid;
+      float mean = 0.f, rstd = 0.f;
+      if (b < L.n) {
+        ln_stats(mom + tid * 2 * L.S - (long long)b * L.S * 2, L.E, L.S, b, L.eps, mean, rstd);
+        if ((long long)b * L.hw >= row0 && (long long)b * L.hw < row0 + TM) {
+          L.stats[b] = mean;
+          L.stats[L.n + b] = rstd;
+        }
+      }
+      lds_stf(F_LN + 8 * tid, mean);
+      lds_stf(F_LN + 8 * tid + 4, rstd);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int i = tid + 256 * u, m = i / (TC / 8);
+      const int sl = min(row0 + m, rows - 1) / L.hw - s0;
+      const float mean = lds_ldf(F_LN + 8 * sl), rstd = lds_ldf(F_LN + 8 * sl + 4);
+      // (x - mean) rstd w + b, as ln_apply_kernel
+      va[u] = make_float4((va[u].x - mean) * rstd * wa[u].x + ba[u].x,
+                          (va[u].y - mean) * rstd * wa[u].y + ba[u].y,
+                          (va[u].z - mean) * rstd * wa[u].z + ba[u].z,
+                          (va[u].w - mean) * rstd * wa[u].w + ba[u].w);
+      vb[u] = make_float4((vb[u].x - mean) * rstd * wb[u].x + bb[u].x,
+                          (vb[u].y - mean) * rstd * wb[u].y + bb[u].y,
+                          (vb[u].z - mean) * rstd * wb[u].z + bb[u].z,
+                          (vb[u].w - mean) * rstd * wb[u].w + bb[u].w);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NI; ++u) {
+    const int i = tid + 256 * u, m = i / (TC / 8), c = i % (TC / 8);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row0 + m < rows) {
+      const float4 a = va[u], b = vb[u];
       v = make_uint4(pk_bf16(a.x, a.y), pk_bf16(a.z, a.w), pk_bf16(b.x, b.y), pk_bf16(b.z, b.w));
       *(uint4*)(Zb + (long long)(row0 + m) * TC + 8 * c) = v;
     }
@@ -337,12 +472,27 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
 // LDS: [0, 32K) dP image (later the dH1 image), [32K, 64K) dH2 image
 constexpr int B_DP = 0, B_DH1 = 0, B_DH2 = TM * TD * 2, B_LDS = 2 * TM * TD * 2;
 
+// LN = true: the IMIM LayerNorm's backward needs, per sample, the sums of
+// g = dZ w and g xhat (xhat = (X - mean) rstd): each workgroup adds its rows'
+// terms (two sample slots: 32 rows span at most two samples of hw >= 32) and
+// writes part[blockIdx.x][slot][2] (PartSrc tail layout) -- no separate pass
+// over dZ and X.
+struct LnBwd {
+  const float* X;         // the LayerNorm input rows [rows][TC]
+  const float* stats;     // mean [n] | rstd [n] (tail_fwd<true>)
+  const float* w;         // affine w as channels-last rows [hw][TC]
+  float* part;            // [gridDim.x][2][2]
+  int hw, n;
+};
+constexpr int B_RED = B_LDS, B_LDS_LN = B_LDS + 4 * 4 * 4;
+
+template <bool LN>
 __global__ __launch_bounds__(256) void tail_bwd_kernel(
     const float* __restrict__ dR, long long lddr, const float* __restrict__ R, long long ldr,
     const float* __restrict__ inv, int rows, float eps, const uint16_t* __restrict__ pk,
     const uint16_t* __restrict__ H1b, const uint16_t* __restrict__ H2b, float* __restrict__ dZ,
     long long lddz, uint16_t* __restrict__ dPb, uint16_t* __restrict__ dH2b,
-    uint16_t* __restrict__ dH1b) {
+    uint16_t* __restrict__ dH1b, LnBwd L) {
   const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE;
   const int lr = lane & 31, h = lane >> 5;
   const int row0 = blockIdx.x * TM;
@@ -494,6 +644,43 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
         o[32] = acc[mt][1][q];
       }
     }
+  if constexpr (LN) {
+    const int s0 = row0 / L.hw;
+    const bool two = s0 + 1 < L.n;
+    const float m0 = L.stats[s0], r0 = L.stats[L.n + s0];
+    const float m1 = two ? L.stats[s0 + 1] : 0.f, r1 = two ? L.stats[L.n + s0 + 1] : 0.f;
+    float sg[2] = {0.f, 0.f}, sgx[2] = {0.f, 0.f};
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = row0 + 32 * mt + acc_row(q, h);
+        if (row >= rows) continue;
+        const int p = row % L.hw, sl = row / L.hw - s0;
+        const float mean = sl ? m1 : m0, rstd = sl ? r1 : r0;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const int c = 64 * w + 32 * ct + lr;
+          const float g = acc[mt][ct][q] * L.w[(long long)p * TC + c];
+          const float xh = (L.X[(long long)row * TC + c] - mean) * rstd;
+          if (sl) { sg[1] += g; sgx[1] += g * xh; }
+          else { sg[0] += g; sgx[0] += g * xh; }
+        }
+      }
+    float* red = (float*)(g_smem + B_RED);
+    const float t0 = wave_sum(sg[0]), t1 = wave_sum(sgx[0]);
+    const float t2 = wave_sum(sg[1]), t3 = wave_sum(sgx[1]);
+    if (lane == 0) {
+      red[4 * w] = t0;
+      red[4 * w + 1] = t1;
+      red[4 * w + 2] = t2;
+      red[4 * w + 3] = t3;
+    }
+    __syncthreads();
+    if (tid < 4)
+      L.part[(long long)blockIdx.x * 4 + tid] =
+          (red[tid] + red[4 + tid]) + (red[8 + tid] + red[12 + tid]);
+  }
 }
 
 // ------------------------------------------------- weight gradients ---
@@ -778,7 +965,7 @@ int tgfr_tail_pack(const float* W1, const float* W2, const float* Wp, uint16_t* 
                    void* stream) {
   if (!W1 || !W2 || !Wp || !pk) return 1001;
   hipLaunchKernelGGL(tail_pack_kernel, dim3((PACK_ELEMS + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, W1, W2, Wp, pk);
+                     (hipStream_t)stream, W1, W2, Wp, pk, nullptr, nullptr, 0, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -792,10 +979,10 @@ int tgfr_tail_fwd(const float* Z, long long ldz, int rows, const uint16_t* pk, c
   if ((Rrows || Rnorm) && (rows_per_item <= 0 || rows_pad < rows_per_item ||
                            rows % rows_per_item || ((uintptr_t)Rrows & 15)))
     return 1001;
-  hipLaunchKernelGGL(tail_fwd_kernel, dim3((rows + TM - 1) / TM), dim3(256), F_LDS,
+  hipLaunchKernelGGL(tail_fwd_kernel<false>, dim3((rows + TM - 1) / TM), dim3(256), F_LDS,
                      (hipStream_t)stream, Z, ldz, rows, pk, b1, b2, bp, eps, R, ldr, Zb, H1b, H2b,
                      inv, Rrows, Rnorm, rows_per_item > 0 ? rows_per_item : 1, rows_pad,
-                     rows_f16 ? 1 : 0);
+                     rows_f16 ? 1 : 0, LnFwd{});
   return (int)hipGetLastError();
 }
 
@@ -807,10 +994,139 @@ int tgfr_tail_bwd(const float* dR, long long lddr, const float* R, long long ldr
   if (((uintptr_t)dR & 15) || ((uintptr_t)R & 15) || !inv || !pk || !H1b || !H2b || !dZ ||
       !dPb || !dH2b || !dH1b)
     return 1001;
-  hipLaunchKernelGGL(tail_bwd_kernel, dim3((rows + TM - 1) / TM), dim3(256), B_LDS,
+  hipLaunchKernelGGL(tail_bwd_kernel<false>, dim3((rows + TM - 1) / TM), dim3(256), B_LDS,
                      (hipStream_t)stream, dR, lddr, R, ldr, inv, rows, eps, pk, H1b, H2b, dZ,
-                     lddz, dPb, dH2b, dH1b);
+                     lddz, dPb, dH2b, dH1b, LnBwd{});
   return (int)hipGetLastError();
+}
+
+// ---- the tail with IMIM's LayerNorm fused in (bf16 / fp16 step path) ----
+// ws floats: LayerNorm workspace (LnWs of n = rows / hw samples, E = hw * 256)
+// | tail_bwd<true>'s per-workgroup sums [ceil(rows / TM)][2][2] | the affine
+// maps as channels-last rows [2][hw][256] (tgfr_tail_pack_ln)
+struct LnTailWs {
+  long long tp, aff, total;
+  int n;
+  long long E;
+};
+static LnTailWs ln_tail_ws(int rows, int hw) {
+  LnTailWs o;
+  o.n = rows / hw;
+  o.E = (long long)hw * TC;
+  const LnWs l = ln_ws(o.n, o.E, TC);
+  o.tp = l.total_bwd;
+  o.aff = o.tp + 4LL * ((rows + TM - 1) / TM);
+  o.total = o.aff + 2 * o.E;
+  return o;
+}
+static bool ln_tail_ok(int rows, int hw) {
+  // (the tail's load combines at most 64 slice moments per sample)
+  return rows > 0 && hw >= TM && rows % hw == 0 && rows / hw <= 65535 &&
+         slices_for(rows / hw, (long long)hw * TC) <= 64;
+}
+
+int tgfr_ln_tail_ws(int rows, int hw, long long* floats) {
+  if (!ln_tail_ok(rows, hw) || !floats) return 1001;
+  *floats = ln_tail_ws(rows, hw).total;
+  return 0;
+}
+
+int tgfr_tail_pack_ln(const float* W1, const float* W2, const float* Wp, const float* lnw,
+                      const float* lnb, int rows, int hw, uint16_t* pk, float* ws, void* stream) {
+  if (!W1 || !W2 || !Wp || !pk || !lnw || !lnb || !ws || !ln_tail_ok(rows, hw)) return 1001;
+  const LnTailWs o = ln_tail_ws(rows, hw);
+  const long long n = PACK_ELEMS + 2 * o.E;
+  hipLaunchKernelGGL(tail_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, W1, W2, Wp, pk, lnw, lnb, hw, ws + o.aff);
+  return (int)hipGetLastError();
+}
+
+int tgfr_imim_pack(const float* const* Wqkv, const float* const* bqkv, int rows_qkv, int C,
+                   const float* gamma, const float* beta, float* Wf, float* bf, const float* W1,
+                   const float* W2, const float* Wp, const float* lnw, const float* lnb,
+                   int rows, int hw, uint16_t* pk, float* ws, void* stream) {
+  if (!Wqkv || !Wqkv[0] || !Wqkv[1] || !Wqkv[2] || rows_qkv <= 0 || C <= 0 || !gamma || !beta ||
+      !Wf || !bf || !W1 || !W2 || !Wp || !pk || !lnw || !lnb || !ws || !ln_tail_ok(rows, hw))
+    return 1001;
+  const Parts P{{Wqkv[0], Wqkv[1], Wqkv[2]},
+                {bqkv ? bqkv[0] : nullptr, bqkv ? bqkv[1] : nullptr, bqkv ? bqkv[2] : nullptr},
+                rows_qkv};
+  const int O = 3 * rows_qkv, nf = (O + 3) / 4;
+  const LnTailWs o = ln_tail_ws(rows, hw);
+  const long long n = PACK_ELEMS + 2 * o.E;
+  hipLaunchKernelGGL(imim_pack_kernel, dim3((unsigned)(nf + (n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, P, O, C, gamma, beta, Wf, bf, nf, W1, W2, Wp, pk, lnw,
+                     lnb, hw, ws + o.aff);
+  return (int)hipGetLastError();
+}
+
+int tgfr_ln_tail_fwd(const float* X, int rows, int hw, float ln_eps, float* ws,
+                     const uint16_t* pk, const float* b1, const float* b2, const float* bp,
+                     float eps, float* R, long long ldr, uint16_t* Zb, uint16_t* H1b,
+                     uint16_t* H2b, float* inv, uint16_t* Rrows, float* Rnorm,
+                     int rows_per_item, int rows_pad, int rows_f16, void* stream) {
+  if (!ln_tail_ok(rows, hw) || !ws || ldr < TD || (ldr & 3) || ((uintptr_t)X & 15)) return 1001;
+  if (!pk || !b1 || !b2 || !bp || !R || !Zb || !H1b || !H2b || !inv) return 1001;
+  if ((Rrows || Rnorm) && (rows_per_item <= 0 || rows_pad < rows_per_item ||
+                           rows % rows_per_item || ((uintptr_t)Rrows & 15)))
+    return 1001;
+  const LnTailWs o = ln_tail_ws(rows, hw);
+  auto* s = (hipStream_t)stream;
+  if (const int e = ln_part_launch(X, o.n, o.E, ws, s)) return e;
+  const LnWs l = ln_ws(o.n, o.E, TC);
+  const LnFwd L{ws, ws + l.stats, ws + o.aff, o.E, slices_for(o.n, o.E), hw, o.n, ln_eps};
+  hipLaunchKernelGGL(tail_fwd_kernel<true>, dim3((rows + TM - 1) / TM), dim3(256), F_LDS_LN, s,
+                     X, (long long)TC, rows, pk, b1, b2, bp, eps, R, ldr, Zb, H1b, H2b, inv,
+                     Rrows, Rnorm, rows_per_item > 0 ? rows_per_item : 1, rows_pad,
+                     rows_f16 ? 1 : 0, L);
+  return (int)hipGetLastError();
+}
+
+static int ln_tail_bwd(const float* dR, const float* R, const float* inv, int rows, float eps,
+                       const uint16_t* pk, const uint16_t* H1b, const uint16_t* H2b,
+                       const float* X, int hw, float* ws, float* dZ, uint16_t* dPb,
+                       uint16_t* dH2b, uint16_t* dH1b, float* dX, float* D, uint16_t* dOb,
+                       float* dlnw, float* dlnb, void* stream) {
+  if (!ln_tail_ok(rows, hw) || !ws || ((uintptr_t)dR & 15) || ((uintptr_t)R & 15) ||
+      ((uintptr_t)X & 15) || ((uintptr_t)dZ & 15) || ((uintptr_t)dX & 15) ||
+      ((uintptr_t)dOb & 7))
+    return 1001;
+  if (!inv || !pk || !H1b || !H2b || !dZ || !dPb || !dH2b || !dH1b || !(dX || (D && dOb)) ||
+      !dlnw || !dlnb)
+    return 1001;
+  const LnTailWs o = ln_tail_ws(rows, hw);
+  const LnWs l = ln_ws(o.n, o.E, TC);
+  auto* s = (hipStream_t)stream;
+  const LnBwd L{X, ws + l.stats, ws + o.aff, ws + o.tp, hw, o.n};
+  hipLaunchKernelGGL(tail_bwd_kernel<true>, dim3((rows + TM - 1) / TM), dim3(256), B_LDS_LN, s,
+                     dR, (long long)TD, R, (long long)TD, inv, rows, eps, pk, H1b, H2b, dZ,
+                     (long long)TC, dPb, dH2b, dH1b, L);
+  if (const int e = (int)hipGetLastError()) return e;
+  return ln_bwd_tail_launch(dZ, X, o.n, o.E, ws + o.aff, TC, ws, ws + o.tp, hw, TM, dX, D, dOb,
+                            dlnw, dlnb, s);
+}
+
+int tgfr_ln_tail_bwd(const float* dR, const float* R, const float* inv, int rows, float eps,
+                     const uint16_t* pk, const uint16_t* H1b, const uint16_t* H2b,
+                     const float* X, int hw, float* ws, float* dZ, uint16_t* dPb,
+                     uint16_t* dH2b, uint16_t* dH1b, float* dX, float* dlnw, float* dlnb,
+                     void* stream) {
+  if (!dX) return 1001;
+  return ln_tail_bwd(dR, R, inv, rows, eps, pk, H1b, H2b, X, hw, ws, dZ, dPb, dH2b, dH1b, dX,
+                     nullptr, nullptr, dlnw, dlnb, stream);
+}
+
+int tgfr_ln_tail_bwd_att(const float* dR, const float* R, const float* inv, int rows, float eps,
+                         const uint16_t* pk, const uint16_t* H1b, const uint16_t* H2b,
+                         const float* X, int hw, float* ws, float* dZ, uint16_t* dPb,
+                         uint16_t* dH2b, uint16_t* dH1b, void* att_ws, float* dlnw, float* dlnb,
+                         void* stream) {
+  if (!att_ws || ((uintptr_t)att_ws & 15)) return 1001;
+  // tgfr_attn_bwd's workspace: D [rows] fp32, then dO [rows][256] bf16 (16-B aligned)
+  float* D = (float*)att_ws;
+  auto* dOb = (uint16_t*)((char*)att_ws + ((long long)rows * 4 + 15) / 16 * 16);
+  return ln_tail_bwd(dR, R, inv, rows, eps, pk, H1b, H2b, X, hw, ws, dZ, dPb, dH2b, dH1b,
+                     nullptr, D, dOb, dlnw, dlnb, stream);
 }
 
 int tgfr_tail_dw_ws(int rows, long long* floats) {

@@ -817,10 +817,16 @@ def attention_core(px, py, cq, ck, cv, scale, mode="fp32"):
 
 
 # ------------------------------------------------- batch norm -> linear ---
-def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf16=False):
+def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf16=False,
+                   xhat_bf16=False, fold3=None):
     """BatchNorm2d (batch or running statistics) folded into the following
     1x1 projection; returns y [N, HW, O] (fp32, or bf16 with out_bf16) and
-    stores what _bn_linear_bwd needs on ctx."""
+    stores what _bn_linear_bwd needs on ctx.  xhat_bf16 (with out_bf16: the
+    bf16 q/k/v path, no BN input gradient): the normalised map is written and
+    kept in bf16 -- the values the bf16 GEMMs read from the fp32 map anyway.
+    fold3 (three-part weight only): a callable (wp, bp, rows, c, g, beta, wf,
+    bf) that launches the fold instead of tgfr_bn_fold3 (ImimFused folds it
+    into IMIM's one weight-preparation launch)."""
     n, c, h, w_ = x.shape
     hw = h * w_
     o = sum(t.shape[0] for t in weight) if isinstance(weight, tuple) else weight.shape[0]
@@ -828,12 +834,13 @@ def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf
     dev = x.device
     mean = torch.empty(c, dtype=torch.float32, device=dev)
     rstd = torch.empty_like(mean)
-    xhat = torch.empty(n, hw, c, dtype=torch.float32, device=dev)
+    xhat_bf16 = xhat_bf16 and out_bf16
+    xhat = torch.empty(n, hw, c, dtype=torch.int16 if xhat_bf16 else torch.float32, device=dev)
     track = training and bn.track_running_stats and bn.running_mean is not None
     if training and track and bn.momentum is None:
         raise NotImplementedError("cumulative-average BatchNorm (momentum=None)")
     use_batch = training or bn.running_mean is None
-    call("tgfr_bn_fwd_cl", ptr(x), n, c, hw, float(bn.eps),
+    call("tgfr_bn_fwd_cl_bf16" if xhat_bf16 else "tgfr_bn_fwd_cl", ptr(x), n, c, hw, float(bn.eps),
          float(bn.momentum or 0.0), int(use_batch),
          ptr(bn.running_mean) if (track or not use_batch) else None,
          ptr(bn.running_var) if (track or not use_batch) else None,
@@ -849,8 +856,11 @@ def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf
         wf = torch.empty(o, c, dtype=torch.float32, device=dev)
         wp = (ctypes.c_void_p * 3)(*[ptr(t) for t in w2])
         bp = (ctypes.c_void_p * 3)(*[ptr(t) for t in b2])
-        call("tgfr_bn_fold3", ctypes.addressof(wp), ctypes.addressof(bp), rows, c, ptr(g),
-             ptr(beta.float().contiguous()), ptr(wf), ptr(bf), _hip.stream())
+        if fold3 is not None:
+            fold3(wp, bp, rows, c, g, beta.float().contiguous(), wf, bf)
+        else:
+            call("tgfr_bn_fold3", ctypes.addressof(wp), ctypes.addressof(bp), rows, c, ptr(g),
+                 ptr(beta.float().contiguous()), ptr(wf), ptr(bf), _hip.stream())
     else:
         w2 = weight.reshape(o, c).float().contiguous()
         wf = torch.empty_like(w2)
@@ -859,8 +869,8 @@ def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf
     rows = n * hw
     if out_bf16:
         y = torch.empty(rows, o, dtype=torch.int16, device=dev)
-        call("tgfr_linear_bf16out", ptr(xhat), c, rows, c, ptr(wf), c, ptr(bf), o, ptr(y), o,
-             _hip.stream())
+        call("tgfr_linear_bf16io" if xhat_bf16 else "tgfr_linear_bf16out", ptr(xhat), c, rows, c,
+             ptr(wf), c, ptr(bf), o, ptr(y), o, _hip.stream())
     else:
         mb = -(-rows // 64) * -(-o // 64)
         y = bgemm(xhat.view(1, rows, c), wf.t().unsqueeze(0), bias=bf, mode=mode,
@@ -949,8 +959,9 @@ class ImimAttention(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, wk, wq, wv, bk, bq, bv, bn, training, scale):
+        # without a BN input gradient (the frozen backbone's map) xhat stays bf16
         px = _bn_linear_fwd(ctx, x, gamma, beta, (wk, wq, wv), (bk, bq, bv), bn, training,
-                            "bf16", out_bf16=True)
+                            "bf16", out_bf16=True, xhat_bf16=not ctx.needs_input_grad[0])
         nb, hw, _ = px.shape
         o = torch.empty(nb, hw, 256, dtype=torch.float32, device=px.device)
         lse = torch.empty(nb * hw, dtype=torch.float32, device=px.device)
@@ -992,8 +1003,8 @@ class ImimAttention(torch.autograd.Function):
         gws = torch.empty(int(out[0]), dtype=torch.float32, device=px.device)
         gm = torch.empty(n, c, dtype=torch.float32, device=px.device)
         s = torch.empty(n, dtype=torch.float32, device=px.device)
-        call("tgfr_dw_bf16", ptr(dpx), ptr(xhat), 1, rows, n, c, ptr(gm), ptr(s), ptr(gws),
-             _hip.stream())
+        call("tgfr_dw_bf16", ptr(dpx), ptr(xhat), int(xhat.dtype == torch.float32), rows, n, c,
+             ptr(gm), ptr(s), ptr(gws), _hip.stream())
         return _imim_grads(_bn_unfold(ctx, gm, s))
 
 
@@ -1158,6 +1169,232 @@ class ImimTail(torch.autograd.Function):
                 dbp, None, None)
 
 
+class ImimLnTail(torch.autograd.Function):
+    """IMIM from the attention output on: LayerNorm([C, H, W]) (models/
+    models.py:401) -> relu(conv1x1_1) -> relu(conv1x1_2) -> project_local ->
+    L2 norm (:399-405, ProjectionHead :98-120) with the LayerNorm fused into
+    the tail's kernels (tgfr_ln_tail_fwd / _bwd): the normalised map is never
+    written, and the LayerNorm backward's first pass (per-sample sums of dZ w
+    and dZ w xhat) runs in the tail backward's epilogue.  Forward: the weight
+    pack (+ the affine maps as channels-last rows), the LayerNorm slice
+    moments, the tail; backward: the tail (+ LN sums), the LN input gradient,
+    its dw/db reduce, the tail weight gradients."""
+
+    @staticmethod
+    def forward(ctx, x, lnw, lnb, w1, b1, w2, b2, wp, bp, ln_eps, eps, rows_spec=None):
+        n, hw, c = x.shape
+        assert c == _TAIL_C and tuple(w1.shape[:2]) == (_TAIL_H, _TAIL_C)
+        assert tuple(w2.shape[:2]) == (_TAIL_C, _TAIL_H) and tuple(wp.shape) == (_TAIL_D, _TAIL_C)
+        assert lnw.numel() == hw * c and lnb.numel() == hw * c
+        x2 = _aligned(x.reshape(-1, c))
+        rows, dev = x2.shape[0], x2.device
+        out = (ctypes.c_longlong * 1)()
+        rc = _hip.lib().tgfr_ln_tail_ws(rows, hw, ctypes.addressof(out))
+        if rc != 0:
+            raise RuntimeError(f"tgfr_ln_tail_ws failed with code {rc}")
+        ws = torch.empty(int(out[0]), dtype=torch.float32, device=dev)
+        pk = torch.empty(_hip.lib().tgfr_tail_pack_elems(), dtype=torch.int16, device=dev)
+        call("tgfr_tail_pack_ln", ptr(_aligned(w1.reshape(_TAIL_H, _TAIL_C))),
+             ptr(_aligned(w2.reshape(_TAIL_C, _TAIL_H))), ptr(_aligned(wp)),
+             ptr(_aligned(lnw.reshape(-1))), ptr(_aligned(lnb.reshape(-1))), rows, hw, ptr(pk),
+             ptr(ws), _hip.stream())
+        r = torch.empty(rows, _TAIL_D, dtype=torch.float32, device=dev)
+        zb = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)
+        h1 = torch.empty(rows, _TAIL_H, dtype=torch.int16, device=dev)
+        h2 = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)
+        inv = torch.empty(rows, dtype=torch.float32, device=dev)
+        rr = rn = None
+        per, pad, f16 = rows_spec if rows_spec else (0, 0, False)
+        if rows_spec:
+            rr = torch.empty(rows // per, pad, _TAIL_D, dtype=torch.int16, device=dev)
+            rn = torch.empty(rows // per, pad, dtype=torch.float32, device=dev)
+        call("tgfr_ln_tail_fwd", ptr(x2), rows, hw, float(ln_eps), ptr(ws), ptr(pk),
+             ptr(_aligned(b1)), ptr(_aligned(b2)), ptr(_aligned(bp)), float(eps), ptr(r), _TAIL_D,
+             ptr(zb), ptr(h1), ptr(h2), ptr(inv), ptr(rr), ptr(rn), per, pad, int(bool(f16)),
+             _hip.stream())
+        ctx.save_for_backward(x2, r, inv, pk, zb, h1, h2, ws)
+        ctx.cfg = (float(eps), x.shape, hw, lnw.shape, w1.shape, w2.shape)
+        out_r = r.reshape(n, hw, _TAIL_D)
+        if rows_spec:
+            ctx.mark_non_differentiable(rr, rn)
+            ctx.set_materialize_grads(False)
+            return out_r, rr, rn
+        return out_r
+
+    @staticmethod
+    def backward(ctx, dr, *unused):
+        if dr is None:
+            return (None,) * 12
+        x2, r, inv, pk, zb, h1, h2, ws = ctx.saved_tensors
+        eps, xshape, hw, lnshape, w1shape, w2shape = ctx.cfg
+        rows, dev = r.shape[0], r.device
+        dr2 = _aligned(dr.reshape(rows, _TAIL_D))
+        dz = torch.empty(rows, _TAIL_C, dtype=torch.float32, device=dev)
+        dp = torch.empty(rows, _TAIL_D, dtype=torch.int16, device=dev)
+        dh2 = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)
+        dh1 = torch.empty(rows, _TAIL_H, dtype=torch.int16, device=dev)
+        dx = torch.empty_like(x2)
+        dlnw = torch.empty(hw * _TAIL_C, dtype=torch.float32, device=dev)
+        dlnb = torch.empty_like(dlnw)
+        call("tgfr_ln_tail_bwd", ptr(dr2), ptr(r), ptr(inv), rows, eps, ptr(pk), ptr(h1),
+             ptr(h2), ptr(x2), hw, ptr(ws), ptr(dz), ptr(dp), ptr(dh2), ptr(dh1), ptr(dx),
+             ptr(dlnw), ptr(dlnb), _hip.stream())
+        wsd = torch.empty(tail_dw_ws_floats(rows), dtype=torch.float32, device=dev)
+        dwp = torch.empty(_TAIL_D, _TAIL_C, dtype=torch.float32, device=dev)
+        dbp = torch.empty(_TAIL_D, dtype=torch.float32, device=dev)
+        dw2 = torch.empty(_TAIL_C, _TAIL_H, dtype=torch.float32, device=dev)
+        db2 = torch.empty(_TAIL_C, dtype=torch.float32, device=dev)
+        dw1 = torch.empty(_TAIL_H, _TAIL_C, dtype=torch.float32, device=dev)
+        db1 = torch.empty(_TAIL_H, dtype=torch.float32, device=dev)
+        call("tgfr_tail_dw", ptr(dp), ptr(h2), ptr(dh2), ptr(h1), ptr(dh1), ptr(zb), rows,
+             ptr(dwp), ptr(dbp), ptr(dw2), ptr(db2), ptr(dw1), ptr(db1), ptr(wsd), _hip.stream())
+        return (dx.reshape(xshape), dlnw.reshape(lnshape), dlnb.reshape(lnshape),
+                dw1.reshape(w1shape), db1, dw2.reshape(w2shape), db2, dwp, dbp, None, None, None)
+
+
+class ImimFused(torch.autograd.Function):
+    """The whole IMIM head in bf16 / fp16 mode (models/models.py:397-405:
+    bn_img -> SelfAttention -> LayerNorm -> conv1x1_1 -> ReLU -> conv1x1_2 ->
+    ReLU -> project_local -> L2 norm) as ONE autograd node, for a frozen input
+    map (no BN input gradient, the trainers' case).  Against ImimAttention ->
+    ImimLnTail it saves two launches per step: the BN fold, the tail weight
+    pack and the LayerNorm affine transposes are one launch (tgfr_imim_pack),
+    and the LayerNorm backward writes the attention backward's operands
+    (bf16 dO and D = rowsum(dO * O)) itself (tgfr_ln_tail_bwd_att ->
+    tgfr_attn_bwd_prepped), so the fp32 dO never exists.
+    Forward: BN statistics + bf16 xhat, the pack, the q/k/v GEMM, attention,
+    LayerNorm moments, the fused tail (7 launches).  Backward: tail + LN sums,
+    LN input gradient (as attention operands), LN dw/db, tail weight
+    gradients (+ reduce), attention dK/dV, dQ, q/k/v weight gradient
+    (+ reduce), BN unfold (10 launches)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, wk, wq, wv, bk, bq, bv, lnw, lnb, w1, b1, w2, b2, wp, bp,
+                bn, training, scale, ln_eps, eps, rows_spec=None):
+        nb, c, h, w_ = x.shape
+        hw = h * w_
+        rows = nb * hw
+        dev = x.device
+        out = (ctypes.c_longlong * 1)()
+        rc = _hip.lib().tgfr_ln_tail_ws(rows, hw, ctypes.addressof(out))
+        if rc != 0:
+            raise RuntimeError(f"tgfr_ln_tail_ws failed with code {rc}")
+        ws = torch.empty(int(out[0]), dtype=torch.float32, device=dev)
+        pk = torch.empty(_hip.lib().tgfr_tail_pack_elems(), dtype=torch.int16, device=dev)
+        tw = (_aligned(w1.reshape(_TAIL_H, _TAIL_C)), _aligned(w2.reshape(_TAIL_C, _TAIL_H)),
+              _aligned(wp), _aligned(lnw.reshape(-1)), _aligned(lnb.reshape(-1)))
+
+        def fold3(wptr, bptr, qrows, cc, g, bt, wf, bf):
+            call("tgfr_imim_pack", ctypes.addressof(wptr), ctypes.addressof(bptr), qrows, cc,
+                 ptr(g), ptr(bt), ptr(wf), ptr(bf), *[ptr(t) for t in tw], rows, hw, ptr(pk),
+                 ptr(ws), _hip.stream())
+
+        px = _bn_linear_fwd(ctx, x, gamma, beta, (wk, wq, wv), (bk, bq, bv), bn, training,
+                            "bf16", out_bf16=True, xhat_bf16=True, fold3=fold3)
+        o = torch.empty(nb, hw, _TAIL_C, dtype=torch.float32, device=dev)
+        lse = torch.empty(rows, dtype=torch.float32, device=dev)
+        call("tgfr_attn_fwd", ptr(px), ptr(px[..., 256:]), ptr(px[..., 512:]), px.stride(1),
+             px.stride(0), nb, hw, float(scale), ptr(o), o.stride(1), o.stride(0), ptr(lse),
+             _hip.stream())
+        r = torch.empty(rows, _TAIL_D, dtype=torch.float32, device=dev)
+        zb = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)
+        h1 = torch.empty(rows, _TAIL_H, dtype=torch.int16, device=dev)
+        h2 = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)
+        inv = torch.empty(rows, dtype=torch.float32, device=dev)
+        rr = rn = None
+        per, pad, f16 = rows_spec if rows_spec else (0, 0, False)
+        if rows_spec:
+            rr = torch.empty(rows // per, pad, _TAIL_D, dtype=torch.int16, device=dev)
+            rn = torch.empty(rows // per, pad, dtype=torch.float32, device=dev)
+        call("tgfr_ln_tail_fwd", ptr(o), rows, hw, float(ln_eps), ptr(ws), ptr(pk),
+             ptr(_aligned(b1)), ptr(_aligned(b2)), ptr(_aligned(bp)), float(eps), ptr(r), _TAIL_D,
+             ptr(zb), ptr(h1), ptr(h2), ptr(inv), ptr(rr), ptr(rn), per, pad, int(bool(f16)),
+             _hip.stream())
+        ctx.save_for_backward(px, o, lse, r, inv, pk, zb, h1, h2, ws)
+        ctx.cfg = (float(scale), float(eps), hw, lnw.shape, w1.shape, w2.shape)
+        out_r = r.reshape(nb, hw, _TAIL_D)
+        if rows_spec:
+            ctx.mark_non_differentiable(rr, rn)
+            ctx.set_materialize_grads(False)
+            return out_r, rr, rn
+        return out_r
+
+    @staticmethod
+    def backward(ctx, dr, *unused):
+        if dr is None:
+            return (None,) * 23
+        px, o, lse, r, inv, pk, zb, h1, h2, ws = ctx.saved_tensors
+        scale, eps, hw, lnshape, w1shape, w2shape = ctx.cfg
+        nb = px.shape[0]
+        rows, dev = r.shape[0], r.device
+        dr2 = _aligned(dr.reshape(rows, _TAIL_D))
+        out = (ctypes.c_longlong * 1)()
+        rc = _hip.lib().tgfr_attn_bwd_ws(nb, hw, ctypes.addressof(out))
+        if rc != 0:
+            raise RuntimeError(f"tgfr_attn_bwd_ws failed with code {rc}")
+        aws = torch.empty(int(out[0]), dtype=torch.uint8, device=dev)
+        dz = torch.empty(rows, _TAIL_C, dtype=torch.float32, device=dev)
+        dp = torch.empty(rows, _TAIL_D, dtype=torch.int16, device=dev)
+        dh2 = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)
+        dh1 = torch.empty(rows, _TAIL_H, dtype=torch.int16, device=dev)
+        dlnw = torch.empty(hw * _TAIL_C, dtype=torch.float32, device=dev)
+        dlnb = torch.empty_like(dlnw)
+        call("tgfr_ln_tail_bwd_att", ptr(dr2), ptr(r), ptr(inv), rows, eps, ptr(pk), ptr(h1),
+             ptr(h2), ptr(o), hw, ptr(ws), ptr(dz), ptr(dp), ptr(dh2), ptr(dh1), ptr(aws),
+             ptr(dlnw), ptr(dlnb), _hip.stream())
+        wsd = torch.empty(tail_dw_ws_floats(rows), dtype=torch.float32, device=dev)
+        dwp = torch.empty(_TAIL_D, _TAIL_C, dtype=torch.float32, device=dev)
+        dbp = torch.empty(_TAIL_D, dtype=torch.float32, device=dev)
+        dw2 = torch.empty(_TAIL_C, _TAIL_H, dtype=torch.float32, device=dev)
+        db2 = torch.empty(_TAIL_C, dtype=torch.float32, device=dev)
+        dw1 = torch.empty(_TAIL_H, _TAIL_C, dtype=torch.float32, device=dev)
+        db1 = torch.empty(_TAIL_H, dtype=torch.float32, device=dev)
+        call("tgfr_tail_dw", ptr(dp), ptr(h2), ptr(dh2), ptr(h1), ptr(dh1), ptr(zb), rows,
+             ptr(dwp), ptr(dbp), ptr(dw2), ptr(db2), ptr(dw1), ptr(db1), ptr(wsd), _hip.stream())
+        dpx = torch.empty(nb, hw, 768, dtype=torch.int16, device=dev)
+        call("tgfr_attn_bwd_prepped", ptr(px), ptr(px[..., 256:]), ptr(px[..., 512:]),
+             px.stride(1), px.stride(0), nb, hw, scale, ptr(lse), ptr(dpx), ptr(dpx[..., 256:]),
+             ptr(dpx[..., 512:]), dpx.stride(1), dpx.stride(0), ptr(aws), _hip.stream())
+        xhat = ctx.bn_saved[0]
+        c = xhat.shape[2]
+        n = dpx.shape[2]
+        rc = _hip.lib().tgfr_dw_bf16_ws(rows, n, c, ctypes.addressof(out))
+        if rc != 0:
+            raise RuntimeError(f"tgfr_dw_bf16_ws failed with code {rc}")
+        gws = torch.empty(int(out[0]), dtype=torch.float32, device=dev)
+        gm = torch.empty(n, c, dtype=torch.float32, device=dev)
+        s = torch.empty(n, dtype=torch.float32, device=dev)
+        call("tgfr_dw_bf16", ptr(dpx), ptr(xhat), 0, rows, n, c, ptr(gm), ptr(s), ptr(gws),
+             _hip.stream())
+        att = _imim_grads(_bn_unfold(ctx, gm, s))[:9]
+        return att + (dlnw.reshape(lnshape), dlnb.reshape(lnshape), dw1.reshape(w1shape), db1,
+                      dw2.reshape(w2shape), db2, dwp, dbp) + (None,) * 6
+
+
+def imim_fused(x, bn, sa, scale, ln, conv1, conv2, proj, eps=1e-12, rows_spec=None):
+    """The IMIM head from the input map on (ImimFused); x must not require a
+    gradient.  Returns R [N, HW, 256] (+ the operand rows with rows_spec)."""
+    out = ImimFused.apply(x, bn.weight, bn.bias, sa.key_proj.weight, sa.query_proj.weight,
+                          sa.value_proj.weight, sa.key_proj.bias, sa.query_proj.bias,
+                          sa.value_proj.bias, ln.weight, ln.bias, conv1.weight, conv1.bias,
+                          conv2.weight, conv2.bias, proj.weight, proj.bias, bn, bn.training,
+                          scale, ln.eps, eps, rows_spec)
+    if rows_spec:
+        return out[0], (out[1], out[2])
+    return out
+
+
+def imim_ln_tail(x, ln, conv1, conv2, proj, eps=1e-12, rows_spec=None):
+    """normalize(proj(relu(conv2(relu(conv1(LayerNorm(x))))))) on the
+    channels-last attention output x [N, HW, 256] (ImimLnTail); rows_spec as
+    imim_tail."""
+    out = ImimLnTail.apply(x, ln.weight, ln.bias, conv1.weight, conv1.bias, conv2.weight,
+                           conv2.bias, proj.weight, proj.bias, ln.eps, eps, rows_spec)
+    if rows_spec:
+        return out[0], (out[1], out[2])
+    return out
+
+
 def imim_tail(z, conv1, conv2, proj, eps=1e-12, rows_spec=None):
     """R = normalize(proj(relu(conv2(relu(conv1(z)))))) on channels-last rows
     z [..., 256] (bf16 operands, fp32 accumulation).  With rows_spec =
@@ -1251,6 +1488,66 @@ def l2norm_rows(x, eps=1e-12):
     return L2NormRows.apply(x, eps)
 
 
+class ProjL2Norm(torch.autograd.Function):
+    """F.normalize(x W^T + b, dim=1, eps) -- nn.Linear then the row l2-norm
+    (ProjectionHead, models/models.py:112-120) -- for a small batch of rows in
+    exact fp32: one launch forward (tgfr_proj_l2norm_fwd), two backward (the
+    l2-norm backward, then dW and db in one launch, tgfr_proj_dw)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        x2 = _aligned(x)
+        w = _aligned(weight)
+        b_ = None if bias is None else bias.float().contiguous()
+        rows, k = x2.shape
+        n = w.shape[0]
+        dev = x2.device
+        out = (ctypes.c_longlong * 1)()
+        rc = _hip.lib().tgfr_proj_l2norm_ws(rows, n, ctypes.addressof(out))
+        if rc != 0:
+            raise RuntimeError(f"tgfr_proj_l2norm_ws failed with code {rc}")
+        ws = torch.empty(int(out[0]), dtype=torch.float32, device=dev)
+        g = torch.empty(rows, n, dtype=torch.float32, device=dev)
+        inv = torch.empty(rows, dtype=torch.float32, device=dev)
+        call("tgfr_proj_l2norm_fwd", ptr(x2), k, rows, k, ptr(w), k, ptr(b_), n, float(eps),
+             ptr(ws), ptr(g), n, ptr(inv), ptr(_hip.counters(dev)), _hip.stream())
+        ctx.save_for_backward(x2, w, g, inv)
+        ctx.cfg = (float(eps), bias is not None)
+        return g
+
+    @staticmethod
+    def backward(ctx, dg):
+        x2, w, g, inv = ctx.saved_tensors
+        eps, has_bias = ctx.cfg
+        rows, k = x2.shape
+        n = w.shape[0]
+        dg = dg.float().contiguous()
+        dy = torch.empty(rows, n, dtype=torch.float32, device=w.device)
+        call("tgfr_l2norm_rows_bwd", ptr(dg), n, ptr(g), n, ptr(inv), rows, n, eps, ptr(dy), n,
+             _hip.stream())
+        db = torch.empty(n, dtype=torch.float32, device=w.device) \
+            if has_bias and ctx.needs_input_grad[2] else None
+        dw = None
+        if ctx.needs_input_grad[1] or db is not None:
+            dw = torch.empty_like(w)
+            call("tgfr_proj_dw", ptr(dy), n, ptr(x2), k, rows, k, n, ptr(dw), k, ptr(db),
+                 _hip.stream())
+        dx = bgemm(dy.unsqueeze(0), w.unsqueeze(0), mode="fp32")[0] \
+            if ctx.needs_input_grad[0] else None
+        return dx, dw if ctx.needs_input_grad[1] else None, db, None
+
+
+def proj_l2norm(x, weight, bias=None, eps=1e-12, mode="fp32"):
+    """normalize(x W^T + b): the exact-fp32 kernels for the trainers' small
+    batches (rows <= 64, N % 32 == 0, N <= 1024, K % 4 == 0, K <= 612), else
+    the Linear GEMM (in `mode`) and the row l2-norm as two Functions."""
+    w = weight.reshape(weight.shape[0], -1)
+    if (x.dim() == 2 and x.shape[0] <= 64 and w.shape[0] % 32 == 0 and w.shape[0] <= 1024 and
+            x.shape[1] % 4 == 0 and x.shape[1] <= 612 and x.shape[1] == w.shape[1]):
+        return ProjL2Norm.apply(x, w, bias, eps)
+    return l2norm_rows(linear_rows(x, weight, bias, mode=mode), eps)
+
+
 class ArcMargin(torch.autograd.Function):
     """The margin part of ArcMarginProduct on a cosine matrix (metrics.py:45-57)."""
 
@@ -1322,15 +1619,25 @@ class ArcHead(torch.autograd.Function):
         ws = torch.empty(nws, dtype=torch.float32, device=w.device) if nws else None
         call("tgfr_arc_bwd", ptr(dl), ptr(cosv), ptr(label), ptr(xn), ptr(w), d, ptr(inv_nw),
              b, d, c, s, m, easy, eps, ptr(dw), d, ptr(dcs), ptr(ws), _hip.stream())
-        dx = None
-        if want_dx:
-            mb = -(-b // 64) * -(-d // 64)
-            dxn = bgemm(dcs.unsqueeze(0), w.unsqueeze(0), mode=mode,
-                        ksplit=_ksplit(c, mb))[0]
-            dx = torch.empty_like(xn)
-            call("tgfr_l2norm_rows_bwd", ptr(dxn), d, ptr(xn), d, ptr(inv_nx), b, d, eps,
-                 ptr(dx), d, _hip.stream())
+        dx = arc_dx(dcs, w, xn, inv_nx, eps) if want_dx else None
         return dx, dw, None, None, None, None, None, None
+
+
+def arc_dx(dcs, w, xn, inv_nx, eps):
+    """An ArcMargin head's input gradient from its backward's dcs [B][C]
+    (= dcos / |W_c|): dxn = dcs W, then the F.normalize backward of x
+    (models/metrics.py:43), exact fp32, in two launches (tgfr_arc_dx)."""
+    b, d = xn.shape
+    c = w.shape[0]
+    out = (ctypes.c_longlong * 1)()
+    rc = _hip.lib().tgfr_arc_dx_ws(int(b), int(c), int(d), ctypes.addressof(out))
+    if rc != 0:
+        raise RuntimeError(f"tgfr_arc_dx_ws failed with code {rc}")
+    ws = torch.empty(int(out[0]), dtype=torch.float32, device=xn.device)
+    dx = torch.empty_like(xn)
+    call("tgfr_arc_dx", ptr(dcs), ptr(w), w.stride(0), b, c, d, ptr(xn), ptr(inv_nx),
+         float(eps), ptr(ws), ptr(dx), _hip.stream())
+    return dx
 
 
 def arc_bwd_ws_floats(b, d, c):
@@ -1443,15 +1750,8 @@ class IdentityHeads(torch.autograd.Function):
                                     ptr(dcs[k]))
         call("tgfr_arc_focal_bwd_heads", ctypes.addressof(heads), 2, b, d, c, m, easy, eps, gamma,
              _hip.stream())
-        dx = [None, None]
-        for k in range(2):
-            if want_dx[k]:
-                mb = -(-b // 64) * -(-d // 64)
-                dxn = bgemm(dcs[k].unsqueeze(0), ws_[k].unsqueeze(0), mode=mode,
-                            ksplit=_ksplit(c, mb))[0]
-                dx[k] = torch.empty_like(per[k]["xn"])
-                call("tgfr_l2norm_rows_bwd", ptr(dxn), d, ptr(per[k]["xn"]), d,
-                     ptr(per[k]["inv_nx"]), b, d, eps, ptr(dx[k]), d, _hip.stream())
+        dx = [arc_dx(dcs[k], ws_[k], per[k]["xn"], per[k]["inv_nx"], eps) if want_dx[k]
+              else None for k in range(2)]
         return (dx[0], dws[0], dx[1], dws[1]) + (None,) * 10
 
 

@@ -34,8 +34,8 @@ class ProjectionHead(nn.Module):
         self.precision = "fp32"
 
     def forward(self, x):
-        y = K.linear_rows(x, self.projection.weight, self.projection.bias, mode=self.precision)
-        return K.l2norm_rows(y)
+        return K.proj_l2norm(x, self.projection.weight, self.projection.bias,
+                             mode=self.precision)
 
 
 class IMIM(nn.Module):
@@ -58,28 +58,51 @@ class IMIM(nn.Module):
     def forward(self, img):
         n, c, h, w = img.shape
         # bn_img folded into the packed q/k/v projection of the self-attention
-        if self.precision in ("bf16", "fp16") and c == 256 and h * w <= 224:
+        lowp = self.precision in ("bf16", "fp16")
+        if lowp and c == 256 and 32 <= h * w <= 224 and not (
+                torch.is_grad_enabled() and img.requires_grad):
+            # the whole head as one node (the frozen backbone's map: no BN
+            # input gradient); the kernel also writes R as the word<->region
+            # operand rows (:403 -> losses.py:96), attached to the returned R
+            f16 = self.precision == "fp16"
+            spec = (h * w, K.RPAD, f16) if h * w == K.NREG else None
+            z = K.imim_fused(img, self.bn_img, self.sa, 1.0 / float(self.sa.sqrt_dim), self.ln,
+                             self.conv1x1_1, self.conv1x1_2, self.project_local.projection,
+                             rows_spec=spec)
+            if spec:
+                z, (r_rows, r_norm) = z
+            out = z.reshape(n, h, w, -1).permute(0, 3, 1, 2)
+            return K.attach_rows(out, r_rows, r_norm, f16) if spec else out
+        if lowp and c == 256 and h * w <= 224:
             # packed projection in bf16 straight into the fused attention kernels
             z = K.imim_attention(img, self.bn_img, self.sa, 1.0 / float(self.sa.sqrt_dim))
         else:
             wq, bq = self.sa.packed_self()
             px = K.bn_linear(img, self.bn_img, wq, bq, mode=self.precision)   # [B, HW, 3C]
             z = self.sa.core_self(px)
-        # LayerNorm over (C, H, W) of each sample == over the channels-last
-        # [HW, C] rows; the [C, H, W] affine maps are read channel-major in place
-        z = K.layer_norm_rows(z, self.ln.weight, self.ln.bias, self.ln.eps, ch=c)
         if self.precision in ("bf16", "fp16"):
-            # conv1x1_1 -> ReLU -> conv1x1_2 -> ReLU -> project_local, fused; the
-            # kernel also writes R as the word<->region operand rows (:403 ->
-            # losses.py:96), attached to the returned R
+            # LayerNorm -> conv1x1_1 -> ReLU -> conv1x1_2 -> ReLU ->
+            # project_local, fused (the LayerNorm applied on the tail's load,
+            # its backward's sums in the tail backward); the kernel also writes
+            # R as the word<->region operand rows (:403 -> losses.py:96),
+            # attached to the returned R
             f16 = self.precision == "fp16"
             spec = (h * w, K.RPAD, f16) if h * w == K.NREG else None
-            z = K.imim_tail(z, self.conv1x1_1, self.conv1x1_2, self.project_local.projection,
-                            rows_spec=spec)
+            if h * w >= 32:
+                z = K.imim_ln_tail(z.reshape(n, h * w, c), self.ln, self.conv1x1_1,
+                                   self.conv1x1_2, self.project_local.projection,
+                                   rows_spec=spec)
+            else:
+                z = K.layer_norm_rows(z, self.ln.weight, self.ln.bias, self.ln.eps, ch=c)
+                z = K.imim_tail(z, self.conv1x1_1, self.conv1x1_2,
+                                self.project_local.projection, rows_spec=spec)
             if spec:
                 z, (r_rows, r_norm) = z
             out = z.reshape(n, h, w, -1).permute(0, 3, 1, 2)
             return K.attach_rows(out, r_rows, r_norm, f16) if spec else out
+        # LayerNorm over (C, H, W) of each sample == over the channels-last
+        # [HW, C] rows; the [C, H, W] affine maps are read channel-major in place
+        z = K.layer_norm_rows(z, self.ln.weight, self.ln.bias, self.ln.eps, ch=c)
         z = K.linear_rows(z, self.conv1x1_1.weight, self.conv1x1_1.bias, relu=True,
                           mode=self.precision)
         z = K.linear_rows(z, self.conv1x1_2.weight, self.conv1x1_2.bias, relu=True,
@@ -102,12 +125,12 @@ class ImageHeading(nn.Module):
         local_image = self.imim(local_image)
         # g' feeds only fp32 consumers (the sentence / global cosine logits and
         # the fp32-MFMA identity head, whose loss is scaled by s * lambda_id =
-        # 3000): its B x 512 x 256 projection runs in the split (fp32) mode in
-        # every precision -- a few microseconds -- so the reduced-precision
-        # modes leave those terms at fp32 accuracy
+        # 3000): its B x 512 x 256 projection runs in exact fp32 in every
+        # precision (one launch each way at the trainers' batch sizes), so the
+        # reduced-precision modes leave those terms at fp32 accuracy
         p = self.project_global
-        y = K.linear_rows(global_image, p.projection.weight, p.projection.bias, mode="fp32")
-        return K.l2norm_rows(y), local_image
+        return K.proj_l2norm(global_image, p.projection.weight, p.projection.bias,
+                             mode="fp32"), local_image
 
 
 class Bert_Word_Mapping(nn.Module):  # noqa: N801  (reference class name)

@@ -427,6 +427,27 @@ int tgfr_ln_tail_bwd_att(const float* dR, const float* R, const float* inv, int 
                          const float* X, int hw, float* ws, float* dZ, uint16_t* dPb,
                          uint16_t* dH2b, uint16_t* dH1b, void* att_ws, float* dlnw, float* dlnb,
                          void* stream);
+/* tgfr_attn_fwd_ln: tgfr_attn_fwd (O dense [B][hw][256]) that also writes
+ * each 32-query tile's LayerNorm moments (mean, M2) into ln_ws (the
+ * tgfr_ln_tail_ws buffer); tgfr_ln_tail_fwd_att: tgfr_ln_tail_fwd taking those
+ * moments instead of running its statistics pass. */
+int tgfr_attn_fwd_ln(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long long ld,
+                     long long sb, int B, int hw, float scale, float* O, float* lse,
+                     float* ln_ws, void* stream);
+int tgfr_ln_tail_fwd_att(const float* X, int rows, int hw, float ln_eps, float* ws,
+                         const uint16_t* pk, const float* b1, const float* b2, const float* bp,
+                         float eps, float* R, long long ldr, uint16_t* Zb, uint16_t* H1b,
+                         uint16_t* H2b, float* inv, uint16_t* Rrows, float* Rnorm,
+                         int rows_per_item, int rows_pad, int rows_f16, void* stream);
+/* tgfr_imim_dw: tgfr_tail_dw and tgfr_dw_bf16 (bf16 Y: the q/k/v projection's
+ * dWq = Xq^T Yq [Nq][Kq], dbq = colsum Xq) in one launch + one reduce; ws:
+ * tgfr_imim_dw_ws floats. */
+int tgfr_imim_dw_ws(int rows, int Nq, int Kq, long long* floats);
+int tgfr_imim_dw(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
+                 const uint16_t* H1b, const uint16_t* dH1b, const uint16_t* Zb, int rows,
+                 float* dWp, float* dbp, float* dW2, float* db2, float* dW1, float* db1,
+                 const uint16_t* Xq, const uint16_t* Yq, int Nq, int Kq, float* dWq, float* dbq,
+                 float* ws, void* stream);
 int tgfr_attn_bwd_prepped(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long long ld,
                           long long sb, int B, int hw, float scale, const float* lse,
                           uint16_t* dQ, uint16_t* dK, uint16_t* dV, long long ldg, long long sbg,

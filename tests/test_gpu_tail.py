@@ -236,10 +236,12 @@ def test_ln_tail_fused(n, hw):
 def test_imim_fused_node(gpu, n, precision):
     """The whole IMIM head as one autograd node (kernels.ImimFused: one weight
     preparation launch, the LayerNorm backward writing the attention
-    backward's bf16 dO and D itself) against the two-node chain ImimAttention
-    -> ImimLnTail on the same module: R, the attached operand rows and every
-    parameter gradient agree to 1e-5 of their max (the same kernels and
-    operand roundings), and BN's running statistics are updated once."""
+    backward's bf16 dO and D itself, the LayerNorm moments from the attention
+    epilogue) against the two-node chain ImimAttention -> ImimLnTail on the same
+    module.  The moments are summed in another order, so a bf16 rounding of
+    the normalised map can differ: R and the attached operand rows within
+    5e-3 of their max (measured 2.3e-3 at B = 64), every parameter gradient
+    within 1e-2; BN's running statistics are updated once."""
     import copy
     from text_guided_face_recognition_amd.config import make_args
     from text_guided_face_recognition_amd.models.models import IMIM
@@ -261,12 +263,22 @@ def test_imim_fused_node(gpu, n, precision):
                                      rows_spec=(196, K.RPAD, f16))
     rb = zb.reshape(n, 14, 14, -1).permute(0, 3, 1, 2)
     (rb * probe).sum().backward()
-    assert _maxrel(ra.detach(), rb.detach()) <= 1e-5
-    assert torch.equal(K.attached_rows(ra, f16)[0], rows_b)
+    assert _maxrel(ra.detach(), rb.detach()) <= 5e-3
+    dt = torch.float16 if f16 else torch.bfloat16
+    assert _maxrel(K.attached_rows(ra, f16)[0].view(dt).float(), rows_b.view(dt).float()) <= 5e-3
+    # the key-role projection's bias only shifts every score of a query by the
+    # same amount (softmax-invariant): its gradient is rounding noise, so the
+    # three projection biases are held to the largest one's scale
+    bscale = max(float(getattr(b.sa, m).bias.grad.abs().max())
+                 for m in ("key_proj", "query_proj", "value_proj"))
     for (na, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
         if pb.grad is None:
             assert pa.grad is None, na
             continue
-        assert _maxrel(pa.grad, pb.grad) <= 1e-5, (na, _maxrel(pa.grad, pb.grad))
+        if na.startswith("sa.") and na.endswith("_proj.bias"):
+            err = float((pa.grad - pb.grad).abs().max()) / bscale
+        else:
+            err = _maxrel(pa.grad, pb.grad)
+        assert err <= 1e-2, (na, err)
     torch.testing.assert_close(a.bn_img.running_mean, b.bn_img.running_mean)
     torch.testing.assert_close(a.bn_img.running_var, b.bn_img.running_var)

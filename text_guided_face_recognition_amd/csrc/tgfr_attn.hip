@@ -170,7 +170,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
                                                        long long ld, long long sb, int hw,
                                                        float scale, float* __restrict__ O,
                                                        long long ldo, long long sbo,
-                                                       float* __restrict__ lse) {
+                                                       float* __restrict__ lse,
+                                                       float* __restrict__ lnm, int lnS) {
   const int tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE, lr = lane & 31, h = lane >> 5;
   const int qsel = w & 1, half = w >> 1;
   const int nt = (hw + 31) / 32, np = (nt + 1) / 2, nh = (nt + 1) / 2;
@@ -295,8 +296,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   const float a1 = m1 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m1 - mm) * c);
   const float lt = l * a0 + l1 * a1;
   const int q = 32 * qt + lr;
-  if (q >= hw) return;
-  if (h == 0) lse[(long long)b * hw + q] = mm * scale + __logf(lt);
+  const bool qv = q < hw;
+  if (qv && h == 0) lse[(long long)b * hw + q] = mm * scale + __logf(lt);
   const float i0 = a0 / lt, i1 = a1 / lt;
   // lane: query q; register r of tile t: column 32 t + acc_row(r, h)
   float* orow = O + b * sbo + (long long)q * ldo;
@@ -304,12 +305,40 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   for (int t = 0; t < AD / 32; ++t)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      float v[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        v[k] = oacc[t][4 * g + k] * i0 + lds_ldf(xch + (16 * t + 4 * g + k) * 4) * i1;
-      *(float4*)(orow + 32 * t + 8 * g + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
+        oacc[t][4 * g + k] =
+            oacc[t][4 * g + k] * i0 + lds_ldf(xch + (16 * t + 4 * g + k) * 4) * i1;
+      if (qv)
+        *(float4*)(orow + 32 * t + 8 * g + 4 * h) =
+            make_float4(oacc[t][4 * g], oacc[t][4 * g + 1], oacc[t][4 * g + 2],
+                        oacc[t][4 * g + 3]);
     }
+  if (lnm) {
+    // the following per-sample LayerNorm's moments of this query tile (mean,
+    // M2 over its valid rows x 256 channels; count implied by the tile),
+    // two passes over the registers: lnm[b][qt][2], slot qt of lnS per sample
+    float sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < AD / 32; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sum += oacc[t][r];
+    const float cnt = (float)(min(32, hw - 32 * qt) * AD);
+    const float mean = wave_sum(qv ? sum : 0.f) / cnt;
+    float m2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < AD / 32; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float d = oacc[t][r] - mean;
+        m2 = fmaf(d, d, m2);
+      }
+    m2 = wave_sum(qv ? m2 : 0.f);
+    if (lane == 0) {
+      lnm[((long long)b * lnS + qt) * 2] = mean;
+      lnm[((long long)b * lnS + qt) * 2 + 1] = m2;
+    }
+  }
 }
 
 // D[row] = sum_c dO[row][c] O[row][c] and dO in bf16 (the backward's operand);
@@ -803,7 +832,22 @@ int tgfr_attn_fwd(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long 
   const int np = ((hw + 31) / 32 + 1) / 2;
   if (const int e = set_max_lds((const void*)attn_fwd_kernel, FWD_LDS)) return e;
   hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * np), dim3(256), FWD_LDS, (hipStream_t)stream, Q, K,
-                     V, ld, sb, hw, scale, O, ldo, sbo, lse);
+                     V, ld, sb, hw, scale, O, ldo, sbo, lse, nullptr, 0);
+  return (int)hipGetLastError();
+}
+
+// tgfr_attn_fwd that also leaves, for the LayerNorm([256, H, W]) that follows
+// (tgfr_ln_tail_fwd_att), each 32-query tile's moments [B][ceil(hw/32)][2] at
+// the start of ln_ws (the tgfr_ln_tail_ws buffer): no separate statistics pass.
+int tgfr_attn_fwd_ln(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long long ld,
+                     long long sb, int B, int hw, float scale, float* O, float* lse,
+                     float* ln_ws, void* stream) {
+  if (B <= 0 || hw <= 0 || hw > 32 * AT || (ld & 7) || (sb & 7) || !ln_ws) return 1001;
+  if (((uintptr_t)Q | (uintptr_t)K | (uintptr_t)V | (uintptr_t)O) & 15) return 1001;
+  const int nt = (hw + 31) / 32, np = (nt + 1) / 2;
+  if (const int e = set_max_lds((const void*)attn_fwd_kernel, FWD_LDS)) return e;
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * np), dim3(256), FWD_LDS, (hipStream_t)stream, Q, K,
+                     V, ld, sb, hw, scale, O, (long long)AD, (long long)hw * AD, lse, ln_ws, nt);
   return (int)hipGetLastError();
 }
 

@@ -78,6 +78,24 @@ __device__ __forceinline__ void ln_stats(const float* part, long long E, int S, 
   rstd = rsqrtf(m2 / n + eps);   // biased variance, as nn.LayerNorm
 }
 
+// The same combine for moments left by the attention forward (tgfr_attn_fwd_ln):
+// nt 32-row tiles of a sample with hw rows of ch channels, tile t holding
+// min(32, hw - 32 t) rows; mom = this sample's [nt][2].
+__device__ __forceinline__ void ln_stats_tiles(const float* mom, int nt, int hw, int ch,
+                                               float eps, float& mean, float& rstd) {
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  for (int t = 0; t < nt; ++t) {
+    const float nb = (float)(min(32, hw - 32 * t) * ch);
+    const float mb = mom[2 * t], m2b = mom[2 * t + 1];
+    const float nn = n + nb, d = mb - mu;
+    mu += d * nb / nn;
+    m2 += m2b + d * d * n * nb / nn;
+    n = nn;
+  }
+  mean = mu;
+  rstd = rsqrtf(m2 / n + eps);
+}
+
 int slices_for(int rows, long long E) {
   long long s = (1024 + rows - 1) / rows;
   s = std::min<long long>(s, std::max<long long>(1, E / 1024));

@@ -188,12 +188,13 @@ constexpr int F_LDS = F_INV + TM * 4;
 // the channels-last affine rows of tail_pack; the first workgroup of each
 // sample stores its (mean, rstd) for the backward.
 struct LnFwd {
-  const float* part;      // ln_part moments [n][S][2]
+  const float* part;      // ln_part moments [n][S][2], or (tiles) the attention's [n][S][2]
   float* stats;           // mean [n] | rstd [n]
   const float* aff;       // w rows [hw][TC] | b rows [hw][TC]
   long long E;            // hw * TC
   int S, hw, n;
   float eps;
+  int tiles;              // 1: the S entries are 32-row tile moments (tgfr_attn_fwd_ln)
 };
 constexpr int F_LN = F_LDS;                 // LN: mean, rstd of the two samples
 constexpr int F_MOM = F_LDS + 16;           // LN: their slice moments [2][S][2], S <= 64
@@ -251,7 +252,10 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(
       const int b = s0 + tid;
       float mean = 0.f, rstd = 0.f;
       if (b < L.n) {
-        ln_stats(mom + tid * 2 * L.S - (long long)b * L.S * 2, L.E, L.S, b, L.eps, mean, rstd);
+        if (L.tiles)
+          ln_stats_tiles(mom + tid * 2 * L.S, L.S, L.hw, TC, L.eps, mean, rstd);
+        else
+          ln_stats(mom + tid * 2 * L.S - (long long)b * L.S * 2, L.E, L.S, b, L.eps, mean, rstd);
         if ((long long)b * L.hw >= row0 && (long long)b * L.hw < row0 + TM) {
           L.stats[b] = mean;
           L.stats[L.n + b] = rstd;
@@ -705,8 +709,9 @@ struct DwProb {
   int first;         // first workgroup of this product
   long long slab;    // float offset of this product's slabs in the workspace
 };
+constexpr int DW_MAXP = 4;   // products per launch
 struct DwArgs {
-  DwProb p[3];
+  DwProb p[DW_MAXP];
   int rows, slices, rows_per;
 };
 
@@ -736,8 +741,9 @@ __global__ __launch_bounds__(256) void tail_dw_kernel(DwArgs A, float* __restric
   // consecutive ids after the remap: the blocks of one (product, slice) on one XCD
   const int wgi = xcd_remap(blockIdx.x, total);
   int pi = 0;
-  if (wgi >= A.p[1].first) pi = 1;
-  if (wgi >= A.p[2].first) pi = 2;
+#pragma unroll
+  for (int i = 1; i < DW_MAXP; ++i)
+    if (wgi >= A.p[i].first) pi = i;
   const DwProb P = A.p[pi];
   const int local = wgi - P.first;
   const int nblk = P.nb_n * P.nb_k;
@@ -858,8 +864,8 @@ __global__ __launch_bounds__(256) void tail_dw_kernel(DwArgs A, float* __restric
 }
 
 struct DwOut {
-  float* dW[3];
-  float* db[3];
+  float* dW[DW_MAXP];
+  float* db[DW_MAXP];
 };
 
 // out = sum over slices, in slice order; thread = 2 consecutive outputs (a
@@ -872,7 +878,7 @@ __global__ __launch_bounds__(256) void tail_dw_reduce_kernel(DwArgs A, DwOut O,
   // which product / region: products laid out as [dW N*K][db N] each
   long long off = e4;
   int pi = 0;
-  for (; pi < 3; ++pi) {
+  for (; pi < DW_MAXP - 1; ++pi) {
     const long long sz = (long long)A.p[pi].N * A.p[pi].K + A.p[pi].N;
     if (off < sz) break;
     off -= sz;
@@ -928,7 +934,7 @@ void dw_plan_n(int rows, int n, const int* NS, const int* KS, int wg_budget, DwA
     first += p.nb_n * p.nb_k * A.slices;
     slab += (long long)A.slices * (p.N * (long long)p.K + p.N);
   }
-  for (int i = n; i < 3; ++i) {        // unused: no workgroup, nothing to reduce
+  for (int i = n; i < DW_MAXP; ++i) {  // unused: no workgroup, nothing to reduce
     A.p[i] = DwProb{nullptr, nullptr, 0, 0, 0, 0, 0, first, slab};
   }
   ws_floats = slab;
@@ -949,7 +955,7 @@ int dw_launch(const DwArgs& A, int n_wg, const DwOut& O, float* ws, hipStream_t 
   if (const int e = set_max_lds((const void*)fn, DW_LDS)) return e;
   hipLaunchKernelGGL(fn, dim3(n_wg), dim3(256), DW_LDS, s, A, ws);
   long long e_total = 0;
-  for (int i = 0; i < 3; ++i) e_total += (long long)A.p[i].N * A.p[i].K + A.p[i].N;
+  for (int i = 0; i < DW_MAXP; ++i) e_total += (long long)A.p[i].N * A.p[i].K + A.p[i].N;
   hipLaunchKernelGGL(tail_dw_reduce_kernel, dim3((unsigned)((e_total / 2 + 255) / 256)),
                      dim3(256), 0, s, A, O, ws, e_total);
   return (int)hipGetLastError();
@@ -1001,11 +1007,13 @@ int tgfr_tail_bwd(const float* dR, long long lddr, const float* R, long long ldr
 }
 
 // ---- the tail with IMIM's LayerNorm fused in (bf16 / fp16 step path) ----
-// ws floats: LayerNorm workspace (LnWs of n = rows / hw samples, E = hw * 256)
-// | tail_bwd<true>'s per-workgroup sums [ceil(rows / TM)][2][2] | the affine
-// maps as channels-last rows [2][hw][256] (tgfr_tail_pack_ln)
+// ws floats: the attention's 32-row tile moments [n][ceil(hw / 32)][2]
+// (tgfr_attn_fwd_ln writes them at the start of the buffer) | the LayerNorm
+// workspace (LnWs of n = rows / hw samples, E = hw * 256) | tail_bwd<true>'s
+// per-workgroup sums [ceil(rows / TM)][2][2] | the affine maps as
+// channels-last rows [2][hw][256] (tgfr_tail_pack_ln)
 struct LnTailWs {
-  long long tp, aff, total;
+  long long ln, tp, aff, total;
   int n;
   long long E;
 };
@@ -1013,8 +1021,9 @@ static LnTailWs ln_tail_ws(int rows, int hw) {
   LnTailWs o;
   o.n = rows / hw;
   o.E = (long long)hw * TC;
+  o.ln = ((long long)o.n * ((hw + 31) / 32) * 2 + 3) & ~3LL;
   const LnWs l = ln_ws(o.n, o.E, TC);
-  o.tp = l.total_bwd;
+  o.tp = o.ln + l.total_bwd;
   o.aff = o.tp + 4LL * ((rows + TM - 1) / TM);
   o.total = o.aff + 2 * o.E;
   return o;
@@ -1060,11 +1069,12 @@ int tgfr_imim_pack(const float* const* Wqkv, const float* const* bqkv, int rows_
   return (int)hipGetLastError();
 }
 
-int tgfr_ln_tail_fwd(const float* X, int rows, int hw, float ln_eps, float* ws,
-                     const uint16_t* pk, const float* b1, const float* b2, const float* bp,
-                     float eps, float* R, long long ldr, uint16_t* Zb, uint16_t* H1b,
-                     uint16_t* H2b, float* inv, uint16_t* Rrows, float* Rnorm,
-                     int rows_per_item, int rows_pad, int rows_f16, void* stream) {
+static int ln_tail_fwd(const float* X, int rows, int hw, float ln_eps, float* ws,
+                       const uint16_t* pk, const float* b1, const float* b2, const float* bp,
+                       float eps, float* R, long long ldr, uint16_t* Zb, uint16_t* H1b,
+                       uint16_t* H2b, float* inv, uint16_t* Rrows, float* Rnorm,
+                       int rows_per_item, int rows_pad, int rows_f16, bool tiles,
+                       void* stream) {
   if (!ln_tail_ok(rows, hw) || !ws || ldr < TD || (ldr & 3) || ((uintptr_t)X & 15)) return 1001;
   if (!pk || !b1 || !b2 || !bp || !R || !Zb || !H1b || !H2b || !inv) return 1001;
   if ((Rrows || Rnorm) && (rows_per_item <= 0 || rows_pad < rows_per_item ||
@@ -1072,9 +1082,13 @@ int tgfr_ln_tail_fwd(const float* X, int rows, int hw, float ln_eps, float* ws,
     return 1001;
   const LnTailWs o = ln_tail_ws(rows, hw);
   auto* s = (hipStream_t)stream;
-  if (const int e = ln_part_launch(X, o.n, o.E, ws, s)) return e;
+  const int S = slices_for(o.n, o.E), nt = (hw + 31) / 32;
+  if (tiles && nt > 64) return 1001;         // (the load combines at most 64 moments)
+  if (!tiles)
+    if (const int e = ln_part_launch(X, o.n, o.E, ws + o.ln, s)) return e;
   const LnWs l = ln_ws(o.n, o.E, TC);
-  const LnFwd L{ws, ws + l.stats, ws + o.aff, o.E, slices_for(o.n, o.E), hw, o.n, ln_eps};
+  const LnFwd L{tiles ? ws : ws + o.ln, ws + o.ln + l.stats, ws + o.aff, o.E, tiles ? nt : S,
+                hw, o.n, ln_eps, tiles ? 1 : 0};
   hipLaunchKernelGGL(tail_fwd_kernel<true>, dim3((rows + TM - 1) / TM), dim3(256), F_LDS_LN, s,
                      X, (long long)TC, rows, pk, b1, b2, bp, eps, R, ldr, Zb, H1b, H2b, inv,
                      Rrows, Rnorm, rows_per_item > 0 ? rows_per_item : 1, rows_pad,
@@ -1097,13 +1111,31 @@ static int ln_tail_bwd(const float* dR, const float* R, const float* inv, int ro
   const LnTailWs o = ln_tail_ws(rows, hw);
   const LnWs l = ln_ws(o.n, o.E, TC);
   auto* s = (hipStream_t)stream;
-  const LnBwd L{X, ws + l.stats, ws + o.aff, ws + o.tp, hw, o.n};
+  const LnBwd L{X, ws + o.ln + l.stats, ws + o.aff, ws + o.tp, hw, o.n};
   hipLaunchKernelGGL(tail_bwd_kernel<true>, dim3((rows + TM - 1) / TM), dim3(256), B_LDS_LN, s,
                      dR, (long long)TD, R, (long long)TD, inv, rows, eps, pk, H1b, H2b, dZ,
                      (long long)TC, dPb, dH2b, dH1b, L);
   if (const int e = (int)hipGetLastError()) return e;
-  return ln_bwd_tail_launch(dZ, X, o.n, o.E, ws + o.aff, TC, ws, ws + o.tp, hw, TM, dX, D, dOb,
+  return ln_bwd_tail_launch(dZ, X, o.n, o.E, ws + o.aff, TC, ws + o.ln, ws + o.tp, hw, TM, dX, D, dOb,
                             dlnw, dlnb, s);
+}
+
+int tgfr_ln_tail_fwd(const float* X, int rows, int hw, float ln_eps, float* ws,
+                     const uint16_t* pk, const float* b1, const float* b2, const float* bp,
+                     float eps, float* R, long long ldr, uint16_t* Zb, uint16_t* H1b,
+                     uint16_t* H2b, float* inv, uint16_t* Rrows, float* Rnorm,
+                     int rows_per_item, int rows_pad, int rows_f16, void* stream) {
+  return ln_tail_fwd(X, rows, hw, ln_eps, ws, pk, b1, b2, bp, eps, R, ldr, Zb, H1b, H2b, inv,
+                     Rrows, Rnorm, rows_per_item, rows_pad, rows_f16, false, stream);
+}
+
+int tgfr_ln_tail_fwd_att(const float* X, int rows, int hw, float ln_eps, float* ws,
+                         const uint16_t* pk, const float* b1, const float* b2, const float* bp,
+                         float eps, float* R, long long ldr, uint16_t* Zb, uint16_t* H1b,
+                         uint16_t* H2b, float* inv, uint16_t* Rrows, float* Rnorm,
+                         int rows_per_item, int rows_pad, int rows_f16, void* stream) {
+  return ln_tail_fwd(X, rows, hw, ln_eps, ws, pk, b1, b2, bp, eps, R, ldr, Zb, H1b, H2b, inv,
+                     Rrows, Rnorm, rows_per_item, rows_pad, rows_f16, true, stream);
 }
 
 int tgfr_ln_tail_bwd(const float* dR, const float* R, const float* inv, int rows, float eps,
@@ -1153,10 +1185,51 @@ int tgfr_tail_dw(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
   A.p[0].X = dPb;  A.p[0].Y = H2b;
   A.p[1].X = dH2b; A.p[1].Y = H1b;
   A.p[2].X = dH1b; A.p[2].Y = Zb;
-  DwOut O;
+  DwOut O = {};
   O.dW[0] = dWp; O.db[0] = dbp;
   O.dW[1] = dW2; O.db[1] = db2;
   O.dW[2] = dW1; O.db[2] = db1;
+  return dw_launch(A, n_wg, O, ws, (hipStream_t)stream);
+}
+
+// IMIM's two weight-gradient sets in ONE launch (+ one reduce): the tail's
+// dWp, dW2, dW1 (tgfr_tail_dw) and the packed q/k/v projection's dW = dX^T Y,
+// db = colsum(dX) (tgfr_dw_bf16 with bf16 Y: X [rows][Nq], Y [rows][Kq]).
+static void imim_dw_plan(int rows, int Nq, int Kq, DwArgs& A, long long& wsf, int& n_wg) {
+  const int NS[4] = {TD, TC, TH, Nq}, KS[4] = {TC, TH, TC, Kq};
+  dw_plan_n(rows, 4, NS, KS, 256, A, wsf, n_wg);
+}
+
+int tgfr_imim_dw_ws(int rows, int Nq, int Kq, long long* floats) {
+  if (rows <= 0 || Nq <= 0 || Kq <= 0 || Nq % DW_NB || Kq % DW_NB || !floats) return 1001;
+  DwArgs A;
+  int n_wg;
+  imim_dw_plan(rows, Nq, Kq, A, *floats, n_wg);
+  return 0;
+}
+
+int tgfr_imim_dw(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
+                 const uint16_t* H1b, const uint16_t* dH1b, const uint16_t* Zb, int rows,
+                 float* dWp, float* dbp, float* dW2, float* db2, float* dW1, float* db1,
+                 const uint16_t* Xq, const uint16_t* Yq, int Nq, int Kq, float* dWq, float* dbq,
+                 float* ws, void* stream) {
+  if (rows <= 0 || !dPb || !H2b || !dH2b || !H1b || !dH1b || !Zb || !dWp || !dbp || !dW2 ||
+      !db2 || !dW1 || !db1 || !Xq || !Yq || !dWq || !dbq || !ws || Nq <= 0 || Kq <= 0 ||
+      Nq % DW_NB || Kq % DW_NB)
+    return 1001;
+  DwArgs A;
+  long long wsf;
+  int n_wg;
+  imim_dw_plan(rows, Nq, Kq, A, wsf, n_wg);
+  A.p[0].X = dPb;  A.p[0].Y = H2b;
+  A.p[1].X = dH2b; A.p[1].Y = H1b;
+  A.p[2].X = dH1b; A.p[2].Y = Zb;
+  A.p[3].X = Xq;   A.p[3].Y = Yq;
+  DwOut O = {};
+  O.dW[0] = dWp; O.db[0] = dbp;
+  O.dW[1] = dW2; O.db[1] = db2;
+  O.dW[2] = dW1; O.db[2] = db1;
+  O.dW[3] = dWq; O.db[3] = dbq;
   return dw_launch(A, n_wg, O, ws, (hipStream_t)stream);
 }
 
@@ -1190,7 +1263,9 @@ int tgfr_dw_bf16(const uint16_t* X, const void* Y, int y_f32, int rows, int N, i
   A.p[0].X = X;
   A.p[0].Y = Y;
   A.p[0].yf32 = y_f32 ? 1 : 0;
-  DwOut O = {{dW, nullptr, nullptr}, {db, nullptr, nullptr}};
+  DwOut O = {};
+  O.dW[0] = dW;
+  O.db[0] = db;
   return dw_launch(A, n_wg, O, ws, (hipStream_t)stream);
 }
 

@@ -2524,14 +2524,19 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
 // its own waits; two waves with complementary mixes let the SIMD overlap one
 // wave's softmax VALU and LDS waits with the other's MFMAs.
 // Per stage t: barrier B1 (X(t+1) landed, M(t-1) written); S: G1(t+1) + SM(t);
-// M: reads M(t-1), G3(t-1), DMA X(t+2); barrier B2 (M(t-1) consumed); S
-// writes M(t).  Captions past the chunk read a zero token table (their M
-// fragments are zero), so the fill / drain stages need no branches.
+// M: reads M(t-1) and marks it consumed in its tile's LDS counter, G3(t-1),
+// DMA X(t+2); S waits for that counter (pairwise, not a workgroup barrier:
+// round 3's second barrier per stage made every wave wait for the slowest
+// role of all four tiles) and writes M(t).  B1 alone orders the X ring: a
+// slot is re-filled two stages after its last readers passed B1.  Captions
+// past the chunk read a zero token table (their M fragments are zero), so
+// the fill / drain stages need no branches.
 constexpr int BD_NB = 4;                        // X ring depth
 constexpr int BD_BUF = B_XIMG + BP_TOK;         // one caption: X image + token table
 constexpr int BD_MS = BD_NB * BD_BUF;           // M hand-off: 4 tiles x 4 KB
 constexpr int BD_ZERO = BD_MS + 4 * 4096;       // a zero token table
-constexpr int BD_LDS = BD_ZERO + BP_TOK;
+constexpr int BD_CNT = BD_ZERO + BP_TOK;        // per tile: M stages consumed (int)
+constexpr int BD_LDS = BD_CNT + 4 * 4;
 constexpr int BD_PF1 = 3;                       // G1 operand prefetch distance (slots)
 constexpr int BD_PF3 = 4;                       // G3 operand prefetch distance (slots)
 
@@ -2539,6 +2544,23 @@ constexpr int BD_PF3 = 4;                       // G3 operand prefetch distance 
 // issued (-1: none): every other slot from slot 1
 __device__ __forceinline__ constexpr int bd_dma_slot(int n) {
   return (n >= 1 && n <= 17 && (n & 1) == 1) ? (n - 1) / 2 : -1;
+}
+
+// LDS hand-off counters between the waves of one workgroup: a release store
+// after the consumer's reads, an acquire load before the producer's writes
+// (workgroup scope: LDS is coherent within the CU; the orderings keep the
+// compiler from moving the data accesses across them)
+__device__ __forceinline__ int lds_ld_acquire(uint32_t off) {
+  return __hip_atomic_load((LDS_AS int*)(lds_base() + off), __ATOMIC_ACQUIRE,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st_release(uint32_t off, int v) {
+  __hip_atomic_store((LDS_AS int*)(lds_base() + off), v, __ATOMIC_RELEASE,
+                     __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// spin (with s_sleep) until the LDS counter at off reaches at least v
+__device__ __forceinline__ void lds_wait_ge(uint32_t off, int v) {
+  while (lds_ld_acquire(off) < v) __builtin_amdgcn_s_sleep(1);
 }
 
 __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
@@ -2636,6 +2658,9 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
         bf16x8 Mi[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) Mi[k] = as_bf8(lds_ld16(ms + k * 1024));
+        // M(t-1) read: the partner S wave may overwrite the slot (pairwise, no
+        // workgroup barrier between the roles' stages)
+        if (lane == 0) lds_st_release(BD_CNT + 4 * wid, t + 1);
         bf16x8 rd[8];
 #pragma unroll
         for (int n = 0; n < BD_PF3; ++n) rd[n] = g3_read(n, x3);
@@ -2651,7 +2676,6 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
 #pragma unroll
         for (int j = 0; j < 9; ++j) dma_piece(t + 2, j);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B2
     }
     if (rt < NRT) store_dr_tile(dR, n_chunks, chunk, b, rt, B_img, lane, out, s_b, s_r, s_d, slab);
     return;
@@ -2793,7 +2817,9 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
       sm_chunk(2 * n + 1, tbs, A0, A1, Mo);
       __builtin_amdgcn_sched_barrier(0);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B2: M(t-1) consumed
+    // M(t-1) consumed by the partner M wave (it reads the slot right after
+    // B1 of stage t, so this rarely waits), then M(t) into the slot
+    lds_wait_ge(BD_CNT + 4 * wid, t + 1);
 #pragma unroll
     for (int k = 0; k < 4; ++k) lds_st16(ms + k * 1024, __builtin_bit_cast(uint4, Mo[k]));
   };
@@ -2808,8 +2834,7 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");     // G1(0) done
   if (!live) {
     // the padding tile (and an empty chunk): only the barriers
-    for (int t = 0; t < T2; ++t)
-      asm volatile("s_barrier\n\ts_barrier" ::: "memory");
+    for (int t = 0; t < T2; ++t) asm volatile("s_barrier" ::: "memory");
     return;
   }
   for (int t = 0; t < T2; t += 2) {
@@ -3095,6 +3120,6 @@ int tgfr_wr_lds_bytes(int which) {
   return which == 0 ? F_LDS : which == 1 ? BwdCfg<MODE_SPLIT>::LDS : FR_LDS;
 }
 
-int tgfr_version(void) { return 300; }
+int tgfr_version(void) { return 400; }
 
 }  // extern "C"

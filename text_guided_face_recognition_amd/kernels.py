@@ -1262,11 +1262,13 @@ class ImimFused(torch.autograd.Function):
     and the LayerNorm backward writes the attention backward's operands
     (bf16 dO and D = rowsum(dO * O)) itself (tgfr_ln_tail_bwd_att ->
     tgfr_attn_bwd_prepped), so the fp32 dO never exists.
-    Forward: BN statistics + bf16 xhat, the pack, the q/k/v GEMM, attention,
-    LayerNorm moments, the fused tail (7 launches).  Backward: tail + LN sums,
-    LN input gradient (as attention operands), LN dw/db, tail weight
-    gradients (+ reduce), attention dK/dV, dQ, q/k/v weight gradient
-    (+ reduce), BN unfold (10 launches)."""
+    The attention forward also writes the LayerNorm's per-tile moments
+    (tgfr_attn_fwd_ln), so no statistics pass runs either.
+    Forward: BN statistics + bf16 xhat, the pack, the q/k/v GEMM, attention
+    (+ LN moments), the fused tail (6 launches).  Backward: tail + LN sums,
+    LN input gradient (as attention operands), LN dw/db, attention dK/dV, dQ,
+    the tail's and the q/k/v projection's weight gradients in one launch
+    (+ reduce), BN unfold (8 launches)."""
 
     @staticmethod
     def forward(ctx, x, gamma, beta, wk, wq, wv, bk, bq, bv, lnw, lnb, w1, b1, w2, b2, wp, bp,
@@ -1293,9 +1295,9 @@ class ImimFused(torch.autograd.Function):
                             "bf16", out_bf16=True, xhat_bf16=True, fold3=fold3)
         o = torch.empty(nb, hw, _TAIL_C, dtype=torch.float32, device=dev)
         lse = torch.empty(rows, dtype=torch.float32, device=dev)
-        call("tgfr_attn_fwd", ptr(px), ptr(px[..., 256:]), ptr(px[..., 512:]), px.stride(1),
-             px.stride(0), nb, hw, float(scale), ptr(o), o.stride(1), o.stride(0), ptr(lse),
-             _hip.stream())
+        # (the attention forward also leaves the LayerNorm's tile moments in ws)
+        call("tgfr_attn_fwd_ln", ptr(px), ptr(px[..., 256:]), ptr(px[..., 512:]), px.stride(1),
+             px.stride(0), nb, hw, float(scale), ptr(o), ptr(lse), ptr(ws), _hip.stream())
         r = torch.empty(rows, _TAIL_D, dtype=torch.float32, device=dev)
         zb = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)
         h1 = torch.empty(rows, _TAIL_H, dtype=torch.int16, device=dev)
@@ -1306,7 +1308,7 @@ class ImimFused(torch.autograd.Function):
         if rows_spec:
             rr = torch.empty(rows // per, pad, _TAIL_D, dtype=torch.int16, device=dev)
             rn = torch.empty(rows // per, pad, dtype=torch.float32, device=dev)
-        call("tgfr_ln_tail_fwd", ptr(o), rows, hw, float(ln_eps), ptr(ws), ptr(pk),
+        call("tgfr_ln_tail_fwd_att", ptr(o), rows, hw, float(ln_eps), ptr(ws), ptr(pk),
              ptr(_aligned(b1)), ptr(_aligned(b2)), ptr(_aligned(bp)), float(eps), ptr(r), _TAIL_D,
              ptr(zb), ptr(h1), ptr(h2), ptr(inv), ptr(rr), ptr(rn), per, pad, int(bool(f16)),
              _hip.stream())
@@ -1342,30 +1344,29 @@ class ImimFused(torch.autograd.Function):
         call("tgfr_ln_tail_bwd_att", ptr(dr2), ptr(r), ptr(inv), rows, eps, ptr(pk), ptr(h1),
              ptr(h2), ptr(o), hw, ptr(ws), ptr(dz), ptr(dp), ptr(dh2), ptr(dh1), ptr(aws),
              ptr(dlnw), ptr(dlnb), _hip.stream())
-        wsd = torch.empty(tail_dw_ws_floats(rows), dtype=torch.float32, device=dev)
+        dpx = torch.empty(nb, hw, 768, dtype=torch.int16, device=dev)
+        call("tgfr_attn_bwd_prepped", ptr(px), ptr(px[..., 256:]), ptr(px[..., 512:]),
+             px.stride(1), px.stride(0), nb, hw, scale, ptr(lse), ptr(dpx), ptr(dpx[..., 256:]),
+             ptr(dpx[..., 512:]), dpx.stride(1), dpx.stride(0), ptr(aws), _hip.stream())
+        # the tail's and the q/k/v projection's weight gradients in one launch
+        xhat = ctx.bn_saved[0]
+        c = xhat.shape[2]
+        n = dpx.shape[2]
+        rc = _hip.lib().tgfr_imim_dw_ws(rows, n, c, ctypes.addressof(out))
+        if rc != 0:
+            raise RuntimeError(f"tgfr_imim_dw_ws failed with code {rc}")
+        wsd = torch.empty(int(out[0]), dtype=torch.float32, device=dev)
         dwp = torch.empty(_TAIL_D, _TAIL_C, dtype=torch.float32, device=dev)
         dbp = torch.empty(_TAIL_D, dtype=torch.float32, device=dev)
         dw2 = torch.empty(_TAIL_C, _TAIL_H, dtype=torch.float32, device=dev)
         db2 = torch.empty(_TAIL_C, dtype=torch.float32, device=dev)
         dw1 = torch.empty(_TAIL_H, _TAIL_C, dtype=torch.float32, device=dev)
         db1 = torch.empty(_TAIL_H, dtype=torch.float32, device=dev)
-        call("tgfr_tail_dw", ptr(dp), ptr(h2), ptr(dh2), ptr(h1), ptr(dh1), ptr(zb), rows,
-             ptr(dwp), ptr(dbp), ptr(dw2), ptr(db2), ptr(dw1), ptr(db1), ptr(wsd), _hip.stream())
-        dpx = torch.empty(nb, hw, 768, dtype=torch.int16, device=dev)
-        call("tgfr_attn_bwd_prepped", ptr(px), ptr(px[..., 256:]), ptr(px[..., 512:]),
-             px.stride(1), px.stride(0), nb, hw, scale, ptr(lse), ptr(dpx), ptr(dpx[..., 256:]),
-             ptr(dpx[..., 512:]), dpx.stride(1), dpx.stride(0), ptr(aws), _hip.stream())
-        xhat = ctx.bn_saved[0]
-        c = xhat.shape[2]
-        n = dpx.shape[2]
-        rc = _hip.lib().tgfr_dw_bf16_ws(rows, n, c, ctypes.addressof(out))
-        if rc != 0:
-            raise RuntimeError(f"tgfr_dw_bf16_ws failed with code {rc}")
-        gws = torch.empty(int(out[0]), dtype=torch.float32, device=dev)
         gm = torch.empty(n, c, dtype=torch.float32, device=dev)
         s = torch.empty(n, dtype=torch.float32, device=dev)
-        call("tgfr_dw_bf16", ptr(dpx), ptr(xhat), 0, rows, n, c, ptr(gm), ptr(s), ptr(gws),
-             _hip.stream())
+        call("tgfr_imim_dw", ptr(dp), ptr(h2), ptr(dh2), ptr(h1), ptr(dh1), ptr(zb), rows,
+             ptr(dwp), ptr(dbp), ptr(dw2), ptr(db2), ptr(dw1), ptr(db1), ptr(dpx), ptr(xhat), n,
+             c, ptr(gm), ptr(s), ptr(wsd), _hip.stream())
         att = _imim_grads(_bn_unfold(ctx, gm, s))[:9]
         return att + (dlnw.reshape(lnshape), dlnb.reshape(lnshape), dw1.reshape(w1shape), db1,
                       dw2.reshape(w2shape), db2, dwp, dbp) + (None,) * 6

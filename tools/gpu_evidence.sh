@@ -6,7 +6,8 @@
 #   4. SQ counter passes of the word<->region kernels (tools/microbench.py)
 #   5. (SIM8=1) the same trace / PMC passes for configs[4]'s per-rank step
 #      (B = 128, T = 62, fp16, --simulate-world 8): prof_<R>_sim8
-# PROF=trace: the kernel trace only; SQ=0: no SQ passes (and no SIM8).
+# PROF=trace: the kernel trace only; SQ=0: no SQ passes (and no SIM8);
+# LAB=1: tools/lab/bench_variants.py after the first tests.
 # Every GPU step has its own time limit; the script stops at the first
 # failure.  Summaries: tools/summarize_profile.py / tools/summarize_sq.py here.
 R=${R:-r4x}
@@ -15,6 +16,10 @@ FIRST=${FIRST:-tests/test_gpu_modules.py}
 mkdir -p $O
 timeout -k 10 300 python3 -u -m pytest $FIRST -q -x --timeout 120 --timeout-method thread > $O/first.log 2>&1
 rc=$?; echo "first rc=$rc"; [ $rc -eq 0 ] || exit $rc
+if [ "${LAB:-0}" = 1 ]; then     # A/B of the lab variants in tools/lab/build
+  LAB_ROUNDS=${LAB_ROUNDS:-3} timeout -k 10 400 python3 -u tools/lab/bench_variants.py > $O/lab.log 2>&1 || exit 9
+  echo lab ok
+fi
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $O/gputest.log 2>&1
 rc=$?; echo "gputest rc=$rc"; [ $rc -le 1 ] || exit $rc
 timeout -k 10 180 python3 -u bench.py > $O/bench.log 2>&1 || exit 12

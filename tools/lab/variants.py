@@ -34,50 +34,26 @@ _SWAVE = ("""  // ==============================================================
   const float gL = g1 * 1.4426950408889634f;""")
 _MWAVE = ("""    // ================================================================ M wave
     // DMA pieces of one caption (bwd_stage's layout): M wave wid issues""")
-# in-kernel stamps of the two-role backward (s_memtime at B1 done, work done,
-# B2 done for stages 8..23 of every wave) into a device array of the variant's
-# own code object, read back by tools/lab/stamps_duo.py (tgfr_lab_stamps)
-_STAMP_DEF = ("""constexpr int BD_PF3 = 4;                       // G3 operand prefetch distance (slots)""",
-              """constexpr int BD_PF3 = 4;                       // G3 operand prefetch distance (slots)
-__device__ unsigned long long g_lab_stamps[512 * 8 * 16 * 4];
-#define LAB_STAMP(t, k) do { if ((t) >= 8 && (t) < 24 && lane == 0) \\
-  g_lab_stamps[((blockIdx.x * 8 + wv) * 16 + ((t) - 8)) * 4 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)""")
-_STAMPS = [
-    _STAMP_DEF,
-    ("""    ring_barrier<0>();                 // B1: X(t+1) landed everywhere""",
-     """    ring_barrier<0>();                 // B1: X(t+1) landed everywhere
-    LAB_STAMP(t, 0);"""),
-    (r"""      __builtin_amdgcn_sched_barrier(0);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B2: M(t-1) consumed""",
-     r"""      __builtin_amdgcn_sched_barrier(0);
-    }
-    LAB_STAMP(t, 1);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B2: M(t-1) consumed
-    LAB_STAMP(t, 2);"""),
-    ("""      ring_barrier<0>();                       // B1: X(t+1) landed; M(t-1) written""",
-     """      ring_barrier<0>();                       // B1: X(t+1) landed; M(t-1) written
-      LAB_STAMP(t, 0);"""),
-    (r"""      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B2
-    }""",
-     r"""      LAB_STAMP(t, 1);
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B2
-      LAB_STAMP(t, 2);
-    }"""),
-    ("""int tgfr_version(void) { return 300; }""",
-     """int tgfr_version(void) { return 300; }
-int tgfr_lab_stamps(void* dst, long long bytes) {
-  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_lab_stamps), bytes, 0, hipMemcpyDeviceToHost);
-}"""),
-]
 VARIANTS = {
     "base": [],
     "head": "HEAD",
+    "pipe": [(_DUO, _PIPE)],          # round 3's one-wave-per-SIMD backward
+    # the second workgroup barrier per stage (before round 4's pairwise counter)
+    "b2": [("""        if (lane == 0) lds_st_release(BD_CNT + 4 * wid, t + 1);""", ""),
+           ("""        for (int j = 0; j < 9; ++j) dma_piece(t + 2, j);
+      }
+    }""", """        for (int j = 0; j < 9; ++j) dma_piece(t + 2, j);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");
+    }"""),
+           ("""    lds_wait_ge(BD_CNT + 4 * wid, t + 1);""",
+            """    asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");"""),
+           ("""    for (int t = 0; t < T2; ++t) asm volatile("s_barrier" ::: "memory");""",
+            """    for (int t = 0; t < T2; ++t) asm volatile("s_barrier\\n\\ts_barrier" ::: "memory");""")],
     "nosm": [(_SM, """      asm volatile("" ::"v"(A0), "v"(A1));""")],
     "nog3": [(_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));""")],
     "nodma": [(_DMA, "")],
     "prio_s": [(_SWAVE, _SWAVE + "\n  __builtin_amdgcn_s_setprio(1);")],
-    "stamps": _STAMPS,
     "pf1_5": [("constexpr int BD_PF1 = 3;", "constexpr int BD_PF1 = 5;")],
     "pf3_6": [("constexpr int BD_PF3 = 4;", "constexpr int BD_PF3 = 6;")],
     "pf56": [("constexpr int BD_PF1 = 3;", "constexpr int BD_PF1 = 5;"),

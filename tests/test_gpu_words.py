@@ -5,7 +5,7 @@ Tolerances: fp32 mode (split-bf16 MFMA) must meet the north-star bar of
 1e-3 absolute on logits and losses with identical row/column argmax; the
 bf16 mode is the perf mode: its operands carry 2^-9 relative rounding, which
 the logit gamma3 * log sum exp(gamma2 cos) amplifies by ~gamma2 * gamma3 = 50,
-so it is held to 5e-2 on the reference fixtures and 1e-1 on random unit
+so it is held to 2e-2 on the reference fixtures and 3e-2 on random unit
 vectors (documented in DESIGN.md).  Region gradients are compared relative
 to their max magnitude.
 """
@@ -104,12 +104,14 @@ def test_words_bf16_bounded_vs_golden(gpu, tag):
     logits, l0, l1, _, dr = _run(g, gpu, "bf16", bounded=True)
     err = np.abs(logits.numpy() - g["logits"]).max()
     print(f"bf16 pipelined {tag}: max |logit error| {err:.3e}")
-    np.testing.assert_allclose(logits.numpy(), g["logits"], atol=5e-2, rtol=0)
+    # (round 4: 3.8e-3 / 4.2e-3 measured on the two fixtures)
+    np.testing.assert_allclose(logits.numpy(), g["logits"], atol=2e-2, rtol=0)
     assert (logits.argmax(1).numpy() == g["logits"].argmax(1)).all()
     assert (logits.argmax(0).numpy() == g["logits"].argmax(0)).all()
-    assert abs(l0 - float(g["loss0"])) < 5e-2 and abs(l1 - float(g["loss1"])) < 5e-2
+    assert abs(l0 - float(g["loss0"])) < 2e-2 and abs(l1 - float(g["loss1"])) < 2e-2
     scale = np.abs(g["d_img"]).max()
     err = np.abs(dr.numpy() - g["d_img"]).max() / scale
+    print(f"  region gradient error {err:.3e} of scale")
     assert err < 3e-2, err
 
 
@@ -137,9 +139,11 @@ def test_words_bf16_bounded_vs_oracle_shapes(gpu, b_img, b_cap, nw):
     (logits * probe.to(gpu)).sum().backward()
     got = logits.detach().cpu()
     assert torch.isfinite(got).all() and torch.isfinite(rg.grad).all()
-    np.testing.assert_allclose(got.numpy(), ref.detach().numpy(), atol=1e-1, rtol=0)
+    lerr = (got - ref.detach()).abs().max().item()
     scale = ro.grad.abs().max().item()
     err = (rg.grad.cpu() - ro.grad).abs().max().item() / scale
+    print(f"bf16 bounded {b_img}x{b_cap} T={nw}: logit err {lerr:.3e}, grad err {err:.3e}")
+    assert lerr < 3e-2, lerr
     assert err < 3e-2, err
 
 
@@ -190,7 +194,7 @@ def test_words_64_token_captions_vs_oracle(gpu, mode, b_img, b_cap, nw):
     (logits * probe.to(gpu)).sum().backward()
     got = logits.detach().cpu()
     assert torch.isfinite(got).all() and torch.isfinite(rg.grad).all()
-    tol, gtol = {"fp32": (1e-3, 2e-3), "bf16": (1e-1, 3e-2), "fp16": (2e-2, 1e-2)}[mode]
+    tol, gtol = {"fp32": (1e-3, 2e-3), "bf16": (3e-2, 3e-2), "fp16": (5e-3, 1e-2)}[mode]
     np.testing.assert_allclose(got.numpy(), ref.detach().numpy(), atol=tol, rtol=0)
     if mode != "bf16":
         assert (got.argmax(1) == ref.argmax(1)).all() and (got.argmax(0) == ref.argmax(0)).all()
@@ -220,7 +224,7 @@ def test_words_64_token_ragged_vs_oracle(gpu, mode):
     (logits * probe.to(gpu)).sum().backward()
     got = logits.detach().cpu()
     assert torch.isfinite(got).all() and torch.isfinite(rg.grad).all()
-    tol, gtol = {"fp32": (1e-3, 2e-3), "bf16": (1e-1, 3e-2), "fp16": (2e-2, 1e-2)}[mode]
+    tol, gtol = {"fp32": (1e-3, 2e-3), "bf16": (3e-2, 3e-2), "fp16": (5e-3, 1e-2)}[mode]
     np.testing.assert_allclose(got.numpy(), ref.detach().numpy(), atol=tol, rtol=0)
     err = (rg.grad.cpu() - ro.grad).abs().max().item() / ro.grad.abs().max().item()
     assert err < gtol, err
@@ -280,7 +284,7 @@ def test_words_config3_rank_shape(gpu, mode):
         assert (got.argmax(1) == refd.argmax(1)).all()
         assert (got.argmax(0) == refd.argmax(0)).all()
     else:
-        assert err < 1e-1 and gerr < 3e-2
+        assert err < 3e-2 and gerr < 1.5e-2     # (round 4: 7.2e-3, 4.4e-3 measured)
         # argmax identity wherever the reference's top-2 gap exceeds twice
         # the measured error (512 random captions leave near-ties the bf16
         # operands cannot resolve; the reference fixtures are checked with
@@ -291,7 +295,8 @@ def test_words_config3_rank_shape(gpu, mode):
         assert (got.argmax(1) == refd.argmax(1))[sure].all()
 
 
-@pytest.mark.parametrize("mode,ltol,gtol", [("fp16", 2e-2, 1e-2), ("bf16", 1e-1, 3e-2)])
+# (round 4 measured: fp16 5.5e-4 / 4.0e-4, bf16 4.3e-3 / 3.0e-3)
+@pytest.mark.parametrize("mode,ltol,gtol", [("fp16", 3e-3, 2e-3), ("bf16", 2e-2, 1e-2)])
 def test_words_config5_rank_shape(gpu, mode, ltol, gtol):
     """BASELINE configs[4] as one rank sees it: B_l = 128 local images against
     B_g = 1024 all-gathered captions (8 ranks x 128), bert_words_num = 64 ->
@@ -343,10 +348,13 @@ def test_words_config5_rank_shape(gpu, mode, ltol, gtol):
     assert (got.argmax(0) == refd.argmax(0))[surec].all()
 
 
+# (round 4 measured, logit / gradient: bf16 c=48 8.2e-3 / 1.9e-2 (T=30), 7.5e-3 /
+# 1.8e-2 (T=62); fp16 c=48 8.4e-4 / 1.9e-3; c=80 1.4e-3 / 4.0e-3 (T=30), 8.5e-4 /
+# 5.1e-3 (T=62); c=144 (fallback) 1.3e-3 / 4.2e-3)
 @pytest.mark.parametrize("mode,nw,wn,rn,ltol,gtol", [
-    ("bf16", 30, 6.0, 8.0, 2e-1, 6e-2), ("bf16", 62, 6.0, 8.0, 3e-2, 4e-2),
-    ("fp16", 62, 6.0, 8.0, 5e-3, 1e-2), ("fp16", 30, 8.0, 10.0, 5e-2, 5e-2),
-    ("fp16", 62, 8.0, 10.0, 5e-2, 5e-2), ("fp16", 30, 12.0, 12.0, 1e-1, 1e-1)])
+    ("bf16", 30, 6.0, 8.0, 3e-2, 5e-2), ("bf16", 62, 6.0, 8.0, 3e-2, 4e-2),
+    ("fp16", 62, 6.0, 8.0, 4e-3, 8e-3), ("fp16", 30, 8.0, 10.0, 6e-3, 1.5e-2),
+    ("fp16", 62, 8.0, 10.0, 4e-3, 1.5e-2), ("fp16", 30, 12.0, 12.0, 6e-3, 1.5e-2)])
 def test_words_bounded_past_unit_norm(gpu, mode, nw, wn, rn, ltol, gtol):
     """The max-free (bounded) kernels fed features far from the unit-norm
     contract through the drop-in path (kernels.word_region_logits with
@@ -404,12 +412,14 @@ def test_words_loss_bert_c80_drop_in(gpu, precision):
     err = max(abs(g0.item() - l0.item()), abs(g1.item() - l1.item()))
     gerr = ((rg.grad.cpu() - ro.grad).abs().max() / ro.grad.abs().max()).item()
     print(f"{precision} c=80: loss err {err:.3e}, grad err {gerr:.3e}")
-    assert err < 5e-2 and gerr < 5e-2
+    assert err < 1e-3 and gerr < 5e-2     # (round 4: 7e-5 / 2.4e-2 bf16, 7e-5 / 5.5e-3 fp16)
 
 
 @pytest.mark.parametrize("tag", ["bert_b64_l32", "bert_b16_l64"])
-@pytest.mark.parametrize("mode,ltol,gtol", [("fp32", 1e-3, 2e-3), ("bf16", 5e-2, 3e-2),
-                                            ("fp16", 1e-2, 1e-2)])
+# (round 4 measured, logit / sampled gradient: bf16 5.4e-3 / 3.4e-3 (B=64), 3.0e-3 /
+# 3.1e-3 (T=62); fp16 6.7e-4 / 1.3e-3, 3.6e-4 / 5.4e-4)
+@pytest.mark.parametrize("mode,ltol,gtol", [("fp32", 1e-3, 2e-3), ("bf16", 2e-2, 1e-2),
+                                            ("fp16", 3e-3, 5e-3)])
 def test_words_seeded_full_shape_vs_reference(gpu, tag, mode, ltol, gtol):
     """The benchmarked (bounded) kernels at the headline batch (B = 64,
     bert_words_num = 32) and at configs[4]'s caption length (bert_words_num =

@@ -121,6 +121,11 @@ class ImageHeading(nn.Module):
         self.imim = IMIM(args, channel_dim=256)
         set_precision(self, getattr(args, "precision", "fp32"))
 
+    def global_features(self, global_image):
+        """g' = normalize(project_global(global_image)) (models.py:336)."""
+        p = self.project_global
+        return K.proj_l2norm(global_image, p.projection.weight, p.projection.bias, mode="fp32")
+
     def forward(self, global_image, local_image):
         local_image = self.imim(local_image)
         # g' feeds only fp32 consumers (the sentence / global cosine logits and

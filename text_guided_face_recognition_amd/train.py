@@ -29,6 +29,8 @@ are broadcast from rank 0.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from . import kernels as K
 from .dist import DistContext, StepCapture
@@ -108,6 +110,19 @@ class Train:
         # same weights, or the gathered words mix different text heads
         self.ctx.broadcast_params(self.params + list(self.text_head.parameters()))
         self.ident_loss = FocalLoss(gamma=2)
+        # one process: the g' branch (projection head, sentence / global
+        # losses, both identity heads, their backward) runs on a side stream
+        # beside IMIM and the word<->region branch -- its kernels are small
+        # latency chains that leave most of the chip idle
+        # (TGFR_FORK: 0 = one linear stream, 1 = the g' branch forked, 2 = the
+        # frozen TextHeading heading that side stream too; round 4 at config 2:
+        # 0.547 / 0.482 / 0.460 ms per step.  Updating the side branch's
+        # parameters on the side stream too -- a partial optimiser step --
+        # and the logged-loss mix there measured slower: 0.469-0.477 ms)
+        fork = os.environ.get("TGFR_FORK", "2")
+        self.fork = not self.ctx.active and fork != "0"
+        self.fork_text = fork == "2"
+        self._side = torch.cuda.Stream(device) if self.fork and torch.cuda.is_available() else None
         # :212 (text_head params would join here; the text side is frozen input)
         # :212 Adam for the head, :219-222 SGD for both classifiers: one launch
         self.optimizer = FusedOptimizer([
@@ -120,10 +135,21 @@ class Train:
         BERT hidden states, class ids) -- then the step runs TextHeading under
         no_grad first (:257, utils/dataset_utils.py:38-46)."""
         args, ctx = self.args, self.ctx
+        text_ev = None
         if len(batch) == 4:
             g, local, hidden, class_ids = batch
-            with torch.no_grad():
-                words, sent = self.text_head(hidden, None)
+            if self._side is not None and self.fork_text:
+                # the frozen TextHeading heads the side stream too (beside IMIM's
+                # forward); the word<->region branch waits for its event
+                main = torch.cuda.current_stream()
+                self._side.wait_stream(main)
+                with torch.cuda.stream(self._side), torch.no_grad():
+                    words, sent = self.text_head(hidden, None)
+                text_ev = torch.cuda.Event()
+                text_ev.record(self._side)
+            else:
+                with torch.no_grad():
+                    words, sent = self.text_head(hidden, None)
         else:
             g, local, words, sent, class_ids = batch
         b = g.shape[0]
@@ -133,19 +159,33 @@ class Train:
         words_g, sent_g, cls_g = self._gather_text(words, sent, class_ids)
         labels = self._labels(ctx.n_global, g.device)
 
-        img_features, words_features = self.image_head(g, local)   # :265
         self.optimizer.zero_grad(set_to_none=True)
+        wi, lc = float(args.lambda_id), float(args.lambda_clip)
+        if self._side is not None:
+            # (the reference's :265 forward, split: g' on the side stream)
+            main, side = torch.cuda.current_stream(), self._side
+            if text_ev is None:
+                side.wait_stream(main)
+            with torch.cuda.stream(side):
+                img_features = self.image_head.global_features(g)
+                s0, s1, cl = sent_global_loss(img_features, sent_g, labels, cls_g, b, args)
+                tid, iid = self._identity(sent, img_features, class_ids, ctx)
+                torch.autograd.backward((s0, s1, cl, tid, iid),
+                                        self._weights((1.0, 1.0, lc, wi, wi), g.device))
+            words_features = self.image_head.imim(local)
+            if text_ev is not None:
+                main.wait_event(text_ev)
+            w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
+            torch.autograd.backward((w0, w1), self._weights((1.0, 1.0), g.device))
+            main.wait_stream(side)
+            return self._finish(w0, w1, s0, s1, cl, tid, iid, lc, wi, None)
+        img_features, words_features = self.image_head(g, local)   # :265
 
         # total = damsm + lambda_clip * cl + lambda_id * (tid + iid) (:279,
         # :316-323) is linear in the terms, so each term's gradient is its
         # constant weight: every branch runs its backward right after its own
-        # forward (no loss-mix backward launch, no join).  One stream: on
-        # MI355X the step replays faster as a linear graph than with the
-        # branches forked onto side streams (0.665 vs 0.694 ms at config 2,
-        # round 2) -- the word<->region kernels fill the chip.  Forking only
-        # the frozen TextHeading off the image head's forward loses too
-        # (0.596 vs 0.573 ms, round 3).
-        wi, lc = float(args.lambda_id), float(args.lambda_clip)
+        # forward (no loss-mix backward launch).  With a process group the
+        # step stays one linear stream (its collectives cut the graphs).
         s0, s1, cl = sent_global_loss(img_features, sent_g, labels, cls_g, b, args)  # :276, :310
         # :293-306, both focal losses from the global-batch mean CE
         tid, iid = self._identity(sent, img_features, class_ids, ctx)
@@ -156,7 +196,10 @@ class Train:
         pending = ctx.reduce_grads_async(self.cls_params)
         w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
         torch.autograd.backward((w0, w1), self._weights((1.0, 1.0), g.device))
-        # the logged terms (and the objective) in one launch
+        return self._finish(w0, w1, s0, s1, cl, tid, iid, lc, wi, pending)
+
+    def _report(self, w0, w1, s0, s1, cl, tid, iid, lc, wi):
+        """The logged terms (and the objective) in one launch."""
         with torch.no_grad():
             _, report = K.loss_mix(
                 (w0, w1, s0, s1, cl, tid, iid),
@@ -164,10 +207,15 @@ class Train:
                  (1, 1, 1, 1, 0, 0, 0),                               # damsm
                  (0, 0, 0, 0, 1, 0, 0),                               # clip
                  (0, 0, 0, 0, 0, wi, wi)])                            # ident
+        return {"damsm": report[0], "clip": report[1], "ident": report[2]}
+
+    def _finish(self, w0, w1, s0, s1, cl, tid, iid, lc, wi, pending):
+        ctx = self.ctx
+        out = self._report(w0, w1, s0, s1, cl, tid, iid, lc, wi)
         ctx.wait_grads(pending)
         ctx.reduce_grads(self.head_params)
         self.optimizer.step()
-        return {"damsm": report[0], "clip": report[1], "ident": report[2]}
+        return out
 
     def _gather_text(self, words, sent, class_ids):
         """(words, sent, class ids) of the global batch in one all-gather.

@@ -343,7 +343,10 @@ def main():
                                 "frozen-backbone outputs"),
                    "global_batch": args.batch * n, "seq_len": args.words,
                    "words_per_caption": n_words, "parallelism": f"dp{n}",
-                   "launch": "hip-graph" if use_graph else "eager"},
+                   "launch": "hip-graph" if use_graph else "eager",
+                   # one process: TextHeading and the g' branch on a side stream
+                   # beside IMIM and the word<->region branch (train.Train.step)
+                   "streams": 2 if getattr(trainer, "_side", None) is not None else 1},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "eager_entry_ms": {k: round(v[1], 4) for k, v in sorted(prof.items())},

@@ -826,7 +826,8 @@ def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf
     kept in bf16 -- the values the bf16 GEMMs read from the fp32 map anyway.
     fold3 (three-part weight only): a callable (wp, bp, rows, c, g, beta, wf,
     bf) that launches the fold instead of tgfr_bn_fold3 (ImimFused folds it
-    into IMIM's one weight-preparation launch)."""
+    into IMIM's one weight-preparation launch; on an auxiliary stream beside
+    the BN statistics it measured slower, 0.471 vs 0.457 ms per step)."""
     n, c, h, w_ = x.shape
     hw = h * w_
     o = sum(t.shape[0] for t in weight) if isinstance(weight, tuple) else weight.shape[0]

@@ -38,6 +38,28 @@ def test_graph_replay_matches_eager(gpu, precision):
         torch.testing.assert_close(p, pe[n], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("fork", ["1", "2"])
+def test_forked_step_matches_linear(gpu, monkeypatch, fork):
+    """The forked single-process step (the g' branch, and with TGFR_FORK=2
+    TextHeading, on a side stream) runs the same kernels on the same inputs
+    as the linear step: losses and parameters after three steps agree to the
+    atomics-order noise of the split reductions."""
+    batch = _batch(gpu)
+    monkeypatch.setenv("TGFR_FORK", "0")
+    lin = _build(gpu, "bf16")
+    monkeypatch.setenv("TGFR_FORK", fork)
+    frk = _build(gpu, "bf16")
+    assert lin._side is None and frk._side is not None
+    outs_l = [lin.step(batch) for _ in range(3)]
+    outs_f = [frk.step(batch) for _ in range(3)]
+    torch.cuda.synchronize()
+    for k in outs_l[-1]:
+        torch.testing.assert_close(outs_f[-1][k], outs_l[-1][k], rtol=1e-5, atol=1e-5)
+    pl = dict(lin.image_head.named_parameters())
+    for n, p in frk.image_head.named_parameters():
+        torch.testing.assert_close(p, pl[n], rtol=1e-5, atol=1e-6)
+
+
 def test_fusion_step(gpu):
     tr = _build(gpu, cls="Fusion", b=8)
     batch = _batch(gpu, b=8)

@@ -14,6 +14,8 @@ R=${R:-r4x}
 O=gpurun_out/$R
 FIRST=${FIRST:-tests/test_gpu_modules.py}
 mkdir -p $O
+timeout -k 10 180 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 8
+echo smoke ok
 timeout -k 10 300 python3 -u -m pytest $FIRST -q -x --timeout 120 --timeout-method thread > $O/first.log 2>&1
 rc=$?; echo "first rc=$rc"; [ $rc -eq 0 ] || exit $rc
 if [ "${LAB:-0}" = 1 ]; then     # A/B of the lab variants in tools/lab/build

@@ -47,15 +47,17 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(
   float s = 0.f, m2 = 0.f, mean;
   if (cnt <= 256 * BN_REG) {
     // the channel's N x HW values, flattened over all 256 threads, loaded once
-    // with every load in flight (one HBM round trip), both moments from registers
+    // with every load in flight (one HBM round trip; clamped indices, so no
+    // branch -- and no wait -- per load), both moments from registers
+    const int last = (int)cnt - 1;
     float v[BN_REG];
 #pragma unroll
     for (int u = 0; u < BN_REG; ++u) {
-      const int e = tid + 256 * u, n = e / HW, hw = e - n * HW;
-      v[u] = e < cnt ? xc[n * sn + hw] : 0.f;
+      const int e = min(tid + 256 * u, last), n = e / HW, hw = e - n * HW;
+      v[u] = xc[n * sn + hw];
     }
 #pragma unroll
-    for (int u = 0; u < BN_REG; ++u) s += v[u];
+    for (int u = 0; u < BN_REG; ++u) s += tid + 256 * u <= last ? v[u] : 0.f;
     s = wave_sum(s);
     if (lane == 0) red[wid] = s;
     __syncthreads();
@@ -113,22 +115,28 @@ __global__ __launch_bounds__(256) void bn_norm_cl_kernel(const float* __restrict
   const int c0 = blockIdx.x * 64, n = blockIdx.y, tid = threadIdx.x;
   const int cn = min(64, C - c0), ld = HW + 1;
   const float* xs = x + ((long long)n * C + c0) * HW;
-  // loads in batches of 16 per thread, all in flight before their LDS stores
-  for (int i0 = 0; i0 < cn * HW; i0 += 256 * 16) {
+  // loads in batches of 16 per thread, all in flight before their LDS stores;
+  // past the end a thread repeats the last element (clamped index: the same
+  // value to the same LDS word), so there is no branch -- and no wait -- per load
+  const int last = cn * HW - 1;
+  for (int i0 = 0; i0 <= last; i0 += 256 * 16) {
     float v[16];
+    int cc[16], hw[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
-      const int i = i0 + 256 * u + tid;
-      v[u] = i < cn * HW ? xs[i] : 0.f;
+      const int i = min(i0 + 256 * u + tid, last);
+      cc[u] = i / HW;
+      hw[u] = i - cc[u] * HW;
+      v[u] = xs[i];
     }
+    float m[16], r[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
-      const int i = i0 + 256 * u + tid;
-      if (i < cn * HW) {
-        const int cc = i / HW, hw = i % HW;
-        tile[cc * ld + hw] = (v[u] - mean[c0 + cc]) * rstd[c0 + cc];
-      }
+      m[u] = mean[c0 + cc[u]];
+      r[u] = rstd[c0 + cc[u]];
     }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) tile[cc[u] * ld + hw[u]] = (v[u] - m[u]) * r[u];
   }
   __syncthreads();
   if constexpr (OBF) {

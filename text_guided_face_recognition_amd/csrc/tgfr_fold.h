@@ -26,18 +26,34 @@ struct Parts {
   }
 };
 
-// Row o of the folded weight and its bias, one wave.
+// Row o of the folded weight and its bias, one wave.  The row's loads go out
+// in batches of 8 per lane before any store: one memory round trip per 512
+// columns, not one per 64.  Indices are clamped, not branched on (a branch per
+// access serialises them): past the end a lane loads and stores column C - 1
+// again -- the same value to the same word.
 __device__ __forceinline__ void bn_fold_row(const Parts& P, int o, int C,
                                             const float* __restrict__ gamma,
                                             const float* __restrict__ beta,
                                             float* __restrict__ Wf, float* __restrict__ bf,
                                             int lane) {
+  constexpr int U = 8;
   const float* wr = P.row(o, C);
   float acc = 0.f;
-  for (int c = lane; c < C; c += WAVE) {
-    const float w = wr[c];
-    Wf[(long long)o * C + c] = w * gamma[c];
-    acc += w * beta[c];
+  for (int c0 = 0; c0 < C; c0 += U * WAVE) {
+    float w[U], g[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = min(c0 + u * WAVE + lane, C - 1);
+      w[u] = wr[c];
+      g[u] = gamma[c];
+      b[u] = beta[c];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + u * WAVE + lane;
+      Wf[(long long)o * C + min(c, C - 1)] = w[u] * g[u];
+      acc += c < C ? w[u] * b[u] : 0.f;
+    }
   }
   acc = wave_sum(acc);
   if (lane == 0) bf[o] = P.bias(o) + acc;

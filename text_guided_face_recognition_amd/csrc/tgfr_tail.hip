@@ -102,11 +102,17 @@ __device__ __forceinline__ const uint16_t* frag_ptr(const uint16_t* pk, int off,
   return pk + off + ((rt * (K / 16) + s) * 64 + lane) * 8;
 }
 
-// element e of the fragment-order pack
-__device__ __forceinline__ void pack_elem(const float* __restrict__ W1,
+constexpr int PACK_UNITS = PACK_ELEMS / 8;    // one lane fragment (8 bf16) per thread
+
+// fragment u (elements 8u .. 8u + 7) of the fragment-order pack: M[r][k .. k + 7]
+// of one lane, M = W or W^T.  All 8 loads are issued before the conversion
+// (two float4 loads of a W row, or 8 column loads that are coalesced across
+// the lanes' consecutive r), then one 16-byte store.
+__device__ __forceinline__ void pack_frag(const float* __restrict__ W1,
                                           const float* __restrict__ W2,
                                           const float* __restrict__ Wp, uint16_t* __restrict__ pk,
-                                          int e) {
+                                          int u) {
+  const int e = 8 * u;
   const float* W;
   int off, K, ld, tr;
   if (e < OFF_W2) { W = W1; off = OFF_W1; K = TC; ld = TC; tr = 0; }
@@ -115,10 +121,24 @@ __device__ __forceinline__ void pack_elem(const float* __restrict__ W1,
   else if (e < OFF_W2T) { W = W1; off = OFF_W1T; K = TH; ld = TC; tr = 1; }
   else if (e < OFF_WPT) { W = W2; off = OFF_W2T; K = TC; ld = TH; tr = 1; }
   else { W = Wp; off = OFF_WPT; K = TD; ld = TC; tr = 1; }
-  const int f = e - off, j = f & 7, lane = (f >> 3) & 63, piece = f >> 9;
+  const int f = e - off, lane = (f >> 3) & 63, piece = f >> 9;
   const int s = piece % (K / 16), rt = piece / (K / 16);
-  const int r = 32 * rt + (lane & 31), k = 16 * s + 8 * (lane >> 5) + j;   // M[r][k]
-  pk[e] = bf_bits(tr ? W[k * ld + r] : W[r * ld + k]);
+  const int r = 32 * rt + (lane & 31), k = 16 * s + 8 * (lane >> 5);   // M[r][k ..]
+  float v[8];
+  if (!tr) {
+    const float4 a = *(const float4*)(W + r * ld + k), b = *(const float4*)(W + r * ld + k + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = W[(k + j) * ld + r];
+  }
+  uint4 o;
+  o.x = bf_bits(v[0]) | ((uint32_t)bf_bits(v[1]) << 16);
+  o.y = bf_bits(v[2]) | ((uint32_t)bf_bits(v[3]) << 16);
+  o.z = bf_bits(v[4]) | ((uint32_t)bf_bits(v[5]) << 16);
+  o.w = bf_bits(v[6]) | ((uint32_t)bf_bits(v[7]) << 16);
+  *(uint4*)(pk + e) = o;
 }
 
 // (aff != NULL: also the IMIM LayerNorm's affine maps, stored [C][H W] by the
@@ -132,15 +152,14 @@ __global__ __launch_bounds__(256) void tail_pack_kernel(const float* __restrict_
                                                         const float* __restrict__ lnb, int hw,
                                                         float* __restrict__ aff) {
   const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= PACK_ELEMS) {
-    const int f = e - PACK_ELEMS, n = hw * TC;
+  if (e >= PACK_UNITS) {
+    const int f = e - PACK_UNITS, n = hw * TC;
     if (!aff || f >= 2 * n) return;
     const int j = f / n, r = f % n, p = r / TC, c = r % TC;
     aff[f] = (j ? lnb : lnw)[(long long)c * hw + p];
     return;
   }
-  // segment: (source, source row length, transposed?, K of M, offset)
-  pack_elem(W1, W2, Wp, pk, e);
+  pack_frag(W1, W2, Wp, pk, e);
 }
 
 // IMIM's whole per-step weight preparation in one launch: blocks [0, nf)
@@ -165,14 +184,14 @@ __global__ __launch_bounds__(256) void imim_pack_kernel(Parts P, int O, int C,
     return;
   }
   const int e = (blockIdx.x - nf) * 256 + threadIdx.x;
-  if (e >= PACK_ELEMS) {
-    const int f = e - PACK_ELEMS, n = hw * TC;
+  if (e >= PACK_UNITS) {
+    const int f = e - PACK_UNITS, n = hw * TC;
     if (f >= 2 * n) return;
     const int j = f / n, r = f % n, p = r / TC, c = r % TC;
     aff[f] = (j ? lnb : lnw)[(long long)c * hw + p];
     return;
   }
-  pack_elem(W1, W2, Wp, pk, e);
+  pack_frag(W1, W2, Wp, pk, e);
 }
 
 // ------------------------------------------------------------ forward ---
@@ -970,7 +989,7 @@ int tgfr_tail_pack_elems(void) { return PACK_ELEMS; }
 int tgfr_tail_pack(const float* W1, const float* W2, const float* Wp, uint16_t* pk,
                    void* stream) {
   if (!W1 || !W2 || !Wp || !pk) return 1001;
-  hipLaunchKernelGGL(tail_pack_kernel, dim3((PACK_ELEMS + 255) / 256), dim3(256), 0,
+  hipLaunchKernelGGL(tail_pack_kernel, dim3((PACK_UNITS + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, W1, W2, Wp, pk, nullptr, nullptr, 0, nullptr);
   return (int)hipGetLastError();
 }
@@ -1044,7 +1063,7 @@ int tgfr_tail_pack_ln(const float* W1, const float* W2, const float* Wp, const f
                       const float* lnb, int rows, int hw, uint16_t* pk, float* ws, void* stream) {
   if (!W1 || !W2 || !Wp || !pk || !lnw || !lnb || !ws || !ln_tail_ok(rows, hw)) return 1001;
   const LnTailWs o = ln_tail_ws(rows, hw);
-  const long long n = PACK_ELEMS + 2 * o.E;
+  const long long n = PACK_UNITS + 2 * o.E;
   hipLaunchKernelGGL(tail_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, W1, W2, Wp, pk, lnw, lnb, hw, ws + o.aff);
   return (int)hipGetLastError();
@@ -1062,7 +1081,7 @@ int tgfr_imim_pack(const float* const* Wqkv, const float* const* bqkv, int rows_
                 rows_qkv};
   const int O = 3 * rows_qkv, nf = (O + 3) / 4;
   const LnTailWs o = ln_tail_ws(rows, hw);
-  const long long n = PACK_ELEMS + 2 * o.E;
+  const long long n = PACK_UNITS + 2 * o.E;
   hipLaunchKernelGGL(imim_pack_kernel, dim3((unsigned)(nf + (n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, P, O, C, gamma, beta, Wf, bf, nf, W1, W2, Wp, pk, lnw,
                      lnb, hw, ws + o.aff);

@@ -134,22 +134,13 @@ class Train:
         """batch: (global, local, words, sent, class ids), or (global, local,
         BERT hidden states, class ids) -- then the step runs TextHeading under
         no_grad first (:257, utils/dataset_utils.py:38-46)."""
+        if self._side is not None:
+            return self._step_forked(batch)
         args, ctx = self.args, self.ctx
-        text_ev = None
         if len(batch) == 4:
             g, local, hidden, class_ids = batch
-            if self._side is not None and self.fork_text:
-                # the frozen TextHeading heads the side stream too (beside IMIM's
-                # forward); the word<->region branch waits for its event
-                main = torch.cuda.current_stream()
-                self._side.wait_stream(main)
-                with torch.cuda.stream(self._side), torch.no_grad():
-                    words, sent = self.text_head(hidden, None)
-                text_ev = torch.cuda.Event()
-                text_ev.record(self._side)
-            else:
-                with torch.no_grad():
-                    words, sent = self.text_head(hidden, None)
+            with torch.no_grad():
+                words, sent = self.text_head(hidden, None)
         else:
             g, local, words, sent, class_ids = batch
         b = g.shape[0]
@@ -161,24 +152,6 @@ class Train:
 
         self.optimizer.zero_grad(set_to_none=True)
         wi, lc = float(args.lambda_id), float(args.lambda_clip)
-        if self._side is not None:
-            # (the reference's :265 forward, split: g' on the side stream)
-            main, side = torch.cuda.current_stream(), self._side
-            if text_ev is None:
-                side.wait_stream(main)
-            with torch.cuda.stream(side):
-                img_features = self.image_head.global_features(g)
-                s0, s1, cl = sent_global_loss(img_features, sent_g, labels, cls_g, b, args)
-                tid, iid = self._identity(sent, img_features, class_ids, ctx)
-                torch.autograd.backward((s0, s1, cl, tid, iid),
-                                        self._weights((1.0, 1.0, lc, wi, wi), g.device))
-            words_features = self.image_head.imim(local)
-            if text_ev is not None:
-                main.wait_event(text_ev)
-            w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
-            torch.autograd.backward((w0, w1), self._weights((1.0, 1.0), g.device))
-            main.wait_stream(side)
-            return self._finish(w0, w1, s0, s1, cl, tid, iid, lc, wi, None)
         img_features, words_features = self.image_head(g, local)   # :265
 
         # total = damsm + lambda_clip * cl + lambda_id * (tid + iid) (:279,
@@ -197,6 +170,60 @@ class Train:
         w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
         torch.autograd.backward((w0, w1), self._weights((1.0, 1.0), g.device))
         return self._finish(w0, w1, s0, s1, cl, tid, iid, lc, wi, pending)
+
+    def _step_forked(self, batch):
+        """One process: the reference's :265 forward split over two streams.
+        IMIM and the word<->region branch on the current (main) stream; the
+        frozen TextHeading (TGFR_FORK=2) and the g' branch (projection head,
+        sentence / global losses, identity heads, their backward) on the side
+        stream, forked at the step's start; the word<->region branch waits for
+        TextHeading's event, the optimiser for the whole side branch.
+
+        Launch order matters under a replayed graph: its nodes are dispatched
+        in capture order, so IMIM's forward is launched first (the main
+        branch is the critical path).  Round 4 at config 2, three interleaved
+        rounds on one box: IMIM first 0.433-0.436 ms per step, the side
+        branch first 0.449-0.460, the g' branch after the word<->region
+        backward 0.442-0.449 (profiles/r04/fork_ab.txt)."""
+        args, ctx = self.args, self.ctx
+        main, side = torch.cuda.current_stream(), self._side
+        start = torch.cuda.Event()
+        start.record(main)
+        words_features = self.image_head.imim(batch[1])
+        side.wait_event(start)
+        text_ev = None
+        if len(batch) == 4:
+            g, local, hidden, class_ids = batch
+            if self.fork_text:
+                with torch.cuda.stream(side), torch.no_grad():
+                    words, sent = self.text_head(hidden, None)
+                text_ev = torch.cuda.Event()
+                text_ev.record(side)
+            else:
+                with torch.no_grad():
+                    words, sent = self.text_head(hidden, None)
+                side.wait_stream(main)       # (after IMIM's forward too)
+        else:
+            g, local, words, sent, class_ids = batch
+        b = g.shape[0]
+        ctx.set_batch(b)
+        args.dist = ctx
+        words_g, sent_g, cls_g = self._gather_text(words, sent, class_ids)
+        labels = self._labels(ctx.n_global, g.device)
+        self.optimizer.zero_grad(set_to_none=True)
+        wi, lc = float(args.lambda_id), float(args.lambda_clip)
+        with torch.cuda.stream(side):
+            img_features = self.image_head.global_features(g)
+            s0, s1, cl = sent_global_loss(img_features, sent_g, labels, cls_g, b, args)
+            tid, iid = self._identity(sent, img_features, class_ids, ctx)
+            torch.autograd.backward((s0, s1, cl, tid, iid),
+                                    self._weights((1.0, 1.0, lc, wi, wi), g.device))
+        if text_ev is not None:
+            main.wait_event(text_ev)
+        w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
+        torch.autograd.backward((w0, w1), self._weights((1.0, 1.0), g.device))
+        main.wait_stream(side)
+        return self._finish(w0, w1, s0, s1, cl, tid, iid, lc, wi, None)
 
     def _report(self, w0, w1, s0, s1, cl, tid, iid, lc, wi):
         """The logged terms (and the objective) in one launch."""

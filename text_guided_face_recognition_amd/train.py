@@ -184,7 +184,8 @@ class Train:
         branch is the critical path).  Round 4 at config 2, three interleaved
         rounds on one box: IMIM first 0.433-0.436 ms per step, the side
         branch first 0.449-0.460, the g' branch after the word<->region
-        backward 0.442-0.449 (profiles/r04/fork_ab.txt)."""
+        backward 0.442-0.449, between the word<->region forward and backward
+        0.444-0.453 (against 0.433-0.446) (profiles/r04/fork_ab.txt)."""
         args, ctx = self.args, self.ctx
         main, side = torch.cuda.current_stream(), self._side
         start = torch.cuda.Event()

@@ -37,6 +37,33 @@ def _setup(dev, cfg, seed=0):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", ["stage1", "stage2"])
+def test_group_subsets_match_one_step(gpu, cfg):
+    """step(groups=[SGD group]) on a second stream, then step(groups=[Adam
+    group]) on the current one (the forked trainer step's split) updates every
+    parameter exactly as one full step, and counts one step."""
+    mine, ref, grads = _setup(gpu, cfg)
+    opt = FusedOptimizer(_groups(mine, True, cfg))
+    full = FusedOptimizer(_groups(ref, True, cfg))
+    sgd_i = [i for i, g in enumerate(opt._all_groups) if g["kind"] != 0][0]
+    adam_i = 1 - sgd_i
+    side = torch.cuda.Stream()
+    for gs in grads:
+        for p, q, g in zip(mine, ref, gs):
+            p.grad = g.to(gpu)
+            q.grad = g.to(gpu)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            opt.step(groups=[sgd_i])
+        opt.step(groups=[adam_i])
+        torch.cuda.current_stream().wait_stream(side)
+        full.step()
+        for p, q in zip(mine, ref):
+            assert torch.equal(p, q)
+    assert opt.step_count == len(grads)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["stage1", "stage2"])
 def test_fused_matches_torch(gpu, cfg):
     mine, ref, grads = _setup(gpu, cfg)
     opt = FusedOptimizer(_groups(mine, True, cfg))

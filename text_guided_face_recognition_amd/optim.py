@@ -171,11 +171,18 @@ class FusedOptimizer:
                 p.grad.zero_()
 
     @torch.no_grad()
-    def step(self):
-        """Update every parameter that has a gradient (one launch)."""
+    def step(self, groups=None):
+        """Update every parameter that has a gradient (one launch).  groups: a
+        subset of the caller's group indices to update in this launch (the
+        rest wait for another call); a subset without an Adam group does not
+        advance the step count (its launch counts on a private counter, so
+        two subset launches may run concurrently on two streams)."""
         n = 0
-        segs = self._segs_c
+        segs = self._segs_c if groups is None else (_Seg * len(self.params))()
+        only = None if groups is None else {self._index[i] for i in groups} - {None}
         for gi, g in enumerate(self.groups):
+            if only is not None and gi not in only:
+                continue
             for p in g["params"]:
                 if p.grad is None:
                     continue
@@ -193,7 +200,12 @@ class FusedOptimizer:
                 n += 1
         if n == 0:
             return
+        counters = self.counters
+        if only is not None and all(self.groups[gi]["kind"] != ADAM for gi in only):
+            counters = self.__dict__.get("_aux_counters")
+            if counters is None:
+                counters = self._aux_counters = torch.zeros_like(self.counters)
         _hip.call("tgfr_optim_step", C.addressof(segs), n, C.addressof(self._groups_c),
-                  len(self.groups), _hip.ptr(self.lr_scale), _hip.ptr(self.counters),
+                  len(self.groups), _hip.ptr(self.lr_scale), _hip.ptr(counters),
                   _hip.stream())
 

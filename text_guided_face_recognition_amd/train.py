@@ -116,9 +116,9 @@ class Train:
         # latency chains that leave most of the chip idle
         # (TGFR_FORK: 0 = one linear stream, 1 = the g' branch forked, 2 = the
         # frozen TextHeading heading that side stream too; round 4 at config 2:
-        # 0.547 / 0.482 / 0.460 ms per step.  Updating the side branch's
-        # parameters on the side stream too -- a partial optimiser step --
-        # and the logged-loss mix there measured slower: 0.469-0.477 ms)
+        # 0.547 / 0.482 / 0.460 ms per step; the classifiers' SGD step on the
+        # side stream as well, _step_forked.  The logged-loss mix there costs
+        # a cross-stream edge and measured slower: 0.50 ms)
         fork = os.environ.get("TGFR_FORK", "2")
         self.fork = not self.ctx.active and fork != "0"
         self.fork_text = fork == "2"
@@ -219,12 +219,16 @@ class Train:
             tid, iid = self._identity(sent, img_features, class_ids, ctx)
             torch.autograd.backward((s0, s1, cl, tid, iid),
                                     self._weights((1.0, 1.0, lc, wi, wi), g.device))
+            # the classifiers' gradients are final: their SGD update (group 1,
+            # most of the optimiser's bytes) runs here, beside the
+            # word<->region branch (0.434-0.437 -> 0.429-0.430 ms per step)
+            self.optimizer.step(groups=[1])
         if text_ev is not None:
             main.wait_event(text_ev)
         w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
         torch.autograd.backward((w0, w1), self._weights((1.0, 1.0), g.device))
         main.wait_stream(side)
-        return self._finish(w0, w1, s0, s1, cl, tid, iid, lc, wi, None)
+        return self._finish(w0, w1, s0, s1, cl, tid, iid, lc, wi, None, groups=[0])
 
     def _report(self, w0, w1, s0, s1, cl, tid, iid, lc, wi):
         """The logged terms (and the objective) in one launch."""
@@ -237,12 +241,12 @@ class Train:
                  (0, 0, 0, 0, 0, wi, wi)])                            # ident
         return {"damsm": report[0], "clip": report[1], "ident": report[2]}
 
-    def _finish(self, w0, w1, s0, s1, cl, tid, iid, lc, wi, pending):
+    def _finish(self, w0, w1, s0, s1, cl, tid, iid, lc, wi, pending, groups=None):
         ctx = self.ctx
         out = self._report(w0, w1, s0, s1, cl, tid, iid, lc, wi)
         ctx.wait_grads(pending)
         ctx.reduce_grads(self.head_params)
-        self.optimizer.step()
+        self.optimizer.step(groups)
         return out
 
     def _gather_text(self, words, sent, class_ids):

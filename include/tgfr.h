@@ -100,6 +100,18 @@ int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const float* Rnorm, 
                     int B_img, int B_cap, float gamma1, float gamma2, float gamma3, float eps,
                     const float* dlogits, int ld, int bounded, int t_pad, float* tok_ws,
                     void* stream);
+/* tgfr_wr_bwd_tok with the contrastive CE's gradient formed in the same
+ * launch instead of read from dlogits (tgfr_ce_grad's formula: logits [B_img]
+ * [ld] from tgfr_wr_fwd, row_lse / col_lse from tgfr_ce_stats, row_offset,
+ * inv_n = 1 / n_global, upstream gradients g0 / g1 (device scalars, nullable:
+ * 1) weighted by w0 / w1 (0: that loss has no gradient)); kernels.WordRegionCE,
+ * one launch fewer per step. */
+int tgfr_wr_bwd_tok_ce(const float* stats, const float* Wnorm, const float* Rnorm,
+                       const int* lens, int B_img, int B_cap, float gamma1, float gamma2,
+                       float gamma3, float eps, const float* logits, int ld, int row_offset,
+                       float inv_n, const float* row_lse, const float* col_lse, const float* g0,
+                       const float* g1, float w0, float w1, int bounded, int t_pad,
+                       float* tok_ws, void* stream);
 int tgfr_wr_bwd_ws(int B_img, int B_cap, int bounded, int t_pad, int mode, long long* floats);
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, int B_img, int B_cap, float gamma1, const float* tok_ws,

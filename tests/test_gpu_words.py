@@ -452,3 +452,32 @@ def test_words_seeded_full_shape_vs_reference(gpu, tag, mode, ltol, gtol):
     assert abs(l0.item() - float(g["loss0"])) < ltol and abs(l1.item() - float(g["loss1"])) < ltol
     assert (got.argmax(1) == ref.argmax(1)).all() and (got.argmax(0) == ref.argmax(0)).all()
     assert gerr < gtol, gerr
+
+
+@pytest.mark.parametrize("mode,b,nw", [("bf16", 64, 30), ("bf16", 9, 22), ("fp32", 12, 30),
+                                       ("fp16", 16, 62)])
+def test_word_region_ce_node_matches_two_nodes(gpu, mode, b, nw):
+    """WordRegionCE (logits + both CEs as one node, the CE gradient formed in
+    the token-table launch) against WordRegionLogits -> ContrastiveCE on the
+    same inputs: identical losses; region gradients equal up to the CE
+    gradient's last-bit rounding (the same formula compiled in another
+    kernel), which in the bf16 / fp16 modes can flip the rounding of a few
+    operand fragments (measured: 0 at B = 64, 1.3e-4 of the largest gradient
+    at B = 9, T = 22, bf16)."""
+    K = _kernels()
+    torch.manual_seed(b + nw)
+    r0 = _unit(torch.randn(b, 14, 14, 256, device=gpu)).permute(0, 3, 1, 2)
+    w = _unit(torch.randn(b, nw, 256, device=gpu))
+    lens = torch.full((b,), nw, dtype=torch.int32, device=gpu)
+    weights = (torch.tensor(1.0, device=gpu), torch.tensor(0.5, device=gpu))
+    r1 = r0.clone().requires_grad_()
+    lg = K.word_region_logits(r1, w, lens, 4.0, 5.0, 10.0, mode=mode, bounded=True)
+    a0, a1 = K.contrastive_ce(lg)
+    torch.autograd.backward((a0, a1), weights)
+    r2 = r0.clone().requires_grad_()
+    c0, c1 = K.word_region_ce(r2, w, lens, 4.0, 5.0, 10.0, mode=mode, bounded=True)
+    torch.autograd.backward((c0, c1), weights)
+    torch.cuda.synchronize()
+    assert torch.equal(c0, a0) and torch.equal(c1, a1)
+    err = ((r2.grad - r1.grad).abs().max() / r1.grad.abs().max()).item()
+    assert err < (1e-5 if mode == "fp32" else 1e-3), err

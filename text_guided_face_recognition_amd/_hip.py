@@ -33,6 +33,8 @@ SIGNATURES = {
     "tgfr_prep_rows_f16": [P, L, L, L, I, I, I, I, P, F, P, P, P],
     "tgfr_wr_fwd": [P, P, P, P, P, P, P, I, I, I, F, F, F, F, P, I, P, P, P, P, I, I, I, I, P],
     "tgfr_wr_bwd_tok": [P, P, P, P, I, I, F, F, F, F, P, I, I, I, P, P],
+    "tgfr_wr_bwd_tok_ce": [P, P, P, P, I, I, F, F, F, F, P, I, I, F, P, P, P, P, F, F, I, I, P,
+                           P],
     "tgfr_wr_bwd_ws": [I, I, I, I, I, P],
     "tgfr_wr_bwd": [P, P, P, P, I, I, F, P, P, P, P, L, L, L, P, I, I, I, P],
     "tgfr_wr_lds_bytes": [I],

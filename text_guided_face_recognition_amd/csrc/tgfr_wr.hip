@@ -1278,6 +1278,27 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
 // a caption's table.
 // TP = token stride (32, or 64 for the two-tile kernels: then every lane of
 // the wave is a token and the softmax over words sums the whole wave).
+// ce.logits != nullptr: dlogits are not given but formed here from the
+// contrastive CE of the logits (ce_grad_kernel's formula, tgfr_ce.hip), so
+// the word<->region backward needs no separate CE-gradient launch
+struct CeGrad {
+  const float* logits;     // [B_img][ld]
+  const float* row_lse;    // [B_img]
+  const float* col_lse;    // [B_cap]
+  const float* g0;         // upstream gradient of loss0 (nullable: 1)
+  const float* g1;         // of loss1
+  float w0, w1, inv_n;     // w: 0 when that loss has no gradient
+  int row_offset;
+};
+
+__device__ __forceinline__ float ce_dlogit(const CeGrad& ce, int ld, int b, int i) {
+  const float v = ce.logits[(long long)b * ld + i];
+  const float onehot = (i == ce.row_offset + b) ? 1.f : 0.f;
+  const float a0 = (ce.g0 ? *ce.g0 : 1.f) * ce.w0 * ce.inv_n;
+  const float a1 = (ce.g1 ? *ce.g1 : 1.f) * ce.w1 * ce.inv_n;
+  return a0 * (__expf(v - ce.row_lse[b]) - onehot) + a1 * (__expf(v - ce.col_lse[i]) - onehot);
+}
+
 template <int TP>
 __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ stats,
                                                      const float* __restrict__ Wnorm,
@@ -1286,7 +1307,7 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
                                                      const float* __restrict__ dlogits, int ld,
                                                      int B_img, int B_cap, float g1, float g2,
                                                      float g3, float eps, int layout,
-                                                     float* __restrict__ tok) {
+                                                     float* __restrict__ tok, CeGrad ce) {
   const long long pair = (blockIdx.x * 256LL + threadIdx.x) / WAVE;
   if (pair >= (long long)B_img * B_cap) return;
   const int b = pair / B_cap, i = pair % B_cap;
@@ -1311,7 +1332,7 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
   const float tot = TP == 64 ? wave_sum(ex) : half_sum(ex);
   float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (valid) {
-    const float G = dlogits[(long long)b * ld + i] * g3;
+    const float G = (ce.logits ? ce_dlogit(ce, ld, b, i) : dlogits[(long long)b * ld + i]) * g3;
     const float dcos = G * g2 * ex / tot;
     const float u = Wnorm[(long long)i * TP + t];
     const float cn = st.z, n = st.y, cosv = st.w;
@@ -3013,24 +3034,49 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   return (int)hipGetLastError();
 }
 
-int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const float* Rnorm, const int* lens,
-                    int B_img,
-                    int B_cap, float gamma1, float gamma2, float gamma3, float eps,
-                    const float* dlogits, int ld, int bounded, int t_pad, float* tok_ws,
-                    void* stream) {
+}  // extern "C"
+
+static int wr_tok_launch(const float* stats, const float* Wnorm, const float* Rnorm,
+                         const int* lens, int B_img, int B_cap, float gamma1, float gamma2,
+                         float gamma3, float eps, const float* dlogits, int ld, int bounded,
+                         int t_pad, float* tok_ws, const CeGrad& ce, void* stream) {
   if (B_img <= 0 || B_cap <= 0 || ld < B_cap) return 1001;
   const long long pairs = (long long)B_img * B_cap;
   if (t_pad == 64)
     hipLaunchKernelGGL(wr_tok_kernel<64>, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, (const float4*)stats, Wnorm, Rnorm, lens, dlogits, ld,
-                       B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 1 : 0, tok_ws);
+                       B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 1 : 0, tok_ws, ce);
   else if (t_pad == 32)
     hipLaunchKernelGGL(wr_tok_kernel<32>, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, (const float4*)stats, Wnorm, Rnorm, lens, dlogits, ld,
-                       B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 1 : 0, tok_ws);
+                       B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 1 : 0, tok_ws, ce);
   else
     return 1001;
   return (int)hipGetLastError();
+}
+
+extern "C" {
+
+int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const float* Rnorm, const int* lens,
+                    int B_img,
+                    int B_cap, float gamma1, float gamma2, float gamma3, float eps,
+                    const float* dlogits, int ld, int bounded, int t_pad, float* tok_ws,
+                    void* stream) {
+  if (!dlogits) return 1001;
+  return wr_tok_launch(stats, Wnorm, Rnorm, lens, B_img, B_cap, gamma1, gamma2, gamma3, eps,
+                       dlogits, ld, bounded, t_pad, tok_ws, CeGrad{}, stream);
+}
+
+int tgfr_wr_bwd_tok_ce(const float* stats, const float* Wnorm, const float* Rnorm,
+                       const int* lens, int B_img, int B_cap, float gamma1, float gamma2,
+                       float gamma3, float eps, const float* logits, int ld, int row_offset,
+                       float inv_n, const float* row_lse, const float* col_lse, const float* g0,
+                       const float* g1, float w0, float w1, int bounded, int t_pad,
+                       float* tok_ws, void* stream) {
+  if (!logits || !row_lse || !col_lse) return 1001;
+  const CeGrad ce{logits, row_lse, col_lse, g0, g1, w0, w1, inv_n, row_offset};
+  return wr_tok_launch(stats, Wnorm, Rnorm, lens, B_img, B_cap, gamma1, gamma2, gamma3, eps,
+                       nullptr, ld, bounded, t_pad, tok_ws, ce, stream);
 }
 
 int tgfr_wr_bwd_ws(int B_img, int B_cap, int bounded, int t_pad, int mode, long long* floats) {

@@ -90,6 +90,110 @@ def wr_bwd_ws_floats(b_img, b_cap, bounded, t_pad, mode):
     return int(out[0])
 
 
+def _wr_fwd(img_features, words, lens, gamma1, gamma2, gamma3, mode, img_offset=0, att_T=0,
+            bounded=False, uniform=False, eps=1e-8):
+    """WordRegionLogits' forward: (logits, att, tensors for the backward, cfg)."""
+    dev = img_features.device
+    regions = regions_view(img_features.float())
+    b_img, b_cap = regions.shape[0], words.shape[0]
+    t_words = words.shape[1]
+    if t_words > 2 * TPAD:
+        raise ValueError(f"at most {2 * TPAD} words per caption (got {t_words})")
+    # token stride: 32, or 64 for 64-token captions (general kernels only)
+    t_pad = TPAD if t_words <= TPAD else 2 * TPAD
+    lens = lens.to(device=dev, dtype=torch.int32).contiguous()
+    m = _wr_mode(mode)
+    f16 = m == MODES["fp16"]
+    bf16 = m != MODES["fp32"]          # single-operand modes (bf16, fp16)
+    # bounded scores: the bf16 path runs the pipelined kernels both ways;
+    # 64-token captions (bf16 / fp16) the bounded backward (log2(e)-scaled
+    # words, no running max)
+    fast = bool(bounded) and (
+        (m == MODES["bf16"] and not att_T and t_pad == TPAD) or
+        (m != MODES["fp32"] and t_pad == 2 * TPAD))
+    pre = attached_rows(img_features, f16) if bf16 else None
+    own_rows = pre is not None
+    if pre is not None:            # written by the IMIM tail kernel
+        (r_hi, r_norm), r_lo = pre, None
+    else:
+        r_hi, r_lo, r_norm = prep_rows(regions, NREG, RPAD, want_norms=bf16, f16=f16)
+    if bf16:
+        # the bf16 / fp16 forward takes log2(e)-scaled words (tgfr.h,
+        # tgfr_wr_fwd), and so does the pipelined backward; the other
+        # backward the plain ones.  (Written by TextHeading when it made
+        # the words; every caption then has t_words valid words.)
+        pre = attached_rows(words, f16, scale=LOG2E) if uniform else None
+        w_attached = pre is not None and pre[0].shape[1] == t_pad
+        if w_attached:
+            w_fwd, w_norm = pre
+        else:
+            if _rows_only(words):
+                raise RuntimeError("words carry only their operand rows "
+                                   "(rows_only_words), which this call cannot use")
+            own_rows = False
+            w_fwd, _, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,
+                                         want_norms=True, scale=LOG2E, f16=f16)
+        # The max-free kernels are exact while the score bound max|W|
+        # max|R| <= WR_BOUND_MAX (csrc/tgfr_wr.hip, bound_shift).  Rows
+        # made by this package's heads are L2-normalised (bound ~1); other
+        # inputs are checked here (one host read, skipped under graph
+        # capture) and past the bound take the exact running-max kernels,
+        # as the reference's softmax never overflows (models/attention.py:28-36)
+        if bounded and not own_rows and not torch.cuda.is_current_stream_capturing():
+            if not float((w_norm.max() * r_norm.max()).item()) <= WR_BOUND_MAX:
+                bounded = fast = False
+        if _rows_only(words) and not fast:
+            raise RuntimeError("words carry only their bounded-kernel operand rows "
+                               "(rows_only_words): this path needs the feature values")
+        w_hi = w_fwd if fast else prep_rows(words.float(), t_words, t_pad, lens=lens,
+                                            f16=f16)[0]
+        w_lo = None
+    else:
+        if _rows_only(words):
+            raise RuntimeError("words carry only their bf16 / fp16 operand rows "
+                               "(rows_only_words): fp32 mode needs the feature values")
+        w_hi, w_lo, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,
+                                       want_norms=True)
+        w_fwd = w_hi
+    logits = torch.empty(b_img, b_cap, dtype=torch.float32, device=dev)
+    stats = torch.empty(b_img, b_cap, t_pad, 4, dtype=torch.float32, device=dev)
+    # C for the backward: bf16 hi (+lo in fp32 mode), chunk-major [pair][32][t_pad][8]
+    c_hi = torch.empty(b_img, b_cap, 32, t_pad, 8, dtype=torch.int16, device=dev)
+    c_lo = torch.empty_like(c_hi) if m == MODES["fp32"] else None
+    att = torch.zeros(b_img, att_T, NREG, dtype=torch.float32, device=dev) \
+        if att_T else None
+    call("tgfr_wr_fwd", ptr(r_hi), ptr(r_lo), ptr(w_fwd), ptr(w_lo), ptr(w_norm),
+         ptr(r_norm), ptr(lens), b_img, b_cap, img_offset, gamma1, gamma2, gamma3, eps,
+         ptr(logits), b_cap, ptr(stats), ptr(c_hi), ptr(c_lo), ptr(att), att_T,
+         int(bool(bounded) and (t_pad == TPAD or m != MODES["fp32"])), t_pad, m,
+         _hip.stream())
+    saved = (r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo)
+    cfg = (gamma1, gamma2, gamma3, eps, m, img_features.shape, fast, t_pad)
+    return logits, att, saved, cfg
+
+
+def _wr_bwd(saved, cfg, tok_call):
+    """WordRegionLogits' backward: d img_features, with the per-(pair, token)
+    table made by tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, fast,
+    t_pad, tok) (tgfr_wr_bwd_tok from dlogits, or tgfr_wr_bwd_tok_ce)."""
+    r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo = saved
+    gamma1, gamma2, gamma3, eps, m, shape, fast, t_pad = cfg
+    b_img, b_cap = stats.shape[0], stats.shape[1]
+    dev = stats.device
+    ws = torch.empty(wr_bwd_ws_floats(b_img, b_cap, fast, t_pad, m), dtype=torch.float32,
+                     device=dev)
+    tok = torch.empty(b_img, b_cap, t_pad, 8, dtype=torch.float32, device=dev)
+    split = m == MODES["fp32"]
+    tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, fast, t_pad, tok)
+    d_reg = torch.empty(b_img, NREG, D, dtype=torch.float32, device=dev)
+    call("tgfr_wr_bwd", ptr(r_hi), ptr(r_lo) if split else None, ptr(w_hi),
+         ptr(w_lo) if split else None, b_img, b_cap, gamma1, ptr(tok),
+         ptr(c_hi), ptr(c_lo) if split else None, ptr(d_reg), NREG * D, D, 1, ptr(ws),
+         int(fast), t_pad, m, _hip.stream())
+    # same logical shape as img_features, channels-last strides
+    return d_reg.transpose(1, 2).reshape(shape)
+
+
 class WordRegionLogits(torch.autograd.Function):
     """gamma3 * log sum_t exp(gamma2 cos(W_t, C_t)) for all (image, caption).
 
@@ -102,107 +206,68 @@ class WordRegionLogits(torch.autograd.Function):
     @staticmethod
     def forward(ctx, img_features, words, lens, gamma1, gamma2, gamma3, mode,
                 img_offset=0, att_T=0, bounded=False, uniform=False, eps=1e-8):
-        dev = img_features.device
-        regions = regions_view(img_features.float())
-        b_img, b_cap = regions.shape[0], words.shape[0]
-        t_words = words.shape[1]
-        if t_words > 2 * TPAD:
-            raise ValueError(f"at most {2 * TPAD} words per caption (got {t_words})")
-        # token stride: 32, or 64 for 64-token captions (general kernels only)
-        t_pad = TPAD if t_words <= TPAD else 2 * TPAD
-        lens = lens.to(device=dev, dtype=torch.int32).contiguous()
-        m = _wr_mode(mode)
-        f16 = m == MODES["fp16"]
-        bf16 = m != MODES["fp32"]          # single-operand modes (bf16, fp16)
-        # bounded scores: the bf16 path runs the pipelined kernels both ways;
-        # 64-token captions (bf16 / fp16) the bounded backward (log2(e)-scaled
-        # words, no running max)
-        fast = bool(bounded) and (
-            (m == MODES["bf16"] and not att_T and t_pad == TPAD) or
-            (m != MODES["fp32"] and t_pad == 2 * TPAD))
-        pre = attached_rows(img_features, f16) if bf16 else None
-        own_rows = pre is not None
-        if pre is not None:            # written by the IMIM tail kernel
-            (r_hi, r_norm), r_lo = pre, None
-        else:
-            r_hi, r_lo, r_norm = prep_rows(regions, NREG, RPAD, want_norms=bf16, f16=f16)
-        if bf16:
-            # the bf16 / fp16 forward takes log2(e)-scaled words (tgfr.h,
-            # tgfr_wr_fwd), and so does the pipelined backward; the other
-            # backward the plain ones.  (Written by TextHeading when it made
-            # the words; every caption then has t_words valid words.)
-            pre = attached_rows(words, f16, scale=LOG2E) if uniform else None
-            w_attached = pre is not None and pre[0].shape[1] == t_pad
-            if w_attached:
-                w_fwd, w_norm = pre
-            else:
-                if _rows_only(words):
-                    raise RuntimeError("words carry only their operand rows "
-                                       "(rows_only_words), which this call cannot use")
-                own_rows = False
-                w_fwd, _, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,
-                                             want_norms=True, scale=LOG2E, f16=f16)
-            # The max-free kernels are exact while the score bound max|W|
-            # max|R| <= WR_BOUND_MAX (csrc/tgfr_wr.hip, bound_shift).  Rows
-            # made by this package's heads are L2-normalised (bound ~1); other
-            # inputs are checked here (one host read, skipped under graph
-            # capture) and past the bound take the exact running-max kernels,
-            # as the reference's softmax never overflows (models/attention.py:28-36)
-            if bounded and not own_rows and not torch.cuda.is_current_stream_capturing():
-                if not float((w_norm.max() * r_norm.max()).item()) <= WR_BOUND_MAX:
-                    bounded = fast = False
-            if _rows_only(words) and not fast:
-                raise RuntimeError("words carry only their bounded-kernel operand rows "
-                                   "(rows_only_words): this path needs the feature values")
-            w_hi = w_fwd if fast else prep_rows(words.float(), t_words, t_pad, lens=lens,
-                                                f16=f16)[0]
-            w_lo = None
-        else:
-            if _rows_only(words):
-                raise RuntimeError("words carry only their bf16 / fp16 operand rows "
-                                   "(rows_only_words): fp32 mode needs the feature values")
-            w_hi, w_lo, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,
-                                           want_norms=True)
-            w_fwd = w_hi
-        logits = torch.empty(b_img, b_cap, dtype=torch.float32, device=dev)
-        stats = torch.empty(b_img, b_cap, t_pad, 4, dtype=torch.float32, device=dev)
-        # C for the backward: bf16 hi (+lo in fp32 mode), chunk-major [pair][32][t_pad][8]
-        c_hi = torch.empty(b_img, b_cap, 32, t_pad, 8, dtype=torch.int16, device=dev)
-        c_lo = torch.empty_like(c_hi) if m == MODES["fp32"] else None
-        att = torch.zeros(b_img, att_T, NREG, dtype=torch.float32, device=dev) \
-            if att_T else None
-        call("tgfr_wr_fwd", ptr(r_hi), ptr(r_lo), ptr(w_fwd), ptr(w_lo), ptr(w_norm),
-             ptr(r_norm), ptr(lens), b_img, b_cap, img_offset, gamma1, gamma2, gamma3, eps,
-             ptr(logits), b_cap, ptr(stats), ptr(c_hi), ptr(c_lo), ptr(att), att_T,
-             int(bool(bounded) and (t_pad == TPAD or m != MODES["fp32"])), t_pad, m,
-             _hip.stream())
-        ctx.save_for_backward(r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo)
-        ctx.cfg = (gamma1, gamma2, gamma3, eps, m, img_features.shape, fast, t_pad)
+        logits, att, saved, cfg = _wr_fwd(img_features, words, lens, gamma1, gamma2, gamma3,
+                                          mode, img_offset, att_T, bounded, uniform, eps)
+        ctx.save_for_backward(*saved)
+        ctx.cfg = cfg
         ctx.mark_non_differentiable(*([att] if att is not None else []))
         return (logits, att) if att is not None else logits
 
     @staticmethod
     def backward(ctx, dlogits, *unused):
-        r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo = ctx.saved_tensors
-        gamma1, gamma2, gamma3, eps, m, shape, fast, t_pad = ctx.cfg
-        b_img, b_cap = stats.shape[0], stats.shape[1]
-        dev = dlogits.device
+        gamma1, gamma2, gamma3, eps = ctx.cfg[:4]
         dlogits = dlogits.float().contiguous()
-        ws = torch.empty(wr_bwd_ws_floats(b_img, b_cap, fast, t_pad, m), dtype=torch.float32,
-                         device=dev)
-        tok = torch.empty(b_img, b_cap, t_pad, 8, dtype=torch.float32, device=dev)
-        split = m == MODES["fp32"]
-        call("tgfr_wr_bwd_tok", ptr(stats), ptr(w_norm), ptr(r_norm), ptr(lens), b_img, b_cap,
-             gamma1, gamma2, gamma3, eps, ptr(dlogits), b_cap, int(fast), t_pad, ptr(tok),
+
+        def tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, fast, t_pad, tok):
+            call("tgfr_wr_bwd_tok", ptr(stats), ptr(w_norm), ptr(r_norm), ptr(lens), b_img,
+                 b_cap, gamma1, gamma2, gamma3, eps, ptr(dlogits), b_cap, int(fast), t_pad,
+                 ptr(tok), _hip.stream())
+        return (_wr_bwd(ctx.saved_tensors, ctx.cfg, tok_call),) + (None,) * 11
+
+
+class WordRegionCE(torch.autograd.Function):
+    """words_loss's (loss0, loss1) as ONE node when one process holds every
+    caption and no attention maps are asked for: WordRegionLogits then
+    ContrastiveCE (its single-launch statistics), with the CE gradient formed
+    inside the word<->region backward's token-table launch
+    (tgfr_wr_bwd_tok_ce) -- one launch fewer per step than the two nodes."""
+
+    @staticmethod
+    def forward(ctx, img_features, words, lens, gamma1, gamma2, gamma3, mode, bounded, uniform,
+                n_global):
+        logits, _, saved, cfg = _wr_fwd(img_features, words, lens, gamma1, gamma2, gamma3,
+                                        mode, 0, 0, bounded, uniform)
+        n_r, n_c = logits.shape
+        dev = logits.device
+        row_lse = torch.empty(n_r, dtype=torch.float32, device=dev)
+        part = torch.empty(2, n_c, dtype=torch.float32, device=dev)
+        col_lse = torch.empty(n_c, dtype=torch.float32, device=dev)
+        loss = torch.empty(2, dtype=torch.float32, device=dev)
+        inv_n = 1.0 / float(n_global)
+        call("tgfr_ce_stats", ptr(logits), n_c, n_r, n_c, ptr(row_lse), ptr(part[0]),
+             ptr(part[1]), ptr(col_lse), 0, inv_n, ptr(loss), ptr(_hip.counters(dev)),
              _hip.stream())
-        d_reg = torch.empty(b_img, NREG, D, dtype=torch.float32, device=dev)
-        call("tgfr_wr_bwd", ptr(r_hi), ptr(r_lo) if split else None, ptr(w_hi),
-             ptr(w_lo) if split else None, b_img, b_cap, gamma1, ptr(tok),
-             ptr(c_hi), ptr(c_lo) if split else None, ptr(d_reg), NREG * D, D, 1, ptr(ws),
-             int(fast), t_pad, m, _hip.stream())
-        # same logical shape as img_features, channels-last strides
-        d_img = d_reg.transpose(1, 2).reshape(shape)
-        return (d_img,) + (None,) * 11
+        ctx.save_for_backward(*saved, logits, row_lse, col_lse)
+        ctx.cfg = cfg
+        ctx.inv_n = inv_n
+        return loss[0], loss[1]
+
+    @staticmethod
+    def backward(ctx, g0, g1):
+        saved = ctx.saved_tensors
+        logits, row_lse, col_lse = saved[10:]
+        gamma1, gamma2, gamma3, eps = ctx.cfg[:4]
+        w0 = 0.0 if g0 is None else 1.0
+        w1 = 0.0 if g1 is None else 1.0
+        g0 = None if g0 is None else g0.float().contiguous()
+        g1 = None if g1 is None else g1.float().contiguous()
+
+        def tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, fast, t_pad, tok):
+            call("tgfr_wr_bwd_tok_ce", ptr(stats), ptr(w_norm), ptr(r_norm), ptr(lens), b_img,
+                 b_cap, gamma1, gamma2, gamma3, eps, ptr(logits), logits.shape[1], 0,
+                 ctx.inv_n, ptr(row_lse), ptr(col_lse), ptr(g0), ptr(g1), w0, w1, int(fast),
+                 t_pad, ptr(tok), _hip.stream())
+        return (_wr_bwd(saved[:10], ctx.cfg, tok_call),) + (None,) * 9
 
 
 def word_region_logits(img_features, words, lens, gamma1, gamma2, gamma3,
@@ -215,6 +280,15 @@ def word_region_logits(img_features, words, lens, gamma1, gamma2, gamma3,
     return WordRegionLogits.apply(img_features, words, lens, float(gamma1),
                                   float(gamma2), float(gamma3), mode, img_offset, att_T,
                                   bool(bounded), bool(uniform))
+
+
+def word_region_ce(img_features, words, lens, gamma1, gamma2, gamma3, mode="fp32",
+                   bounded=False, uniform=False, n_global=None):
+    """(loss0, loss1) of words_loss for one process holding every caption
+    (WordRegionCE): word_region_logits + contrastive_ce in one node."""
+    n_global = img_features.shape[0] if n_global is None else n_global
+    return WordRegionCE.apply(img_features, words, lens, float(gamma1), float(gamma2),
+                              float(gamma3), mode, bool(bounded), bool(uniform), n_global)
 
 
 # -------------------------------------------------------- func_attention ---

@@ -109,6 +109,15 @@ def words_loss(img_features, words_emb, labels, cap_lens, class_ids, batch_size,
     row_offset, n_global, group = _dist(args)
     smooth = args.TRAIN.SMOOTH
     want_maps = getattr(args, "return_att_maps", True)
+    if labels is not None and not want_maps and group is None and row_offset == 0:
+        # one process, every caption here: logits + both CEs as one node (the
+        # CE gradient formed in the backward's token-table launch)
+        loss0, loss1 = K.word_region_ce(img_features, words, lens, smooth.GAMMA1, smooth.GAMMA2,
+                                        smooth.GAMMA3, mode=_precision(args),
+                                        bounded=args.en_type == "BERT",
+                                        uniform=args.en_type == "BERT",
+                                        n_global=n_global or b_img)
+        return loss0, loss1, []
     # BERT-path features are L2-normalised (TextHeading models/models.py:212,
     # IMIM :403), so the scores are bounded by 1 and the forward needs no
     # running max over the words

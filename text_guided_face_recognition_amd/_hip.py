@@ -133,6 +133,9 @@ SIGNATURES = {
 def lib():
     """The loaded kernel library (raises if it has not been built)."""
     global _lib
+    if _lib is None and os.environ.get("TGFR_LIB"):
+        # a lab build of the library (tools/lab/variants.py), for A/B timing
+        _lib = _bind(C.CDLL(os.environ["TGFR_LIB"], mode=C.RTLD_GLOBAL))
     if _lib is None:
         if _build.stale():
             import sys
@@ -142,15 +145,18 @@ def lib():
             except Exception as e:  # noqa: BLE001
                 raise RuntimeError(f"{LIB} could not be built ({e}); there is no CPU "
                                    "fallback") from e
-        handle = C.CDLL(LIB, mode=C.RTLD_GLOBAL)
-        for name, argtypes in SIGNATURES.items():
-            fn = getattr(handle, name, None)
-            if fn is None:
-                continue
-            fn.argtypes = argtypes
-            fn.restype = I
-        _lib = handle
+        _lib = _bind(C.CDLL(LIB, mode=C.RTLD_GLOBAL))
     return _lib
+
+
+def _bind(handle):
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(handle, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = argtypes
+        fn.restype = I
+    return handle
 
 
 def exported_symbols():

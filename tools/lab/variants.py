@@ -66,27 +66,39 @@ VARIANTS = {
 }
 
 
-def build_variant(name, subs):
+# variants of other sources: name -> (file, substitutions); the timing
+# harness for these is the whole bench step (TGFR_LIB=<lib> bench.py)
+FILE_VARIANTS = {
+    # IMIM weight gradients: 24 row slices (2 workgroups per CU) instead of 12
+    "dw512": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 256, A, wsf, n_wg);",
+                                 "  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg);")]),
+    "dw128": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 256, A, wsf, n_wg);",
+                                 "  dw_plan_n(rows, 4, NS, KS, 128, A, wsf, n_wg);")]),
+}
+
+
+def build_variant(name, subs, fname="tgfr_wr.hip"):
     if subs == "HEAD":          # the committed source, for A/B against the work tree
-        src = subprocess.run(["git", "show", "HEAD:text_guided_face_recognition_amd/csrc/tgfr_wr.hip"],
+        src = subprocess.run(["git", "show", f"HEAD:text_guided_face_recognition_amd/csrc/{fname}"],
                              cwd=ROOT, check=True, capture_output=True, text=True).stdout
         subs = []
     else:
-        src = open(os.path.join(B.CSRC, "tgfr_wr.hip")).read()
+        src = open(os.path.join(B.CSRC, fname)).read()
     for old, new in subs:
         if old not in src:
             raise SystemExit(f"{name}: substitution not found: {old[:60]!r}")
         src = src.replace(old, new)
     os.makedirs(OUT, exist_ok=True)
-    vsrc = os.path.join(OUT, f"tgfr_wr_{name}.hip")
+    stem = fname[:-4]
+    vsrc = os.path.join(OUT, f"{stem}_{name}.hip")
     open(vsrc, "w").write(src)
-    obj = os.path.join(OUT, f"tgfr_wr_{name}.o")
+    obj = os.path.join(OUT, f"{stem}_{name}.o")
     cmd = [B.HIPCC, f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-fPIC", "-fno-gpu-rdc",
            "-Wno-unused-result", "-Wno-unused-value", "-I", B.CSRC,
-           *B.FILE_FLAGS["tgfr_wr.hip"], "-c", vsrc, "-o", obj]
+           *B.FILE_FLAGS.get(fname, []), "-c", vsrc, "-o", obj]
     subprocess.run(cmd, check=True, capture_output=True)
     others = [os.path.join(B.OBJ_DIR, os.path.basename(s).replace(".hip", ".o"))
-              for s in B.sources() if not s.endswith("tgfr_wr.hip")]
+              for s in B.sources() if not s.endswith(fname)]
     lib = os.path.join(OUT, f"lib_{name}.so")
     subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-fno-gpu-rdc",
                     "-o", lib, obj, *others], check=True, capture_output=True)
@@ -95,9 +107,10 @@ def build_variant(name, subs):
 
 def main(names=None):
     B.build()
-    todo = {k: v for k, v in VARIANTS.items() if not names or k in names}
+    todo = [(k, v, "tgfr_wr.hip") for k, v in VARIANTS.items() if not names or k in names]
+    todo += [(k, v[1], v[0]) for k, v in FILE_VARIANTS.items() if names and k in names]
     with ThreadPoolExecutor(4) as ex:
-        for lib in ex.map(lambda kv: build_variant(*kv), todo.items()):
+        for lib in ex.map(lambda a: build_variant(*a), todo):
             print(lib)
 
 

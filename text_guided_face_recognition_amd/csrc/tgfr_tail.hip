@@ -1214,9 +1214,13 @@ int tgfr_tail_dw(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
 // IMIM's two weight-gradient sets in ONE launch (+ one reduce): the tail's
 // dWp, dW2, dW1 (tgfr_tail_dw) and the packed q/k/v projection's dW = dX^T Y,
 // db = colsum(dX) (tgfr_dw_bf16 with bf16 Y: X [rows][Nq], Y [rows][Kq]).
+// Budget 512 workgroups (24 row slices at config 2: two 61-KB workgroups per
+// CU hide each other's staging latency; the larger slab read by the reduce
+// costs less): 0.440-0.450 -> 0.434-0.437 ms per step against 256 (128: 0.46;
+// tools/lab/lib_ab.sh, profiles/r04/fork_ab.txt).
 static void imim_dw_plan(int rows, int Nq, int Kq, DwArgs& A, long long& wsf, int& n_wg) {
   const int NS[4] = {TD, TC, TH, Nq}, KS[4] = {TC, TH, TC, Kq};
-  dw_plan_n(rows, 4, NS, KS, 256, A, wsf, n_wg);
+  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg);
 }
 
 int tgfr_imim_dw_ws(int rows, int Nq, int Kq, long long* floats) {

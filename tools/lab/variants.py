@@ -69,11 +69,12 @@ VARIANTS = {
 # variants of other sources: name -> (file, substitutions); the timing
 # harness for these is the whole bench step (TGFR_LIB=<lib> bench.py)
 FILE_VARIANTS = {
-    # IMIM weight gradients: 24 row slices (2 workgroups per CU) instead of 12
-    "dw512": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 256, A, wsf, n_wg);",
-                                 "  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg);")]),
-    "dw128": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 256, A, wsf, n_wg);",
-                                 "  dw_plan_n(rows, 4, NS, KS, 128, A, wsf, n_wg);")]),
+    # IMIM weight gradients: the workgroup budget of the row-slice split
+    # (512 kept in round 4; 256 and 128 measured slower)
+    "dw768": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg);",
+                                 "  dw_plan_n(rows, 4, NS, KS, 768, A, wsf, n_wg);")]),
+    "dw256": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg);",
+                                 "  dw_plan_n(rows, 4, NS, KS, 256, A, wsf, n_wg);")]),
 }
 
 

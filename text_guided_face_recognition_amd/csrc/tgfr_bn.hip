@@ -102,18 +102,19 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(
   }
 }
 
-// grid (ceil(C / 64), N); 256 threads; LDS [64][HW + 1] floats.  OBF: y is
+// grid (ceil(C / BN_CT), N); 256 threads; LDS [BN_CT][HW + 1] floats.  OBF: y is
 // bf16 (the bf16-mode consumers -- the q/k/v projection GEMM and its weight
 // gradient -- round their xhat operand to bf16 anyway: same values, half the
 // bytes written and read).
+constexpr int BN_CT = 64;   // channels per normalise workgroup
 template <bool OBF>
 __global__ __launch_bounds__(256) void bn_norm_cl_kernel(const float* __restrict__ x, int C,
                                                          int HW, const float* __restrict__ mean,
                                                          const float* __restrict__ rstd,
                                                          void* __restrict__ yv) {
   extern __shared__ float tile[];
-  const int c0 = blockIdx.x * 64, n = blockIdx.y, tid = threadIdx.x;
-  const int cn = min(64, C - c0), ld = HW + 1;
+  const int c0 = blockIdx.x * BN_CT, n = blockIdx.y, tid = threadIdx.x;
+  const int cn = min(BN_CT, C - c0), ld = HW + 1;
   const float* xs = x + ((long long)n * C + c0) * HW;
   // loads in batches of 16 per thread, all in flight before their LDS stores;
   // past the end a thread repeats the last element (clamped index: the same
@@ -268,19 +269,19 @@ int tgfr_bn_bwd_cl(const float* dxh, const float* xhat, const float* rstd, int N
 static int bn_fwd_cl(const float* x, int N, int C, int HW, float eps, float momentum,
                      int training, float* running_mean, float* running_var, long long* nbt,
                      float* mean, float* rstd, void* xhat, bool obf, hipStream_t st) {
-  if (N <= 0 || C <= 0 || HW <= 0 || (64 * (HW + 1) * 4 > 160 * 1024)) return 1001;
+  if (N <= 0 || C <= 0 || HW <= 0 || (BN_CT * (HW + 1) * 4 > 160 * 1024)) return 1001;
   if (!training && (!running_mean || !running_var)) return 1001;
   hipLaunchKernelGGL(bn_stats_kernel, dim3(C), dim3(256), 0, st, x, N, C, HW, eps, momentum,
                      training, running_mean, running_var, nbt, mean, rstd);
-  const int lds = 64 * (HW + 1) * 4;
+  const int lds = BN_CT * (HW + 1) * 4;
   const void* fn = obf ? (const void*)bn_norm_cl_kernel<true> : (const void*)bn_norm_cl_kernel<false>;
   if (lds > 64 * 1024)
     if (const int e = set_max_lds(fn, lds)) return e;
   if (obf)
-    hipLaunchKernelGGL(bn_norm_cl_kernel<true>, dim3((C + 63) / 64, N), dim3(256), lds, st, x, C,
+    hipLaunchKernelGGL(bn_norm_cl_kernel<true>, dim3((C + BN_CT - 1) / BN_CT, N), dim3(256), lds, st, x, C,
                        HW, mean, rstd, xhat);
   else
-    hipLaunchKernelGGL(bn_norm_cl_kernel<false>, dim3((C + 63) / 64, N), dim3(256), lds, st, x,
+    hipLaunchKernelGGL(bn_norm_cl_kernel<false>, dim3((C + BN_CT - 1) / BN_CT, N), dim3(256), lds, st, x,
                        C, HW, mean, rstd, xhat);
   return (int)hipGetLastError();
 }

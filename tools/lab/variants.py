@@ -69,6 +69,10 @@ VARIANTS = {
 # variants of other sources: name -> (file, substitutions); the timing
 # harness for these is the whole bench step (TGFR_LIB=<lib> bench.py)
 FILE_VARIANTS = {
+    # optimiser: 2 float4 per thread (twice the workgroups) instead of 4
+    "opt2": ("tgfr_optim.hip", [("VEC_PER_BLOCK = 4 * THREADS;", "VEC_PER_BLOCK = 2 * THREADS;")]),
+    # BatchNorm normalise: 32 channels per workgroup (512 workgroups) instead of 64
+    "bnct32": ("tgfr_bn.hip", [("constexpr int BN_CT = 64;", "constexpr int BN_CT = 32;")]),
     # IMIM weight gradients: the workgroup budget of the row-slice split
     # (512 kept in round 4; 256 and 128 measured slower)
     "dw768": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg);",

@@ -69,6 +69,13 @@ VARIANTS = {
 # variants of other sources: name -> (file, substitutions); the timing
 # harness for these is the whole bench step (TGFR_LIB=<lib> bench.py)
 FILE_VARIANTS = {
+    # q/k/v projection (bf16 in / out): 512-workgroup budget instead of 256
+    "gemm512": ("tgfr_gemm.hip", [("""  const int per_slice = std::max(1, std::min(m_tiles, 256 / n_slices));
+  const int lds = WR_TN * K * 2 + WR_NS * WR_STG;
+  auto fn = K == 256 ? &bgemm_wres_kernel<256, true, true> : &bgemm_wres_kernel<128, true, true>;""",
+                                   """  const int per_slice = std::max(1, std::min(m_tiles, 512 / n_slices));
+  const int lds = WR_TN * K * 2 + WR_NS * WR_STG;
+  auto fn = K == 256 ? &bgemm_wres_kernel<256, true, true> : &bgemm_wres_kernel<128, true, true>;""")]),
     # optimiser: 2 float4 per thread (twice the workgroups) instead of 4
     "opt2": ("tgfr_optim.hip", [("VEC_PER_BLOCK = 4 * THREADS;", "VEC_PER_BLOCK = 2 * THREADS;")]),
     # BatchNorm normalise: 32 channels per workgroup (512 workgroups) instead of 64

@@ -50,7 +50,7 @@ def test_dp_world2_matches_global(gpu, tmp_path):
         assert r["rows_bytes_per_caption"] * 1.3 < r["words_bytes_per_caption"], r
 
 
-@pytest.mark.parametrize("precision,bert", [("fp32", 0), ("bf16", 0), ("bf16", 1)])
+@pytest.mark.parametrize("precision,bert", [("fp32", 0), ("bf16", 0), ("bf16", 1), ("fp16", 1)])
 def test_dp_graphed_train_step(gpu, tmp_path, precision, bert):
     """2 ranks: the stage-1 step replayed as graphs cut at its collectives
     equals eager stepping, and the replicas stay identical.  bert = 1: the

@@ -58,6 +58,17 @@ def test_forked_step_matches_linear(gpu, monkeypatch, fork):
     pl = dict(lin.image_head.named_parameters())
     for n, p in frk.image_head.named_parameters():
         torch.testing.assert_close(p, pl[n], rtol=1e-5, atol=1e-6)
+    # the classifiers: updated on the side stream by their own (Adam-free)
+    # optimiser launch in the forked step -- parameters and SGD momentum
+    # buffers must match the linear step's single launch
+    for mod in ("image_cls", "text_cls"):
+        ml, mf = getattr(lin, mod), getattr(frk, mod)
+        for (n, p), q in zip(mf.named_parameters(), ml.parameters()):
+            torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6, msg=f"{mod}.{n}")
+            sf, sl = frk.optimizer.state[p], lin.optimizer.state[q]
+            assert len(sf) == len(sl) >= 1, (mod, n)
+            for a, b in zip(sf, sl):
+                torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6, msg=f"{mod}.{n} state")
 
 
 def test_fusion_step(gpu):

@@ -135,6 +135,10 @@ def lib():
     global _lib
     if _lib is None and os.environ.get("TGFR_LIB"):
         # a lab build of the library (tools/lab/variants.py), for A/B timing
+        # only: it bypasses the stamp check, so it takes an explicit opt-in
+        if os.environ.get("TGFR_LAB") != "1":
+            raise RuntimeError("TGFR_LIB names a lab build of the kernel library; set "
+                               "TGFR_LAB=1 to load it (A/B timing only)")
         _lib = _bind(C.CDLL(os.environ["TGFR_LIB"], mode=C.RTLD_GLOBAL))
     if _lib is None:
         if _build.stale():

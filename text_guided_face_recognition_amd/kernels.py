@@ -46,6 +46,23 @@ LOG2E = 1.4426950408889634
 WR_BOUND_MAX = 85.9
 
 
+def wr_fast(mode, t_words, bounded, att_T=0):
+    """True when the word<->region forward / backward take the bounded
+    (max-free) kernels, which read only the words' operand rows: bf16 with
+    t_pad = 32, or bf16 / fp16 with t_pad = 64 (_wr_fwd)."""
+    m = _wr_mode(mode)
+    t_pad = TPAD if t_words <= TPAD else 2 * TPAD
+    return bool(bounded) and (
+        (m == MODES["bf16"] and not att_T and t_pad == TPAD) or
+        (m != MODES["fp32"] and t_pad == 2 * TPAD))
+
+
+def wr_rows_path(mode, t_words, bounded):
+    """Whether gathered words may travel as their operand rows alone
+    (rows_only_words): only when every consumer takes the fast path."""
+    return mode in ("bf16", "fp16") and wr_fast(mode, t_words, bounded)
+
+
 def prep_rows(x, n_rows, rows_pad, lens=None, want_norms=False, scale=1.0, f16=False):
     """fp32 [items, rows, 256] (any strides) -> bf16 hi/lo of scale * x
     [items, rows_pad, 256] (f16: fp16 bits in hi, no lo).
@@ -108,9 +125,7 @@ def _wr_fwd(img_features, words, lens, gamma1, gamma2, gamma3, mode, img_offset=
     # bounded scores: the bf16 path runs the pipelined kernels both ways;
     # 64-token captions (bf16 / fp16) the bounded backward (log2(e)-scaled
     # words, no running max)
-    fast = bool(bounded) and (
-        (m == MODES["bf16"] and not att_T and t_pad == TPAD) or
-        (m != MODES["fp32"] and t_pad == 2 * TPAD))
+    fast = wr_fast(mode, t_words, bounded, att_T)
     pre = attached_rows(img_features, f16) if bf16 else None
     own_rows = pre is not None
     if pre is not None:            # written by the IMIM tail kernel

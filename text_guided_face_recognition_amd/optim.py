@@ -201,10 +201,23 @@ class FusedOptimizer:
         if n == 0:
             return
         counters = self.counters
-        if only is not None and all(self.groups[gi]["kind"] != ADAM for gi in only):
+        aux = only is not None and all(self.groups[gi]["kind"] != ADAM for gi in only)
+        if aux:
             counters = self.__dict__.get("_aux_counters")
             if counters is None:
                 counters = self._aux_counters = torch.zeros_like(self.counters)
+        # a group's first-step flag (SGD momentum init) comes from the counter
+        # its launch counts on: one group must always count on the same one
+        # (calling it through an Adam-free subset and through a full step()
+        # would re-initialise its momentum, or never initialise it)
+        which = self.__dict__.setdefault("_counter_of", {})
+        for gi in (range(len(self.groups)) if only is None else only):
+            prev = which.setdefault(gi, aux)
+            if prev != aux:
+                raise RuntimeError(
+                    f"optimiser group {gi} was stepped both through an Adam-free subset "
+                    "step(groups=...) and through a step that advances the main counter; "
+                    "use one calling mode per group")
         _hip.call("tgfr_optim_step", C.addressof(segs), n, C.addressof(self._groups_c),
                   len(self.groups), _hip.ptr(self.lr_scale), _hip.ptr(counters),
                   _hip.stream())

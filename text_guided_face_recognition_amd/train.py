@@ -87,6 +87,8 @@ def synthetic_batch_lstm(b, max_words, device, seed, n_ids=1000):
 class Train:
     """Stage-1 BERT trainer step (src/train_encoders_bert.py)."""
 
+    _forks = True       # step() takes _step_forked on one process (subclasses may not)
+
     def __init__(self, args, device, ctx=None):
         self.args = args
         self.ctx = ctx or DistContext()
@@ -120,7 +122,7 @@ class Train:
         # side stream as well, _step_forked.  The logged-loss mix there costs
         # a cross-stream edge and measured slower: 0.50 ms)
         fork = os.environ.get("TGFR_FORK", "2")
-        self.fork = not self.ctx.active and fork != "0"
+        self.fork = self._forks and not self.ctx.active and fork != "0"
         self.fork_text = fork == "2"
         self._side = torch.cuda.Stream(device) if self.fork and torch.cuda.is_available() else None
         # :212 (text_head params would join here; the text side is frozen input)
@@ -260,7 +262,8 @@ class Train:
         words_bt = words.transpose(1, 2)               # [B, T, 256] storage
         f16 = self.args.precision == "fp16"
         pre = K.attached_rows(words_bt, f16, scale=K.LOG2E) \
-            if ctx.active and self.args.precision in ("bf16", "fp16") else None
+            if ctx.active and K.wr_rows_path(self.args.precision, words.shape[2],
+                                             self.args.en_type == "BERT") else None
         if pre is not None:
             rows, norms = pre
             rows_g, norms_g, sent_g, cls_g = ctx.gather_text(rows, norms, sent, class_ids)
@@ -304,6 +307,8 @@ class TrainLSTM(Train):
     The reference also steps an Adam on the text encoder (:178-181), but the
     encoder runs under no_grad (utils/dataset_utils.py:25-33), so that step
     never changes it; the text side here is frozen input as for BERT."""
+
+    _forks = False      # one linear stream (step() below)
 
     def __init__(self, args, device, ctx=None):
         args.en_type = "LSTM"

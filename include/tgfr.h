@@ -68,17 +68,26 @@ int tgfr_prep_rows_f16(const float* x, long long s_item, long long s_row, long l
  * [B_cap][32].  Mode 0 keeps the image's R resident in LDS (Rlo/Wlo unused, may
  * be NULL) and takes the words scaled by log2(e) (Whi = bf16(log2(e) W),
  * tgfr_prep_rows scale).  bounded = 1 (with Rnorm = |R_r| [B_img][224]) lets
- * the mode-0 forward run without a running max (max-free kernels: exact for
- * any input whose score bound max|W| max|R| is <= 85.9 -- unshifted up to
- * 84.5, shifted by the bound beyond; the unit-norm BERT-path features have
- * ~1); otherwise the exact-max kernel runs.  C is stored unnormalised
+ * the mode-0 forward run without a running max.  t_pad 32 (with Sp): the
+ * max-free pipelined kernel, exact for ANY input -- each caption whose
+ * score bound max|W| max|R| exceeds 84.5 takes its running-max variant on
+ * the device (the unit-norm BERT-path features have ~1) -- which also
+ * writes the scores S' = log2(e) R.W of every (pair, 32-region tile) for the
+ * backward into Sp (uint16 [B_img][B_cap][7][1088]: per record 64 lanes x 16
+ * fp16 scores in MFMA accumulator order, then 32 fp32 region maxima; a
+ * caption past the bound stores S' - max and the maxima); Sp NULL runs the
+ * exact-max kernel instead.
+ * t_pad 64: exact while the bound is <= 85.9 (unshifted up to 84.5, shifted
+ * by the bound beyond); the caller routes larger inputs to bounded = 0.
+ * Otherwise the exact-max kernel runs.  C is stored unnormalised
  * (C-hat = Z C); tgfr_wr_bwd_tok folds the 1/Z back in. */
 int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, const float* Wnorm, const float* Rnorm, const int* lens,
                 int B_img, int B_cap,
                 int img_offset, float gamma1, float gamma2, float gamma3, float eps,
                 float* logits, int ld_logits, float* stats, uint16_t* Chi, uint16_t* Clo,
-                float* att, int att_T, int bounded, int t_pad, int mode, void* stream);
+                uint16_t* Sp, float* att, int att_T, int bounded, int t_pad, int mode,
+                void* stream);
 
 /* Backward of tgfr_wr_fwd w.r.t. the image regions given dL/dlogits, in two
  * calls.  tgfr_wr_bwd_tok: per-(pair, token) scalars from the forward stats
@@ -88,14 +97,15 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
  * accumulated.  ws: tgfr_wr_bwd_ws floats of workspace: caption-chunk partial
  * slabs, added in chunk order into dR by a reduction launch inside the call.
  * Rnorm (bounded only; the forward's |R_r| [B_img][224]): the pair's score
- * bound c = max|W| max|R| is formed again here and the recomputed scores are
- * shifted exactly as the bounded forward shifted them (none below c = 84.5).
+ * bound c = max|W| max|R| is formed again here, giving the same per-caption
+ * variant (t_pad 32) / score shift (t_pad 64) as the forward's.
  * The text side is detached in the reference (utils/dataset_utils.py:42).
  * bounded = 1 (mode 0 with t_pad 32 after a bounded forward, or modes 0 / 2
  * with t_pad 64; scores bounded as for tgfr_wr_fwd): both calls must pass
- * it, Whi is the forward's
- * log2(e)-scaled words, and the max-free kernels run (t_pad 32: the two-role
- * one, wr_bwd_duo_kernel). */
+ * it, Whi is the forward's log2(e)-scaled words, and the max-free kernels
+ * run (t_pad 32: the two-role one, wr_bwd_duo_kernel, which reads the
+ * forward's stored scores Sp instead of recomputing them -- required then;
+ * NULL otherwise). */
 int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const float* Rnorm, const int* lens,
                     int B_img, int B_cap, float gamma1, float gamma2, float gamma3, float eps,
                     const float* dlogits, int ld, int bounded, int t_pad, float* tok_ws,
@@ -115,9 +125,9 @@ int tgfr_wr_bwd_tok_ce(const float* stats, const float* Wnorm, const float* Rnor
 int tgfr_wr_bwd_ws(int B_img, int B_cap, int bounded, int t_pad, int mode, long long* floats);
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, int B_img, int B_cap, float gamma1, const float* tok_ws,
-                const uint16_t* Chi, const uint16_t* Clo, float* dR, long long s_b,
-                long long s_r, long long s_d, float* ws, int bounded, int t_pad, int mode,
-                void* stream);
+                const uint16_t* Chi, const uint16_t* Clo, const uint16_t* Sp, float* dR,
+                long long s_b, long long s_r, long long s_d, float* ws, int bounded, int t_pad,
+                int mode, void* stream);
 
 /* Verification pair scores (utils/modules.py:152-153): out[i] = x_i.y_i /
  * max(|x_i| |y_i|, eps) for matched rows of x [rows][d] (ldx) and y (ldy). */

@@ -350,18 +350,22 @@ def test_words_config5_rank_shape(gpu, mode, ltol, gtol):
 
 # (round 4 measured, logit / gradient: bf16 c=48 8.2e-3 / 1.9e-2 (T=30), 7.5e-3 /
 # 1.8e-2 (T=62); fp16 c=48 8.4e-4 / 1.9e-3; c=80 1.4e-3 / 4.0e-3 (T=30), 8.5e-4 /
-# 5.1e-3 (T=62); c=144 (fallback) 1.3e-3 / 4.2e-3)
+# 5.1e-3 (T=62); c=144 (fallback) 1.3e-3 / 4.2e-3; round 5: bf16 T=30 c=144, the
+# running-max variant of the max-free kernels: 1.2e-2 / 4.0e-2)
 @pytest.mark.parametrize("mode,nw,wn,rn,ltol,gtol", [
     ("bf16", 30, 6.0, 8.0, 3e-2, 5e-2), ("bf16", 62, 6.0, 8.0, 3e-2, 4e-2),
     ("fp16", 62, 6.0, 8.0, 4e-3, 8e-3), ("fp16", 30, 8.0, 10.0, 6e-3, 1.5e-2),
-    ("fp16", 62, 8.0, 10.0, 4e-3, 1.5e-2), ("fp16", 30, 12.0, 12.0, 6e-3, 1.5e-2)])
+    ("fp16", 62, 8.0, 10.0, 4e-3, 1.5e-2), ("fp16", 30, 12.0, 12.0, 6e-3, 1.5e-2),
+    ("bf16", 30, 12.0, 12.0, 3e-2, 1e-1)])
 def test_words_bounded_past_unit_norm(gpu, mode, nw, wn, rn, ltol, gtol):
     """The max-free (bounded) kernels fed features far from the unit-norm
     contract through the drop-in path (kernels.word_region_logits with
     bounded=True, as words_loss does for en_type BERT): |W| = 6, |R| = 8 (score
     bound c = 48) and |W| = 8, |R| = 10 (c = 80): exact, no shift (the window
     of csrc/tgfr_wr.hip bound_shift, c <= 84.5); |W| = |R| = 12 (c = 144):
-    past WR_BOUND_MAX, so the host takes the exact running-max kernels.
+    bf16 with 30 words takes the running-max variant of the max-free kernels
+    on the device (per caption, BIG_C); 62 words / fp16 past WR_BOUND_MAX the
+    host takes the exact running-max kernels.
     Logits and gradients finite and matching the oracle (models/losses.py:83-109
     on unnormalised BERT-path features); the tolerance grows with c because
     the operands' relative rounding scales every score by |W| |R|."""
@@ -386,6 +390,64 @@ def test_words_bounded_past_unit_norm(gpu, mode, nw, wn, rn, ltol, gtol):
     print(f"{mode} T={nw} c={wn * rn:.0f}: logit err {lerr:.3e}, grad err {gerr:.3e}")
     assert lerr < ltol, lerr
     assert gerr < gtol, gerr
+
+
+def _past_bound_case(gpu, wn, rn, nw, seed):
+    torch.manual_seed(seed)
+    b_img, b_cap = 7, 11
+    r = rn * _unit(torch.randn(b_img, 14, 14, 256)).permute(0, 3, 1, 2)
+    w = wn * _unit(torch.randn(b_cap, nw, 256)).transpose(1, 2)
+    ro = r.clone().requires_grad_()
+    _, _, _, ref = O.words_loss(ro, w, None, None, nw, 4.0, 5.0, 10.0, batch_size=b_cap)
+    probe = torch.randn(b_img, b_cap)
+    (ref * probe).sum().backward()
+    return r, w, ro.grad, ref.detach(), probe
+
+
+# bf16, 30 words: the bound c = |W| |R| past 84.5 runs the running-max variant
+# of the max-free kernels, chosen per caption on the device (no host check)
+# (round 5 measured, logit / gradient: c=144 1.0e-2 / 4.3e-2, c=2000 3.6e-2 / 2.8e-1)
+@pytest.mark.parametrize("wn,rn,ltol,gtol", [(12.0, 12.0, 3e-2, 1e-1), (40.0, 50.0, 1e-1, 5e-1)])
+def test_words_bounded_graph_captured_past_bound(gpu, wn, rn, ltol, gtol):
+    """words_loss's bounded kernels captured in a graph
+    (torch.cuda.graph, so no host read can run) on inputs far past the
+    unit-norm contract -- c = 144 and c = 2000: finite logits and gradients
+    that match the oracle (models/losses.py:83-109, attention.py:27-41) within
+    the bf16 operand rounding, which grows with c (each score carries ~c 2^-9);
+    the same replay as an eager call, bit for bit."""
+    K = _kernels()
+    nw = 30
+    r, w, ref_g, ref, probe = _past_bound_case(gpu, wn, rn, nw, 91)
+    rg = r.to(gpu).requires_grad_()
+    wv = K.words_view(w.to(gpu), nw)
+    lens = torch.full((w.shape[0],), nw, dtype=torch.int32, device=gpu)
+    pr = probe.to(gpu)
+
+    def step():
+        rg.grad = None
+        logits = K.word_region_logits(rg, wv, lens, 4.0, 5.0, 10.0, mode="bf16", bounded=True)
+        (logits * pr).sum().backward()
+        return logits.detach()
+
+    eager = step().clone()
+    eager_g = rg.grad.clone()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = step()
+    graph.replay()
+    torch.cuda.synchronize()
+    got, grad = out.cpu(), rg.grad.cpu()
+    assert torch.isfinite(got).all() and torch.isfinite(grad).all()
+    assert torch.equal(got, eager.cpu()) and torch.equal(grad, eager_g.cpu())
+    lerr = (got - ref).abs().max().item()
+    gerr = (grad - ref_g).abs().max().item() / ref_g.abs().max().item()
+    print(f"captured bf16 c={wn * rn:.0f}: logit err {lerr:.3e}, grad err {gerr:.3e}")
+    assert lerr < ltol and gerr < gtol, (lerr, gerr)
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp16"])

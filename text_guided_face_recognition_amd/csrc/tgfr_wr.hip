@@ -30,6 +30,7 @@
 #include "tgfr_common.h"
 
 #include <algorithm>
+#include <type_traits>
 
 using namespace tgfr;
 
@@ -957,18 +958,57 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
 // exact in real arithmetic (any shift cancels in the normalisation), and no
 // term overflows and no region's sum underflows while c <= 84.5 (c = 1 for
 // the L2-normalised BERT-path features, models/models.py:212,403; <= 16 for
-// the LSTM's tanh outputs against unit regions).  GEMM1's accumulator starts
-// at the word bias (0, or -1e30 for padding words).  Past c = 84.5 it also
-// carries the shift -log2(e) bound_shift(c); the shift is added back in the
-// statistics.  The shift is applied only where needed: N = sum_r E S then
-// cancels c Z, which costs ~1e-4 of N when Z is formed from the bf16 E of
-// GEMM2 -- visible as ~0.05 logit error through cos = N / (|W| |C|) with
-// |C| ~ 0.07 for diffuse attention.  The host routes other inputs to
-// wr_fwd_res_kernel (exact running max).  Padding
-// words carry bias -1e30 (p = 0; their E = exp(0) = 1 only feeds their own
-// unused statistics and C-hat rows); padding regions (tile 6) get -1e30
-// inside the second exp2.  Outputs: logits, stats {Z, n, |C|, cos}, C-hat
-// (store_cq).  No attention maps (the host uses wr_fwd_res_kernel for those).
+// the LSTM's tanh outputs against unit regions).  A caption whose c exceeds
+// 84.5 (BIG_C; wave-uniform, formed on the device from the row norms) takes
+// the running-max variant of the same pipeline (a uniform branch per caption
+// into a second instantiation of the body): each region's max over the words
+// is subtracted before the exp, exactly as the reference's softmax
+// (models/attention.py:29), so the kernel is exact for ANY input and under
+// graph capture (no host check).  GEMM1's accumulator starts at the word
+// bias: 0, or for padding words -60000 (-1e30 for a BIG_C caption: its valid
+// scores may lie below -60000); padding words then have p = 0, and their
+// E = exp(0) = 1 only feeds their own unused statistics and C-hat rows;
+// padding regions (tile 6) get -1e30 inside the second exp2.
+// Outputs: logits, stats {Z, n, |C|, cos}, C-hat (store_cq) and, for the
+// backward (wr_bwd_duo_kernel, which then runs no S' GEMM), the scores S'
+// of every tile in accumulator order as fp16 (the bias -60000 is
+// representable); for a BIG_C caption S' - m_r (m_r = the region's max over
+// the words: values <= 0, fp16-exact near the max, clamped at -60000) plus
+// m_r itself as fp32 -- one SP_REC record per (pair, region tile).  No
+// attention maps (the host uses wr_fwd_res_kernel for those).
+constexpr float BIG_C = 84.5f;
+constexpr float PAD_BIAS = -60000.f;
+constexpr int SP_REC = 64 * 16 + 64;   // uint16 per (pair, tile): 64 lanes x 16 fp16 + 32 fp32 m_r
+// the score bound's image factor max_r |R_r| (norm rows 0..223; one wave):
+// formed identically by the forward and the backward's token-table kernel,
+// so both take the same BIG_C decision for a pair
+__device__ __forceinline__ float image_rmax(const float* rn, int lane) {
+  return wave_max(fmaxf(fmaxf(rn[lane], rn[lane + 64]),
+                        fmaxf(rn[lane + 128], lane < 32 ? rn[lane + 192] : 0.f)));
+}
+// 8 of a lane's 16 S' values -> 16 B of the backward's record (fp16, round
+// toward zero); BIG: S' - m, clamped at -60000 (padding words)
+template <bool BIG>
+__device__ __forceinline__ uint4 sp_pack(const f32x16& v, int o, float m) {
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float a = v[o + 2 * k], b = v[o + 2 * k + 1];
+    if constexpr (BIG) {
+      a = fmaxf(a - m, PAD_BIAS);
+      b = fmaxf(b - m, PAD_BIAS);
+    }
+    w[k] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+// one 32-bit word of a stored S' tile -> two fp32 scores
+__device__ __forceinline__ void sp_unpack(uint32_t w, float& a, float& b) {
+  const f16x2 h = __builtin_bit_cast(f16x2, w);
+  a = (float)h[0];
+  b = (float)h[1];
+}
 __device__ __forceinline__ float max3f(float a, float b, float c) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -1000,7 +1040,6 @@ constexpr int FWD_SLOTS = 16 + 5 * 34 + 18 + 34;
 // LDS operand prefetch distance in MFMA slots (ring of 8; see the wrap
 // argument at the issue site: no live slot is overwritten for 3 <= PF <= 6)
 constexpr int PF_FWD = 3;
-constexpr int PF_BWD = 5;      // (3: +0.7 us, 4: +1.4 us at config 2)
 // the caption's slots in issue order
 __device__ __forceinline__ constexpr FwdSlot fwd_slot(int n) {
   if (n < 16) return {0, 1, n, 0, n};
@@ -1022,7 +1061,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     const float* __restrict__ Wnorm, const float* __restrict__ Rnorm,
     const int* __restrict__ lens, int B_img, int B_cap, int n_chunks, float g1, float g2,
     float g3, float eps, float* __restrict__ logits, int ld_logits,
-    float4* __restrict__ stats, uint16_t* __restrict__ Chi) {
+    float4* __restrict__ stats, uint16_t* __restrict__ Chi, uint16_t* __restrict__ Sp) {
   const int work = xcd_remap(blockIdx.x, n_chunks * B_img);
   const int b = work / n_chunks, chunk = work % n_chunks;
   const int per = (B_cap + n_chunks - 1) / n_chunks;
@@ -1050,23 +1089,19 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
   if (i >= c1) return;
 
   // max_r |R_r| of this image (the score bound's image factor)
-  float rmax = INFINITY;
-  if (Rnorm) {
-    const float* rn = Rnorm + (long long)b * RPAD;
-    rmax = fmaxf(fmaxf(rn[lane], rn[lane + 64]), fmaxf(rn[lane + 128], lane < 32 ? rn[lane + 192] : 0.f));
-    rmax = wave_max(rmax);
-  }
+  const float rmax = Rnorm ? image_rmax(Rnorm + (long long)b * RPAD, lane) : INFINITY;
   constexpr float L2E = 1.4426950408889634f;
-  // per-caption bound c (wave-uniform) and GEMM1's initial value; wn = this
-  // lane's |W_t| of the caption
-  auto caption_init = [&](int ii, float wn, float& c) {
+  // per caption: the bound c = max_t |W_t| max_r |R_r| (wave-uniform) decides
+  // the variant (big: c > BIG_C, running max); GEMM1's initial value is the
+  // word bias row.  wn = this lane's |W_t| of the caption
+  auto caption_init = [&](int ii, float wn, int& big) {
     const int len = lens[ii];
-    c = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(half_max(wn) * rmax)));
-    c = bound_shift(c);             // no shift below c = 84.5 (bound_shift)
-    const float sh = -L2E * c;
+    const float c = half_max(wn) * rmax;
+    big = __builtin_amdgcn_readfirstlane((int)(c > BIG_C));
+    const float pad = big ? -1e30f : PAD_BIAS;
     f32x16 init;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) init[q] = acc_row(q, h) < len ? sh : -1e30f;
+    for (int q = 0; q < 16; ++q) init[q] = acc_row(q, h) < len ? 0.f : pad;
     return init;
   };
 
@@ -1131,14 +1166,30 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
   f32x16 C[9];           // C^T tiles (d tiles 0..7) and Z^T (8)
   float np[16], p[16];
   uint32_t pk[8];
-  float ma[4], kk = 0.f;
-  // softmax chunk c (0..31) of the tile in S (region tile j), E^T -> etb
-  auto sm_chunk = [&](int c, int j, const f32x16& S, uint32_t etb) {
+  float ma[4], kk = 0.f, rm = 0.f;
+  // softmax chunk c (0..31) of the tile in S (region tile j), E^T -> etb;
+  // chunks 0-3 store the tile's scores for the backward (and, big, form each
+  // region's max over the words first)
+  auto sm_chunk = [&](auto bigc, int c, int j, const f32x16& S, uint32_t etb, uint16_t* spt) {
+    constexpr bool BIG = decltype(bigc)::value;
     if (c < 4) {
+      if constexpr (BIG) {
+        if (c == 0) rm = max3f(max3f(S[0], S[1], S[2]), max3f(S[3], S[4], S[5]), max3f(S[6], S[7], S[8]));
+        if (c == 1) {
+          rm = xhalf_max(max3f(max3f(rm, S[9], S[10]), max3f(S[11], S[12], S[13]), fmaxf(S[14], S[15])));
+          ((float*)(spt + 1024))[lr] = rm;     // (both halves: the same value)
+        }
+      }
+      if (c >= 2) *(uint4*)(spt + lane * 16 + 8 * (c - 2)) = sp_pack<BIG>(S, 8 * (c - 2), rm);
     } else if (c < 12) {
       const int q = 2 * (c - 4);
-      p[q] = __builtin_amdgcn_exp2f(S[q]);
-      p[q + 1] = __builtin_amdgcn_exp2f(S[q + 1]);
+      if constexpr (BIG) {
+        p[q] = __builtin_amdgcn_exp2f(S[q] - rm);
+        p[q + 1] = __builtin_amdgcn_exp2f(S[q + 1] - rm);
+      } else {
+        p[q] = __builtin_amdgcn_exp2f(S[q]);
+        p[q + 1] = __builtin_amdgcn_exp2f(S[q + 1]);
+      }
     } else if (c == 12) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) ma[q] = p[q] + p[q + 8];
@@ -1164,8 +1215,8 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
   };
 
   // ---- prologue: first caption's words, GEMM1 of its tile 0, first reads
-  float c_cur, c_next;
-  f32x16 init = caption_init(i, Wnorm[(long long)i * TPAD + lr], c_cur);
+  int big_cur, big_next;
+  f32x16 init = caption_init(i, Wnorm[(long long)i * TPAD + lr], big_cur);
   load_w(i);
   f32x16 S[7];           // S[j]: GEMM1 result of tile j (two live at a time)
   {
@@ -1179,10 +1230,14 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
 #pragma unroll
   for (int n = 0; n < PF_FWD; ++n) issue_read(fwd_slot(n), rd[n]);
 
-  for (; i < c1; i += 4) {
+  // one caption (and the next one's GEMM1 of tile 0); bigc: this caption's
+  // variant (std::true_type: running max)
+  auto caption = [&](auto bigc) {
     const int len = lens[i];
     const int inext = min(i + 4, c1 - 1);   // the last caption recomputes itself
     const float wn_next = Wnorm[(long long)inext * TPAD + lr];
+    const long long pair = (long long)b * B_cap + i;
+    uint16_t* sp = Sp + pair * (NRT * SP_REC);     // wave-uniform
     f32x16 initn;
 #pragma unroll
     for (int q = 0; q < 16; ++q) np[q] = 0.f;
@@ -1218,19 +1273,20 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
       if (stage <= 6) {
         const int j = stage;                       // softmax tile
         const uint32_t etb = et + (j & 1) * 2048;
+        uint16_t* spt = sp + j * SP_REC;
         if (stage == 0 || stage == 6) {
           if (m < 16) {
-            sm_chunk(2 * m, j, S[j], etb);
-            sm_chunk(2 * m + 1, j, S[j], etb);
+            sm_chunk(bigc, 2 * m, j, S[j], etb, spt);
+            sm_chunk(bigc, 2 * m + 1, j, S[j], etb, spt);
           }
         } else if (m < 32) {
-          sm_chunk(m, j, S[j], etb);
+          sm_chunk(bigc, m, j, S[j], etb, spt);
         }
       }
       // the next caption's words, once GEMM1 of tile 6 is issued; its GEMM1
       // initial value once this caption's is dead
       if (n == 186) load_w(inext);
-      if (n == 190) initn = caption_init(inext, wn_next, c_next);
+      if (n == 190) initn = caption_init(inext, wn_next, big_next);
       __builtin_amdgcn_sched_barrier(0);
     }
     // ---- N per token: reduce-scatter over the region lanes -> LDS
@@ -1247,8 +1303,8 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
       for (int q = 0; q < 16; ++q) csq = fmaf(C[dt][q], C[dt][q], csq);
     csq = xhalf_sum(csq);
     const float Z = C[8][0];
-    // np sums E * (S' + init) = log2(e) (N - c Z) over the regions
-    const float nhat = lds_ldf(tok + t * 4) * (1.f / L2E) + c_cur * Z;
+    // np sums E * S' = log2(e) N over the regions (valid tokens: bias 0)
+    const float nhat = lds_ldf(tok + t * 4) * (1.f / L2E);
     const bool tvalid = t < len;
     const float zinv = __builtin_amdgcn_rcpf(Z);
     const float cn = sqrtf(csq) * zinv;
@@ -1256,13 +1312,18 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     const float u = Wnorm[(long long)i * TPAD + t];
     const float cosv = n_ / fmaxf(u * cn, eps);
     const float ex = half_sum(tvalid ? __expf(g2 * cosv) : 0.f);
-    const long long pair = (long long)b * B_cap + i;
     logits[(long long)b * ld_logits + i] = g3 * __logf(ex);
     stats[pair * TPAD + t] =
         tvalid ? make_float4(Z, n_, cn, cosv) : make_float4(0.f, 0.f, 0.f, 0.f);
     store_cq<MODE_BF16>(Chi, nullptr, pair, t, h, C);
     init = initn;
-    c_cur = c_next;
+    big_cur = big_next;
+  };
+  for (; i < c1; i += 4) {
+    if (big_cur)
+      caption(std::true_type{});
+    else
+      caption(std::false_type{});
   }
 }
 
@@ -1315,18 +1376,18 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
   const int len = lens[i];
   const bool valid = t < len;
   const float4 st = valid ? stats[pair * TP + t] : make_float4(1.f, 0.f, 0.f, 0.f);
-  // layout 1: the pair's score bound c = max_t |W_t| max_r |R_r| (as the
-  // bounded forwards form it); the max-free backwards shift S' by -log2(e)
-  // bound_shift(c) through the G1 initial row, and sigma absorbs alpha times it
-  float cb = 0.f;
+  // layouts 1 / 2: the pair's score bound c = max_t |W_t| max_r |R_r| (as the
+  // bounded forwards form it).  Layout 1 (wr_bwd_wide2_kernel): the max-free
+  // backward shifts S' by -log2(e) bound_shift(c) through the G1 initial row,
+  // and sigma absorbs alpha times it.  Layout 2 (wr_bwd_duo_kernel): no shift;
+  // row 6 carries the forward's variant (1: c > BIG_C, running max)
+  float cb = 0.f, big = 0.f;
   if (layout != 0 && Rnorm) {
-    const float* rn = Rnorm + (long long)b * RPAD;
-    const int l = threadIdx.x % WAVE;
-    float rmax = fmaxf(fmaxf(rn[l], rn[l + 64]), fmaxf(rn[l + 128], l < 4 ? rn[l + 192] : 0.f));
-    rmax = wave_max(rmax);
+    const float rmax = image_rmax(Rnorm + (long long)b * RPAD, threadIdx.x % WAVE);
     const float wn = Wnorm[(long long)i * TP + t];
     cb = (TP == 64 ? wave_max(wn) : half_max(wn)) * rmax;
-    cb = bound_shift(cb);
+    big = cb > BIG_C ? 1.f : 0.f;
+    cb = layout == 1 ? bound_shift(cb) : 0.f;
   }
   const float ex = valid ? __expf(g2 * st.w) : 0.f;
   const float tot = TP == 64 ? wave_sum(ex) : half_sum(ex);
@@ -1365,7 +1426,10 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
   }
   if (layout != 0) {
     if (!valid) o[0] = -INFINITY;       // exp2 offset of a padding token: A2 = 0
-    o[6] = valid ? -1.4426950408889634f * cb : -1e30f;   // G1's initial value row
+    if (layout == 1)
+      o[6] = valid ? -1.4426950408889634f * cb : -1e30f;   // G1's initial value row
+    else
+      o[6] = big;                       // the pair's variant, in every token's row
     if ((threadIdx.x % WAVE) < TP) {    // 8 rows of TP tokens per pair
 #pragma unroll
       for (int k = 0; k < 8; ++k) tok[pair * 8 * TP + k * TP + t] = o[k];
@@ -2213,350 +2277,46 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
                                   slab);
 }
 
-// -------------------------------------------- bwd, bf16, bounded, pipelined ---
-// Backward of wr_fwd_pipe_kernel (bf16 mode, bounded scores, log2(e)-scaled
-// words W').  Same work split and slab output as wr_bwd_kernel: workgroup =
-// (image, 4 region tiles, caption chunk), one wave per 32-region tile; the
-// wave's R tile is held as MFMA B fragments in registers.  Per caption:
-//   G1  [S'^T ; Q-hat^T] = [W' ; C-hat] R_tile^T        32 MFMAs (asm, VGPRs)
-//   SM  softmax-1 recompute (p = exp2(S'); no max: the scores are bounded)
-//       and both softmax backwards, per lane (tokens in registers, the
-//       region on the lane); the per-token scalars of wr_tok_kernel's
-//       bounded layout fold gamma1, 1/Z and log2(e), so an element costs
-//       2 exp2 + 13 VALU
-//   G3  dR_tile += [M_w | M_c] [W' ; C-hat]             32 MFMAs (AGPRs)
-// Captions run as a software pipeline: stage t issues G1 of caption t+1 and
-// G3 of caption t-1 alternately (64 MFMA slots, order fixed in the source,
-// LDS reads three slots ahead) while SM of caption t runs in their issue
-// gaps.  X images ([W'; C-hat] + token table) stream through a 4-deep LDS
-// ring by LDS DMA issued two captions ahead; one barrier per stage.
-// Captions past the chunk read a zero token table: their M fragments are
-// zero, so the fill / drain stages need no branches.
-// Each caption chunk writes its partial dR tiles to its own slab; one
-// reduction launch (wr_reduce_kernel) adds them in chunk order.  (An in-launch
-// last-arriver sum measured slower here: the last arrivers' cross-XCD slab
-// reads run at low memory parallelism, ~15 us against ~10 us for the
-// chip-wide reduction launch.)
-constexpr int BP_NB = 4;                       // ring depth
-constexpr int BP_TOK = 1024;                   // token table bytes
-constexpr int BP_BUF = B_XIMG + BP_TOK;        // one caption: X image + table
-constexpr int BP_ZERO = BP_NB * BP_BUF;        // a zero token table
-constexpr int BP_LDS = BP_ZERO + BP_TOK;
-// MFMA slot of the stage after which DMA piece j of X(t + 2) is issued (-1:
-// none): every other slot from slot 2 (config 2, interleaved A/B rounds,
-// tools/lab/bench_variants.py: 84.8 us against 85.3 with a piece every fourth
-// slot and ~86.5 with all nine at the stage head)
-__device__ __forceinline__ constexpr int bp_dma_slot(int n) {
-  return (n >= 2 && n <= 18 && (n & 1) == 0) ? (n - 2) / 2 : -1;
-}
-
-__global__ __launch_bounds__(256, 1) void wr_bwd_pipe_kernel(
-    const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi, int B_img, int B_cap,
-    int n_chunks, float g1, const float* __restrict__ tok, const uint16_t* __restrict__ Chi,
-    float* __restrict__ out, long long s_b, long long s_r, long long s_d,
-    uint16_t* __restrict__ slab) {
-  const int total = n_chunks * 2 * B_img;
-  const int work = xcd_remap(blockIdx.x, total);
-  const int b = work / (2 * n_chunks);
-  const int rem = work % (2 * n_chunks);
-  const int tg = rem / n_chunks, chunk = rem % n_chunks;
-  const int per = (B_cap + n_chunks - 1) / n_chunks;
-  const int c0 = chunk * per, c1 = min(B_cap, c0 + per);
-  const int K = max(0, c1 - c0);
-  const int tid = threadIdx.x, lane = tid % WAVE;
-  const int wid = __builtin_amdgcn_readfirstlane(tid / WAVE);
-  const int lr = lane & 31, h = lane >> 5;
-  const int rt = tg * 4 + wid;                 // region tile (7: padding only)
-  const int g16 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-  const float gL = g1 * 1.4426950408889634f;
-
-  // zero the ring (the first G3 reads an empty buffer) and the zero table
-  for (int o = tid * 16; o < BP_LDS; o += 256 * 16) lds_st16(o, make_uint4(0, 0, 0, 0));
-  // R tile as B fragments: lane (r, h), k-step s -> d = 16 s + 8 h .. + 7
-  bf16x8 Rf[16];
-  {
-    const long long roff = ((long long)b * RPAD + min(rt, NRT - 1) * 32 + lr) * D;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) Rf[s] = as_bf8(*(const uint4*)(Rhi + roff + s * 16 + h * 8));
-  }
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  // DMA pieces of one caption (bwd_stage's layout, MODE_BF16): wave wid
-  // issues pieces k = wid + 4 j (j < 8); rows 4 (k % 16) + lane / 16 are W'
-  // rows for j % 4 < 2 and C-hat rows otherwise, so each piece's source is a
-  // caption-uniform base (SGPRs) plus a per-lane byte offset fixed here
-  uint32_t dma_off[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = wid + 4 * j, p = k % 32, half = p / 16;
-    const int row = 4 * (p % 16) + lane / 16, pc = lane % 16;
-    const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
-    const int c = half * 16 + (pc ^ sw);
-    dma_off[j] = (j % 4 < 2) ? (uint32_t)((row * D + c * 8) * 2)
-                             : (uint32_t)(((c * 32) + (row - 32)) * 8 * 2);
-  }
-  // DMA piece j (< 8: X image, 8: token table) of caption c0 + k -> ring slot
-  // k % 4.  Branch-free: past the chunk the last caption is fetched again
-  // (its fill / drain stages read a zero token table, and every slot holds
-  // finite data); the token table is issued by every wave (identical bytes)
-  // rather than by one behind a branch, which would split the unrolled
-  // stage into basic blocks.
-  auto dma_piece = [&](int k, int j) {
-    const int kc = min(k, K - 1);
-    const uint32_t base = (k % BP_NB) * BP_BUF;
-    const long long pair = (long long)b * B_cap + c0 + kc;
-    if (j == 8) {
-      glds16s(tok + pair * TPAD * 8, lane * 16, base + B_XIMG);
-    } else {
-      const int kk = wid + 4 * j, p = kk % 32;
-      const void* src = j % 4 < 2 ? (const void*)(Whi + (long long)(c0 + kc) * TPAD * D)
-                                  : (const void*)(Chi + pair * 32 * 32 * 8);
-      glds16s(src, dma_off[j], base + (p / 16) * (64 * 256) + 4 * (p % 16) * 256);
-    }
-  };
-  if (K > 0) {
-#pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      dma_piece(0, j);
-      dma_piece(1, j);
-    }
-  }
-
-  // per-lane parts of the swizzled X-image addresses (xoff), as wr_bwd_kernel
-  uint32_t g1o[8], g2o[2][4];
-  {
-    const int sw1 = ((lr & 3) << 2) | ((lr >> 2) & 3);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) g1o[k] = lr * 256 + (((2 * k + h) ^ sw1) << 4);
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-      for (int dd = 0; dd < 4; ++dd)
-        g2o[bb][dd] = (4 * h + q4 + 8 * bb) * 256 + ((dd ^ q4) << 6) +
-                      (((2 * (g16 & 1) + (p4 >> 1)) ^ ((h + 2 * bb) & 3)) << 4) + (p4 & 1) * 8;
-  }
-
-  f32x16 dR[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) dR[j][q] = 0.f;
-
-  // G1 operand read u (0..15 W' rows, 16..31 C-hat rows) of the image at xb
-  auto g1_read = [&](int u, uint32_t xb) {
-    const int s = u & 15;
-    return __builtin_bit_cast(
-        u32x4, lds_ld16(xb + g1o[s & 7] + (s >> 3) * (64 * 256) + (u >= 16 ? 32 * 256 : 0)));
-  };
-  // G3 operand read u: d tile dt = u >> 2, k block ks = u & 3
-  auto g3_read = [&](int u, uint32_t xb) {
-    const int dt = u >> 2, ks = u & 3;
-    const uint32_t kb = xb + (dt >> 2) * (64 * 256) + ((ks >> 1) * 32 + (ks & 1) * 16) * 256;
-    return __builtin_bit_cast(u32x4, join_tr(lds_tr4(kb + g2o[0][dt & 3]),
-                                             lds_tr4(kb + g2o[1][dt & 3])));
-  };
-  // (builtins, not inline asm: the operands are produced by VALU ops -- AGPR
-  // reads, register moves -- right before, and only the compiler's hazard
-  // recognizer inserts the VALU-write -> MFMA-read wait states)
-  auto g1_mfma = [&](int u, const u32x4& op, f32x16& A0, f32x16& A1, const f32x16& init) {
-    const bf16x8 x = __builtin_bit_cast(bf16x8, op);
-    const int s = u & 15;
-    if (u < 16)
-      A0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, Rf[s], s == 0 ? init : A0, 0, 0, 0);
-    else
-      A1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, Rf[s], s == 0 ? (f32x16){} : A1, 0, 0,
-                                                   0);
-  };
-  // token scalar k for the lane's tokens 8g + 4h + 0..3 (q = 4g .. 4g+3)
-  auto scal = [&](uint32_t tb, int k, int g) {
-    return __builtin_bit_cast(u32x4, lds_ld16(tb + k * 128 + g * 32 + h * 16));
-  };
-  auto init_of = [&](uint32_t tb) {   // the token-bias row (scalar 6) as G1's init
-    f32x16 r;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const u32x4 x = scal(tb, 6, g);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) r[4 * g + k] = __uint_as_float(x[k]);
-    }
-    return r;
-  };
-
-  // softmax state of the caption in SM
-  float p[16], a1[16], ax[16], v[16];
-  float s8[8], inv = 0.f, kq = 0.f, rho = 0.f;
-  u32x4 fb[2][4], fc[2][2];     // scalars f0..f3 (phase B) / f4, f5 (phase C), by group parity
-  uint32_t mw2[8], mc2[8];
-  auto fl = [](const u32x4& x, int q) { return __uint_as_float(x[q & 3]); };
-  // SM chunk c (0..63) of the caption with token table tb and G1 results A0, A1;
-  // its M fragments go to Mo
-  auto sm_chunk = [&](int c, uint32_t tb, const f32x16& A0, const f32x16& A1, bf16x8* Mo) {
-    // scalar prefetch: f0..f3 of group g four chunks before its phase-B span
-    // (13 + 8g), f4, f5 three chunks before its phase-C span (46 + 4g)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      if (c == 9 + 8 * g)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) fb[g & 1][k] = scal(tb, k, g);
-      if (c == 43 + 4 * g) {
-        fc[g & 1][0] = scal(tb, 4, g);
-        fc[g & 1][1] = scal(tb, 5, g);
-      }
-    }
-    if (c < 8) {                  // phase A: p = exp2(S') (bias rows: 0)
-      p[2 * c] = __builtin_amdgcn_exp2f(A0[2 * c]);
-      p[2 * c + 1] = __builtin_amdgcn_exp2f(A0[2 * c + 1]);
-    } else if (c == 8) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) s8[k] = p[k] + p[k + 8];
-    } else if (c == 9) {
-#pragma unroll
-      for (int k = 4; k < 8; ++k) s8[k] = p[k] + p[k + 8];
-    } else if (c == 10) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) s8[k] += s8[k + 4];
-    } else if (c == 11) {
-      inv = xhalf_sum((s8[0] + s8[1]) + (s8[2] + s8[3]));
-    } else if (c == 12) {
-      inv = __builtin_amdgcn_rcpf(sum_floor(inv));
-      kq = gL * inv;
-      rho = 0.f;
-    } else if (c < 45) {          // phase B, two chunks per token q
-      const int q = (c - 13) >> 1, g = q >> 2;
-      const u32x4* f = fb[g & 1];
-      if (((c - 13) & 1) == 0) {
-        a1[q] = p[q] * inv;                                   // A1
-        ax[q] = __builtin_amdgcn_exp2f(fmaf(p[q], kq, fl(f[0], q)));   // g1 A2 / log2e
-      } else {
-        // (dA2 - sigma) = (alpha / log2e) S' + (beta / Z) Q-hat - sigma
-        const float du = fmaf(fl(f[1], q), A0[q], fmaf(fl(f[2], q), A1[q], -fl(f[3], q)));
-        v[q] = a1[q] * (ax[q] * du);                         // A1 dA1 / log2e
-        rho += v[q];
-      }
-    } else if (c == 45) {
-      rho = xhalf_sum(rho);
-    } else if (c < 62) {          // phase C, one chunk per token q
-      const int q = c - 46, g = q >> 2;
-      const u32x4* f = fc[g & 1];
-      const float dsx = fmaf(-a1[q], rho, v[q]);              // dS / log2e
-      p[q] = fmaf(fl(f[0], q), ax[q], dsx);                   // M_w (scaled for W')
-      s8[q & 7] = fl(f[1], q) * ax[q];                        // M_c (for C-hat)
-      if (q & 1) {
-        mw2[q >> 1] = pk_bf16(p[q - 1], p[q]);
-        mc2[q >> 1] = pk_bf16(s8[(q - 1) & 7], s8[q & 7]);
-      }
-      if (q == 15) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          Mo[k] = __builtin_bit_cast(bf16x8, make_uint4(mw2[4 * k], mw2[4 * k + 1],
-                                                          mw2[4 * k + 2], mw2[4 * k + 3]));
-          Mo[2 + k] = __builtin_bit_cast(bf16x8, make_uint4(mc2[4 * k], mc2[4 * k + 1],
-                                                              mc2[4 * k + 2], mc2[4 * k + 3]));
-        }
-        // pin phase C here: without a use in this stage the compiler sinks it
-        // past the stage boundary into the next stage's first MFMA gap
-        asm volatile("" ::"v"(Mo[0]), "v"(Mo[1]), "v"(Mo[2]), "v"(Mo[3]));
-      }
-    }
-  };
-
-  // one pipeline stage t: G1(t+1) -> (A0n, A1n), SM(t) on (A0, A1) -> Mo,
-  // G3(t-1) with Mi
-  auto stage = [&](int t, f32x16& A0, f32x16& A1, f32x16& A0n, f32x16& A1n,
-                   const bf16x8* Mi, bf16x8* Mo) {
-    ring_barrier<0>();                 // X(t+1) landed everywhere; X(t-2) retired
-    const uint32_t x1 = ((t + 1) % BP_NB) * BP_BUF;          // G1 image
-    const uint32_t x3 = ((t + 3) % BP_NB) * BP_BUF;          // G3 image (t-1)
-    const uint32_t tbs = t < K ? (t % BP_NB) * BP_BUF + B_XIMG : BP_ZERO;
-    const uint32_t tb1 = x1 + B_XIMG;
-    const f32x16 init = init_of(tb1);
-    u32x4 rd[8];
-    // slot n: even -> G1 MFMA n/2, odd -> G3 MFMA n/2
-    auto read = [&](int n) { return (n & 1) ? g3_read(n >> 1, x3) : g1_read(n >> 1, x1); };
-#pragma unroll
-    for (int n = 0; n < PF_BWD; ++n) rd[n] = read(n);
-#pragma clang loop unroll(full)
-    for (int n = 0; n < 64; ++n) {
-      const u32x4 op = rd[n & 7];
-      if (n & 1) {
-        const int u = n >> 1, ks = u & 3;
-        dR[u >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            Mi[ks], __builtin_bit_cast(bf16x8, op), dR[u >> 2], 0, 0, 0);
-      } else {
-        g1_mfma(n >> 1, op, A0n, A1n, init);
-      }
-      if (n + PF_BWD < 64) rd[(n + PF_BWD) & 7] = read(n + PF_BWD);
-      // X(t + 2) pieces early in the stage, between MFMAs (a burst at the
-      // stage head issued ~80 cycles per piece with the matrix core idle)
-      if (bp_dma_slot(n) >= 0) dma_piece(t + 2, bp_dma_slot(n));
-      sm_chunk(n, tbs, A0, A1, Mo);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-  if (rt >= NRT || K == 0) {
-    // the padding-only tile (and an empty chunk): no MFMA / softmax work, only
-    // this wave's share of the ring traffic, so the other waves' barriers and
-    // DMA pieces stay as they are
-    if (K > 0) {
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      const int T2p = (K + 2) & ~1;
-      for (int t = 0; t < T2p; ++t) {
-        ring_barrier<0>();
-#pragma unroll
-        for (int j = 0; j < 9; ++j) dma_piece(t + 2, j);
-      }
-    }
-    if (rt < NRT) store_dr_tile(dR, n_chunks, chunk, b, rt, B_img, lane, out, s_b, s_r, s_d, slab);
-    return;
-  }
-  // ---- prologue: G1 of caption 0
-  f32x16 Aa0, Aa1, Ab0, Ab1;
-  bf16x8 Ma[4], Mb[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) Ma[k] = Mb[k] = as_bf8(make_uint4(0, 0, 0, 0));
-  {
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const f32x16 init = init_of(B_XIMG);
-#pragma unroll
-    for (int u = 0; u < 32; ++u) g1_mfma(u, g1_read(u, 0), Aa0, Aa1, init);
-  }
-  const int T2 = (K + 2) & ~1;         // stages 0..K, padded to even
-  for (int t = 0; t < T2; t += 2) {
-    stage(t, Aa0, Aa1, Ab0, Ab1, Ma, Mb);
-    stage(t + 1, Ab0, Ab1, Aa0, Aa1, Mb, Ma);
-  }
-  store_dr_tile(dR, n_chunks, chunk, b, rt, B_img, lane, out, s_b, s_r, s_d, slab);
-}
-
 // ------------------------------- bwd, bf16, bounded, two roles per SIMD ---
-// The same arithmetic as wr_bwd_pipe_kernel, with each region tile's work
-// split between two waves that share one SIMD (512-thread workgroup, waves w
-// and w + 4 on one SIMD):
-//   S wave (waves 0-3): G1 [S'^T ; Q-hat^T] = [W' ; C-hat] R_tile^T of
-//       caption t + 1 (32 MFMAs) in the issue gaps of the softmax recompute
-//       and both softmax backwards of caption t (the VALU-heavy half); hands
-//       the caption's M fragments [M_w | M_c] (4 KB per tile) to its partner
-//       through LDS.
-//   M wave (waves 4-7): G3 dR_tile += [M_w | M_c] [W' ; C-hat] of caption
+// Backward of wr_fwd_pipe_kernel (bf16 mode, bounded scores, log2(e)-scaled
+// words W').  Workgroup = (image, 4 region tiles, caption chunk), 512
+// threads; each region tile's work is split between two waves that share one
+// SIMD (waves w and w + 4):
+//   S wave (waves 0-3): G1  Q-hat^T = C-hat R_tile^T of caption t + 1 (16
+//       MFMAs; the R tile as B fragments in registers) in the issue gaps of
+//       SM(t): the softmax-1 terms from the scores the FORWARD stored (S' in
+//       accumulator order, fp16; S' - m_r and m_r for a BIG_C caption;
+//       loaded one caption ahead: no S' GEMM here -- the reference's autograd keeps its
+//       attention too and spends 6 R D T per pair, models/losses.py:96-109,
+//       models/attention.py:27-41), then both softmax backwards; hands the
+//       caption's M fragments [M_w | M_c] (4 KB per tile) to its partner
+//       through an LDS slot.
+//   M wave (waves 4-7): G3  dR_tile += [M_w | M_c] [W' ; C-hat] of caption
 //       t - 1 (32 MFMAs, operands read transposed from the X image) and the
 //       X-image DMA of caption t + 2.
-// One wave per SIMD could hide only ~5 issue slots per MFMA gap and none of
-// its own waits; two waves with complementary mixes let the SIMD overlap one
-// wave's softmax VALU and LDS waits with the other's MFMAs.
-// Per stage t: barrier B1 (X(t+1) landed, M(t-1) written); S: G1(t+1) + SM(t);
-// M: reads M(t-1) and marks it consumed in its tile's LDS counter, G3(t-1),
-// DMA X(t+2); S waits for that counter (pairwise, not a workgroup barrier:
-// round 3's second barrier per stage made every wave wait for the slowest
-// role of all four tiles) and writes M(t).  B1 alone orders the X ring: a
-// slot is re-filled two stages after its last readers passed B1.  Captions
-// past the chunk read a zero token table (their M fragments are zero), so
-// the fill / drain stages need no branches.
+// So one SIMD's matrix pipe is fed by two instruction streams (48 MFMAs per
+// caption and tile, 6 R D T + the padding), and the softmax VALU of caption t
+// runs while the M wave's MFMAs of caption t - 1 occupy the pipe.
+// Per stage t: barrier B1 (X(t+1) landed, M(t-1) written); S: G1(t+1) +
+// SM(t); M: reads M(t-1) and marks it consumed in its tile's LDS counter,
+// G3(t-1), DMA X(t+2); S waits for that counter (pairwise, not a workgroup
+// barrier) and writes M(t).  B1 alone orders the X ring: a slot is re-filled
+// two stages after its last readers passed B1.  Captions past the chunk read
+// a zero token table (their M fragments are zero; their S' and variant flag
+// are the last caption's, so every value stays finite), so the fill / drain
+// stages need no branches.
+// Per-token scalars (wr_tok_kernel layout 2, rows of 32 tokens): f0 = the
+// exp2 offset log2(g1 / (Z log2e)) (-inf: padding), f1 = alpha / log2e,
+// f2 = beta / Z, f3 = sigma, f4 = alpha / g1, f5 = beta log2e / (g1 Z),
+// row 6 = the pair's variant (1: c > BIG_C: the stored scores are S' - m_r,
+// so p = exp2(stored) is the forward's running-max softmax term, and the
+// score itself is stored + m_r).  An element costs 2 exp2 + ~14 VALU.
 constexpr int BD_NB = 4;                        // X ring depth
-constexpr int BD_BUF = B_XIMG + BP_TOK;         // one caption: X image + token table
+constexpr int BD_TOK = 1024;                    // token table bytes
+constexpr int BD_BUF = B_XIMG + BD_TOK;         // one caption: X image + token table
 constexpr int BD_MS = BD_NB * BD_BUF;           // M hand-off: 4 tiles x 4 KB
 constexpr int BD_ZERO = BD_MS + 4 * 4096;       // a zero token table
-constexpr int BD_CNT = BD_ZERO + BP_TOK;        // per tile: M stages consumed (int)
+constexpr int BD_CNT = BD_ZERO + BD_TOK;        // per tile: M stages consumed (int)
 constexpr int BD_LDS = BD_CNT + 4 * 4;
 constexpr int BD_PF1 = 3;                       // G1 operand prefetch distance (slots)
 constexpr int BD_PF3 = 4;                       // G3 operand prefetch distance (slots)
@@ -2587,8 +2347,8 @@ __device__ __forceinline__ void lds_wait_ge(uint32_t off, int v) {
 __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi, int B_img, int B_cap,
     int n_chunks, float g1, const float* __restrict__ tok, const uint16_t* __restrict__ Chi,
-    float* __restrict__ out, long long s_b, long long s_r, long long s_d,
-    uint16_t* __restrict__ slab) {
+    const uint16_t* __restrict__ Sp, float* __restrict__ out, long long s_b, long long s_r,
+    long long s_d, uint16_t* __restrict__ slab) {
   const int total = n_chunks * 2 * B_img;
   const int work = xcd_remap(blockIdx.x, total);
   const int b = work / (2 * n_chunks);
@@ -2614,9 +2374,11 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
 
   if (role == 1) {
     // ================================================================ M wave
-    // DMA pieces of one caption (bwd_stage's layout): M wave wid issues
-    // pieces k = wid + 4 j (j < 8) of the X image and (every M wave, the
-    // same bytes) the token table
+    // DMA pieces of one caption: M wave wid issues pieces k = wid + 4 j
+    // (j < 8) of the X image -- rows 4 (k % 16) + lane / 16 are W' rows for
+    // j % 4 < 2 and C-hat rows otherwise, so each piece's source is a
+    // caption-uniform base (SGPRs) plus a per-lane byte offset fixed here --
+    // and (every M wave, the same bytes) the token table
     uint32_t dma_off[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -2627,6 +2389,9 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
       dma_off[j] = (j % 4 < 2) ? (uint32_t)((row * D + c * 8) * 2)
                                : (uint32_t)(((c * 32) + (row - 32)) * 8 * 2);
     }
+    // DMA piece j (< 8: X image, 8: token table) of caption c0 + k -> ring
+    // slot k % 4.  Branch-free: past the chunk the last caption is fetched
+    // again
     auto dma_piece = [&](int k, int j) {
       const int kc = min(k, K - 1);
       const uint32_t base = (k % BD_NB) * BD_BUF;
@@ -2717,88 +2482,106 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
 #pragma unroll
     for (int k = 0; k < 8; ++k) g1o[k] = lr * 256 + (((2 * k + h) ^ sw1) << 4);
   }
-  // G1 operand read u (0..15 W' rows, 16..31 C-hat rows) of the image at xb
-  auto g1_read = [&](int u, uint32_t xb) {
-    const int s = u & 15;
-    return __builtin_bit_cast(
-        u32x4, lds_ld16(xb + g1o[s & 7] + (s >> 3) * (64 * 256) + (u >= 16 ? 32 * 256 : 0)));
+  // G1 operand read s (k step 0..15) of the C-hat rows of the image at xb
+  auto g1_read = [&](int s, uint32_t xb) {
+    return __builtin_bit_cast(u32x4,
+                              lds_ld16(xb + g1o[s & 7] + (s >> 3) * (64 * 256) + 32 * 256));
   };
-  auto g1_mfma = [&](int u, const u32x4& op, f32x16& A0, f32x16& A1, const f32x16& init) {
-    const bf16x8 x = __builtin_bit_cast(bf16x8, op);
-    const int s = u & 15;
-    if (u < 16)
-      A0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, Rf[s], s == 0 ? init : A0, 0, 0, 0);
-    else
-      A1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, Rf[s], s == 0 ? (f32x16){} : A1, 0, 0,
-                                                   0);
+  auto g1_mfma = [&](int s, const u32x4& op, f32x16& A) {
+    A = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, op), Rf[s],
+                                                s == 0 ? (f32x16){} : A, 0, 0, 0);
+  };
+  // stored S' of caption k (clamped to the chunk) for this tile: 2 x 16 B per
+  // lane, and the region max m_r of a BIG_C caption (unused otherwise)
+  const uint16_t* spb = Sp + ((long long)b * B_cap + c0) * (NRT * SP_REC) +
+                        min(rt, NRT - 1) * SP_REC;
+  auto sp_load = [&](int k, uint4 (&dst)[2], float& m) {
+    const uint16_t* rec = spb + (long long)min(k, K - 1) * (NRT * SP_REC);
+    dst[0] = ((const uint4*)(rec + lane * 16))[0];
+    dst[1] = ((const uint4*)(rec + lane * 16))[1];
+    m = ((const float*)(rec + 1024))[lr];
   };
   // token scalar k for the lane's tokens 8g + 4h + 0..3 (q = 4g .. 4g+3)
   auto scal = [&](uint32_t tb, int k, int g) {
     return __builtin_bit_cast(u32x4, lds_ld16(tb + k * 128 + g * 32 + h * 16));
   };
-  auto init_of = [&](uint32_t tb) {   // the token-bias row (scalar 6) as G1's init
-    f32x16 r;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const u32x4 x = scal(tb, 6, g);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) r[4 * g + k] = __uint_as_float(x[k]);
-    }
-    return r;
+  // the variant flag (row 6) of caption k's table in its ring slot
+  auto big_of = [&](int k) {
+    return __builtin_amdgcn_readfirstlane(
+        (int)(lds_ldf((k % BD_NB) * BD_BUF + B_XIMG + 6 * 128) != 0.f));
   };
   auto fl = [](const u32x4& x, int q) { return __uint_as_float(x[q & 3]); };
 
-  // softmax state of the caption in SM (a1 overwrites p in place)
-  float a1[16], ax[16], v[16];
+  // softmax state of the caption in SM (p, then A1, in a1)
+  float sd[16], a1[16], ax[16], v[16];
   float s8[8], inv = 0.f, kq = 0.f, rho = 0.f;
   u32x4 fb[2][4], fc[2][2];     // scalars f0..f3 (phase B) / f4, f5 (phase C), by group parity
   uint32_t mw2[8], mc2[8];
-  // SM chunk c (0..63) of the caption with token table tb and G1 results A0, A1
-  auto sm_chunk = [&](int c, uint32_t tb, const f32x16& A0, const f32x16& A1, bf16x8* Mo) {
+  // SM chunk c of the caption with token table tb, stored scores spw (and
+  // region max m, BIG) and Q-hat Q; its M fragments go to Mo.  Phase A (the
+  // exps of softmax 1) starts after the scores' decode
+  auto sm_chunk = [&](auto bigc, int c, uint32_t tb, const uint4 (&spw)[2], float m,
+                      const f32x16& Q, bf16x8* Mo) {
+    constexpr bool BIG = decltype(bigc)::value;
+    constexpr int A0 = 2;
+    constexpr int P = A0 + 8;             // sums of p
+    constexpr int PB = P + 5;             // phase B
+    constexpr int PC = PB + 33;           // phase C
+    // scalar prefetch: f0..f3 of group g four chunks before its phase-B span,
+    // f4, f5 three chunks before its phase-C span
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      if (c == 9 + 8 * g)
+      if (c == PB - 4 + 8 * g)
 #pragma unroll
         for (int k = 0; k < 4; ++k) fb[g & 1][k] = scal(tb, k, g);
-      if (c == 43 + 4 * g) {
+      if (c == PC - 3 + 4 * g) {
         fc[g & 1][0] = scal(tb, 4, g);
         fc[g & 1][1] = scal(tb, 5, g);
       }
     }
-    if (c < 8) {                  // phase A: p = exp2(S') (bias rows: 0)
-      a1[2 * c] = __builtin_amdgcn_exp2f(A0[2 * c]);
-      a1[2 * c + 1] = __builtin_amdgcn_exp2f(A0[2 * c + 1]);
-    } else if (c == 8) {
+    if (c < A0) {                 // decode the stored scores
+      const uint4 w = spw[c];
+      sp_unpack(w.x, sd[8 * c + 0], sd[8 * c + 1]);
+      sp_unpack(w.y, sd[8 * c + 2], sd[8 * c + 3]);
+      sp_unpack(w.z, sd[8 * c + 4], sd[8 * c + 5]);
+      sp_unpack(w.w, sd[8 * c + 6], sd[8 * c + 7]);
+    } else if (c < P) {           // phase A: p = exp2(S' [- m])
+      const int q = 2 * (c - A0);
+      a1[q] = __builtin_amdgcn_exp2f(sd[q]);
+      a1[q + 1] = __builtin_amdgcn_exp2f(sd[q + 1]);
+    } else if (c == P) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) s8[k] = a1[k] + a1[k + 8];
-    } else if (c == 9) {
+    } else if (c == P + 1) {
 #pragma unroll
       for (int k = 4; k < 8; ++k) s8[k] = a1[k] + a1[k + 8];
-    } else if (c == 10) {
+    } else if (c == P + 2) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) s8[k] += s8[k + 4];
-    } else if (c == 11) {
+    } else if (c == P + 3) {
       inv = xhalf_sum((s8[0] + s8[1]) + (s8[2] + s8[3]));
-    } else if (c == 12) {
+    } else if (c == P + 4) {
       inv = __builtin_amdgcn_rcpf(sum_floor(inv));
       kq = gL * inv;
       rho = 0.f;
-    } else if (c < 45) {          // phase B, two chunks per token q
-      const int q = (c - 13) >> 1;
+    } else if (c < PB + 32) {     // phase B, two chunks per token q
+      const int q = (c - PB) >> 1;
       const u32x4* fb_ = fb[(q >> 2) & 1];
-      if (((c - 13) & 1) == 0) {
+      if (((c - PB) & 1) == 0) {
         ax[q] = __builtin_amdgcn_exp2f(fmaf(a1[q], kq, fl(fb_[0], q)));   // g1 A2 / log2e
         a1[q] = a1[q] * inv;                                              // A1
       } else {
         // (dA2 - sigma) = (alpha / log2e) S' + (beta / Z) Q-hat - sigma
-        const float du = fmaf(fl(fb_[1], q), A0[q], fmaf(fl(fb_[2], q), A1[q], -fl(fb_[3], q)));
+        // (BIG: S' = stored + m)
+        const float f3 = BIG ? fmaf(fl(fb_[1], q), m, -fl(fb_[3], q)) : -fl(fb_[3], q);
+        const float du = fmaf(fl(fb_[1], q), sd[q], fmaf(fl(fb_[2], q), Q[q], f3));
         v[q] = a1[q] * (ax[q] * du);                         // A1 dA1 / log2e
         rho += v[q];
       }
-    } else if (c == 45) {
+    } else if (c == PB + 32) {
       rho = xhalf_sum(rho);
-    } else if (c < 62) {          // phase C, one chunk per token q
-      const int q = c - 46;
+    } else if (c < PC + 16) {     // phase C, one chunk per token q
+      const int q = c - PC;
       const u32x4* fc_ = fc[(q >> 2) & 1];
       const float dsx = fmaf(-a1[q], rho, v[q]);              // dS / log2e
       v[q] = fmaf(fl(fc_[0], q), ax[q], dsx);                  // M_w (scaled for W')
@@ -2815,27 +2598,34 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
           Mo[2 + k] = __builtin_bit_cast(bf16x8, make_uint4(mc2[4 * k], mc2[4 * k + 1],
                                                               mc2[4 * k + 2], mc2[4 * k + 3]));
         }
+        // pin phase C here: without a use in this stage the compiler sinks it
+        // past the stage boundary into the next stage's first MFMA gap
         asm volatile("" ::"v"(Mo[0]), "v"(Mo[1]), "v"(Mo[2]), "v"(Mo[3]));
       }
     }
   };
 
-  // one stage t: G1(t+1) -> (A0n, A1n) in the gaps of SM(t) on (A0, A1)
-  auto stage = [&](int t, f32x16& A0, f32x16& A1, f32x16& A0n, f32x16& A1n) {
+  // one stage t: G1(t+1) -> Qn in the gaps of SM(t) on (spc, mc, Q); loads
+  // the scores of caption t+1 into (spn, mn) and returns its variant in bign
+  auto stage = [&](auto bigc, int t, const f32x16& Q, f32x16& Qn, const uint4 (&spc)[2],
+                   float mc, uint4 (&spn)[2], float& mn, int& bign) {
+    constexpr int NCH = 64;            // SM chunks over the 16 MFMA slots
     ring_barrier<0>();                 // B1: X(t+1) landed everywhere
+    sp_load(t + 1, spn, mn);
+    bign = big_of(t + 1);
     const uint32_t x1 = ((t + 1) % BD_NB) * BD_BUF;          // G1 image
     const uint32_t tbs = t < K ? (t % BD_NB) * BD_BUF + B_XIMG : BD_ZERO;
-    const f32x16 init = init_of(x1 + B_XIMG);
     bf16x8 Mo[4];
     u32x4 rd[4];
 #pragma unroll
     for (int n = 0; n < BD_PF1; ++n) rd[n] = g1_read(n, x1);
 #pragma clang loop unroll(full)
-    for (int n = 0; n < 32; ++n) {
-      g1_mfma(n, rd[n & 3], A0n, A1n, init);
-      if (n + BD_PF1 < 32) rd[(n + BD_PF1) & 3] = g1_read(n + BD_PF1, x1);
-      sm_chunk(2 * n, tbs, A0, A1, Mo);
-      sm_chunk(2 * n + 1, tbs, A0, A1, Mo);
+    for (int n = 0; n < 16; ++n) {
+      g1_mfma(n, rd[n & 3], Qn);
+      if (n + BD_PF1 < 16) rd[(n + BD_PF1) & 3] = g1_read(n + BD_PF1, x1);
+#pragma unroll
+      for (int c = n * NCH / 16; c < (n + 1) * NCH / 16; ++c)
+        sm_chunk(bigc, c, tbs, spc, mc, Q, Mo);
       __builtin_amdgcn_sched_barrier(0);
     }
     // M(t-1) consumed by the partner M wave (it reads the slot right after
@@ -2846,11 +2636,18 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
   };
 
   asm volatile("s_barrier" ::: "memory");                             // X(0), X(1) landed
-  f32x16 Aa0, Aa1, Ab0, Ab1;
+  f32x16 Qa, Qb;
+  uint4 spa[2], spq[2];
+  float ma = 0.f, mq = 0.f;
+  int big0 = 0, big1 = 0;
   if (live) {
-    const f32x16 init = init_of(B_XIMG);
+    sp_load(0, spa, ma);
+    big0 = big_of(0);
+    u32x4 rd[16];
 #pragma unroll
-    for (int u = 0; u < 32; ++u) g1_mfma(u, g1_read(u, 0), Aa0, Aa1, init);
+    for (int s = 0; s < 16; ++s) rd[s] = g1_read(s, 0);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) g1_mfma(s, rd[s], Qa);
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");     // G1(0) done
   if (!live) {
@@ -2859,8 +2656,14 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
     return;
   }
   for (int t = 0; t < T2; t += 2) {
-    stage(t, Aa0, Aa1, Ab0, Ab1);
-    stage(t + 1, Ab0, Ab1, Aa0, Aa1);
+    if (big0)
+      stage(std::true_type{}, t, Qa, Qb, spa, ma, spq, mq, big1);
+    else
+      stage(std::false_type{}, t, Qa, Qb, spa, ma, spq, mq, big1);
+    if (big1)
+      stage(std::true_type{}, t + 1, Qb, Qa, spq, mq, spa, ma, big0);
+    else
+      stage(std::false_type{}, t + 1, Qb, Qa, spq, mq, spa, ma, big0);
   }
 }
 
@@ -2963,7 +2766,8 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 int B_img, int B_cap,
                 int img_offset, float gamma1, float gamma2, float gamma3, float eps,
                 float* logits, int ld_logits, float* stats, uint16_t* Chi, uint16_t* Clo,
-                float* att, int att_T, int bounded, int t_pad, int mode, void* stream) {
+                uint16_t* Sp, float* att, int att_T, int bounded, int t_pad, int mode,
+                void* stream) {
   if (B_img <= 0 || B_cap <= 0 || ld_logits < B_cap || !Rhi || !Whi) return 1001;
   if (t_pad != 32 && t_pad != 64) return 1001;
   // the general kernels stage the R lo plane in every mode (read only in
@@ -3019,10 +2823,10 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   else if (mode == MODE_BF16) {
     // R resident in LDS; caption chunks sized for >= ~256 workgroups
     const int n_chunks = max(1, min((B_cap + 3) / 4, (256 + B_img - 1) / B_img));
-    if (bounded && Rnorm && !att && stats && Chi)
+    if (bounded && Rnorm && !att && stats && Chi && Sp)
       hipLaunchKernelGGL(wr_fwd_pipe_kernel, dim3(n_chunks * B_img), dim3(256), FR_LDS, s,
                          Rhi, Whi, Wnorm, Rnorm, lens, B_img, B_cap, n_chunks, gamma1, gamma2,
-                         gamma3, eps, logits, ld_logits, (float4*)stats, Chi);
+                         gamma3, eps, logits, ld_logits, (float4*)stats, Chi, Sp);
     else
       hipLaunchKernelGGL(wr_fwd_res_kernel, dim3(n_chunks * B_img), dim3(256), FR_LDS, s,
                          Rhi, Whi, Wnorm, lens, B_img, B_cap, n_chunks, img_offset, gamma1,
@@ -3049,7 +2853,7 @@ static int wr_tok_launch(const float* stats, const float* Wnorm, const float* Rn
   else if (t_pad == 32)
     hipLaunchKernelGGL(wr_tok_kernel<32>, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, (const float4*)stats, Wnorm, Rnorm, lens, dlogits, ld,
-                       B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 1 : 0, tok_ws, ce);
+                       B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 2 : 0, tok_ws, ce);
   else
     return 1001;
   return (int)hipGetLastError();
@@ -3087,7 +2891,8 @@ int tgfr_wr_bwd_ws(int B_img, int B_cap, int bounded, int t_pad, int mode, long 
 
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, int B_img, int B_cap, float gamma1, const float* tok_ws,
-                const uint16_t* Chi, const uint16_t* Clo, float* dR, long long s_b,
+                const uint16_t* Chi, const uint16_t* Clo, const uint16_t* Sp, float* dR,
+                long long s_b,
                 long long s_r, long long s_d, float* ws, int bounded, int t_pad, int mode,
                 void* stream) {
   if (B_img <= 0 || B_cap <= 0 || !dR || !ws) return 1001;
@@ -3112,11 +2917,12 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
     return frag_reduce(n_chunks, B_img, (const uint16_t*)ws, dR, s_b, s_r, s_d, s,
                        mode == MODE_F16);
   } else if (bounded) {
-    if (t_pad != 32) return 1001;
+    if (t_pad != 32 || !Sp) return 1001;
     if (mode != MODE_BF16) return 1002;
     if (const int e = allow_lds(wr_bwd_duo_kernel, BD_LDS)) return e;
     hipLaunchKernelGGL(wr_bwd_duo_kernel, dim3(grid), dim3(512), BD_LDS, s, Rhi, Whi, B_img,
-                       B_cap, n_chunks, gamma1, tok_ws, Chi, dR, s_b, s_r, s_d, (uint16_t*)ws);
+                       B_cap, n_chunks, gamma1, tok_ws, Chi, Sp, dR, s_b, s_r, s_d,
+                       (uint16_t*)ws);
     return frag_reduce(n_chunks, B_img, (const uint16_t*)ws, dR, s_b, s_r, s_d, s);
   } else if (mode == MODE_SPLIT && (!Rlo || !Wlo || !Clo)) {
     return 1001;
@@ -3166,6 +2972,6 @@ int tgfr_wr_lds_bytes(int which) {
   return which == 0 ? F_LDS : which == 1 ? BwdCfg<MODE_SPLIT>::LDS : FR_LDS;
 }
 
-int tgfr_version(void) { return 400; }
+int tgfr_version(void) { return 500; }
 
 }  // extern "C"

@@ -17,6 +17,9 @@ D = 256
 RPAD = 224
 NREG = 196
 TPAD = 32
+NREG_TILES = RPAD // 32
+SP_REC = 64 * 16 + 64   # stored scores per (pair, region tile), int16 units (csrc SP_REC)
+N_WR_SAVED = 11         # tensors _wr_fwd saves for _wr_bwd
 
 MODES = {"bf16": 0, "fp32": 1, "fp16": 2}
 
@@ -148,13 +151,17 @@ def _wr_fwd(img_features, words, lens, gamma1, gamma2, gamma3, mode, img_offset=
             own_rows = False
             w_fwd, _, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,
                                          want_norms=True, scale=LOG2E, f16=f16)
-        # The max-free kernels are exact while the score bound max|W|
-        # max|R| <= WR_BOUND_MAX (csrc/tgfr_wr.hip, bound_shift).  Rows
-        # made by this package's heads are L2-normalised (bound ~1); other
-        # inputs are checked here (one host read, skipped under graph
-        # capture) and past the bound take the exact running-max kernels,
-        # as the reference's softmax never overflows (models/attention.py:28-36)
-        if bounded and not own_rows and not torch.cuda.is_current_stream_capturing():
+        # 32-token captions: the max-free kernels decide per caption on the
+        # device (a caption whose score bound max|W| max|R| exceeds 84.5
+        # takes their running-max variant), exact for any input, also under
+        # graph capture.  64-token captions: exact while the bound is <=
+        # WR_BOUND_MAX (csrc/tgfr_wr.hip, bound_shift); rows made by this
+        # package's heads are L2-normalised (bound ~1), other inputs are
+        # checked here (one host read, skipped under graph capture) and past
+        # the bound take the exact running-max kernels, as the reference's
+        # softmax never overflows (models/attention.py:28-36)
+        if bounded and t_pad != TPAD and not own_rows and \
+                not torch.cuda.is_current_stream_capturing():
             if not float((w_norm.max() * r_norm.max()).item()) <= WR_BOUND_MAX:
                 bounded = fast = False
         if _rows_only(words) and not fast:
@@ -177,12 +184,16 @@ def _wr_fwd(img_features, words, lens, gamma1, gamma2, gamma3, mode, img_offset=
     c_lo = torch.empty_like(c_hi) if m == MODES["fp32"] else None
     att = torch.zeros(b_img, att_T, NREG, dtype=torch.float32, device=dev) \
         if att_T else None
+    # the scores S' of every (pair, region tile) for the two-role backward,
+    # written by the bounded bf16 forward (fp16 / bf16 bits, accumulator order)
+    sp = torch.empty(b_img, b_cap, NREG_TILES, SP_REC, dtype=torch.int16, device=dev) \
+        if fast and t_pad == TPAD else None
     call("tgfr_wr_fwd", ptr(r_hi), ptr(r_lo), ptr(w_fwd), ptr(w_lo), ptr(w_norm),
          ptr(r_norm), ptr(lens), b_img, b_cap, img_offset, gamma1, gamma2, gamma3, eps,
-         ptr(logits), b_cap, ptr(stats), ptr(c_hi), ptr(c_lo), ptr(att), att_T,
+         ptr(logits), b_cap, ptr(stats), ptr(c_hi), ptr(c_lo), ptr(sp), ptr(att), att_T,
          int(bool(bounded) and (t_pad == TPAD or m != MODES["fp32"])), t_pad, m,
          _hip.stream())
-    saved = (r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo)
+    saved = (r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo, sp)
     cfg = (gamma1, gamma2, gamma3, eps, m, img_features.shape, fast, t_pad)
     return logits, att, saved, cfg
 
@@ -191,7 +202,7 @@ def _wr_bwd(saved, cfg, tok_call):
     """WordRegionLogits' backward: d img_features, with the per-(pair, token)
     table made by tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, fast,
     t_pad, tok) (tgfr_wr_bwd_tok from dlogits, or tgfr_wr_bwd_tok_ce)."""
-    r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo = saved
+    r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo, sp = saved
     gamma1, gamma2, gamma3, eps, m, shape, fast, t_pad = cfg
     b_img, b_cap = stats.shape[0], stats.shape[1]
     dev = stats.device
@@ -203,7 +214,7 @@ def _wr_bwd(saved, cfg, tok_call):
     d_reg = torch.empty(b_img, NREG, D, dtype=torch.float32, device=dev)
     call("tgfr_wr_bwd", ptr(r_hi), ptr(r_lo) if split else None, ptr(w_hi),
          ptr(w_lo) if split else None, b_img, b_cap, gamma1, ptr(tok),
-         ptr(c_hi), ptr(c_lo) if split else None, ptr(d_reg), NREG * D, D, 1, ptr(ws),
+         ptr(c_hi), ptr(c_lo) if split else None, ptr(sp), ptr(d_reg), NREG * D, D, 1, ptr(ws),
          int(fast), t_pad, m, _hip.stream())
     # same logical shape as img_features, channels-last strides
     return d_reg.transpose(1, 2).reshape(shape)
@@ -270,7 +281,7 @@ class WordRegionCE(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g0, g1):
         saved = ctx.saved_tensors
-        logits, row_lse, col_lse = saved[10:]
+        logits, row_lse, col_lse = saved[N_WR_SAVED:]
         gamma1, gamma2, gamma3, eps = ctx.cfg[:4]
         w0 = 0.0 if g0 is None else 1.0
         w1 = 0.0 if g1 is None else 1.0
@@ -282,7 +293,7 @@ class WordRegionCE(torch.autograd.Function):
                  b_cap, gamma1, gamma2, gamma3, eps, ptr(logits), logits.shape[1], 0,
                  ctx.inv_n, ptr(row_lse), ptr(col_lse), ptr(g0), ptr(g1), w0, w1, int(fast),
                  t_pad, ptr(tok), _hip.stream())
-        return (_wr_bwd(saved[:10], ctx.cfg, tok_call),) + (None,) * 9
+        return (_wr_bwd(saved[:N_WR_SAVED], ctx.cfg, tok_call),) + (None,) * 9
 
 
 def word_region_logits(img_features, words, lens, gamma1, gamma2, gamma3,

@@ -18,50 +18,99 @@ from text_guided_face_recognition_amd import build as B  # noqa: E402
 OUT = os.path.join(ROOT, "tools", "lab", "build")
 
 # name -> list of (old, new) substitutions in tgfr_wr.hip
-# round 4: the two-role backward (wr_bwd_duo_kernel) against round 3's
-# one-wave-per-SIMD pipe kernel
-_DUO = ("""    if (const int e = allow_lds(wr_bwd_duo_kernel, BD_LDS)) return e;
-    hipLaunchKernelGGL(wr_bwd_duo_kernel, dim3(grid), dim3(512), BD_LDS, s, Rhi, Whi, B_img,""")
-_PIPE = ("""    if (const int e = allow_lds(wr_bwd_pipe_kernel, BP_LDS)) return e;
-    hipLaunchKernelGGL(wr_bwd_pipe_kernel, dim3(grid), dim3(256), BP_LDS, s, Rhi, Whi, B_img,""")
-# ablations of the two-role backward (timing only: results are wrong)
-_SM = ("""      sm_chunk(2 * n, tbs, A0, A1, Mo);
-      sm_chunk(2 * n + 1, tbs, A0, A1, Mo);""")
+# round 5: the two-role backward on the forward's stored scores
+_SM = ("""        sm_chunk(bigc, c, tbs, spc, mc, Q, Mo);""")
 _G3 = ("""          dR[n >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Mi[n & 3], rd[n & 7], dR[n >> 2],
                                                               0, 0, 0);""")
 _DMA = ("""          if (bd_dma_slot(n) >= 0) dma_piece(t + 2, bd_dma_slot(n));""")
+_G1 = ("""      g1_mfma(n, rd[n & 3], Qn);""")
 _SWAVE = ("""  // ================================================================== S wave
   const float gL = g1 * 1.4426950408889634f;""")
 _MWAVE = ("""    // ================================================================ M wave
-    // DMA pieces of one caption (bwd_stage's layout): M wave wid issues""")
+    // DMA pieces of one caption: M wave wid issues pieces k = wid + 4 j""")
+# per-stage s_memtime stamps (tools/lab/stamps.py reads them back through
+# tgfr_lab_stamps): S wave after B1 / after its slot loop / after the M-slot
+# wait; M wave after B1 / after its G3 loop
+_STAMP_DECL = ("""constexpr int BD_NB = 4;                        // X ring depth""",
+               """__device__ unsigned long long g_st[256 * 8 * 64 * 4];
+#define STAMP(t, k) do { if (blockIdx.x < 256 && (t) < 64) \\
+  g_st[((blockIdx.x * 8 + wv) * 64 + (t)) * 4 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+constexpr int BD_NB = 4;                        // X ring depth""")
+_STAMPS = [
+    _STAMP_DECL,
+    ("""      ring_barrier<0>();                       // B1: X(t+1) landed; M(t-1) written
+""", """      ring_barrier<0>();                       // B1: X(t+1) landed; M(t-1) written
+      STAMP(t, 0);
+"""),
+    ("""          if (bd_dma_slot(n) >= 0) dma_piece(t + 2, bd_dma_slot(n));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+""", """          if (bd_dma_slot(n) >= 0) dma_piece(t + 2, bd_dma_slot(n));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        STAMP(t, 1);
+"""),
+    ("""    ring_barrier<0>();                 // B1: X(t+1) landed everywhere
+    sp_load(t + 1, spn, mn);""", """    ring_barrier<0>();                 // B1: X(t+1) landed everywhere
+    STAMP(t, 0);
+    sp_load(t + 1, spn, mn);"""),
+    ("""    lds_wait_ge(BD_CNT + 4 * wid, t + 1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lds_st16(ms + k * 1024, __builtin_bit_cast(uint4, Mo[k]));""",
+     """    STAMP(t, 1);
+    lds_wait_ge(BD_CNT + 4 * wid, t + 1);
+    STAMP(t, 2);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lds_st16(ms + k * 1024, __builtin_bit_cast(uint4, Mo[k]));"""),
+    ("""int tgfr_version(void) { return 500; }""",
+     """int tgfr_version(void) { return 500; }
+int tgfr_lab_stamps(void* dst) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_st), sizeof(g_st), 0, hipMemcpyDeviceToHost);
+}"""),
+]
 VARIANTS = {
     "base": [],
     "head": "HEAD",
-    "pipe": [(_DUO, _PIPE)],          # round 3's one-wave-per-SIMD backward
-    # the second workgroup barrier per stage (before round 4's pairwise counter)
-    "b2": [("""        if (lane == 0) lds_st_release(BD_CNT + 4 * wid, t + 1);""", ""),
-           ("""        for (int j = 0; j < 9; ++j) dma_piece(t + 2, j);
-      }
-    }""", """        for (int j = 0; j < 9; ++j) dma_piece(t + 2, j);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");
-    }"""),
-           ("""    lds_wait_ge(BD_CNT + 4 * wid, t + 1);""",
-            """    asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");"""),
-           ("""    for (int t = 0; t < T2; ++t) asm volatile("s_barrier" ::: "memory");""",
-            """    for (int t = 0; t < T2; ++t) asm volatile("s_barrier\\n\\ts_barrier" ::: "memory");""")],
-    "nosm": [(_SM, """      asm volatile("" ::"v"(A0), "v"(A1));""")],
+    "stamp": _STAMPS,
+    # ablations of the two-role backward (timing only: results are wrong)
+    "nosm": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));""")],
     "nog3": [(_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));""")],
+    "nog1": [(_G1, """      asm volatile("" ::"v"(rd[n & 3]));""")],
     "nodma": [(_DMA, "")],
-    "prio_s": [(_SWAVE, _SWAVE + "\n  __builtin_amdgcn_s_setprio(1);")],
-    "pf1_5": [("constexpr int BD_PF1 = 3;", "constexpr int BD_PF1 = 5;")],
-    "pf3_6": [("constexpr int BD_PF3 = 4;", "constexpr int BD_PF3 = 6;")],
-    "pf56": [("constexpr int BD_PF1 = 3;", "constexpr int BD_PF1 = 5;"),
-             ("constexpr int BD_PF3 = 4;", "constexpr int BD_PF3 = 6;")],
+    # timing probes: the stored scores / the X images always from the chunk's
+    # first caption (L2-resident: no HBM latency behind the loads)
+    "spl2": [("""    const uint16_t* rec = spb + (long long)min(k, K - 1) * (NRT * SP_REC);""",
+              """    const uint16_t* rec = spb;""")],
+    "dmal2": [("""      const int kc = min(k, K - 1);
+      const uint32_t base = (k % BD_NB) * BD_BUF;""", """      const int kc = 0;
+      const uint32_t base = (k % BD_NB) * BD_BUF;""")],
+    "skel": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
+             (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
+             (_G1, """      asm volatile("" ::"v"(rd[n & 3]));""")],
+    "skel_nodma": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
+                   (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
+                   (_G1, """      asm volatile("" ::"v"(rd[n & 3]));"""), (_DMA, "")],
+    "mfma_only": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
+                  (_DMA, "")],
+    "pf3_7": [("constexpr int BD_PF3 = 4;", "constexpr int BD_PF3 = 7;")],
+    "skel_l2": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
+                (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
+                (_G1, """      asm volatile("" ::"v"(rd[n & 3]));"""),
+                ("""      const int kc = min(k, K - 1);
+      const uint32_t base = (k % BD_NB) * BD_BUF;""", """      const int kc = 0;
+      const uint32_t base = (k % BD_NB) * BD_BUF;""")],
+    "skel_chat": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
+                  (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
+                  (_G1, """      asm volatile("" ::"v"(rd[n & 3]));"""),
+                  ("""          if (bd_dma_slot(n) >= 0) dma_piece(t + 2, bd_dma_slot(n));""",
+                   """          if (bd_dma_slot(n) >= 0 && (bd_dma_slot(n) % 4 >= 2 || bd_dma_slot(n) == 8)) dma_piece(t + 2, bd_dma_slot(n));""")],
+    "skel_notr": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
+                  (_G3, """          asm volatile("" ::"v"(Mi[n & 3]));"""),
+                  ("""          if (n + BD_PF3 < 32) rd[(n + BD_PF3) & 7] = g3_read(n + BD_PF3, x3);""", ""),
+                  (_G1, """      asm volatile("" ::"v"(rd[n & 3]));""")],
     "dma_early": [("return (n >= 1 && n <= 17 && (n & 1) == 1) ? (n - 1) / 2 : -1;",
                    "return n < 9 ? n : -1;")],
-    "prio_s2": [(_SWAVE, _SWAVE + "\n  __builtin_amdgcn_s_setprio(2);"),
-                (_MWAVE, _MWAVE.replace("    // DMA", "    __builtin_amdgcn_s_setprio(0);\n    // DMA"))],
+    "prio_s": [(_SWAVE, _SWAVE + "\n  __builtin_amdgcn_s_setprio(1);")],
     "prio_m": [(_MWAVE, _MWAVE.replace("    // DMA", "    __builtin_amdgcn_s_setprio(1);\n    // DMA"))],
 }
 

@@ -959,7 +959,8 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
 // term overflows and no region's sum underflows while c <= 84.5 (c = 1 for
 // the L2-normalised BERT-path features, models/models.py:212,403; <= 16 for
 // the LSTM's tanh outputs against unit regions).  A caption whose c exceeds
-// 84.5 (BIG_C; wave-uniform, formed on the device from the row norms) takes
+// BIG_C = 10 (wave-uniform, formed on the device from the row norms; the
+// backward keeps p = exp2(S') in fp16, finite while c < 11) takes
 // the running-max variant of the same pipeline (a uniform branch per caption
 // into a second instantiation of the body): each region's max over the words
 // is subtracted before the exp, exactly as the reference's softmax
@@ -976,7 +977,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
 // the words: values <= 0, fp16-exact near the max, clamped at -60000) plus
 // m_r itself as fp32 -- one SP_REC record per (pair, region tile).  No
 // attention maps (the host uses wr_fwd_res_kernel for those).
-constexpr float BIG_C = 84.5f;
+constexpr float BIG_C = 10.f;
 constexpr float PAD_BIAS = -60000.f;
 constexpr int SP_REC = 64 * 16 + 64;   // uint16 per (pair, tile): 64 lanes x 16 fp16 + 32 fp32 m_r
 // the score bound's image factor max_r |R_r| (norm rows 0..223; one wave):
@@ -1003,6 +1004,18 @@ __device__ __forceinline__ uint4 sp_pack(const f32x16& v, int o, float m) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+// fp32 results of fp16 operands on v_fma_mix_f32 (the conversion is free):
+// h * f, and h + g
+__device__ __forceinline__ float mix_mul(_Float16 h, float f) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(h), "v"(f));
+  return d;
+}
+__device__ __forceinline__ float mix_add(_Float16 h, _Float16 g) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel_hi:[1,0,1]" : "=v"(d) : "v"(h), "v"(g));
+  return d;
+}
 // one 32-bit word of a stored S' tile -> two fp32 scores
 __device__ __forceinline__ void sp_unpack(uint32_t w, float& a, float& b) {
   const f16x2 h = __builtin_bit_cast(f16x2, w);
@@ -1022,10 +1035,10 @@ __device__ __forceinline__ void mfma_result_wait(f32x16& acc) {
 }
 
 // slot decode of a 34-slot stage: G1 x4, (G2 G1) x12, G2 x6
-__device__ __forceinline__ constexpr bool s34_is_g1(int m) {
+__host__ __device__ constexpr bool s34_is_g1(int m) {
   return m < 4 || (m < 28 && ((m - 4) & 1));
 }
-__device__ __forceinline__ constexpr int s34_idx(int m) {
+__host__ __device__ constexpr int s34_idx(int m) {
   return m < 4 ? m : m < 28 ? ((m - 4) & 1 ? 4 + (m - 4) / 2 : (m - 4) / 2) : 12 + (m - 28);
 }
 
@@ -1037,11 +1050,10 @@ struct FwdSlot {
   int m;      // slot within the stage
 };
 constexpr int FWD_SLOTS = 16 + 5 * 34 + 18 + 34;
-// LDS operand prefetch distance in MFMA slots (ring of 8; see the wrap
-// argument at the issue site: no live slot is overwritten for 3 <= PF <= 6)
+// LDS operand prefetch distance in MFMA slots (see fwd_ring)
 constexpr int PF_FWD = 3;
 // the caption's slots in issue order
-__device__ __forceinline__ constexpr FwdSlot fwd_slot(int n) {
+__host__ __device__ constexpr FwdSlot fwd_slot(int n) {
   if (n < 16) return {0, 1, n, 0, n};
   if (n < 186) {
     const int j = 1 + (n - 16) / 34, m = (n - 16) % 34;
@@ -1053,8 +1065,34 @@ __device__ __forceinline__ constexpr FwdSlot fwd_slot(int n) {
   return s34_is_g1(m) ? FwdSlot{0, 0, s34_idx(m), 7, m} : FwdSlot{1, 6, s34_idx(m), 7, m};
 }
 // GEMM2 index v -> k block s (16 regions) and d tile (8 = the Z row of ones)
-__device__ __forceinline__ constexpr int g2_s(int v) { return v < 9 ? 0 : 1; }
-__device__ __forceinline__ constexpr int g2_dt(int v) { return v < 9 ? v : v - 9; }
+__host__ __device__ constexpr int g2_s(int v) { return v < 9 ? 0 : 1; }
+__host__ __device__ constexpr int g2_dt(int v) { return v < 9 ? v : v - 9; }
+// the LDS operand ring is indexed by the count of operand-reading slots
+// before slot n (the Z row's 14 slots per caption read nothing): 224 reads
+// per caption, a multiple of the ring's 4, so the index runs on across the
+// caption seam and 4 registers hold every read in flight (PF_FWD = 3)
+__host__ __device__ constexpr bool fwd_reads(int n) {
+  return fwd_slot(n).kind == 0 || g2_dt(fwd_slot(n).idx) < 8;
+}
+struct FwdRing {
+  int r[FWD_SLOTS];
+};
+__host__ __device__ constexpr FwdRing make_fwd_ring() {
+  FwdRing t{};
+  int c = 0;
+  for (int n = 0; n < FWD_SLOTS; ++n) {
+    t.r[n] = c & 3;
+    c += fwd_reads(n) ? 1 : 0;
+  }
+  return t;
+}
+constexpr FwdRing kFwdRing = make_fwd_ring();
+static_assert([] {
+  int c = 0;
+  for (int n = 0; n < FWD_SLOTS; ++n) c += fwd_reads(n) ? 1 : 0;
+  return c % 4 == 0;
+}(), "operand reads per caption must be a multiple of the ring size");
+__device__ __forceinline__ int fwd_ring(int n) { return kFwdRing.r[n]; }
 
 __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi,
@@ -1098,7 +1136,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     const int len = lens[ii];
     const float c = half_max(wn) * rmax;
     big = __builtin_amdgcn_readfirstlane((int)(c > BIG_C));
-    const float pad = big ? -1e30f : PAD_BIAS;
+    const float pad = big ? -1e30f : PAD_BIAS;   // (big: valid scores may lie below PAD_BIAS)
     f32x16 init;
 #pragma unroll
     for (int q = 0; q < 16; ++q) init[q] = acc_row(q, h) < len ? 0.f : pad;
@@ -1146,7 +1184,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
       Wc[s] = as_bf8(*(const uint4*)(Whi + ((long long)ii * TPAD + lr) * D + s * 16 + h * 8));
   };
   // LDS operand reads, ring indexed by slot, issued PF_FWD slots ahead
-  u32x4 rd[8];
+  u32x4 rd[4];
   auto issue_read = [&](const FwdSlot sl, u32x4& dst) {
     if (sl.kind == 0) {
       const int s = sl.idx;
@@ -1167,6 +1205,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
   float np[16], p[16];
   uint32_t pk[8];
   float ma[4], kk = 0.f, rm = 0.f;
+  uint32_t spk[4];
   // softmax chunk c (0..31) of the tile in S (region tile j), E^T -> etb;
   // chunks 0-3 store the tile's scores for the backward (and, big, form each
   // region's max over the words first)
@@ -1180,16 +1219,24 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
           ((float*)(spt + 1024))[lr] = rm;     // (both halves: the same value)
         }
       }
-      if (c >= 2) *(uint4*)(spt + lane * 16 + 8 * (c - 2)) = sp_pack<BIG>(S, 8 * (c - 2), rm);
     } else if (c < 12) {
+      // p = exp2(S' [- m]) and the stored fp16 pair of the same values (one
+      // read of the accumulators for both); 16 B out after every 4 pairs
       const int q = 2 * (c - 4);
+      float s0 = S[q], s1 = S[q + 1];
       if constexpr (BIG) {
-        p[q] = __builtin_amdgcn_exp2f(S[q] - rm);
-        p[q + 1] = __builtin_amdgcn_exp2f(S[q + 1] - rm);
-      } else {
-        p[q] = __builtin_amdgcn_exp2f(S[q]);
-        p[q + 1] = __builtin_amdgcn_exp2f(S[q + 1]);
+        s0 -= rm;
+        s1 -= rm;
       }
+      p[q] = __builtin_amdgcn_exp2f(s0);
+      p[q + 1] = __builtin_amdgcn_exp2f(s1);
+      if constexpr (BIG) {
+        s0 = fmaxf(s0, PAD_BIAS);
+        s1 = fmaxf(s1, PAD_BIAS);
+      }
+      spk[(q >> 1) & 3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(s0, s1));
+      if ((q & 6) == 6)
+        *(uint4*)(spt + lane * 16 + (q & 8)) = make_uint4(spk[0], spk[1], spk[2], spk[3]);
     } else if (c == 12) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) ma[q] = p[q] + p[q + 8];
@@ -1228,7 +1275,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     S[0] = acc;
   }
 #pragma unroll
-  for (int n = 0; n < PF_FWD; ++n) issue_read(fwd_slot(n), rd[n]);
+  for (int n = 0; n < PF_FWD; ++n) issue_read(fwd_slot(n), rd[fwd_ring(n)]);
 
   // one caption (and the next one's GEMM1 of tile 0); bigc: this caption's
   // variant (std::true_type: running max)
@@ -1251,7 +1298,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
       if (stage >= 1 && m == 0) eb[0] = read_e(etg, 0);
       if (stage >= 1 && m == (stage == 6 ? 5 : 14)) eb[1] = read_e(etg, 1);
       // ---- the MFMA of this slot
-      const u32x4 opnd = rd[n & 7];
+      const u32x4 opnd = rd[fwd_ring(n)];
       if (sl.kind == 0) {
         // builtins (not inline asm): the compiler's hazard recognizer then
         // places the VALU-write -> MFMA-read and MFMA -> VALU-read waits
@@ -1268,7 +1315,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
           C[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, eb[s], C[dt], 0, 0, 0);
       }
       // ---- reads of the slot three ahead (wrapping into the next caption)
-      issue_read(fwd_slot((n + PF_FWD) % FWD_SLOTS), rd[((n + PF_FWD) % FWD_SLOTS) & 7]);
+      issue_read(fwd_slot((n + PF_FWD) % FWD_SLOTS), rd[fwd_ring((n + PF_FWD) % FWD_SLOTS)]);
       // ---- the softmax VALU of this slot
       if (stage <= 6) {
         const int j = stage;                       // softmax tile
@@ -2310,7 +2357,11 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
 // f2 = beta / Z, f3 = sigma, f4 = alpha / g1, f5 = beta log2e / (g1 Z),
 // row 6 = the pair's variant (1: c > BIG_C: the stored scores are S' - m_r,
 // so p = exp2(stored) is the forward's running-max softmax term, and the
-// score itself is stored + m_r).  An element costs 2 exp2 + ~14 VALU.
+// score itself is stored + m_r).  p = exp2 of the fp16 score in fp16
+// (v_exp_f16: |S'| <= log2(e) BIG_C keeps p and its 32-term sum finite;
+// terms below 2^-24 of a BIG_C caption's max flush, as fp32 would far below
+// the sum's rounding), read by v_fma_mix_f32 wherever it enters fp32 math, so
+// the scores need no conversion pass.  An element costs 2 exp + ~12 VALU.
 constexpr int BD_NB = 4;                        // X ring depth
 constexpr int BD_TOK = 1024;                    // token table bytes
 constexpr int BD_BUF = B_XIMG + BD_TOK;         // one caption: X image + token table
@@ -2322,10 +2373,10 @@ constexpr int BD_PF1 = 3;                       // G1 operand prefetch distance 
 constexpr int BD_PF3 = 4;                       // G3 operand prefetch distance (slots)
 
 // MFMA slot of the M wave's stage after which DMA piece j of X(t + 2) is
-// issued (-1: none): every other slot from slot 1
-__device__ __forceinline__ constexpr int bd_dma_slot(int n) {
-  return (n >= 1 && n <= 17 && (n & 1) == 1) ? (n - 1) / 2 : -1;
-}
+// issued (-1: none): one per slot from slot 0 (round 5, config 2: 69.9 us
+// against 72.3 with a piece every other slot from slot 1 -- the pieces must
+// land by the next stage barrier, so the earlier the better)
+__device__ __forceinline__ constexpr int bd_dma_slot(int n) { return n < 9 ? n : -1; }
 
 // LDS hand-off counters between the waves of one workgroup: a release store
 // after the consumer's reads, an acquire load before the producer's writes
@@ -2511,9 +2562,16 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
         (int)(lds_ldf((k % BD_NB) * BD_BUF + B_XIMG + 6 * 128) != 0.f));
   };
   auto fl = [](const u32x4& x, int q) { return __uint_as_float(x[q & 3]); };
+  // scores q, q + 1 (q even) of a stored tile as an fp16 pair
+  auto sc16 = [](const uint4 (&w)[2], int q) {
+    const uint4 v = w[q >> 3];
+    const int k = (q >> 1) & 3;
+    return __builtin_bit_cast(f16x2, k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w);
+  };
 
-  // softmax state of the caption in SM (p, then A1, in a1)
-  float sd[16], a1[16], ax[16], v[16];
+  // softmax state of the caption in SM (p in fp16; A1 in a1)
+  _Float16 ph[16];
+  float a1[16], ax[16], v[16];
   float s8[8], inv = 0.f, kq = 0.f, rho = 0.f;
   u32x4 fb[2][4], fc[2][2];     // scalars f0..f3 (phase B) / f4, f5 (phase C), by group parity
   uint32_t mw2[8], mc2[8];
@@ -2523,7 +2581,7 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
   auto sm_chunk = [&](auto bigc, int c, uint32_t tb, const uint4 (&spw)[2], float m,
                       const f32x16& Q, bf16x8* Mo) {
     constexpr bool BIG = decltype(bigc)::value;
-    constexpr int A0 = 2;
+    constexpr int A0 = 0;
     constexpr int P = A0 + 8;             // sums of p
     constexpr int PB = P + 5;             // phase B
     constexpr int PC = PB + 33;           // phase C
@@ -2539,22 +2597,17 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
         fc[g & 1][1] = scal(tb, 5, g);
       }
     }
-    if (c < A0) {                 // decode the stored scores
-      const uint4 w = spw[c];
-      sp_unpack(w.x, sd[8 * c + 0], sd[8 * c + 1]);
-      sp_unpack(w.y, sd[8 * c + 2], sd[8 * c + 3]);
-      sp_unpack(w.z, sd[8 * c + 4], sd[8 * c + 5]);
-      sp_unpack(w.w, sd[8 * c + 6], sd[8 * c + 7]);
-    } else if (c < P) {           // phase A: p = exp2(S' [- m])
+    if (c < P) {                  // phase A: p = exp2(S' [- m]), fp16
       const int q = 2 * (c - A0);
-      a1[q] = __builtin_amdgcn_exp2f(sd[q]);
-      a1[q + 1] = __builtin_amdgcn_exp2f(sd[q + 1]);
+      const f16x2 h = sc16(spw, q);
+      ph[q] = __builtin_elementwise_exp2(h[0]);
+      ph[q + 1] = __builtin_elementwise_exp2(h[1]);
     } else if (c == P) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) s8[k] = a1[k] + a1[k + 8];
+      for (int k = 0; k < 4; ++k) s8[k] = mix_add(ph[k], ph[k + 8]);
     } else if (c == P + 1) {
 #pragma unroll
-      for (int k = 4; k < 8; ++k) s8[k] = a1[k] + a1[k + 8];
+      for (int k = 4; k < 8; ++k) s8[k] = mix_add(ph[k], ph[k + 8]);
     } else if (c == P + 2) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) s8[k] += s8[k + 4];
@@ -2568,13 +2621,14 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
       const int q = (c - PB) >> 1;
       const u32x4* fb_ = fb[(q >> 2) & 1];
       if (((c - PB) & 1) == 0) {
-        ax[q] = __builtin_amdgcn_exp2f(fmaf(a1[q], kq, fl(fb_[0], q)));   // g1 A2 / log2e
-        a1[q] = a1[q] * inv;                                              // A1
+        ax[q] = __builtin_amdgcn_exp2f(fmaf((float)ph[q], kq, fl(fb_[0], q)));   // g1 A2 / log2e
+        a1[q] = mix_mul(ph[q], inv);                                            // A1
       } else {
         // (dA2 - sigma) = (alpha / log2e) S' + (beta / Z) Q-hat - sigma
         // (BIG: S' = stored + m)
         const float f3 = BIG ? fmaf(fl(fb_[1], q), m, -fl(fb_[3], q)) : -fl(fb_[3], q);
-        const float du = fmaf(fl(fb_[1], q), sd[q], fmaf(fl(fb_[2], q), Q[q], f3));
+        const float du = fmaf(fl(fb_[1], q), (float)sc16(spw, q & ~1)[q & 1],
+                              fmaf(fl(fb_[2], q), Q[q], f3));
         v[q] = a1[q] * (ax[q] * du);                         // A1 dA1 / log2e
         rho += v[q];
       }
@@ -2612,7 +2666,10 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
     constexpr int NCH = 64;            // SM chunks over the 16 MFMA slots
     ring_barrier<0>();                 // B1: X(t+1) landed everywhere
     sp_load(t + 1, spn, mn);
-    bign = big_of(t + 1);
+    // caption t+1's variant flag: read now, made uniform at the stage's end
+    // (its LDS latency off the stage head)
+    const float bigv = lds_ldf(((t + 1) % BD_NB) * BD_BUF + B_XIMG + 6 * 128);
+    int cnt = 0;
     const uint32_t x1 = ((t + 1) % BD_NB) * BD_BUF;          // G1 image
     const uint32_t tbs = t < K ? (t % BD_NB) * BD_BUF + B_XIMG : BD_ZERO;
     bf16x8 Mo[4];
@@ -2626,11 +2683,17 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
 #pragma unroll
       for (int c = n * NCH / 16; c < (n + 1) * NCH / 16; ++c)
         sm_chunk(bigc, c, tbs, spc, mc, Q, Mo);
+      // the partner's M-slot counter, read mid-stage (latency hidden)
+      if (n == 8)
+        cnt = __hip_atomic_load((LDS_AS int*)(lds_base() + BD_CNT + 4 * wid), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_WORKGROUP);
       __builtin_amdgcn_sched_barrier(0);
     }
+    bign = __builtin_amdgcn_readfirstlane((int)(bigv != 0.f));
     // M(t-1) consumed by the partner M wave (it reads the slot right after
     // B1 of stage t, so this rarely waits), then M(t) into the slot
-    lds_wait_ge(BD_CNT + 4 * wid, t + 1);
+    if (cnt < t + 1) lds_wait_ge(BD_CNT + 4 * wid, t + 1);
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int k = 0; k < 4; ++k) lds_st16(ms + k * 1024, __builtin_bit_cast(uint4, Mo[k]));
   };

@@ -54,14 +54,12 @@ _STAMPS = [
     sp_load(t + 1, spn, mn);""", """    ring_barrier<0>();                 // B1: X(t+1) landed everywhere
     STAMP(t, 0);
     sp_load(t + 1, spn, mn);"""),
-    ("""    lds_wait_ge(BD_CNT + 4 * wid, t + 1);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) lds_st16(ms + k * 1024, __builtin_bit_cast(uint4, Mo[k]));""",
+    ("""    if (cnt < t + 1) lds_wait_ge(BD_CNT + 4 * wid, t + 1);
+    asm volatile("" ::: "memory");""",
      """    STAMP(t, 1);
-    lds_wait_ge(BD_CNT + 4 * wid, t + 1);
-    STAMP(t, 2);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) lds_st16(ms + k * 1024, __builtin_bit_cast(uint4, Mo[k]));"""),
+    if (cnt < t + 1) lds_wait_ge(BD_CNT + 4 * wid, t + 1);
+    asm volatile("" ::: "memory");
+    STAMP(t, 2);"""),
     ("""int tgfr_version(void) { return 500; }""",
      """int tgfr_version(void) { return 500; }
 int tgfr_lab_stamps(void* dst) {
@@ -108,8 +106,27 @@ VARIANTS = {
                   (_G3, """          asm volatile("" ::"v"(Mi[n & 3]));"""),
                   ("""          if (n + BD_PF3 < 32) rd[(n + BD_PF3) & 7] = g3_read(n + BD_PF3, x3);""", ""),
                   (_G1, """      asm volatile("" ::"v"(rd[n & 3]));""")],
-    "dma_early": [("return (n >= 1 && n <= 17 && (n & 1) == 1) ? (n - 1) / 2 : -1;",
-                   "return n < 9 ? n : -1;")],
+    "fblead": [("      if (c == PB - 4 + 8 * g)", "      if (c == PB - 8 + 8 * g)")],
+    "fblead2": [("      if (c == PB - 4 + 8 * g)", "      if (c == PB - 8 + 8 * g)"),
+                ("      if (c == PC - 3 + 4 * g) {", "      if (c == PC - 4 + 4 * g) {")],
+    "pf1_4": [("constexpr int BD_PF1 = 3; ", "constexpr int BD_PF1 = 4; "),
+              ("    u32x4 rd[4];\n#pragma unroll\n    for (int n = 0; n < BD_PF1; ++n) rd[n] = g1_read(n, x1);",
+               "    u32x4 rd[8];\n#pragma unroll\n    for (int n = 0; n < BD_PF1; ++n) rd[n] = g1_read(n, x1);"),
+              ("      g1_mfma(n, rd[n & 3], Qn);\n      if (n + BD_PF1 < 16) rd[(n + BD_PF1) & 3] = g1_read(n + BD_PF1, x1);",
+               "      g1_mfma(n, rd[n & 7], Qn);\n      if (n + BD_PF1 < 16) rd[(n + BD_PF1) & 7] = g1_read(n + BD_PF1, x1);")],
+    # forward probes: one caption body only (big captions wrong: timing), no S' stores
+    "fnobig": [("""    if (big_cur)
+      caption(std::true_type{});
+    else
+      caption(std::false_type{});""", """    caption(std::false_type{});""")],
+    "fnostore": [("""        *(uint4*)(spt + lane * 16 + (q & 8)) = make_uint4(spk[0], spk[1], spk[2], spk[3]);""",
+                  """        asm volatile("" ::"v"(spk[0]), "v"(spk[1]), "v"(spk[2]), "v"(spk[3]));""")],
+    "fnoboth": [("""    if (big_cur)
+      caption(std::true_type{});
+    else
+      caption(std::false_type{});""", """    caption(std::false_type{});"""),
+                ("""        *(uint4*)(spt + lane * 16 + (q & 8)) = make_uint4(spk[0], spk[1], spk[2], spk[3]);""",
+                  """        asm volatile("" ::"v"(spk[0]), "v"(spk[1]), "v"(spk[2]), "v"(spk[3]));""")],
     "prio_s": [(_SWAVE, _SWAVE + "\n  __builtin_amdgcn_s_setprio(1);")],
     "prio_m": [(_MWAVE, _MWAVE.replace("    // DMA", "    __builtin_amdgcn_s_setprio(1);\n    // DMA"))],
 }

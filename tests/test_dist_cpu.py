@@ -21,8 +21,15 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from text_guided_face_recognition_amd.dist import DistContext
-        from text_guided_face_recognition_amd.kernels import (combine_col_partials,
-                                                              exchange_col_partials)
+        from text_guided_face_recognition_amd.kernels import gather_col_partials
+
+        def combine_col_partials(parts):
+            # the math of tgfr_col_lse_combine (a kernel: device tensors only)
+            gmax = parts[:, 0].max(0).values
+            return gmax + torch.log((parts[:, 1] * torch.exp(parts[:, 0] - gmax)).sum(0))
+
+        def exchange_col_partials(part, group):
+            return combine_col_partials(gather_col_partials(part, group))
         torch.manual_seed(0)
         b_l = 3
         full = torch.randn(world * b_l, world * b_l) * 4            # global logits

@@ -102,3 +102,43 @@ def test_overlapped_grad_reduce_graphed(gpu, precision):
         assert (out_g[k] - outs_e[-1][k]).abs().max().item() < 1e-4, k
     for a, b in zip(graphed.params, eager.params):
         assert (a - b).abs().max().item() < 1e-5
+
+
+def test_dp_glue_kernels(gpu):
+    """The data-parallel glue on the device: tgfr_col_lse_combine against the
+    log-sum-exp of the gathered row blocks, and tgfr_focal_global (pack, a
+    simulated 3-rank sum, finish) against FocalLoss on the global mean CE
+    (models/losses.py:313-325)."""
+    from text_guided_face_recognition_amd import kernels as K
+    from text_guided_face_recognition_amd._hip import call, ptr, stream
+    torch.manual_seed(3)
+    world, b_l, n_c = 3, 5, 15
+    full = torch.randn(world * b_l, n_c, device=gpu) * 6
+    parts = []
+    for r in range(world):
+        blk = full[r * b_l:(r + 1) * b_l]
+        m = blk.max(0).values
+        parts.append(torch.stack([m, torch.exp(blk - m).sum(0)]))
+    got = K.combine_col_partials(torch.stack(parts))
+    assert (got - torch.logsumexp(full, 0)).abs().max().item() < 1e-5
+    # focal: two heads, local mean CE in ws[rows]; ranks' sums added by hand
+    rows, gamma, n_global = 4, 2.0, 12
+    ws = [torch.zeros(2 * rows + 1, device=gpu) for _ in range(2)]
+    means = [0.7, 1.9]
+    for k in range(2):
+        ws[k][rows] = means[k]
+    sums = torch.empty(2, device=gpu)
+    call("tgfr_focal_global", 0, ptr(sums), 2, rows, 1.0 / n_global, gamma, ptr(ws[0]),
+         ptr(ws[1]), None, None, stream())
+    torch.cuda.synchronize()
+    assert torch.allclose(sums.cpu(), torch.tensor([m * rows for m in means]))
+    sums.mul_(world)                       # three identical ranks
+    loss = [torch.empty(1, device=gpu) for _ in range(2)]
+    call("tgfr_focal_global", 1, ptr(sums), 2, rows, 1.0 / n_global, gamma, ptr(ws[0]),
+         ptr(ws[1]), ptr(loss[0]), ptr(loss[1]), stream())
+    torch.cuda.synchronize()
+    for k in range(2):
+        logp = torch.tensor(means[k] * rows * world / n_global)
+        ref = (1 - torch.exp(-logp)) ** gamma * logp
+        assert abs(ws[k][rows].item() - logp.item()) < 1e-6
+        assert abs(loss[k].item() - ref.item()) < 1e-5

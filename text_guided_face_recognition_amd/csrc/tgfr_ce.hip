@@ -198,6 +198,48 @@ __global__ __launch_bounds__(256) void ce_grad_kernel(const float* __restrict__ 
   dL[b * ldd + c] = g0 * (__expf(v - row_lse[b]) - onehot) + g1 * (__expf(v - col_lse[c]) - onehot);
 }
 
+// ------------------------------------------ data-parallel glue (one rank) ---
+// Global column log-sum-exp from the ranks' gathered (max, sum exp(x - max))
+// column partials [world][2][n_c] (the contrastive CE's one exchange): one
+// thread per column, the ranks combined in rank order
+__global__ __launch_bounds__(256) void col_lse_combine_kernel(const float* __restrict__ parts,
+                                                              int world, int n_c,
+                                                              float* __restrict__ col_lse) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= n_c) return;
+  float m = -INFINITY;
+  for (int w = 0; w < world; ++w) m = fmaxf(m, parts[(long long)w * 2 * n_c + c]);
+  float s = 0.f;
+  for (int w = 0; w < world; ++w) {
+    const float* p = parts + (long long)w * 2 * n_c;
+    s += p[n_c + c] * __expf(p[c] - m);
+  }
+  col_lse[c] = m + __logf(s);
+}
+
+// The focal identity losses on the GLOBAL mean cross-entropy (FocalLoss,
+// models/losses.py:313-325, on the reference's gathered batch): phase 0 packs
+// each head's local NLL sum (rows x its local mean, ws[rows]) into sums[k]
+// for the one all-reduce; phase 1 turns the reduced sums into logp = sum /
+// n_global, writes it back into ws[rows] (the backward's factor) and forms
+// loss_k = (1 - exp(-logp))^gamma logp.  One thread per head.
+struct FocalHeads {
+  float* ws[2];
+  float* loss[2];
+};
+__global__ void focal_global_kernel(int phase, float* __restrict__ sums, int n_heads, int rows,
+                                    float inv_n, float gamma, FocalHeads H) {
+  const int k = threadIdx.x;
+  if (k >= n_heads) return;
+  if (phase == 0) {
+    sums[k] = H.ws[k][rows] * (float)rows;
+    return;
+  }
+  const float logp = sums[k] * inv_n;
+  H.ws[k][rows] = logp;
+  H.loss[k][0] = powf(1.f - __expf(-logp), gamma) * logp;
+}
+
 // ------------------------------------- sent_loss + global_loss, one rank ---
 // The two contrastive losses of the stage-1 step on the same pair of feature
 // sets (sent_loss, models/losses.py:19-57, and global_loss, :329-351: both
@@ -703,6 +745,24 @@ int tgfr_sent_global_dist_bwd(const float* gs0, const float* gs1, const float* g
   hipLaunchKernelGGL(sgd_bwd_kernel, dim3(n_r), dim3(256), n_c * sizeof(float),
                      (hipStream_t)stream, gs0, gs1, ggl, x, ldx, n_r, y, ldy, n_c, cls,
                      row_offset, s_sent, s_glob, eps, inv_n, cosv, stats, nrm, dx, lddx);
+  return (int)hipGetLastError();
+}
+
+int tgfr_col_lse_combine(const float* parts, int world, int n_c, float* col_lse, void* stream) {
+  if (world <= 0 || n_c <= 0 || !parts || !col_lse) return 1001;
+  hipLaunchKernelGGL(col_lse_combine_kernel, dim3((n_c + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, parts, world, n_c, col_lse);
+  return (int)hipGetLastError();
+}
+
+int tgfr_focal_global(int phase, float* sums, int n_heads, int rows, float inv_n, float gamma,
+                      float* ws0, float* ws1, float* loss0, float* loss1, void* stream) {
+  if ((phase != 0 && phase != 1) || !sums || n_heads < 1 || n_heads > 2 || rows <= 0 || !ws0 ||
+      (n_heads == 2 && !ws1) || (phase == 1 && (!loss0 || (n_heads == 2 && !loss1))))
+    return 1001;
+  FocalHeads H{{ws0, ws1}, {loss0, loss1}};
+  hipLaunchKernelGGL(focal_global_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, phase, sums,
+                     n_heads, rows, inv_n, gamma, H);
   return (int)hipGetLastError();
 }
 

@@ -408,20 +408,44 @@ def cos_logits(x, y, scale, normalize=True, cls=None, row_offset=0, eps=1e-8):
 
 
 # ---------------------------------------------------------- contrastive CE ---
+def _focal_global(group, n_global, rows, gamma, wss, losses):
+    """Focal losses of 1-2 heads on the global mean CE: pack the local NLL sums
+    (tgfr_focal_global phase 0), ONE all-reduce, finish (phase 1) into the
+    heads' workspaces and 1-element loss tensors."""
+    from .dist import all_reduce_sum_
+    dev = wss[0].device
+    sums = torch.empty(len(wss), dtype=torch.float32, device=dev)
+    a = [ptr(w) for w in wss] + [None] * (2 - len(wss))
+    lo = [ptr(l) for l in losses] + [None] * (2 - len(losses))
+    call("tgfr_focal_global", 0, ptr(sums), len(wss), rows, 1.0 / float(n_global), float(gamma),
+         a[0], a[1], None, None, _hip.stream())
+    all_reduce_sum_(sums, group)
+    call("tgfr_focal_global", 1, ptr(sums), len(wss), rows, 1.0 / float(n_global), float(gamma),
+         a[0], a[1], lo[0], lo[1], _hip.stream())
+
+
 def combine_col_partials(parts):
     """[world, 2, n_c] per-rank (column max, sum exp(x - max)) -> global column
-    log-sum-exp [n_c]."""
-    gmax = parts[:, 0].max(0).values
-    return (gmax + torch.log((parts[:, 1] * torch.exp(parts[:, 0] - gmax)).sum(0))).contiguous()
+    log-sum-exp [n_c] (tgfr_col_lse_combine, one launch)."""
+    parts = parts.float().contiguous()
+    world, _, n_c = parts.shape
+    out = torch.empty(n_c, dtype=torch.float32, device=parts.device)
+    call("tgfr_col_lse_combine", ptr(parts), world, n_c, ptr(out), _hip.stream())
+    return out
+
+
+def gather_col_partials(part, group):
+    """The one collective of the contrastive CE: all_gather of this rank's
+    [2, n_c] column partials -> [world, 2, n_c] (rank-major)."""
+    if group is None:
+        return part.unsqueeze(0)
+    from .dist import all_gather_cat
+    return all_gather_cat(part.unsqueeze(0), group)
 
 
 def exchange_col_partials(part, group):
-    """The one collective of the contrastive CE: all_gather of [2, n_c] partials."""
-    if group is None:
-        return combine_col_partials(part.unsqueeze(0))
-    from .dist import all_gather_cat
-    allp = all_gather_cat(part.unsqueeze(0), group)
-    return combine_col_partials(allp)
+    """Global column log-sum-exp from this rank's partials: gather + combine."""
+    return combine_col_partials(gather_col_partials(part, group))
 
 
 class ContrastiveCE(torch.autograd.Function):
@@ -1809,15 +1833,10 @@ class IdentityHeads(torch.autograd.Function):
              ptr(out[0]["loss"]), ptr(out[1]["loss"]), _hip.stream())
         losses = [out[0]["loss"][0], out[1]["loss"][0]]
         if group is not None:
-            from .dist import all_reduce_sum_
             # fws[b] holds the local mean CE (FocalCE's layout): both heads'
             # NLL sums in one collective, then the global mean goes back in
-            sums = torch.cat([out[k]["fws"][b:b + 1] * b for k in range(2)])
-            all_reduce_sum_(sums, group)
-            for k in range(2):
-                logp = sums[k:k + 1] / float(n_global)
-                out[k]["fws"][b:b + 1].copy_(logp)
-                losses[k] = ((1.0 - torch.exp(-logp)).pow(float(gamma)) * logp)[0]
+            _focal_global(group, n_global, b, gamma, [out[0]["fws"], out[1]["fws"]],
+                          [out[0]["loss"], out[1]["loss"]])
         ctx.save_for_backward(ws_[0], ws_[1], label,
                               *[out[k][n] for k in range(2)
                                 for n in ("logits", "cosv", "xn", "inv_nx", "inv_nw", "fws")])
@@ -1896,16 +1915,14 @@ class FocalCE(torch.autograd.Function):
             saved += [logits, target, ws]
         rows_l = [saved[3 * k].shape[0] for k in range(n)]
         if group is not None:
-            from .dist import all_reduce_sum_
-            # every pair's local NLL sum in one collective
-            sums = torch.cat([saved[3 * k + 2][rows_l[k]:rows_l[k] + 1] * rows_l[k]
-                              for k in range(n)])
-            all_reduce_sum_(sums, group)
-            for k in range(n):
-                ws = saved[3 * k + 2]
-                logp = sums[k:k + 1] / float(n_global)
-                ws[rows_l[k]:rows_l[k] + 1].copy_(logp)
-                outs[k] = (1.0 - torch.exp(-logp)).pow(float(gamma)) * logp
+            # every pair's local NLL sum in one collective (heads with one
+            # batch size: tgfr_focal_global; otherwise the same per row count)
+            for r in sorted(set(rows_l)):
+                ks = [k for k in range(n) if rows_l[k] == r]
+                for i in range(0, len(ks), 2):
+                    kk = ks[i:i + 2]
+                    _focal_global(group, n_global, r, gamma, [saved[3 * k + 2] for k in kk],
+                                  [outs[k] for k in kk])
         ctx.save_for_backward(*saved)
         ctx.cfg = (float(gamma), n, rows_l, n_global if group is not None else None)
         return tuple(o[0] for o in outs)

@@ -1,7 +1,7 @@
 # Interleaved bench A/B of lab builds of the library (tools/lab/variants.py
 # FILE_VARIANTS): LIBS lists variant names ("product" = the in-tree library);
 # ROUNDS rounds each.
-O=gpurun_out/${R:-libab}
+O=gpurun_out/${R:-libab}/ab
 mkdir -p $O
 for i in $(seq 1 ${ROUNDS:-3}); do
   for v in ${LIBS}; do

@@ -220,7 +220,8 @@ int tgfr_sent_global_dist_fwd(const float* x, long long ldx, int n_r, const floa
                               float* colpart, float* nrm, void* stream);
 int tgfr_sent_global_dist_loss(const float* cosv, int n_r, int n_c, int row_offset, float s_sent,
                                float s_glob, const float* rowpart, const float* colparts,
-                               int world, float inv_n, float* stats, float* loss, void* stream);
+                               int world, long long ld_parts, float inv_n, float* stats,
+                               float* loss, void* stream);
 int tgfr_sent_global_dist_bwd(const float* gs0, const float* gs1, const float* ggl,
                               const float* x, long long ldx, int n_r, const float* y,
                               long long ldy, int n_c, const long long* cls, int row_offset,
@@ -230,18 +231,23 @@ int tgfr_sent_global_dist_bwd(const float* gs0, const float* gs1, const float* g
 
 /* Data-parallel glue (one rank's step; no host work between collectives):
  * tgfr_col_lse_combine: the global column log-sum-exp col_lse [n_c] from the
- * ranks' gathered column partials parts [world][2][n_c] = (max, sum exp(x -
- * max)) of tgfr_ce_stats (ranks combined in rank order).
+ * ranks' gathered column partials -- rank w's [2][n_c] = (max, sum exp(x -
+ * max)) of tgfr_ce_stats at parts + w * ld (ld >= 2 n_c: the partials may
+ * ride in a merged exchange buffer) -- combined in rank order.
  * tgfr_focal_global: the focal identity losses on the GLOBAL mean CE
  * (models/losses.py:313-325 on the gathered batch) for 1 or 2 heads whose
  * tgfr_focal_ce / tgfr_focal_ce2 workspaces ws0 / ws1 hold the local mean CE
- * at [rows]: phase 0 writes sums[k] = rows * that mean (the input of ONE
- * all-reduce); phase 1 reads the reduced sums, writes logp = sums[k] * inv_n
- * back into ws_k[rows] (the backward's factor) and loss_k[0] = (1 -
- * exp(-logp))^gamma logp. */
-int tgfr_col_lse_combine(const float* parts, int world, int n_c, float* col_lse, void* stream);
-int tgfr_focal_global(int phase, float* sums, int n_heads, int rows, float inv_n, float gamma,
-                      float* ws0, float* ws1, float* loss0, float* loss1, void* stream);
+ * at [rows]: phase 0 writes sums[k] = rows * that mean (the input of the one
+ * collective); phase 1 adds the world ranks' sums (rank w's at sums + w * ld;
+ * world 1: already all-reduced), writes logp = total * inv_n back into
+ * ws_k[rows] (the backward's factor) and loss_k[0] = (1 - exp(-logp))^gamma
+ * logp.  tgfr_sent_global_dist_loss reads rank r's column partials at
+ * colparts + r * ld_parts (0: 4 n_c, the plain gathered layout). */
+int tgfr_col_lse_combine(const float* parts, int world, long long ld, int n_c, float* col_lse,
+                         void* stream);
+int tgfr_focal_global(int phase, float* sums, int world, long long ld, int n_heads, int rows,
+                      float inv_n, float gamma, float* ws0, float* ws1, float* loss0,
+                      float* loss1, void* stream);
 
 /* loss[0] = inv_n * sum_b (row_lse[b] - L[b][b+off]), loss[1] = inv_n * sum_b
  * (col_lse[b+off] - L[b][b+off]): this rank's share of nn.CrossEntropyLoss on

@@ -50,8 +50,10 @@ def test_dp_world2_matches_global(gpu, tmp_path):
         assert r["rows_bytes_per_caption"] * 1.3 < r["words_bytes_per_caption"], r
 
 
-@pytest.mark.parametrize("precision,bert", [("fp32", 0), ("bf16", 0), ("bf16", 1), ("fp16", 1)])
-def test_dp_graphed_train_step(gpu, tmp_path, precision, bert):
+@pytest.mark.parametrize("precision,bert,fork", [("fp32", 0, "0"), ("bf16", 0, "0"), ("bf16", 1, "0"),
+                                               ("fp16", 1, "0"), ("bf16", 1, "2"),
+                                               ("fp16", 1, "2"), ("fp32", 0, "2")])
+def test_dp_graphed_train_step(gpu, tmp_path, precision, bert, fork):
     """2 ranks: the stage-1 step replayed as graphs cut at its collectives
     equals eager stepping, and the replicas stay identical.  bert = 1: the
     batches carry BERT hidden states, so each rank runs the frozen TextHeading
@@ -59,19 +61,22 @@ def test_dp_graphed_train_step(gpu, tmp_path, precision, bert):
     the text side is gathered as operand rows (rows-only words)."""
     import json
     out = str(tmp_path / "dpt")
-    _run("dp_train_worker.py", out, TGFR_DP_PRECISION=precision, TGFR_DP_BERT=str(bert))
+    _run("dp_train_worker.py", out, TGFR_DP_PRECISION=precision, TGFR_DP_BERT=str(bert),
+         TGFR_FORK=fork)
     for rank in range(2):
         r = json.load(open(f"{out}.{rank}"))
-        # text gather, 2 column exchanges (word<->region; sentence + global
-        # together), the focal NLL-sum all-reduce, the classifiers' gradient
-        # all-reduce (overlapped on NCCL; in place over gloo), the head's
-        # gradient all-reduce -> 7 graphs
-        assert r["segments"] == 7, r
+        # linear: text gather, 2 column exchanges (word<->region; sentence +
+        # global together), the focal NLL-sum all-reduce, the classifiers'
+        # gradient all-reduce (overlapped on NCCL; in place over gloo), the
+        # head's gradient all-reduce -> 7 graphs.  Forked (Train._step_forked_dp):
+        # text gather, ONE merged mid-step all-gather, one gradient all-reduce
+        # -> 4 graphs
+        assert r["segments"] == (4 if fork != "0" else 7), r
         assert r["err_out"] < 1e-4 and r["err_par"] < 1e-5 and r["err_rank"] == 0.0, r
 
 
 @pytest.mark.parametrize("precision", ["bf16"])
-def test_overlapped_grad_reduce_graphed(gpu, precision):
+def test_overlapped_grad_reduce_graphed(gpu, precision, monkeypatch):
     """The classifiers' gradient all-reduce runs on a side stream overlapping
     the word<->region branch (dist.reduce_grads_async; StepCapture.cut_async /
     join).  One process as rank 0 of 4 replicas (dist.ReplicaGroup: the
@@ -81,6 +86,7 @@ def test_overlapped_grad_reduce_graphed(gpu, precision):
     from text_guided_face_recognition_amd.config import make_args
     from text_guided_face_recognition_amd.dist import DistContext, ReplicaGroup
     from text_guided_face_recognition_amd.train import GraphedStep, Train, synthetic_batch
+    monkeypatch.setenv("TGFR_FORK", "0")           # the linear DP step
 
     def build():
         torch.manual_seed(5)
@@ -128,17 +134,69 @@ def test_dp_glue_kernels(gpu):
     for k in range(2):
         ws[k][rows] = means[k]
     sums = torch.empty(2, device=gpu)
-    call("tgfr_focal_global", 0, ptr(sums), 2, rows, 1.0 / n_global, gamma, ptr(ws[0]),
+    call("tgfr_focal_global", 0, ptr(sums), 1, 0, 2, rows, 1.0 / n_global, gamma, ptr(ws[0]),
          ptr(ws[1]), None, None, stream())
     torch.cuda.synchronize()
     assert torch.allclose(sums.cpu(), torch.tensor([m * rows for m in means]))
-    sums.mul_(world)                       # three identical ranks
+    # (a) an all-reduced total (world 1 of the kernel), (b) the three ranks'
+    # sums gathered into a merged buffer of row stride 7
     loss = [torch.empty(1, device=gpu) for _ in range(2)]
-    call("tgfr_focal_global", 1, ptr(sums), 2, rows, 1.0 / n_global, gamma, ptr(ws[0]),
+    tot = sums * world
+    call("tgfr_focal_global", 1, ptr(tot), 1, 0, 2, rows, 1.0 / n_global, gamma, ptr(ws[0]),
          ptr(ws[1]), ptr(loss[0]), ptr(loss[1]), stream())
+    gathered = torch.zeros(world, 7, device=gpu)
+    gathered[:, 3:5] = sums
+    loss2 = [torch.empty(1, device=gpu) for _ in range(2)]
+    ws2 = [w.clone() for w in ws]
+    for w, m in zip(ws2, means):
+        w[rows] = m
+    g = gathered[:, 3:]
+    call("tgfr_focal_global", 1, ptr(g), world, g.stride(0), 2, rows, 1.0 / n_global, gamma,
+         ptr(ws2[0]), ptr(ws2[1]), ptr(loss2[0]), ptr(loss2[1]), stream())
     torch.cuda.synchronize()
     for k in range(2):
         logp = torch.tensor(means[k] * rows * world / n_global)
         ref = (1 - torch.exp(-logp)) ** gamma * logp
-        assert abs(ws[k][rows].item() - logp.item()) < 1e-6
-        assert abs(loss[k].item() - ref.item()) < 1e-5
+        for w_, l_ in ((ws, loss), (ws2, loss2)):
+            assert abs(w_[k][rows].item() - logp.item()) < 1e-6
+            assert abs(l_[k].item() - ref.item()) < 1e-5
+    # column partials inside a merged buffer (row stride > 2 n_c)
+    big = torch.zeros(world, 2 * n_c + 9, device=gpu)
+    big[:, 5:5 + 2 * n_c] = torch.stack(parts).reshape(world, -1)
+    got2 = K.combine_col_partials(big[:, 5:5 + 2 * n_c].reshape(world, 2, n_c))
+    assert torch.equal(got2, got)
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_dp_forked_step_matches_linear(gpu, precision, monkeypatch):
+    """Train._step_forked_dp (two streams, three collectives: the text gather,
+    ONE merged all-gather of the three losses' partials, one gradient
+    all-reduce) against the linear DP step (six collectives and a join), one
+    process as rank 0 of 4 replicas (dist.ReplicaGroup): the same losses and
+    parameters after three steps, eagerly and replayed as graphs."""
+    from text_guided_face_recognition_amd.config import make_args
+    from text_guided_face_recognition_amd.dist import DistContext, ReplicaGroup
+    from text_guided_face_recognition_amd.train import GraphedStep, Train, synthetic_batch
+
+    def build(fork):
+        monkeypatch.setenv("TGFR_FORK", fork)
+        torch.manual_seed(5)
+        args = make_args(batch_size=16, num_classes=300, precision=precision,
+                         bert_words_num=32)
+        return Train(args, gpu, DistContext(ReplicaGroup(4)))
+
+    batch = synthetic_batch(16, 30, gpu, seed=9, n_ids=300, bert_hidden=True)
+    lin, frk, gfr = build("0"), build("2"), build("2")
+    assert lin._side is None and frk._side is not None
+    outs_l = [lin.step(batch) for _ in range(3)]
+    outs_f = [frk.step(batch) for _ in range(3)]
+    gs = GraphedStep(gfr, tuple(t.clone() for t in batch), warmup=2)
+    out_g = {k: v.clone() for k, v in gs.step().items()}
+    torch.cuda.synchronize()
+    assert len(gs.capture.graphs) == 4
+    for k in outs_l[-1]:
+        assert (outs_f[-1][k] - outs_l[-1][k]).abs().max().item() < 1e-4, k
+        assert (out_g[k] - outs_f[-1][k]).abs().max().item() < 1e-4, k
+    for a, b, c in zip(frk.params, lin.params, gfr.params):
+        assert (a - b).abs().max().item() < 1e-5
+        assert (c - a).abs().max().item() < 1e-5

@@ -146,7 +146,7 @@ def test_sent_global_dist_ranks(gpu, n_r, world):
     dx = torch.empty(n, 256, device=gpu)
     for r, t_ in enumerate(ranks):
         call("tgfr_sent_global_dist_loss", ptr(t_["cosv"]), n_r, n, r * n_r, 10.0, 10.0,
-             ptr(t_["rowpart"]), ptr(parts), world, 1.0 / n, ptr(t_["stats"]), ptr(t_["loss"]),
+             ptr(t_["rowpart"]), ptr(parts), world, 0, 1.0 / n, ptr(t_["stats"]), ptr(t_["loss"]),
              stream())
         call("tgfr_sent_global_dist_bwd", ptr(gw[0]), ptr(gw[1]), ptr(gw[2]), ptr(t_["x"]), 256,
              n_r, ptr(yg), 256, n, ptr(cg), r * n_r, 10.0, 10.0, 1e-8, 1.0 / n,

@@ -42,8 +42,8 @@ SIGNATURES = {
     "tgfr_cos_logits_bwd": [P, L, L, P, L, P, L, I, I, I, I, F, F, P, L, P],
     "tgfr_ce_stats": [P, L, I, I, P, P, P, P, I, F, P, P, P],
     "tgfr_ce_loss": [P, L, I, I, F, P, P, P, P],
-    "tgfr_col_lse_combine": [P, I, I, P, P],
-    "tgfr_focal_global": [I, P, I, I, F, F, P, P, P, P, P],
+    "tgfr_col_lse_combine": [P, I, L, I, P, P],
+    "tgfr_focal_global": [I, P, I, L, I, I, F, F, P, P, P, P, P],
     "tgfr_ce_grad": [P, L, I, I, I, F, P, P, P, P, F, F, P, L, P],
     "tgfr_bgemm": [P, L, L, L, P, L, L, L, P, L, L, L, I, I, I, I, F, I, P, I, I, P, P, I, P],
     "tgfr_attn_softmax": [P, P, P, L, I, L, F, P],
@@ -94,7 +94,7 @@ SIGNATURES = {
     "tgfr_sent_global_bwd": [P, P, P, P, L, P, L, I, P, F, F, F, P, P, P, P, L, P],
     "tgfr_sent_global_dist_ws": [I, I, P, P, P],
     "tgfr_sent_global_dist_fwd": [P, L, I, P, L, I, P, I, F, F, F, P, P, P, P, P],
-    "tgfr_sent_global_dist_loss": [P, I, I, I, F, F, P, P, I, F, P, P, P],
+    "tgfr_sent_global_dist_loss": [P, I, I, I, F, F, P, P, I, L, F, P, P, P],
     "tgfr_sent_global_dist_bwd": [P, P, P, P, L, I, P, L, I, P, I, F, F, F, F, P, P, P, P, L,
                                   P],
     "tgfr_focal_ce2": [P, P, I, I, P, F, P, P, P, P, P, P],

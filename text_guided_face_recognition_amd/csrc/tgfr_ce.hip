@@ -200,18 +200,19 @@ __global__ __launch_bounds__(256) void ce_grad_kernel(const float* __restrict__ 
 
 // ------------------------------------------ data-parallel glue (one rank) ---
 // Global column log-sum-exp from the ranks' gathered (max, sum exp(x - max))
-// column partials [world][2][n_c] (the contrastive CE's one exchange): one
+// column partials, rank w's [2][n_c] at parts + w * ld (the contrastive CE's
+// one exchange; ld > 2 n_c when it rides in a merged exchange buffer): one
 // thread per column, the ranks combined in rank order
 __global__ __launch_bounds__(256) void col_lse_combine_kernel(const float* __restrict__ parts,
-                                                              int world, int n_c,
+                                                              int world, long long ld, int n_c,
                                                               float* __restrict__ col_lse) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= n_c) return;
   float m = -INFINITY;
-  for (int w = 0; w < world; ++w) m = fmaxf(m, parts[(long long)w * 2 * n_c + c]);
+  for (int w = 0; w < world; ++w) m = fmaxf(m, parts[(long long)w * ld + c]);
   float s = 0.f;
   for (int w = 0; w < world; ++w) {
-    const float* p = parts + (long long)w * 2 * n_c;
+    const float* p = parts + (long long)w * ld;
     s += p[n_c + c] * __expf(p[c] - m);
   }
   col_lse[c] = m + __logf(s);
@@ -220,22 +221,27 @@ __global__ __launch_bounds__(256) void col_lse_combine_kernel(const float* __res
 // The focal identity losses on the GLOBAL mean cross-entropy (FocalLoss,
 // models/losses.py:313-325, on the reference's gathered batch): phase 0 packs
 // each head's local NLL sum (rows x its local mean, ws[rows]) into sums[k]
-// for the one all-reduce; phase 1 turns the reduced sums into logp = sum /
-// n_global, writes it back into ws[rows] (the backward's factor) and forms
-// loss_k = (1 - exp(-logp))^gamma logp.  One thread per head.
+// for the one collective; phase 1 adds the world ranks' sums (rank w's at
+// sums + w * ld: an all-gather; world 1: already all-reduced), turns the
+// total into logp = sum / n_global, writes it back into ws[rows] (the
+// backward's factor) and forms loss_k = (1 - exp(-logp))^gamma logp.  One
+// thread per head.
 struct FocalHeads {
   float* ws[2];
   float* loss[2];
 };
-__global__ void focal_global_kernel(int phase, float* __restrict__ sums, int n_heads, int rows,
-                                    float inv_n, float gamma, FocalHeads H) {
+__global__ void focal_global_kernel(int phase, float* __restrict__ sums, int world, long long ld,
+                                    int n_heads, int rows, float inv_n, float gamma,
+                                    FocalHeads H) {
   const int k = threadIdx.x;
   if (k >= n_heads) return;
   if (phase == 0) {
     sums[k] = H.ws[k][rows] * (float)rows;
     return;
   }
-  const float logp = sums[k] * inv_n;
+  float tot = 0.f;
+  for (int w = 0; w < world; ++w) tot += sums[(long long)w * ld + k];
+  const float logp = tot * inv_n;
   H.ws[k][rows] = logp;
   H.loss[k][0] = powf(1.f - __expf(-logp), gamma) * logp;
 }
@@ -540,18 +546,19 @@ __global__ __launch_bounds__(SG_T) void sgd_fwd_kernel(
 __global__ __launch_bounds__(SG_T) void sgd_loss_kernel(
     const float* __restrict__ cosv, int n_r, int n_c, int row_offset, float s_sent, float s_glob,
     int tiles, const float* __restrict__ rowpart, const float* __restrict__ colparts, int world,
-    float inv_n, float* __restrict__ stats, float* __restrict__ loss) {
+    long long ld_parts, float inv_n, float* __restrict__ stats, float* __restrict__ loss) {
   __shared__ float rl[2][SG_N], cl[2][SG_N];
   __shared__ float red[SG_T / WAVE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   float* row_lse = stats;
   float* col_lse = stats + 2 * n_r;
-  // column LSEs over every rank's partials (rank-major [world][2 sets][2][n_c])
+  // column LSEs over every rank's partials (rank r's [2 sets][2][n_c] at
+  // colparts + r * ld_parts)
   for (int e = tid; e < 2 * n_c; e += SG_T) {
     const int set = e / n_c, c = e % n_c;
     float m = -INFINITY, sum = 0.f;
     for (int r = 0; r < world; ++r) {
-      const float* cp = colparts + (long long)r * 4 * n_c + set * 2 * n_c;
+      const float* cp = colparts + (long long)r * ld_parts + set * 2 * n_c;
       lse_merge(m, sum, cp[c], cp[n_c + c]);
     }
     const float lse = m + __logf(sum);
@@ -723,13 +730,16 @@ int tgfr_sent_global_dist_fwd(const float* x, long long ldx, int n_r, const floa
 
 int tgfr_sent_global_dist_loss(const float* cosv, int n_r, int n_c, int row_offset, float s_sent,
                                float s_glob, const float* rowpart, const float* colparts,
-                               int world, float inv_n, float* stats, float* loss, void* stream) {
+                               int world, long long ld_parts, float inv_n, float* stats,
+                               float* loss, void* stream) {
   if (n_r <= 0 || n_r > SG_N || n_c <= 0 || world <= 0 || !cosv || !rowpart || !colparts ||
       !stats || !loss)
     return 1001;
+  if (ld_parts == 0) ld_parts = 4LL * n_c;
+  if (ld_parts < 4LL * n_c) return 1001;
   hipLaunchKernelGGL(sgd_loss_kernel, dim3(1), dim3(SG_T), 0, (hipStream_t)stream, cosv, n_r, n_c,
                      row_offset, s_sent, s_glob, (n_c + SG_N - 1) / SG_N, rowpart, colparts,
-                     world, inv_n, stats, loss);
+                     world, ld_parts, inv_n, stats, loss);
   return (int)hipGetLastError();
 }
 
@@ -748,21 +758,24 @@ int tgfr_sent_global_dist_bwd(const float* gs0, const float* gs1, const float* g
   return (int)hipGetLastError();
 }
 
-int tgfr_col_lse_combine(const float* parts, int world, int n_c, float* col_lse, void* stream) {
-  if (world <= 0 || n_c <= 0 || !parts || !col_lse) return 1001;
+int tgfr_col_lse_combine(const float* parts, int world, long long ld, int n_c, float* col_lse,
+                         void* stream) {
+  if (world <= 0 || n_c <= 0 || !parts || !col_lse || (world > 1 && ld < 2LL * n_c)) return 1001;
   hipLaunchKernelGGL(col_lse_combine_kernel, dim3((n_c + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, parts, world, n_c, col_lse);
+                     (hipStream_t)stream, parts, world, ld, n_c, col_lse);
   return (int)hipGetLastError();
 }
 
-int tgfr_focal_global(int phase, float* sums, int n_heads, int rows, float inv_n, float gamma,
-                      float* ws0, float* ws1, float* loss0, float* loss1, void* stream) {
+int tgfr_focal_global(int phase, float* sums, int world, long long ld, int n_heads, int rows,
+                      float inv_n, float gamma, float* ws0, float* ws1, float* loss0,
+                      float* loss1, void* stream) {
   if ((phase != 0 && phase != 1) || !sums || n_heads < 1 || n_heads > 2 || rows <= 0 || !ws0 ||
-      (n_heads == 2 && !ws1) || (phase == 1 && (!loss0 || (n_heads == 2 && !loss1))))
+      (n_heads == 2 && !ws1) || (phase == 1 && (!loss0 || (n_heads == 2 && !loss1))) ||
+      world <= 0 || (world > 1 && ld < n_heads))
     return 1001;
   FocalHeads H{{ws0, ws1}, {loss0, loss1}};
   hipLaunchKernelGGL(focal_global_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, phase, sums,
-                     n_heads, rows, inv_n, gamma, H);
+                     world, ld, n_heads, rows, inv_n, gamma, H);
   return (int)hipGetLastError();
 }
 

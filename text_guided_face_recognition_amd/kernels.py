@@ -417,20 +417,22 @@ def _focal_global(group, n_global, rows, gamma, wss, losses):
     sums = torch.empty(len(wss), dtype=torch.float32, device=dev)
     a = [ptr(w) for w in wss] + [None] * (2 - len(wss))
     lo = [ptr(l) for l in losses] + [None] * (2 - len(losses))
-    call("tgfr_focal_global", 0, ptr(sums), len(wss), rows, 1.0 / float(n_global), float(gamma),
-         a[0], a[1], None, None, _hip.stream())
+    call("tgfr_focal_global", 0, ptr(sums), 1, 0, len(wss), rows, 1.0 / float(n_global),
+         float(gamma), a[0], a[1], None, None, _hip.stream())
     all_reduce_sum_(sums, group)
-    call("tgfr_focal_global", 1, ptr(sums), len(wss), rows, 1.0 / float(n_global), float(gamma),
-         a[0], a[1], lo[0], lo[1], _hip.stream())
+    call("tgfr_focal_global", 1, ptr(sums), 1, 0, len(wss), rows, 1.0 / float(n_global),
+         float(gamma), a[0], a[1], lo[0], lo[1], _hip.stream())
 
 
 def combine_col_partials(parts):
     """[world, 2, n_c] per-rank (column max, sum exp(x - max)) -> global column
     log-sum-exp [n_c] (tgfr_col_lse_combine, one launch)."""
-    parts = parts.float().contiguous()
+    if parts.dtype != torch.float32 or parts.stride(2) != 1 or parts.stride(1) != parts.shape[2]:
+        parts = parts.float().contiguous()
     world, _, n_c = parts.shape
     out = torch.empty(n_c, dtype=torch.float32, device=parts.device)
-    call("tgfr_col_lse_combine", ptr(parts), world, n_c, ptr(out), _hip.stream())
+    call("tgfr_col_lse_combine", ptr(parts), world, parts.stride(0), n_c, ptr(out),
+         _hip.stream())
     return out
 
 
@@ -460,14 +462,24 @@ class ContrastiveCE(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, logits, row_offset, n_global, group):
+    def forward(ctx, logits, row_offset, n_global, group, pre=None):
         logits = logits.float().contiguous()
         n_r, n_c = logits.shape
         dev = logits.device
-        row_lse = torch.empty(n_r, dtype=torch.float32, device=dev)
-        part = torch.empty(2, n_c, dtype=torch.float32, device=dev)
         loss = torch.empty(2, dtype=torch.float32, device=dev)
         inv_n = 1.0 / float(n_global)
+        if pre is not None:
+            # ce_partials ran earlier and its column partials rode in a merged
+            # exchange (train.Train._step_forked_dp): row LSE + gathered parts
+            row_lse, parts = pre
+            col_lse = combine_col_partials(parts)
+            call("tgfr_ce_loss", ptr(logits), n_c, n_r, int(row_offset), inv_n, ptr(row_lse),
+                 ptr(col_lse), ptr(loss), _hip.stream())
+            ctx.save_for_backward(logits, row_lse, col_lse)
+            ctx.cfg = (int(row_offset), inv_n)
+            return loss[0], loss[1]
+        row_lse = torch.empty(n_r, dtype=torch.float32, device=dev)
+        part = torch.empty(2, n_c, dtype=torch.float32, device=dev)
         if group is None:
             # one launch: stats, final column LSE and both losses
             col_lse = torch.empty(n_c, dtype=torch.float32, device=dev)
@@ -496,12 +508,27 @@ class ContrastiveCE(torch.autograd.Function):
         dl = torch.empty_like(logits)
         call("tgfr_ce_grad", ptr(logits), n_c, n_r, n_c, row_offset, inv_n, ptr(row_lse),
              ptr(col_lse), ptr(g0), ptr(g1), w0, w1, ptr(dl), n_c, _hip.stream())
-        return dl, None, None, None
+        return dl, None, None, None, None
 
 
-def contrastive_ce(logits, row_offset=0, n_global=None, group=None):
+def contrastive_ce(logits, row_offset=0, n_global=None, group=None, pre=None):
+    """(CE rows, CE columns) of a logit block; pre = (row_lse, gathered column
+    partials [world, 2, n_c]) from ce_partials and a merged exchange."""
     n_global = logits.shape[0] if n_global is None else n_global
-    return ContrastiveCE.apply(logits, row_offset, n_global, group)
+    return ContrastiveCE.apply(logits, row_offset, n_global, group, pre)
+
+
+def ce_partials(logits, part):
+    """Stage 1 of a data-parallel contrastive CE: the row LSE [n_r] and this
+    rank's column partials (max, sum exp(x - max)) written into `part` [2, n_c]
+    (a view of a merged exchange buffer) by tgfr_ce_stats; no loss."""
+    logits = logits.detach().float().contiguous()
+    n_r, n_c = logits.shape
+    row_lse = torch.empty(n_r, dtype=torch.float32, device=logits.device)
+    assert part.shape == (2, n_c) and part.stride(1) == 1 and part.stride(0) == n_c
+    call("tgfr_ce_stats", ptr(logits), n_c, n_r, n_c, ptr(row_lse), ptr(part[0]), ptr(part[1]),
+         None, 0, 0.0, None, None, _hip.stream())
+    return row_lse
 
 
 class SentGlobal(torch.autograd.Function):
@@ -566,31 +593,37 @@ class SentGlobalDist(torch.autograd.Function):
     (sum over ranks = the global-batch losses), as ContrastiveCE does."""
 
     @staticmethod
-    def forward(ctx, x, y, cls, s_sent, s_glob, eps, row_offset, n_global, group):
+    def forward(ctx, x, y, cls, s_sent, s_glob, eps, row_offset, n_global, group, pre=None):
         x = _aligned(x)
         y = _aligned(y)
         n_r, n_c = x.shape[0], y.shape[0]
         dev = x.device
         cls = cls.to(device=dev, dtype=torch.int64).contiguous()
         n_rp, n_cp, n_st = _sgd_ws(n_r, n_c)
-        cosv = torch.empty(n_r, n_c, dtype=torch.float32, device=dev)
-        rowpart = torch.empty(n_rp, dtype=torch.float32, device=dev)
-        colpart = torch.empty(n_cp, dtype=torch.float32, device=dev)
-        nrm = torch.empty(n_r + n_c, dtype=torch.float32, device=dev)
         stats = torch.empty(n_st, dtype=torch.float32, device=dev)
         loss = torch.empty(3, dtype=torch.float32, device=dev)
-        call("tgfr_sent_global_dist_fwd", ptr(x), x.stride(0), n_r, ptr(y), y.stride(0), n_c,
-             ptr(cls), int(row_offset), float(s_sent), float(s_glob), float(eps), ptr(cosv),
-             ptr(rowpart), ptr(colpart), ptr(nrm), _hip.stream())
-        world = 1
-        parts = colpart
-        if group is not None:
-            from .dist import all_gather_cat
-            parts = all_gather_cat(colpart.unsqueeze(0), group)
-            world = parts.shape[0]
+        if pre is not None:
+            # sent_global_dist_parts ran earlier; its column partials rode in a
+            # merged exchange: [world, >= n_cp] rows (any row stride)
+            cosv, rowpart, nrm, parts = pre
+            world, ld = parts.shape[0], parts.stride(0)
+        else:
+            cosv = torch.empty(n_r, n_c, dtype=torch.float32, device=dev)
+            rowpart = torch.empty(n_rp, dtype=torch.float32, device=dev)
+            colpart = torch.empty(n_cp, dtype=torch.float32, device=dev)
+            nrm = torch.empty(n_r + n_c, dtype=torch.float32, device=dev)
+            call("tgfr_sent_global_dist_fwd", ptr(x), x.stride(0), n_r, ptr(y), y.stride(0), n_c,
+                 ptr(cls), int(row_offset), float(s_sent), float(s_glob), float(eps), ptr(cosv),
+                 ptr(rowpart), ptr(colpart), ptr(nrm), _hip.stream())
+            world, ld = 1, 0
+            parts = colpart
+            if group is not None:
+                from .dist import all_gather_cat
+                parts = all_gather_cat(colpart.unsqueeze(0), group)
+                world = parts.shape[0]
         inv_n = 1.0 / float(n_global)
         call("tgfr_sent_global_dist_loss", ptr(cosv), n_r, n_c, int(row_offset), float(s_sent),
-             float(s_glob), ptr(rowpart), ptr(parts), world, inv_n, ptr(stats), ptr(loss),
+             float(s_glob), ptr(rowpart), ptr(parts), world, ld, inv_n, ptr(stats), ptr(loss),
              _hip.stream())
         ctx.save_for_backward(x, y, cls, cosv, stats, nrm)
         ctx.cfg = (float(s_sent), float(s_glob), float(eps), int(row_offset), inv_n)
@@ -607,13 +640,40 @@ class SentGlobalDist(torch.autograd.Function):
         call("tgfr_sent_global_dist_bwd", ptr(g[0]), ptr(g[1]), ptr(g[2]), ptr(x), x.stride(0),
              n_r, ptr(y), y.stride(0), n_c, ptr(cls), row_offset, s_sent, s_glob, eps, inv_n,
              ptr(cosv), ptr(stats), ptr(nrm), ptr(dx), dx.stride(0), _hip.stream())
-        return (dx,) + (None,) * 8
+        return (dx,) + (None,) * 9
 
 
 def sent_global_dist(x, y, cls, s_sent, s_glob, eps=1e-8, row_offset=0, n_global=None,
-                     group=None):
+                     group=None, pre=None):
+    """pre: sent_global_dist_parts' (cosv, rowpart, nrm) + the gathered column
+    partials [world, >= n_cp] of a merged exchange."""
     return SentGlobalDist.apply(x, y, cls, s_sent, s_glob, eps, row_offset,
-                                n_global or x.shape[0], group)
+                                n_global or x.shape[0], group, pre)
+
+
+def sent_global_dist_cols(n_r, n_c):
+    """Floats of this rank's sent/global column partials (tgfr_sent_global_dist_ws)."""
+    return _sgd_ws(n_r, n_c)[1]
+
+
+def sent_global_dist_parts(x, y, cls, s_sent, s_glob, eps, row_offset, colpart):
+    """Stage 1 of SentGlobalDist: cosines, row partials and norms, this rank's
+    column partials written into `colpart` (a view of a merged exchange
+    buffer, sent_global_dist_cols floats); returns (cosv, rowpart, nrm)."""
+    x = _aligned(x.detach())
+    y = _aligned(y)
+    n_r, n_c = x.shape[0], y.shape[0]
+    dev = x.device
+    cls = cls.to(device=dev, dtype=torch.int64).contiguous()
+    n_rp, n_cp, _ = _sgd_ws(n_r, n_c)
+    assert colpart.numel() == n_cp and colpart.is_contiguous()
+    cosv = torch.empty(n_r, n_c, dtype=torch.float32, device=dev)
+    rowpart = torch.empty(n_rp, dtype=torch.float32, device=dev)
+    nrm = torch.empty(n_r + n_c, dtype=torch.float32, device=dev)
+    call("tgfr_sent_global_dist_fwd", ptr(x), x.stride(0), n_r, ptr(y), y.stride(0), n_c,
+         ptr(cls), int(row_offset), float(s_sent), float(s_glob), float(eps), ptr(cosv),
+         ptr(rowpart), ptr(colpart), ptr(nrm), _hip.stream())
+    return cosv, rowpart, nrm
 
 
 # ------------------------------------------------------------------ bgemm ---
@@ -1787,6 +1847,36 @@ class _ArcHeadArgs(ctypes.Structure):
                 ("g", ctypes.c_void_p), ("dW", ctypes.c_void_p), ("dcs", ctypes.c_void_p)]
 
 
+def _heads_fwd(x_t, w_t, x_i, w_i, label, s_t, s_i, m, easy, eps, gamma):
+    """Both identity heads' ArcMargin forward (one launch) and both focal CEs
+    on the local rows (one launch): per head the tensors IdentityHeads saves."""
+    xs = [_aligned(x_t), _aligned(x_i)]
+    ws_ = [w_t, w_i]
+    b, d = xs[0].shape
+    c = ws_[0].shape[0]
+    dev = xs[0].device
+    out = []
+    heads = (_ArcHeadArgs * 2)()
+    for k, sc in enumerate((s_t, s_i)):
+        t = {"logits": torch.empty(b, c, dtype=torch.float32, device=dev),
+             "cosv": torch.empty(b, c, dtype=torch.float32, device=dev),
+             "xn": torch.empty_like(xs[k]),
+             "inv_nx": torch.empty(b, dtype=torch.float32, device=dev),
+             "inv_nw": torch.empty(c, dtype=torch.float32, device=dev),
+             "fws": torch.empty(2 * b + 1, dtype=torch.float32, device=dev),
+             "loss": torch.empty(1, dtype=torch.float32, device=dev)}
+        out.append(t)
+        heads[k] = _ArcHeadArgs(ptr(xs[k]), ptr(ws_[k]), ptr(label), float(sc),
+                                ptr(t["logits"]), ptr(t["cosv"]), ptr(t["xn"]),
+                                ptr(t["inv_nx"]), ptr(t["inv_nw"]), None, None, None, None)
+    call("tgfr_arc_fwd_heads", ctypes.addressof(heads), 2, b, d, c, float(m), int(easy),
+         float(eps), _hip.stream())
+    call("tgfr_focal_ce2", ptr(out[0]["logits"]), ptr(out[1]["logits"]), b, c, ptr(label),
+         float(gamma), ptr(out[0]["fws"]), ptr(out[1]["fws"]), ptr(_hip.counters(dev)),
+         ptr(out[0]["loss"]), ptr(out[1]["loss"]), _hip.stream())
+    return out
+
+
 class IdentityHeads(torch.autograd.Function):
     """The stage-1 step's two identity losses, focal(ArcMargin_text(sent)) and
     focal(ArcMargin_image(img)) (src/train_encoders_bert.py:293-306, one
@@ -1805,32 +1895,25 @@ class IdentityHeads(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x_t, w_t, x_i, w_i, label, s_t, s_i, m, easy, eps, gamma, mode,
-                group=None, n_global=None):
-        xs = [_aligned(x_t), _aligned(x_i)]
+                group=None, n_global=None, pre=None):
         ws_ = [_aligned(w_t), _aligned(w_i)]
         label = label.to(torch.int64).contiguous()
-        b, d = xs[0].shape
-        c = ws_[0].shape[0]
-        dev = xs[0].device
-        out = []
-        heads = (_ArcHeadArgs * 2)()
-        for k, sc in enumerate((s_t, s_i)):
-            t = {"logits": torch.empty(b, c, dtype=torch.float32, device=dev),
-                 "cosv": torch.empty(b, c, dtype=torch.float32, device=dev),
-                 "xn": torch.empty_like(xs[k]),
-                 "inv_nx": torch.empty(b, dtype=torch.float32, device=dev),
-                 "inv_nw": torch.empty(c, dtype=torch.float32, device=dev),
-                 "fws": torch.empty(2 * b + 1, dtype=torch.float32, device=dev),
-                 "loss": torch.empty(1, dtype=torch.float32, device=dev)}
-            out.append(t)
-            heads[k] = _ArcHeadArgs(ptr(xs[k]), ptr(ws_[k]), ptr(label), float(sc),
-                                    ptr(t["logits"]), ptr(t["cosv"]), ptr(t["xn"]),
-                                    ptr(t["inv_nx"]), ptr(t["inv_nw"]), None, None, None, None)
-        call("tgfr_arc_fwd_heads", ctypes.addressof(heads), 2, b, d, c, float(m), int(easy),
-             float(eps), _hip.stream())
-        call("tgfr_focal_ce2", ptr(out[0]["logits"]), ptr(out[1]["logits"]), b, c, ptr(label),
-             float(gamma), ptr(out[0]["fws"]), ptr(out[1]["fws"]), ptr(_hip.counters(dev)),
-             ptr(out[0]["loss"]), ptr(out[1]["loss"]), _hip.stream())
+        if pre is not None:
+            # identity_heads_parts ran earlier; both heads' NLL sums rode in a
+            # merged all-gather: gathered [world, >= 2] rows (any row stride)
+            out, gsums = pre
+            b = out[0]["xn"].shape[0]
+            call("tgfr_focal_global", 1, ptr(gsums), gsums.shape[0], gsums.stride(0), 2, b,
+                 1.0 / float(n_global), float(gamma), ptr(out[0]["fws"]), ptr(out[1]["fws"]),
+                 ptr(out[0]["loss"]), ptr(out[1]["loss"]), _hip.stream())
+            ctx.save_for_backward(ws_[0], ws_[1], label,
+                                  *[out[k][n] for k in range(2)
+                                    for n in ("logits", "cosv", "xn", "inv_nx", "inv_nw", "fws")])
+            ctx.cfg = (float(s_t), float(s_i), float(m), int(easy), float(eps), float(gamma), mode,
+                       b / float(n_global))
+            return out[0]["loss"][0], out[1]["loss"][0]
+        out = _heads_fwd(x_t, ws_[0], x_i, ws_[1], label, s_t, s_i, m, easy, eps, gamma)
+        b = out[0]["xn"].shape[0]
         losses = [out[0]["loss"][0], out[1]["loss"][0]]
         if group is not None:
             # fws[b] holds the local mean CE (FocalCE's layout): both heads'
@@ -1873,17 +1956,34 @@ class IdentityHeads(torch.autograd.Function):
              _hip.stream())
         dx = [arc_dx(dcs[k], ws_[k], per[k]["xn"], per[k]["inv_nx"], eps) if want_dx[k]
               else None for k in range(2)]
-        return (dx[0], dws[0], dx[1], dws[1]) + (None,) * 10
+        return (dx[0], dws[0], dx[1], dws[1]) + (None,) * 11
 
 
 def identity_heads(x_t, head_t, x_i, head_i, label, gamma, eps=1e-12, group=None,
-                   n_global=None):
+                   n_global=None, pre=None):
     """(focal(head_t(x_t)), focal(head_i(x_i))) for two ArcMarginProduct
     modules of one (D, C) and margin: kernels.IdentityHeads (with a process
-    group: this rank's rows, focal factor of the global-batch mean CE)."""
+    group: this rank's rows, focal factor of the global-batch mean CE).
+    pre: identity_heads_parts' state + the gathered NLL sums [world, >= 2] of
+    a merged exchange."""
     return IdentityHeads.apply(x_t, head_t.weight, x_i, head_i.weight, label, head_t.s, head_i.s,
                                head_t.m, head_t.easy_margin, eps, gamma, head_t.precision,
-                               group, n_global)
+                               group, n_global, pre)
+
+
+def identity_heads_parts(x_t, head_t, x_i, head_i, label, gamma, sums, eps=1e-12):
+    """Stage 1 of the data-parallel identity heads: both ArcMargin forwards and
+    local focal CEs, and both heads' local NLL sums written into `sums` [2] (a
+    view of a merged exchange buffer; tgfr_focal_global phase 0).  Returns the
+    heads' state for identity_heads(..., pre=(state, gathered sums))."""
+    label = label.to(torch.int64).contiguous()
+    out = _heads_fwd(x_t.detach(), _aligned(head_t.weight.detach()), x_i.detach(),
+                     _aligned(head_i.weight.detach()), label, head_t.s, head_i.s, head_t.m,
+                     head_t.easy_margin, eps, gamma)
+    b = out[0]["xn"].shape[0]
+    call("tgfr_focal_global", 0, ptr(sums), 1, 0, 2, b, 1.0, float(gamma), ptr(out[0]["fws"]),
+         ptr(out[1]["fws"]), None, None, _hip.stream())
+    return out
 
 
 class FocalCE(torch.autograd.Function):

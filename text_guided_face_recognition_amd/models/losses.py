@@ -142,6 +142,22 @@ def words_loss(img_features, words_emb, labels, cap_lens, class_ids, batch_size,
     return loss0, loss1, att_maps
 
 
+def words_logits_bert(img_features, words_emb, args):
+    """words_loss's logit block for the BERT path with no attention maps (the
+    data-parallel forked step computes its CE in stages around a merged
+    exchange, train.Train._step_forked_dp): [B_img, B_cap] through
+    kernels.word_region_logits, exactly as words_loss forms it."""
+    b_cap = words_emb.shape[0]
+    n_words = args.bert_words_num - 2
+    lens = _const_lens(b_cap, n_words, img_features.device)
+    row_offset, _, _ = _dist(args)
+    smooth = args.TRAIN.SMOOTH
+    return K.word_region_logits(img_features, K.words_view(words_emb, n_words), lens,
+                                smooth.GAMMA1, smooth.GAMMA2, smooth.GAMMA3,
+                                mode=_precision(args), img_offset=row_offset, att_T=0,
+                                bounded=True, uniform=True)
+
+
 def global_loss(cnn_code, rnn_code, eps=1e-8, temp3=10.0, args=None):
     """losses.py:329-351 -> loss0 + loss1 (labels are arange(batch))."""
     row_offset, n_global, group = _dist(args)

@@ -35,7 +35,8 @@ import torch
 from . import kernels as K
 from .dist import DistContext, StepCapture
 from .models.fusion_nets import Working, set_precision
-from .models.losses import ClipLoss, FocalLoss, sent_global_loss, words_loss
+from .models.losses import (ClipLoss, FocalLoss, _class_tensor, sent_global_loss, words_loss,
+                            words_logits_bert)
 from .models.metrics import ArcMarginProduct
 from .models.models import ImageHeading, TextHeading
 from .optim import FusedOptimizer, adam_group, sgd_group
@@ -121,8 +122,10 @@ class Train:
         # 0.547 / 0.482 / 0.460 ms per step; the classifiers' SGD step on the
         # side stream as well, _step_forked.  The logged-loss mix there costs
         # a cross-stream edge and measured slower: 0.50 ms)
+        # With a process group the forked step is _step_forked_dp (its three
+        # mid-step collectives merged into one, so the fork is not cut apart).
         fork = os.environ.get("TGFR_FORK", "2")
-        self.fork = self._forks and not self.ctx.active and fork != "0"
+        self.fork = self._forks and fork != "0"
         self.fork_text = fork == "2"
         self._side = torch.cuda.Stream(device) if self.fork and torch.cuda.is_available() else None
         # :212 (text_head params would join here; the text side is frozen input)
@@ -137,7 +140,10 @@ class Train:
         BERT hidden states, class ids) -- then the step runs TextHeading under
         no_grad first (:257, utils/dataset_utils.py:38-46)."""
         if self._side is not None:
-            return self._step_forked(batch)
+            if not self.ctx.active:
+                return self._step_forked(batch)
+            if self._dp_forkable(batch):
+                return self._step_forked_dp(batch)
         args, ctx = self.args, self.ctx
         if len(batch) == 4:
             g, local, hidden, class_ids = batch
@@ -231,6 +237,95 @@ class Train:
         torch.autograd.backward((w0, w1), self._weights((1.0, 1.0), g.device))
         main.wait_stream(side)
         return self._finish(w0, w1, s0, s1, cl, tid, iid, lc, wi, None, groups=[0])
+
+    def _dp_forkable(self, batch):
+        """The data-parallel forked step needs the fused loss paths: the BERT
+        word<->region path without attention maps, this rank's <= 64 images
+        (sentence / global and identity-head kernels) against <= 8192 gathered
+        captions, and two identity heads of one (D, C) and margin."""
+        tc, ic = self.text_cls, self.image_cls
+        b = batch[0].shape[0]
+        return (self.args.en_type == "BERT" and b <= 64 and b * self.ctx.world <= 8192
+                and tc.weight.shape == ic.weight.shape and tc.m == ic.m
+                and tc.easy_margin == ic.easy_margin)
+
+    def _step_forked_dp(self, batch):
+        """One process per GPU: the forked step of _step_forked with the
+        reference's DataParallel global-batch semantics
+        (src/train_encoders_bert.py:146-169), cut at only three collectives:
+
+          1. the text side's all-gather (after the frozen TextHeading);
+          2. ONE all-gather of every rank's mid-step partials -- the word<->
+             region CE's column (max, sum exp) partials, the sentence / global
+             losses' column partials and both identity heads' NLL sums -- packed
+             in one buffer by the three losses' first stages (kernels.ce_partials,
+             sent_global_dist_parts, identity_heads_parts); their second stages
+             read the gathered rows in place (any row stride);
+          3. one flat all-reduce of every trained gradient, then the optimiser.
+
+        Between 1 and 2 the main stream runs IMIM and the word<->region
+        forward while the side stream runs the g' projection and the
+        sentence / global and identity-head forwards; between 2 and 3 the main
+        stream runs the word<->region and IMIM backward while the side runs
+        the g' branch's losses and backward.  (The linear DP step cuts at six
+        collectives and a join and runs the g' branch in series.)"""
+        args, ctx = self.args, self.ctx
+        main, side = torch.cuda.current_stream(), self._side
+        if len(batch) == 4:
+            g, local, hidden, class_ids = batch
+            with torch.no_grad():
+                words, sent = self.text_head(hidden, None)
+        else:
+            g, local, words, sent, class_ids = batch
+        b = g.shape[0]
+        ctx.set_batch(b)
+        args.dist = ctx
+        words_g, sent_g, cls_g = self._gather_text(words, sent, class_ids)      # 1
+        n_c = words_g.shape[0]
+        dev = g.device
+        self.optimizer.zero_grad(set_to_none=True)
+        wi, lc = float(args.lambda_id), float(args.lambda_clip)
+        gamma3, eps, temp3 = args.TRAIN.SMOOTH.GAMMA3, 1e-8, 10.0
+        row_offset, n_global = ctx.row_offset, ctx.n_global
+        # this rank's mid-step partials: [words CE 2 n_c | sent/global | NLL sums 2]
+        n_sg = K.sent_global_dist_cols(b, n_c)
+        buf = torch.empty(2 * n_c + n_sg + 2, dtype=torch.float32, device=dev)
+        cls_t = _class_tensor(cls_g, dev)
+        start = torch.cuda.Event()
+        start.record(main)
+        words_features = self.image_head.imim(local)
+        side.wait_event(start)
+        with torch.cuda.stream(side):
+            img_features = self.image_head.global_features(g)
+            sg = K.sent_global_dist_parts(img_features, sent_g, cls_t, gamma3, temp3, eps,
+                                          row_offset, buf[2 * n_c:2 * n_c + n_sg])
+            ih = K.identity_heads_parts(sent, self.text_cls, img_features, self.image_cls,
+                                        class_ids, self.ident_loss.gamma, buf[2 * n_c + n_sg:])
+        logits = words_logits_bert(words_features, words_g, args)
+        row_lse = K.ce_partials(logits, buf[:2 * n_c].view(2, n_c))
+        main.wait_stream(side)
+        from .dist import all_gather_cat
+        allp = all_gather_cat(buf.unsqueeze(0), ctx.group)                        # 2
+        world = allp.shape[0]
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            s0, s1, cl = K.sent_global_dist(img_features, sent_g, cls_t, gamma3, temp3, eps,
+                                            row_offset, n_global, ctx.group,
+                                            pre=sg + (allp[:, 2 * n_c:2 * n_c + n_sg],))
+            tid, iid = K.identity_heads(sent, self.text_cls, img_features, self.image_cls,
+                                        class_ids, self.ident_loss.gamma, group=ctx.group,
+                                        n_global=n_global,
+                                        pre=(ih, allp[:, 2 * n_c + n_sg:]))
+            torch.autograd.backward((s0, s1, cl, tid, iid),
+                                    self._weights((1.0, 1.0, lc, wi, wi), dev))
+        w0, w1 = K.contrastive_ce(logits, row_offset, n_global, ctx.group,
+                                  pre=(row_lse, allp[:, :2 * n_c].reshape(world, 2, n_c)))
+        torch.autograd.backward((w0, w1), self._weights((1.0, 1.0), dev))
+        main.wait_stream(side)
+        out = self._report(w0, w1, s0, s1, cl, tid, iid, lc, wi)
+        ctx.reduce_grads(self.params)                                             # 3
+        self.optimizer.step()
+        return out
 
     def _report(self, w0, w1, s0, s1, cl, tid, iid, lc, wi):
         """The logged terms (and the objective) in one launch."""

@@ -78,8 +78,10 @@ int tgfr_prep_rows_f16(const float* x, long long s_item, long long s_row, long l
  * caption past the bound stores S' - max and the maxima); Sp NULL runs the
  * exact-max kernel instead.
  * t_pad 64: exact while the bound is <= 85.9 (unshifted up to 84.5, shifted
- * by the bound beyond); the caller routes larger inputs to bounded = 0.
- * Otherwise the exact-max kernel runs.  C is stored unnormalised
+ * by the bound beyond).  For inputs not known to be unit rows pass a guard
+ * (tgfr_wr_guard, below; NULL: none): the max-free kernel and its exact
+ * running-max twin are then both launched and the guard picks one on the
+ * device.  Otherwise the exact-max kernel runs.  C is stored unnormalised
  * (C-hat = Z C); tgfr_wr_bwd_tok folds the 1/Z back in. */
 int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, const float* Wnorm, const float* Rnorm, const int* lens,
@@ -87,7 +89,18 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 int img_offset, float gamma1, float gamma2, float gamma3, float eps,
                 float* logits, int ld_logits, float* stats, uint16_t* Chi, uint16_t* Clo,
                 uint16_t* Sp, float* att, int att_T, int bounded, int t_pad, int mode,
-                void* stream);
+                const int* guard, void* stream);
+
+/* Device-side choice of the 64-token bounded path (ABI 510):
+ * *guard = !(max Wnorm[0..n_w) * max Rnorm[0..n_r) <= 85.9), one 1024-thread
+ * workgroup.  With the guard, tgfr_wr_fwd / tgfr_wr_bwd_tok(_ce) /
+ * tgfr_wr_bwd (bounded = 1, t_pad 64, modes 0 / 2) launch the max-free
+ * kernels and their exact twins, each exiting at once unless the guard
+ * selects it -- so a call captured into a HIP graph stays exact for any
+ * input, as the reference's softmaxes (models/attention.py:28-36) are, with
+ * no host read.  Replaces the host-side norm check of round 4. */
+int tgfr_wr_guard(const float* Wnorm, int n_w, const float* Rnorm, int n_r, int* guard,
+                  void* stream);
 
 /* Backward of tgfr_wr_fwd w.r.t. the image regions given dL/dlogits, in two
  * calls.  tgfr_wr_bwd_tok: per-(pair, token) scalars from the forward stats
@@ -105,11 +118,13 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
  * it, Whi is the forward's log2(e)-scaled words, and the max-free kernels
  * run (t_pad 32: the two-role one, wr_bwd_duo_kernel, which reads the
  * forward's stored scores Sp instead of recomputing them -- required then;
- * NULL otherwise). */
+ * NULL otherwise).  guard: the forward's (tgfr_wr_guard; NULL: none); with
+ * it tgfr_wr_bwd also takes Wplain, the plain (unscaled) word rows of the
+ * exact twin (tgfr_prep_rows with scale 1). */
 int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const float* Rnorm, const int* lens,
                     int B_img, int B_cap, float gamma1, float gamma2, float gamma3, float eps,
                     const float* dlogits, int ld, int bounded, int t_pad, float* tok_ws,
-                    void* stream);
+                    const int* guard, void* stream);
 /* tgfr_wr_bwd_tok with the contrastive CE's gradient formed in the same
  * launch instead of read from dlogits (tgfr_ce_grad's formula: logits [B_img]
  * [ld] from tgfr_wr_fwd, row_lse / col_lse from tgfr_ce_stats, row_offset,
@@ -121,13 +136,13 @@ int tgfr_wr_bwd_tok_ce(const float* stats, const float* Wnorm, const float* Rnor
                        float gamma3, float eps, const float* logits, int ld, int row_offset,
                        float inv_n, const float* row_lse, const float* col_lse, const float* g0,
                        const float* g1, float w0, float w1, int bounded, int t_pad,
-                       float* tok_ws, void* stream);
+                       float* tok_ws, const int* guard, void* stream);
 int tgfr_wr_bwd_ws(int B_img, int B_cap, int bounded, int t_pad, int mode, long long* floats);
 int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Wlo, int B_img, int B_cap, float gamma1, const float* tok_ws,
                 const uint16_t* Chi, const uint16_t* Clo, const uint16_t* Sp, float* dR,
                 long long s_b, long long s_r, long long s_d, float* ws, int bounded, int t_pad,
-                int mode, void* stream);
+                int mode, const uint16_t* Wplain, const int* guard, void* stream);
 
 /* Verification pair scores (utils/modules.py:152-153): out[i] = x_i.y_i /
  * max(|x_i| |y_i|, eps) for matched rows of x [rows][d] (ldx) and y (ldy). */

@@ -258,9 +258,9 @@ def test_train_step_with_text_heading_matches_oracle(gpu, precision, b):
     fp32 as test_train_step_matches_oracle, except Adam's first update at 1e-3
     of scale (its sign decision on |g| ~ 1e-5 elements moves with the ~1e-5
     word differences TextHeading's own fp32 convs leave: 1.1e-4 measured);
-    bf16 as the reduced-precision step,
-    with the sentence-side terms at 1e-2 (TextHeading's bf16 convs: words and
-    sentence codes within 2e-2, test_text_heading_vs_oracle)."""
+    bf16 as the reduced-precision step, except the DAMSM group at 6e-3 and the
+    identity terms at 1e-2 (TextHeading's bf16 convs: words and sentence codes
+    within 2e-2, test_text_heading_vs_oracle; 2.1e-3 / 2.6e-2 measured)."""
     from text_guided_face_recognition_amd.config import make_args
     from text_guided_face_recognition_amd.train import Train, synthetic_batch
     nw = 30
@@ -279,8 +279,10 @@ def test_train_step_with_text_heading_matches_oracle(gpu, precision, b):
     errs = {k: abs(out[k].item() - v) for k, v in ref["groups"].items()}
     print(f"{precision} B={b}: groups", {k: f"{v:.3e}" for k, v in errs.items()})
     fp32 = precision == "fp32"
-    assert errs["damsm"] < (1e-3 if fp32 else 4e-2), errs
-    assert errs["clip"] < (1e-3 if fp32 else 1e-2), errs
+    # (round 5 measured, bf16 B = 64: damsm 2.1e-3, clip 1.8e-4, ident 2.6e-2,
+    # worst head gradient 1.5e-2 of scale, SGD updates 4.0e-4 of scale)
+    assert errs["damsm"] < (1e-3 if fp32 else 6e-3), errs
+    assert errs["clip"] < 1e-3, errs
     assert errs["ident"] < 2 * args.lambda_id * (1e-3 if fp32 else 1e-2), errs
     named = dict(tr.image_head.named_parameters())
     g_all = max(x.abs().max().item() for x in ref["grads"].values())
@@ -289,13 +291,13 @@ def test_train_step_with_text_heading_matches_oracle(gpu, precision, b):
         gmax = max(gmax, _check_adam(named[k], ref["old"][v], ref["hp"][v].detach(),
                                      ref["grads"][v], args.lr_head, k, g_all,
                                      **(dict(utol=1e-3) if fp32 else
-                                        dict(gtol=1e-1, utol=1e-3, gfloor=1e-3))))
+                                        dict(gtol=5e-2, utol=1e-3, gfloor=1e-3))))
     print(f"  worst head gradient error {gmax:.3e} of its tensor's scale")
     for new, want in ((tr.image_cls.weight, ref["arc_i"]), (tr.text_cls.weight, ref["arc_t"])):
         scale = want.abs().max().clamp(min=1e-6)
         err = ((new.detach().cpu() - want).abs().max() / scale).item()
         print(f"  SGD update error {err:.3e} of scale")
-        assert err < (1e-4 if fp32 else 1e-2), err
+        assert err < (1e-4 if fp32 else 2e-3), err
 
 
 def _words_logits(ri, words, lens, nw, precision):

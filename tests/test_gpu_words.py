@@ -104,15 +104,16 @@ def test_words_bf16_bounded_vs_golden(gpu, tag):
     logits, l0, l1, _, dr = _run(g, gpu, "bf16", bounded=True)
     err = np.abs(logits.numpy() - g["logits"]).max()
     print(f"bf16 pipelined {tag}: max |logit error| {err:.3e}")
-    # (round 4: 3.8e-3 / 4.2e-3 measured on the two fixtures)
-    np.testing.assert_allclose(logits.numpy(), g["logits"], atol=2e-2, rtol=0)
+    # (round 5: 3.8e-3 / 4.2e-3 measured on the two fixtures, region
+    # gradients 4.5e-3 / 4.6e-3 of scale)
+    np.testing.assert_allclose(logits.numpy(), g["logits"], atol=1e-2, rtol=0)
     assert (logits.argmax(1).numpy() == g["logits"].argmax(1)).all()
     assert (logits.argmax(0).numpy() == g["logits"].argmax(0)).all()
-    assert abs(l0 - float(g["loss0"])) < 2e-2 and abs(l1 - float(g["loss1"])) < 2e-2
+    assert abs(l0 - float(g["loss0"])) < 1e-2 and abs(l1 - float(g["loss1"])) < 1e-2
     scale = np.abs(g["d_img"]).max()
     err = np.abs(dr.numpy() - g["d_img"]).max() / scale
     print(f"  region gradient error {err:.3e} of scale")
-    assert err < 3e-2, err
+    assert err < 1.5e-2, err
 
 
 def _unit(x):
@@ -143,8 +144,9 @@ def test_words_bf16_bounded_vs_oracle_shapes(gpu, b_img, b_cap, nw):
     scale = ro.grad.abs().max().item()
     err = (rg.grad.cpu() - ro.grad).abs().max().item() / scale
     print(f"bf16 bounded {b_img}x{b_cap} T={nw}: logit err {lerr:.3e}, grad err {err:.3e}")
-    assert lerr < 3e-2, lerr
-    assert err < 3e-2, err
+    # (round 5 measured: logits 3.9e-3..7.9e-3, gradients 3.7e-3..4.8e-3 of scale)
+    assert lerr < 2e-2, lerr
+    assert err < 1.5e-2, err
 
 
 @pytest.mark.parametrize("b_img,b_cap,nw", [(9, 13, 30), (16, 16, 22), (3, 40, 7)])
@@ -365,7 +367,7 @@ def test_words_bounded_past_unit_norm(gpu, mode, nw, wn, rn, ltol, gtol):
     of csrc/tgfr_wr.hip bound_shift, c <= 84.5); |W| = |R| = 12 (c = 144):
     bf16 with 30 words takes the running-max variant of the max-free kernels
     on the device (per caption, BIG_C); 62 words / fp16 past WR_BOUND_MAX the
-    host takes the exact running-max kernels.
+    device guard (tgfr_wr_guard) runs the exact running-max twins.
     Logits and gradients finite and matching the oracle (models/losses.py:83-109
     on unnormalised BERT-path features); the tolerance grows with c because
     the operands' relative rounding scales every score by |W| |R|."""
@@ -448,6 +450,62 @@ def test_words_bounded_graph_captured_past_bound(gpu, wn, rn, ltol, gtol):
     gerr = (grad - ref_g).abs().max().item() / ref_g.abs().max().item()
     print(f"captured bf16 c={wn * rn:.0f}: logit err {lerr:.3e}, grad err {gerr:.3e}")
     assert lerr < ltol and gerr < gtol, (lerr, gerr)
+
+
+# 62 words (configs[4]'s captions): ONE captured graph, replayed on unit rows
+# (c = 1: the max-free kernels) and on the same buffers scaled to c = 144 and
+# c = 400 (past WR_BOUND_MAX: the exact running-max twins) -- the device guard
+# (tgfr_wr_guard) picks the kernels at replay time, with no host read
+@pytest.mark.parametrize("mode", ["bf16", "fp16"])
+def test_words_t62_device_guard_in_captured_graph(gpu, mode):
+    K = _kernels()
+    nw = 62
+    r, w, _, _, probe = _past_bound_case(gpu, 1.0, 1.0, nw, 92)
+    rg = r.to(gpu).requires_grad_()
+    wd = w.to(gpu)
+    wv = K.words_view(wd, nw)
+    lens = torch.full((w.shape[0],), nw, dtype=torch.int32, device=gpu)
+    pr = probe.to(gpu)
+
+    def step():
+        rg.grad = None
+        logits = K.word_region_logits(rg, wv, lens, 4.0, 5.0, 10.0, mode=mode, bounded=True)
+        (logits * pr).sum().backward()
+        return logits.detach()
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = step()
+    grad = rg.grad
+    # (tolerances: the operands' relative rounding scales every score by c)
+    # (round 5 measured, bf16 logit / gradient: c=1 3.0e-3 / 3.7e-3, c=144
+    # 8.5e-3 / 6.4e-2)
+    tol = {"bf16": {1.0: (1e-2, 2e-2), 12.0: (3e-2, 1.5e-1), 20.0: (6e-2, 3e-1)},
+           "fp16": {1.0: (3e-3, 5e-3), 12.0: (6e-3, 2e-2), 20.0: (1.5e-2, 5e-2)}}[mode]
+    for scale in (1.0, 12.0, 20.0):
+        with torch.no_grad():
+            rg.copy_(r.to(gpu) * scale)
+            wd.copy_(w.to(gpu) * scale)
+        graph.replay()
+        torch.cuda.synchronize()
+        got, g = out.cpu(), grad.cpu()
+        ws = scale
+        ro = (r * scale).requires_grad_()
+        _, _, _, ref = O.words_loss(ro, w * ws, None, None, nw, 4.0, 5.0, 10.0,
+                                    batch_size=w.shape[0])
+        (ref * probe).sum().backward()
+        assert torch.isfinite(got).all() and torch.isfinite(g).all()
+        lerr = (got - ref.detach()).abs().max().item()
+        gerr = (g - ro.grad).abs().max().item() / ro.grad.abs().max().item()
+        print(f"captured {mode} T=62 c={scale * ws:.0f}: logit err {lerr:.3e}, "
+              f"grad err {gerr:.3e}")
+        ltol, gtol = tol[scale]
+        assert lerr < ltol and gerr < gtol, (scale, lerr, gerr)
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp16"])

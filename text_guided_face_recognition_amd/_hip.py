@@ -31,12 +31,14 @@ SIGNATURES = {
     "tgfr_version": [],
     "tgfr_prep_rows": [P, L, L, L, I, I, I, I, P, F, P, P, P, P],
     "tgfr_prep_rows_f16": [P, L, L, L, I, I, I, I, P, F, P, P, P],
-    "tgfr_wr_fwd": [P, P, P, P, P, P, P, I, I, I, F, F, F, F, P, I, P, P, P, P, P, I, I, I, I, P],
-    "tgfr_wr_bwd_tok": [P, P, P, P, I, I, F, F, F, F, P, I, I, I, P, P],
+    "tgfr_wr_fwd": [P, P, P, P, P, P, P, I, I, I, F, F, F, F, P, I, P, P, P, P, P, I, I, I, I, P,
+                    P],
+    "tgfr_wr_guard": [P, I, P, I, P, P],
+    "tgfr_wr_bwd_tok": [P, P, P, P, I, I, F, F, F, F, P, I, I, I, P, P, P],
     "tgfr_wr_bwd_tok_ce": [P, P, P, P, I, I, F, F, F, F, P, I, I, F, P, P, P, P, F, F, I, I, P,
-                           P],
+                           P, P],
     "tgfr_wr_bwd_ws": [I, I, I, I, I, P],
-    "tgfr_wr_bwd": [P, P, P, P, I, I, F, P, P, P, P, P, L, L, L, P, I, I, I, P],
+    "tgfr_wr_bwd": [P, P, P, P, I, I, F, P, P, P, P, P, L, L, L, P, I, I, I, P, P, P],
     "tgfr_wr_lds_bytes": [I],
     "tgfr_cos_logits": [P, L, P, L, I, I, I, I, F, F, I, P, I, P, L, P],
     "tgfr_cos_logits_bwd": [P, L, L, P, L, P, L, I, I, I, I, F, F, P, L, P],

@@ -55,6 +55,17 @@ constexpr int NRT = 7;         // region tiles
 __device__ __forceinline__ float bound_shift(float c) { return fmaxf(c - 84.5f, 0.f); }
 __device__ __forceinline__ float sum_floor(float s) { return fmaxf(s, 0x1p-126f); }
 
+// Guarded 64-token launches (tgfr_wr_guard): *guard = 1 when some pair's
+// score bound may exceed WR_BOUND_MAX.  Every step of the path is then
+// launched twice, max-free kernel first and its exact running-max twin
+// second; the one that does not match the flag exits at once, so the choice
+// is made on the device (also inside a captured graph, where the host cannot
+// read the norms).  guard == nullptr: no guard, every kernel runs.
+constexpr float WR_BOUND_MAX = 85.9f;      // bound_shift's exact window (kernels.py)
+__device__ __forceinline__ bool guard_skip(const int* guard, bool exact_kernel) {
+  return guard && ((*guard != 0) != exact_kernel);
+}
+
 // ----------------------------------------------------------------- prep ---
 __global__ __launch_bounds__(256) void prep_rows_kernel(
     const float* __restrict__ x, long long s_item, long long s_row, long long s_col,
@@ -677,9 +688,11 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
     const float* __restrict__ Wnorm, const float* __restrict__ Rnorm, const int* __restrict__ lens,
     int B_img, int B_cap, int n_chunks, int img_offset, float g1, float g2, float g3, float eps,
     float* __restrict__ logits, int ld_logits, float4* __restrict__ stats,
-    uint16_t* __restrict__ Chi, float* __restrict__ att, int att_T) {
+    uint16_t* __restrict__ Chi, float* __restrict__ att, int att_T,
+    const int* __restrict__ guard) {
   constexpr int TP = 64;
   constexpr float L2E = 1.4426950408889634f;
+  if (guard_skip(guard, !BOUNDED)) return;
   const int work = xcd_remap(blockIdx.x, n_chunks * B_img);
   const int b = work / n_chunks, chunk = work % n_chunks;
   const int per = (B_cap + n_chunks - 1) / n_chunks;
@@ -1415,7 +1428,9 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
                                                      const float* __restrict__ dlogits, int ld,
                                                      int B_img, int B_cap, float g1, float g2,
                                                      float g3, float eps, int layout,
-                                                     float* __restrict__ tok, CeGrad ce) {
+                                                     float* __restrict__ tok, CeGrad ce,
+                                                     const int* __restrict__ guard) {
+  if (guard && *guard) layout = 0;         // the exact backward's table
   const long long pair = (blockIdx.x * 256LL + threadIdx.x) / WAVE;
   if (pair >= (long long)B_img * B_cap) return;
   const int b = pair / B_cap, i = pair % B_cap;
@@ -1840,10 +1855,11 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Rlo,
     const uint16_t* __restrict__ Whi, const uint16_t* __restrict__ Wlo, int B_img, int B_cap,
     int n_chunks, float g1, const float* __restrict__ tok, const uint16_t* __restrict__ Chi,
-    const uint16_t* __restrict__ Clo, float* __restrict__ slab) {
+    const uint16_t* __restrict__ Clo, float* __restrict__ slab, const int* __restrict__ guard) {
   constexpr int NIMG = BwdWCfg<MODE>::NIMG;
   constexpr int BUF = BwdWCfg<MODE>::BUF;
   constexpr int NB = BwdWCfg<MODE>::NB;
+  if (guard_skip(guard, true)) return;
   const int total = n_chunks * 2 * B_img;
   const int work = xcd_remap(blockIdx.x, total);
   const int b = work / (2 * n_chunks);
@@ -2062,7 +2078,9 @@ __global__ __launch_bounds__(256) void wr_reduce_frag_kernel(const uint16_t* __r
                                                              int n_chunks, int B_img,
                                                              float* __restrict__ out,
                                                              long long s_b, long long s_r,
-                                                             long long s_d) {
+                                                             long long s_d,
+                                                             const int* __restrict__ guard) {
+  if (guard_skip(guard, false)) return;
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= B_img * NRT * 8 * 64) return;
   const int lane = e & 63, dt = (e >> 6) & 7, tile = e >> 9;      // tile = b * NRT + rt
@@ -2119,9 +2137,10 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi, int B_img, int B_cap,
     int n_chunks, float g1, const float* __restrict__ tok, const uint16_t* __restrict__ Chi,
     float* __restrict__ out, long long s_b, long long s_r, long long s_d,
-    uint16_t* __restrict__ slab) {
+    uint16_t* __restrict__ slab, const int* __restrict__ guard) {
   constexpr int BUF = BwdWCfg<MODE>::BUF;
   static_assert(BwdWCfg<MODE>::NB == 2, "two-deep ring");
+  if (guard_skip(guard, false)) return;
   const int total = n_chunks * 2 * B_img;
   const int work = xcd_remap(blockIdx.x, total);
   const int b = work / (2 * n_chunks);
@@ -2160,21 +2179,45 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
                       (((2 * (g16 & 1) + (p4 >> 1)) ^ ((h + 2 * bb) & 3)) << 4) + (p4 & 1) * 8;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (c0 < c1)
-    bwd_stage_wide<MODE>(0, Whi, nullptr, Chi, nullptr, tok, (long long)b * B_cap + c0, c0, wid,
-                         lane);
   // token scalar k of tile u for the lane's tokens 8g + 4h + 0..3 (q = 4g..4g+3)
   auto scal = [&](uint32_t tb, int k, int u, int g) {
     return __builtin_bit_cast(u32x4, lds_ld16(tb + k * 256 + u * 128 + g * 32 + h * 16));
   };
   auto fl = [](const u32x4& x, int q) { return __uint_as_float(x[q & 3]); };
 
+  // DMA piece j (< 16: 1-KiB pieces k = wid + 4 j of the X image, as
+  // bwd_stage_wide lays them out; 16, 17: the token table's two, identical
+  // bytes from every wave) of caption ii into the ring slot at nb.  Row
+  // 4 (wid + 4 j') + lane / 16 of piece j (j' = j % 8) has the same swizzle
+  // for every j, so each lane keeps one byte offset per source (W', C-hat)
+  // and a piece is a scalar base + that offset (saddr form: nothing per
+  // piece on the VALU, nothing hoisted into long-lived registers).
+  const int sw = ((lane >> 4) << 2) | wid;
+  const uint32_t voff_w = (uint32_t)(((4 * wid + (lane >> 4)) * D + ((lane & 15) ^ sw) * 8) * 2);
+  const uint32_t voff_c = (uint32_t)((((lane & 15) ^ sw) * 64 + 4 * wid + (lane >> 4)) * 16);
+  auto dma_piece = [&](int ii, uint32_t nb, int j) {
+    const long long pair = (long long)b * B_cap + ii;
+    if (j >= 16) {
+      glds16s(tok + pair * 64 * 8, lane * 16 + (j - 16) * 1024,
+              nb + W_XIMG + (j - 16) * 1024);
+      return;
+    }
+    const int jj = j % 8, half = j / 8;
+    const uint32_t dst = nb + half * (128 * 256) + 4 * (wid + 4 * jj) * 256;
+    if (jj < 4)
+      glds16s(Whi + ((long long)ii * 64 + 16 * jj) * D + half * 128, voff_w, dst);
+    else
+      glds16s(Chi + pair * 32 * 64 * 8 + half * 16 * 64 * 8 + (jj - 4) * 16 * 8, voff_c, dst);
+  };
+
+  if (c0 < c1)
+#pragma unroll
+    for (int j = 0; j < 18; ++j) dma_piece(c0, 0, j);
   for (int i = c0; i < c1; ++i) {
     const int it = i - c0;
     ring_barrier<0>();     // caption i landed; caption i-1's buffer retired
-    if (i + 1 < c1)
-      bwd_stage_wide<MODE>(((it + 1) & 1) * BUF, Whi, nullptr, Chi, nullptr, tok,
-                           (long long)b * B_cap + i + 1, i + 1, wid, lane);
+    const bool has_next = i + 1 < c1;
+    const uint32_t nb = ((it + 1) & 1) * BUF;   // the next caption's slot
     const uint32_t base = (it & 1) * BUF;
     const uint32_t tk = base + W_XIMG;
     // ---- [S'^T ; Q-hat^T] of both token tiles = [W' ; C-hat] R_tile^T, S'
@@ -2191,12 +2234,19 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
           A1[u][4 * g + k] = 0.f;
         }
       }
-    // 64 MFMAs n = (k-step s, tile u, W'/C-hat), operands read WPF slots ahead
+    // 64 MFMAs n = (W' / C-hat block c, k-step s, tile u): the 32 S' MFMAs
+    // of both token tiles first, then the 32 Q-hat ones, whose issue gaps
+    // carry phase A of the softmax (p = exp2(S') and its per-region sum: S'
+    // is complete by then) and the next caption's X-image DMA (one piece
+    // every 4 slots: the burst at the stage head cost ~100 cycles of issue a
+    // piece with the matrix core idle).  Operands read WPF slots ahead
     // through a ring (one wave per SIMD: an LDS read waited on right before
-    // its MFMA stalls the wave for the whole LDS latency)
+    // its MFMA stalls the wave for the whole LDS latency).
+    float a1[2][16], ax[2][16], v[2][16];
+    float sum = 0.f;
     {
       auto rd1 = [&](int n) {
-        const int s = n >> 2, u = (n >> 1) & 1, c = n & 1;
+        const int c = n >> 5, s = (n >> 1) & 15, u = n & 1;
         return lds_ld16(base + g1o[s & 7] + (s >> 3) * (128 * 256) + u * 32 * 256 +
                         c * 64 * 256);
       };
@@ -2205,24 +2255,27 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
       for (int n = 0; n < WPF; ++n) ring[n] = rd1(n);
 #pragma unroll
       for (int n = 0; n < 64; ++n) {
-        const int s = n >> 2, u = (n >> 1) & 1;
+        const int c = n >> 5, s = (n >> 1) & 15, u = n & 1;
         const bf16x8 x = as_bf8(ring[n & 7]);
-        if (n & 1) mma<MODE>(A1[u], x, x, Rf[s], Rf[s]);
+        if (c) mma<MODE>(A1[u], x, x, Rf[s], Rf[s]);
         else mma<MODE>(A0[u], x, x, Rf[s], Rf[s]);
         if (n + WPF < 64) ring[(n + WPF) & 7] = rd1(n + WPF);
+        if (has_next && (n & 3) == 1) dma_piece(i + 1, nb, n >> 2);
+        if (has_next && (n == 3 || n == 7)) dma_piece(i + 1, nb, 16 + (n >> 2));
+        if (n >= 34) {                   // elements 0..29 of phase A
+          const int e = n - 34, uu = e >> 4, q = e & 15;
+          a1[uu][q] = __builtin_amdgcn_exp2f(A0[uu][q]);
+          sum += a1[uu][q];
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
     // ---- softmax over the 64 words (p = exp2(S'), bounded) and both backwards
-    float a1[2][16], ax[2][16], v[2][16];
-    float sum = 0.f;
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        a1[u][q] = __builtin_amdgcn_exp2f(A0[u][q]);
-        sum += a1[u][q];
-      }
+    for (int e = 30; e < 32; ++e) {
+      a1[e >> 4][e & 15] = __builtin_amdgcn_exp2f(A0[e >> 4][e & 15]);
+      sum += a1[e >> 4][e & 15];
+    }
     const float inv = __builtin_amdgcn_rcpf(sum_floor(xhalf_sum(sum)));
     const float kq = gL * inv;
     float rho = 0.f;
@@ -2734,7 +2787,9 @@ __global__ __launch_bounds__(256) void wr_reduce_kernel(const float* __restrict_
                                                         int n_chunks, int B_img,
                                                         float* __restrict__ out, long long s_b,
                                                         long long s_r, long long s_d,
-                                                        int accumulate) {
+                                                        int accumulate,
+                                                        const int* __restrict__ guard) {
+  if (guard_skip(guard, true)) return;
   // thread = 4 consecutive d of one (image, region) row
   const int n4 = B_img * NREG * (D / 4);
   for (int e = blockIdx.x * 256 + threadIdx.x; e < n4; e += gridDim.x * 256) {
@@ -2781,15 +2836,16 @@ static int slab_chunks(int B_img, int B_cap) {
 // the bounded kernels' dR: written in place by the kernel (one chunk), else
 // the chunks' fragment-order bf16 partials summed by wr_reduce_frag_kernel
 static int frag_reduce(int n_chunks, int B_img, const uint16_t* slab, float* dR, long long s_b,
-                       long long s_r, long long s_d, hipStream_t s, bool f32_partials = false) {
+                       long long s_r, long long s_d, hipStream_t s, bool f32_partials = false,
+                       const int* guard = nullptr) {
   if (n_chunks > 1) {
     const int threads = B_img * NRT * 8 * 64;
     if (f32_partials)
       hipLaunchKernelGGL(wr_reduce_frag_kernel<true>, dim3((threads + 255) / 256), dim3(256), 0, s,
-                         slab, n_chunks, B_img, dR, s_b, s_r, s_d);
+                         slab, n_chunks, B_img, dR, s_b, s_r, s_d, guard);
     else
       hipLaunchKernelGGL(wr_reduce_frag_kernel<false>, dim3((threads + 255) / 256), dim3(256), 0,
-                         s, slab, n_chunks, B_img, dR, s_b, s_r, s_d);
+                         s, slab, n_chunks, B_img, dR, s_b, s_r, s_d, guard);
   }
   return (int)hipGetLastError();
 }
@@ -2800,7 +2856,53 @@ static int allow_lds(K kernel, int bytes) {
 }
 
 // ============================================================== C ABI ===
+// *guard = !(max Wnorm * max Rnorm <= WR_BOUND_MAX): one workgroup, every
+// thread's loads issued before its max chain (a NaN norm sets the guard)
+__global__ __launch_bounds__(1024) void wr_guard_kernel(const float* __restrict__ Wn, int n_w,
+                                                        const float* __restrict__ Rn, int n_r,
+                                                        int* __restrict__ guard) {
+  __shared__ float red[2][16];
+  const int tid = threadIdx.x;
+  auto nanmax = [](float a, float x) { return (x > a || x != x) ? x : a; };
+  float m[2] = {0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float* x = k ? Rn : Wn;
+    const int n = k ? n_r : n_w;
+    for (int i0 = 0; i0 < n; i0 += 1024 * 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = x[min(i0 + j * 1024 + tid, n - 1)];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[k] = nanmax(m[k], v[j]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m[k] = nanmax(m[k], __shfl_xor(m[k], o));
+  }
+  if (tid % WAVE == 0) {
+    red[0][tid / WAVE] = m[0];
+    red[1][tid / WAVE] = m[1];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float mw = 0.f, mr = 0.f;
+    for (int w = 0; w < 16; ++w) {
+      mw = nanmax(mw, red[0][w]);
+      mr = nanmax(mr, red[1][w]);
+    }
+    guard[0] = (mw * mr <= WR_BOUND_MAX) ? 0 : 1;
+  }
+}
+
 extern "C" {
+
+int tgfr_wr_guard(const float* Wnorm, int n_w, const float* Rnorm, int n_r, int* guard,
+                  void* stream) {
+  if (!Wnorm || !Rnorm || !guard || n_w <= 0 || n_r <= 0) return 1001;
+  hipLaunchKernelGGL(wr_guard_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, Wnorm, n_w,
+                     Rnorm, n_r, guard);
+  return (int)hipGetLastError();
+}
 
 int tgfr_prep_rows(const float* x, long long s_item, long long s_row, long long s_col,
                    int n_items, int n_rows, int n_cols, int rows_pad, const int* lens,
@@ -2830,9 +2932,11 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 int img_offset, float gamma1, float gamma2, float gamma3, float eps,
                 float* logits, int ld_logits, float* stats, uint16_t* Chi, uint16_t* Clo,
                 uint16_t* Sp, float* att, int att_T, int bounded, int t_pad, int mode,
-                void* stream) {
+                const int* guard, void* stream) {
   if (B_img <= 0 || B_cap <= 0 || ld_logits < B_cap || !Rhi || !Whi) return 1001;
   if (t_pad != 32 && t_pad != 64) return 1001;
+  // a guard makes sense only where a max-free 64-token kernel would run
+  if (guard && (t_pad != 64 || !bounded || !Rnorm || mode == MODE_SPLIT)) return 1001;
   // the general kernels stage the R lo plane in every mode (read only in
   // split mode): single-operand modes without one stage hi twice
   if (!Rlo) {
@@ -2853,19 +2957,27 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
       // R resident in LDS; caption chunks sized for >= ~256 workgroups
       const int n_chunks = max(1, min((B_cap + 1) / 2, (256 + B_img - 1) / B_img));
       const dim3 g(n_chunks * B_img);
-#define TGFR_RES2(M, A, BD)                                                                 \
+#define TGFR_RES2(M, A, BD, G)                                                              \
   do {                                                                                     \
     if (const int e = allow_lds(wr_fwd_res2_kernel<M, A, BD>, FR2_LDS)) return e;          \
     hipLaunchKernelGGL((wr_fwd_res2_kernel<M, A, BD>), g, dim3(256), FR2_LDS, s, Rhi, Whi,   \
                        Wnorm, Rnorm, lens, B_img, B_cap, n_chunks, img_offset, gamma1, gamma2, \
-                       gamma3, eps, logits, ld_logits, (float4*)stats, Chi, att, att_T);   \
+                       gamma3, eps, logits, ld_logits, (float4*)stats, Chi, att, att_T, G); \
   } while (0)
-      if (mode == MODE_BF16 && att) TGFR_RES2(MODE_BF16, true, false);
-      else if (mode == MODE_BF16 && bounded && Rnorm) TGFR_RES2(MODE_BF16, false, true);
-      else if (mode == MODE_BF16) TGFR_RES2(MODE_BF16, false, false);
-      else if (mode == MODE_F16 && att) TGFR_RES2(MODE_F16, true, false);
-      else if (mode == MODE_F16 && bounded && Rnorm) TGFR_RES2(MODE_F16, false, true);
-      else if (mode == MODE_F16) TGFR_RES2(MODE_F16, false, false);
+      // (attention maps: the exact kernel alone, guard or not)
+      if (guard && !att && mode == MODE_BF16) {        // max-free, then its exact twin
+        TGFR_RES2(MODE_BF16, false, true, guard);
+        TGFR_RES2(MODE_BF16, false, false, guard);
+      } else if (guard && !att && mode == MODE_F16) {
+        TGFR_RES2(MODE_F16, false, true, guard);
+        TGFR_RES2(MODE_F16, false, false, guard);
+      }
+      else if (mode == MODE_BF16 && att) TGFR_RES2(MODE_BF16, true, false, nullptr);
+      else if (mode == MODE_BF16 && bounded && Rnorm) TGFR_RES2(MODE_BF16, false, true, nullptr);
+      else if (mode == MODE_BF16) TGFR_RES2(MODE_BF16, false, false, nullptr);
+      else if (mode == MODE_F16 && att) TGFR_RES2(MODE_F16, true, false, nullptr);
+      else if (mode == MODE_F16 && bounded && Rnorm) TGFR_RES2(MODE_F16, false, true, nullptr);
+      else if (mode == MODE_F16) TGFR_RES2(MODE_F16, false, false, nullptr);
       else return 1002;
 #undef TGFR_RES2
       return (int)hipGetLastError();
@@ -2906,17 +3018,21 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
 static int wr_tok_launch(const float* stats, const float* Wnorm, const float* Rnorm,
                          const int* lens, int B_img, int B_cap, float gamma1, float gamma2,
                          float gamma3, float eps, const float* dlogits, int ld, int bounded,
-                         int t_pad, float* tok_ws, const CeGrad& ce, void* stream) {
+                         int t_pad, float* tok_ws, const CeGrad& ce, const int* guard,
+                         void* stream) {
   if (B_img <= 0 || B_cap <= 0 || ld < B_cap) return 1001;
+  if (guard && (t_pad != 64 || !bounded)) return 1001;
   const long long pairs = (long long)B_img * B_cap;
   if (t_pad == 64)
     hipLaunchKernelGGL(wr_tok_kernel<64>, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, (const float4*)stats, Wnorm, Rnorm, lens, dlogits, ld,
-                       B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 1 : 0, tok_ws, ce);
+                       B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 1 : 0, tok_ws, ce,
+                       guard);
   else if (t_pad == 32)
     hipLaunchKernelGGL(wr_tok_kernel<32>, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, (const float4*)stats, Wnorm, Rnorm, lens, dlogits, ld,
-                       B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 2 : 0, tok_ws, ce);
+                       B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 2 : 0, tok_ws, ce,
+                       nullptr);
   else
     return 1001;
   return (int)hipGetLastError();
@@ -2928,10 +3044,10 @@ int tgfr_wr_bwd_tok(const float* stats, const float* Wnorm, const float* Rnorm, 
                     int B_img,
                     int B_cap, float gamma1, float gamma2, float gamma3, float eps,
                     const float* dlogits, int ld, int bounded, int t_pad, float* tok_ws,
-                    void* stream) {
+                    const int* guard, void* stream) {
   if (!dlogits) return 1001;
   return wr_tok_launch(stats, Wnorm, Rnorm, lens, B_img, B_cap, gamma1, gamma2, gamma3, eps,
-                       dlogits, ld, bounded, t_pad, tok_ws, CeGrad{}, stream);
+                       dlogits, ld, bounded, t_pad, tok_ws, CeGrad{}, guard, stream);
 }
 
 int tgfr_wr_bwd_tok_ce(const float* stats, const float* Wnorm, const float* Rnorm,
@@ -2939,11 +3055,11 @@ int tgfr_wr_bwd_tok_ce(const float* stats, const float* Wnorm, const float* Rnor
                        float gamma3, float eps, const float* logits, int ld, int row_offset,
                        float inv_n, const float* row_lse, const float* col_lse, const float* g0,
                        const float* g1, float w0, float w1, int bounded, int t_pad,
-                       float* tok_ws, void* stream) {
+                       float* tok_ws, const int* guard, void* stream) {
   if (!logits || !row_lse || !col_lse) return 1001;
   const CeGrad ce{logits, row_lse, col_lse, g0, g1, w0, w1, inv_n, row_offset};
   return wr_tok_launch(stats, Wnorm, Rnorm, lens, B_img, B_cap, gamma1, gamma2, gamma3, eps,
-                       nullptr, ld, bounded, t_pad, tok_ws, ce, stream);
+                       nullptr, ld, bounded, t_pad, tok_ws, ce, guard, stream);
 }
 
 int tgfr_wr_bwd_ws(int B_img, int B_cap, int bounded, int t_pad, int mode, long long* floats) {
@@ -2957,9 +3073,10 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
                 const uint16_t* Chi, const uint16_t* Clo, const uint16_t* Sp, float* dR,
                 long long s_b,
                 long long s_r, long long s_d, float* ws, int bounded, int t_pad, int mode,
-                void* stream) {
+                const uint16_t* Wplain, const int* guard, void* stream) {
   if (B_img <= 0 || B_cap <= 0 || !dR || !ws) return 1001;
   if (mode != MODE_SPLIT && mode != MODE_BF16 && mode != MODE_F16) return 1002;
+  if (guard && (!bounded || t_pad != 64 || !Wplain || mode == MODE_SPLIT)) return 1001;
   auto* s = (hipStream_t)stream;
   // caption-chunk partial slabs in ws, summed into dR by wr_reduce_kernel
   const int n_chunks = slab_chunks(B_img, B_cap);
@@ -2970,16 +3087,21 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
     if (mode == MODE_BF16)
       hipLaunchKernelGGL(wr_bwd_wide2_kernel<MODE_BF16>, dim3(grid), dim3(256),
                          BwdWCfg<MODE_BF16>::LDS, s, Rhi, Whi, B_img, B_cap, n_chunks, gamma1,
-                         tok_ws, Chi, dR, s_b, s_r, s_d, (uint16_t*)ws);
+                         tok_ws, Chi, dR, s_b, s_r, s_d, (uint16_t*)ws, guard);
     else if (mode == MODE_F16)
       hipLaunchKernelGGL(wr_bwd_wide2_kernel<MODE_F16>, dim3(grid), dim3(256),
                          BwdWCfg<MODE_F16>::LDS, s, Rhi, Whi, B_img, B_cap, n_chunks, gamma1,
-                         tok_ws, Chi, dR, s_b, s_r, s_d, (uint16_t*)ws);
+                         tok_ws, Chi, dR, s_b, s_r, s_d, (uint16_t*)ws, guard);
     else
       return 1002;
-    return frag_reduce(n_chunks, B_img, (const uint16_t*)ws, dR, s_b, s_r, s_d, s,
-                       mode == MODE_F16);
-  } else if (bounded) {
+    if (const int e = frag_reduce(n_chunks, B_img, (const uint16_t*)ws, dR, s_b, s_r, s_d, s,
+                                  mode == MODE_F16, guard))
+      return e;
+    if (!guard) return 0;
+    // the exact twin (runs when *guard): plain word rows, layout-0 token table
+    Whi = Wplain;
+  }
+  if (bounded && t_pad != 64) {
     if (t_pad != 32 || !Sp) return 1001;
     if (mode != MODE_BF16) return 1002;
     if (const int e = allow_lds(wr_bwd_duo_kernel, BD_LDS)) return e;
@@ -2996,15 +3118,15 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
     if (mode == MODE_SPLIT)
       hipLaunchKernelGGL(wr_bwd_wide_kernel<MODE_SPLIT>, dim3(grid), dim3(256),
                          BwdWCfg<MODE_SPLIT>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
-                         gamma1, tok_ws, Chi, Clo, ws);
+                         gamma1, tok_ws, Chi, Clo, ws, nullptr);
     else if (mode == MODE_F16)
       hipLaunchKernelGGL(wr_bwd_wide_kernel<MODE_F16>, dim3(grid), dim3(256),
-                         BwdWCfg<MODE_F16>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
-                         gamma1, tok_ws, Chi, Clo, ws);
+                         BwdWCfg<MODE_F16>::LDS, s, Rhi, Rlo ? Rlo : Rhi, Whi, Wlo, B_img, B_cap,
+                         n_chunks, gamma1, tok_ws, Chi, Clo, ws, guard);
     else
       hipLaunchKernelGGL(wr_bwd_wide_kernel<MODE_BF16>, dim3(grid), dim3(256),
-                         BwdWCfg<MODE_BF16>::LDS, s, Rhi, Rlo, Whi, Wlo, B_img, B_cap, n_chunks,
-                         gamma1, tok_ws, Chi, Clo, ws);
+                         BwdWCfg<MODE_BF16>::LDS, s, Rhi, Rlo ? Rlo : Rhi, Whi, Wlo, B_img, B_cap,
+                         n_chunks, gamma1, tok_ws, Chi, Clo, ws, guard);
   } else if (t_pad == 32) {
     if (const int e = allow_lds(wr_bwd_kernel<MODE_SPLIT>, BwdCfg<MODE_SPLIT>::LDS)) return e;
     if (const int e = allow_lds(wr_bwd_kernel<MODE_BF16>, BwdCfg<MODE_BF16>::LDS)) return e;
@@ -3027,7 +3149,7 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   const long long n = (long long)B_img * NREG * (D / 4);
   const int rgrid = (int)min((n + 255) / 256, 8192LL);
   hipLaunchKernelGGL(wr_reduce_kernel, dim3(rgrid), dim3(256), 0, s, ws, n_chunks, B_img, dR, s_b,
-                     s_r, s_d, 0);
+                     s_r, s_d, 0, guard);
   return (int)hipGetLastError();
 }
 
@@ -3035,6 +3157,6 @@ int tgfr_wr_lds_bytes(int which) {
   return which == 0 ? F_LDS : which == 1 ? BwdCfg<MODE_SPLIT>::LDS : FR_LDS;
 }
 
-int tgfr_version(void) { return 500; }
+int tgfr_version(void) { return 510; }
 
 }  // extern "C"

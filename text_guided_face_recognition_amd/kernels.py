@@ -19,7 +19,7 @@ NREG = 196
 TPAD = 32
 NREG_TILES = RPAD // 32
 SP_REC = 64 * 16 + 64   # stored scores per (pair, region tile), int16 units (csrc SP_REC)
-N_WR_SAVED = 11         # tensors _wr_fwd saves for _wr_bwd
+N_WR_SAVED = 13         # tensors _wr_fwd saves for _wr_bwd
 
 MODES = {"bf16": 0, "fp32": 1, "fp16": 2}
 
@@ -114,6 +114,7 @@ def _wr_fwd(img_features, words, lens, gamma1, gamma2, gamma3, mode, img_offset=
             bounded=False, uniform=False, eps=1e-8):
     """WordRegionLogits' forward: (logits, att, tensors for the backward, cfg)."""
     dev = img_features.device
+    guard = w_plain = None          # the 64-token device guard (tgfr_wr_guard)
     regions = regions_view(img_features.float())
     b_img, b_cap = regions.shape[0], words.shape[0]
     t_words = words.shape[1]
@@ -155,15 +156,23 @@ def _wr_fwd(img_features, words, lens, gamma1, gamma2, gamma3, mode, img_offset=
         # device (a caption whose score bound max|W| max|R| exceeds 84.5
         # takes their running-max variant), exact for any input, also under
         # graph capture.  64-token captions: exact while the bound is <=
-        # WR_BOUND_MAX (csrc/tgfr_wr.hip, bound_shift); rows made by this
-        # package's heads are L2-normalised (bound ~1), other inputs are
-        # checked here (one host read, skipped under graph capture) and past
-        # the bound take the exact running-max kernels, as the reference's
-        # softmax never overflows (models/attention.py:28-36)
-        if bounded and t_pad != TPAD and not own_rows and \
-                not torch.cuda.is_current_stream_capturing():
-            if not float((w_norm.max() * r_norm.max()).item()) <= WR_BOUND_MAX:
-                bounded = fast = False
+        # WR_BOUND_MAX (csrc/tgfr_wr.hip, bound_shift).  Rows made by this
+        # package's heads are L2-normalised (bound ~1); other inputs get a
+        # device guard (tgfr_wr_guard): every launch of the path has its exact
+        # running-max twin beside it and the guard picks one on the device --
+        # exact for any input, also under graph capture, with no host read --
+        # as the reference's softmax never overflows (models/attention.py:28-36)
+        if bounded and t_pad != TPAD and not own_rows:
+            if not _rows_only(words):
+                guard = torch.empty(1, dtype=torch.int32, device=dev)
+                call("tgfr_wr_guard", ptr(w_norm), w_norm.numel(), ptr(r_norm), r_norm.numel(),
+                     ptr(guard), _hip.stream())
+                w_plain = prep_rows(words.float(), t_words, t_pad, lens=lens, f16=f16)[0]
+            elif not torch.cuda.is_current_stream_capturing():
+                # gathered operand rows of this package's TextHeading (unit
+                # rows) beside foreign regions: checked on the host
+                if not float((w_norm.max() * r_norm.max()).item()) <= WR_BOUND_MAX:
+                    bounded = fast = False
         if _rows_only(words) and not fast:
             raise RuntimeError("words carry only their bounded-kernel operand rows "
                                "(rows_only_words): this path needs the feature values")
@@ -191,9 +200,9 @@ def _wr_fwd(img_features, words, lens, gamma1, gamma2, gamma3, mode, img_offset=
     call("tgfr_wr_fwd", ptr(r_hi), ptr(r_lo), ptr(w_fwd), ptr(w_lo), ptr(w_norm),
          ptr(r_norm), ptr(lens), b_img, b_cap, img_offset, gamma1, gamma2, gamma3, eps,
          ptr(logits), b_cap, ptr(stats), ptr(c_hi), ptr(c_lo), ptr(sp), ptr(att), att_T,
-         int(bool(bounded) and (t_pad == TPAD or m != MODES["fp32"])), t_pad, m,
+         int(bool(bounded) and (t_pad == TPAD or m != MODES["fp32"])), t_pad, m, ptr(guard),
          _hip.stream())
-    saved = (r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo, sp)
+    saved = (r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo, sp, w_plain, guard)
     cfg = (gamma1, gamma2, gamma3, eps, m, img_features.shape, fast, t_pad)
     return logits, att, saved, cfg
 
@@ -202,7 +211,7 @@ def _wr_bwd(saved, cfg, tok_call):
     """WordRegionLogits' backward: d img_features, with the per-(pair, token)
     table made by tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, fast,
     t_pad, tok) (tgfr_wr_bwd_tok from dlogits, or tgfr_wr_bwd_tok_ce)."""
-    r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo, sp = saved
+    r_hi, r_lo, r_norm, w_hi, w_lo, w_norm, lens, stats, c_hi, c_lo, sp, w_plain, guard = saved
     gamma1, gamma2, gamma3, eps, m, shape, fast, t_pad = cfg
     b_img, b_cap = stats.shape[0], stats.shape[1]
     dev = stats.device
@@ -210,12 +219,12 @@ def _wr_bwd(saved, cfg, tok_call):
                      device=dev)
     tok = torch.empty(b_img, b_cap, t_pad, 8, dtype=torch.float32, device=dev)
     split = m == MODES["fp32"]
-    tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, fast, t_pad, tok)
+    tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, fast, t_pad, tok, guard)
     d_reg = torch.empty(b_img, NREG, D, dtype=torch.float32, device=dev)
     call("tgfr_wr_bwd", ptr(r_hi), ptr(r_lo) if split else None, ptr(w_hi),
          ptr(w_lo) if split else None, b_img, b_cap, gamma1, ptr(tok),
          ptr(c_hi), ptr(c_lo) if split else None, ptr(sp), ptr(d_reg), NREG * D, D, 1, ptr(ws),
-         int(fast), t_pad, m, _hip.stream())
+         int(fast), t_pad, m, ptr(w_plain), ptr(guard), _hip.stream())
     # same logical shape as img_features, channels-last strides
     return d_reg.transpose(1, 2).reshape(shape)
 
@@ -244,10 +253,10 @@ class WordRegionLogits(torch.autograd.Function):
         gamma1, gamma2, gamma3, eps = ctx.cfg[:4]
         dlogits = dlogits.float().contiguous()
 
-        def tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, fast, t_pad, tok):
+        def tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, fast, t_pad, tok, guard):
             call("tgfr_wr_bwd_tok", ptr(stats), ptr(w_norm), ptr(r_norm), ptr(lens), b_img,
                  b_cap, gamma1, gamma2, gamma3, eps, ptr(dlogits), b_cap, int(fast), t_pad,
-                 ptr(tok), _hip.stream())
+                 ptr(tok), ptr(guard), _hip.stream())
         return (_wr_bwd(ctx.saved_tensors, ctx.cfg, tok_call),) + (None,) * 11
 
 
@@ -288,11 +297,11 @@ class WordRegionCE(torch.autograd.Function):
         g0 = None if g0 is None else g0.float().contiguous()
         g1 = None if g1 is None else g1.float().contiguous()
 
-        def tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, fast, t_pad, tok):
+        def tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, fast, t_pad, tok, guard):
             call("tgfr_wr_bwd_tok_ce", ptr(stats), ptr(w_norm), ptr(r_norm), ptr(lens), b_img,
                  b_cap, gamma1, gamma2, gamma3, eps, ptr(logits), logits.shape[1], 0,
                  ctx.inv_n, ptr(row_lse), ptr(col_lse), ptr(g0), ptr(g1), w0, w1, int(fast),
-                 t_pad, ptr(tok), _hip.stream())
+                 t_pad, ptr(tok), ptr(guard), _hip.stream())
         return (_wr_bwd(saved[:N_WR_SAVED], ctx.cfg, tok_call),) + (None,) * 9
 
 

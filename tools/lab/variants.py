@@ -60,15 +60,74 @@ _STAMPS = [
     if (cnt < t + 1) lds_wait_ge(BD_CNT + 4 * wid, t + 1);
     asm volatile("" ::: "memory");
     STAMP(t, 2);"""),
-    ("""int tgfr_version(void) { return 500; }""",
-     """int tgfr_version(void) { return 500; }
+    ("""int tgfr_version(void) { return 510; }""",
+     """int tgfr_version(void) { return 510; }
 int tgfr_lab_stamps(void* dst) {
   return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_st), sizeof(g_st), 0, hipMemcpyDeviceToHost);
 }"""),
 ]
+# per-stage s_memtime stamps of the T=64 backward (wr_bwd_wide2_kernel):
+# stage head (after its barrier) / after G1 / before G3 / after G3
+_WSTAMP_DECL = ("""constexpr int WPF = 4;      // wr_bwd_wide2_kernel's LDS operand prefetch distance (slots)""",
+                """constexpr int WPF = 4;      // wr_bwd_wide2_kernel's LDS operand prefetch distance (slots)
+__device__ unsigned long long g_wst[256 * 4 * 64 * 4];
+#define WSTAMP(t, k) do { if (blockIdx.x < 256 && (t) < 64) \
+  g_wst[((blockIdx.x * 4 + wid) * 64 + (t)) * 4 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)""")
+_WSTAMPS = [
+    _WSTAMP_DECL,
+    ("""    const bool has_next = i + 1 < c1;
+    const uint32_t nb = ((it + 1) & 1) * BUF;   // the next caption's slot""",
+     """    const bool has_next = i + 1 < c1;
+    WSTAMP(it, 0);
+    const uint32_t nb = ((it + 1) & 1) * BUF;   // the next caption's slot"""),
+    ("""    // ---- softmax over the 64 words (p = exp2(S'), bounded) and both backwards
+#pragma unroll
+    for (int e = 30; e < 32; ++e) {""", """    // ---- softmax over the 64 words (p = exp2(S'), bounded) and both backwards
+    WSTAMP(it, 1);
+#pragma unroll
+    for (int e = 30; e < 32; ++e) {"""),
+    ("""      uint32_t w2[8], c2[8];
+      u32x4 f4 = scal(tk, 4, 1, 0), f5 = scal(tk, 5, 1, 0);""",
+     """      uint32_t w2[8], c2[8];
+      WSTAMP(it, 2);
+      u32x4 f4 = scal(tk, 4, 1, 0), f5 = scal(tk, 5, 1, 0);"""),
+    ("""        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  if (rt >= NRT) return;""", """        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    WSTAMP(it, 3);
+  }
+  if (rt >= NRT) return;"""),
+    ("""int tgfr_version(void) { return 510; }""",
+     """int tgfr_version(void) { return 510; }
+int tgfr_lab_stamps(void* dst) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_wst), sizeof(g_wst), 0, hipMemcpyDeviceToHost);
+}"""),
+]
 VARIANTS = {
     "base": [],
+    "wstamp": _WSTAMPS,
     "head": "HEAD",
+    # T=64 backward: phase A of the softmax after G1 instead of under its Q-hat block
+    # (and "burst": also the next caption's DMA as one burst at the stage head)
+    "burst": [("""        if (n >= 34) {                   // elements 0..29 of phase A""",
+               """        if (false) {"""),
+              ("""    for (int e = 30; e < 32; ++e) {""", """    for (int e = 0; e < 32; ++e) {"""),
+              ("""        if (has_next && (n & 3) == 1) dma_piece(i + 1, nb, n >> 2);
+        if (has_next && (n == 3 || n == 7)) dma_piece(i + 1, nb, 16 + (n >> 2));
+""", ""),
+              ("""    const uint32_t tk = base + W_XIMG;
+    // ---- [S'^T ; Q-hat^T] of both token tiles""", """    const uint32_t tk = base + W_XIMG;
+    if (has_next)
+#pragma unroll
+      for (int j = 0; j < 18; ++j) dma_piece(i + 1, nb, j);
+    // ---- [S'^T ; Q-hat^T] of both token tiles""")],
+    "nopha": [("""        if (n >= 34) {                   // elements 0..29 of phase A""",
+               """        if (false) {"""),
+              ("""    for (int e = 30; e < 32; ++e) {""", """    for (int e = 0; e < 32; ++e) {""")],
     "stamp": _STAMPS,
     # ablations of the two-role backward (timing only: results are wrong)
     "nosm": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));""")],

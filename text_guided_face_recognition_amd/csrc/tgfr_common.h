@@ -188,6 +188,17 @@ __device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32
                : "memory", "m0");
 }
 
+// 128-bit buffer descriptor over [p, p + bytes) from wave-uniform inputs
+// (readfirstlane: provably uniform, so no waterfall loop per memory op).  A
+// buffer op then takes only a 32-bit lane offset: no per-lane 64-bit address
+// for the compiler to hoist out of a loop and spill.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
+  const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)p >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(lo | (hi << 32)), 0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
 // Retire this wave's DMA down to N outstanding ops and its LDS reads, then
 // meet the other waves.  One asm statement: nothing moves across it.
 template <int N>

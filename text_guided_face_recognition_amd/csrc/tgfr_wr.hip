@@ -752,37 +752,56 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
   const uint32_t eob = (8 * h + q4 + 4) * 64 + ((ec ^ (2 * h + 1)) << 4) + (p4 & 1) * 8;
   const uint32_t ew = lr * 64 + h * 8;
   const int ewx = (lr >> 2) & 3;
+  // global traffic of the loop through buffer descriptors built per caption
+  // from uniform values, with fixed 32-bit lane offsets: no per-lane 64-bit
+  // address for the compiler to hoist out of the loop and spill (a spill
+  // reload is a vmcnt wait behind every earlier load AND store)
+  const uint32_t voff_w = (uint32_t)(((32 * tt + lr) * D + h * 8) * 2);
   bf16x8 Wc[16];
+  float wn_n;
   auto load_w = [&](int ii) {
+    // the word norms first: the step's first consumer
+    wn_n = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+        uniform_rsrc(Wnorm + (long long)ii * TP, TP * 4), lane * 4, 0, 0));
+    const auto rw = uniform_rsrc(Whi + (long long)ii * TP * D, TP * D * 2);
 #pragma unroll
     for (int s = 0; s < 16; ++s)
-      Wc[s] = as_bf8(
-          *(const uint4*)(Whi + ((long long)ii * TP + 32 * tt + lr) * D + s * 16 + h * 8));
+      Wc[s] = as_bf8(__builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rw, voff_w + s * 32, 0, 0)));
   };
   const int npairs = (c1 - c0 + 1) / 2;
+  // the caption's length (a scalar load) and word norms are fetched one
+  // pair-step ahead with its word rows
+  int len_n = lens[min(c0 + slot, c1 - 1)];
   load_w(min(c0 + slot, c1 - 1));
+  {
+    // as many dropped stores (no records) as the loop issues after its
+    // prefetch: the loop is entered with the same vmcnt picture from both
+    // sides, so the compiler's waits for the word rows count past the
+    // previous step's stores instead of waiting for them to retire
+    const auto none = uniform_rsrc(logits, 0);
+#pragma unroll
+    for (int k = 0; k < 34; ++k) __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0, 0, 0);
+  }
   for (int k = 0; k < npairs; ++k) {
     const int i = c0 + 2 * k + slot;
     const bool active = i < c1;
     const int ic = active ? i : c1 - 1;
-    const int tl = lens[ic] - 32 * tt;           // valid words of this tile
+    const int tl = len_n - 32 * tt;              // valid words of this tile
+    const float wn = wn_n;                       // |W_t| of token `lane`
     // ---- GEMM1: S'^T[t][r] = W'[t][d] R[r][d]
     // (accumulators start at the word bias: 0, or -1e30 for padding words,
     // whose E = exp(0) = 1 then only feeds their own unused statistics and
     // C-hat rows, as in wr_fwd_pipe_kernel)
     // (BOUNDED: valid words start at -log2(e) bound_shift(c), c = max|W|
     // max|R| of the caption; both token tiles' waves form the same c)
-    float cb = 0.f;
-    if (BOUNDED) {
-      cb = wave_max(Wnorm[(long long)ic * TP + lane]) * rmax;
-      cb = bound_shift(cb);
-    }
-    const float sh = -L2E * cb;
+    // (the shift enters in the softmax: the step starts on the scalar-loaded
+    // length alone, with no wait on the prefetched word norms)
     f32x16 S[NRT];
 #pragma unroll
     for (int j = 0; j < NRT; ++j)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) S[j][q] = acc_row(q, h) < tl ? sh : -1e30f;
+      for (int q = 0; q < 16; ++q) S[j][q] = acc_row(q, h) < tl ? 0.f : -1e30f;
     {
       // 112 MFMAs n = (k-step s, region tile j), R operands read RPF ahead
       auto rd1 = [&](int n) { return lds_ld16(f1o[(n / NRT) >> 3][(n / NRT) & 7] + (n % NRT) * 32 * 256); };
@@ -801,9 +820,14 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
     // ---- softmax over the caption's words, per region: max and sum over
     // both token tiles (partner wave = wid ^ 1)
     // (BOUNDED: p = exp2(S' - log2(e) bound_shift(c)) needs no max)
+    float cb = 0.f;
+    if (BOUNDED) {
+      cb = wave_max(wn) * rmax;
+      cb = bound_shift(cb);
+    }
     float mj[NRT];
 #pragma unroll
-    for (int j = 0; j < NRT; ++j) mj[j] = 0.f;
+    for (int j = 0; j < NRT; ++j) mj[j] = L2E * cb;
     if constexpr (!BOUNDED) {
 #pragma unroll
       for (int j = 0; j < NRT; ++j) {
@@ -847,21 +871,22 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
     for (int j = 0; j < 8; ++j)
 #pragma unroll
       for (int q = 0; q < 16; ++q) C[j][q] = 0.f;
-#pragma unroll
-    for (int j = 0; j < NRT; ++j) {
+    // E of tile j + 1 is formed in the MFMA gaps of tile j's GEMM2 (one
+    // element per gap: its two exp and ~4 VALU hide beside the MFMA) and
+    // written to the other half of the wave's double-buffered E^T tile
+    auto e_elem = [&](int j, int q) {
       const float rb = j * 32 + lr < NREG ? 0.f : -1e30f;   // padding regions
       const float kj = g1 * L2E * __builtin_amdgcn_rcpf(sum_floor(sj[j]));
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const float p = __builtin_amdgcn_exp2f(S[j][q] - mj[j]);
-        const float e = __builtin_amdgcn_exp2f(j == NRT - 1 ? fmaf(p, kj, rb) : p * kj);
-        zp[q] += e;
-        np[q] = fmaf(e, S[j][q], np[q]);
-        S[j][q] = e;
-      }
-      // E^T tile [32 regions][32 words], 64-B rows, 16-B chunk g of row r at
-      // g ^ ((r >> 2) & 3) (wr_fwd_pipe_kernel's layout: conflict-free for the
-      // 8-B row-chunk writes and the transposed reads)
+      const float p = __builtin_amdgcn_exp2f(S[j][q] - mj[j]);
+      const float e = __builtin_amdgcn_exp2f(j == NRT - 1 ? fmaf(p, kj, rb) : p * kj);
+      zp[q] += e;
+      np[q] = fmaf(e, S[j][q], np[q]);
+      S[j][q] = e;
+    };
+    // E^T tile [32 regions][32 words], 64-B rows, 16-B chunk g of row r at
+    // g ^ ((r >> 2) & 3) (wr_fwd_pipe_kernel's layout: conflict-free for the
+    // 8-B row-chunk writes and the transposed reads)
+    auto e_store = [&](int j) {
       const uint32_t etj = et + (j & 1) * 2048;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -871,6 +896,13 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
         lds_st8(etj + ew + ((g ^ ewx) << 4),
                 make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3])));
       }
+    };
+#pragma unroll
+    for (int q = 0; q < 16; ++q) e_elem(0, q);
+    e_store(0);
+#pragma unroll
+    for (int j = 0; j < NRT; ++j) {
+      const uint32_t etj = et + (j & 1) * 2048;
       {
         // 16 MFMAs n = (region block s, d tile dt); R^T operands read RPF ahead
         auto rd2 = [&](int n) {
@@ -890,9 +922,11 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
           const bf16x8 bb = n < 8 ? eb0 : eb1;
           mma<MODE>(C[n & 7], aa, aa, bb, bb);
           if (n + RPF < 16) ring[(n + RPF) & 3] = rd2(n + RPF);
+          if (j + 1 < NRT) e_elem(j + 1, n);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      if (j + 1 < NRT) e_store(j + 1);
     }
     const float zr = rs16(zp, lr), nr = rs16(np, lr);
     if ((lr & 1) == 0) {
@@ -912,7 +946,10 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
             dst[tg * NREG + r] = S[j][q] * __builtin_amdgcn_rcpf(lds_ldf(tok + tq * 4));
         }
     }
-    if (k + 1 < npairs) load_w(min(i + 2, c1 - 1));
+    if (k + 1 < npairs) {
+      len_n = lens[min(i + 2, c1 - 1)];
+      load_w(min(i + 2, c1 - 1));
+    }
     // ---- per-token epilogue (lane t = lr), log-sum-exp over both tiles
     const int t = lr, tg = 32 * tt + lr;
     float csq = 0.f;
@@ -922,25 +959,51 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
       for (int q = 0; q < 16; ++q) csq = fmaf(C[dt][q], C[dt][q], csq);
     csq += __shfl_xor(csq, 32);
     const float Z = lds_ldf(tok + t * 4);
-    // (np sums E (S' + sh) = log2(e) (N - c Z) over the regions)
-    const float nhat = lds_ldf(tok + 128 + t * 4) * (1.f / L2E) + cb * Z;
+    // (np sums E S' = log2(e) N over the regions)
+    const float nhat = lds_ldf(tok + 128 + t * 4) * (1.f / L2E);
     const bool tvalid = t < tl;
     const float zinv = 1.f / Z;
     const float cn = sqrtf(csq) * zinv;
     const float n = nhat * zinv;
-    const float u = Wnorm[(long long)ic * TP + tg];
+    const float u = __shfl(wn, tg);
     const float cosv = n / fmaxf(u * cn, eps);
     float ex = half_sum(tvalid ? __expf(g2 * cosv) : 0.f);
     if (lane == 0) lds_stf(FR2_OFF_XL + wid * 4, ex);
     __syncthreads();
     ex += lds_ldf(FR2_OFF_XL + (wid ^ 1) * 4);
-    if (!active) continue;
-    const long long pair = (long long)b * B_cap + i;
-    if (lane == 0 && tt == 0) logits[(long long)b * ld_logits + i] = g3 * __logf(ex);
-    if (stats && h == 0)
-      stats[pair * TP + tg] =
-          tvalid ? make_float4(Z, n, cn, cosv) : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (Chi) store_cq<MODE, TP>(Chi, nullptr, pair, tg, h, C);
+    // The stores are unconditional buffer ops (a descriptor with no records
+    // or a lane offset past its end drops the ones that do not apply): the
+    // compiler then counts them, and the next step's waits on the loads
+    // prefetched above (issued before these stores) do not wait for the
+    // stores to retire -- vmcnt counts stores and retires in order.
+    const long long pair = (long long)b * B_cap + ic;
+    constexpr uint32_t OOB = 0x80000000u;
+    __builtin_amdgcn_raw_buffer_store_b32(
+        __float_as_uint(g3 * __logf(ex)),
+        uniform_rsrc(logits + (long long)b * ld_logits + ic, active ? 4 : 0),
+        lane == 0 && tt == 0 ? 0 : OOB, 0, 0);
+    {
+      const float4 sv = tvalid ? make_float4(Z, n, cn, cosv) : make_float4(0.f, 0.f, 0.f, 0.f);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(u32x4, sv),
+          uniform_rsrc(stats + pair * TP, stats && active ? TP * 16 : 0), h == 0 ? tg * 16 : OOB,
+          0, 0);
+    }
+    {
+      const auto rc = uniform_rsrc(Chi + pair * 32 * TP * 8, Chi && active ? 32 * TP * 16 : 0);
+      const uint32_t vo = (tg * 8 + 4 * h) * 2;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          uint16_t hh[4];
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) hh[kk] = lowp_bits<MODE>(C[dt][4 * g + kk]);
+          __builtin_amdgcn_raw_buffer_store_b64(
+              __builtin_bit_cast(u32x2, make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3]))),
+              rc, vo + (4 * dt + g) * TP * 16, 0, 0);
+        }
+    }
   }
 }
 

@@ -107,8 +107,58 @@ int tgfr_lab_stamps(void* dst) {
   return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_wst), sizeof(g_wst), 0, hipMemcpyDeviceToHost);
 }"""),
 ]
+# per-pair-step s_memtime stamps of the T=64 forward (wr_fwd_res2_kernel):
+# loop top / after GEMM1 / after the softmax sums / after the tile loop /
+# after the epilogue barrier
+_RSTAMP_DECL = ("""constexpr int RPF = 3;      // wr_fwd_res2_kernel's LDS operand prefetch distance (slots)""",
+                """constexpr int RPF = 3;      // wr_fwd_res2_kernel's LDS operand prefetch distance (slots)
+__device__ unsigned long long g_rst[256 * 4 * 64 * 8];
+#define RSTAMP(t, k) do { if (blockIdx.x < 256 && (t) < 64) \
+  g_rst[((blockIdx.x * 4 + wid) * 64 + (t)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)""")
+_RSTAMPS = [
+    _RSTAMP_DECL,
+    ("""    const int tl = len_n - 32 * tt;              // valid words of this tile""",
+     """    const int tl = len_n - 32 * tt;              // valid words of this tile
+    RSTAMP(k, 0);"""),
+    ("""    // ---- softmax over the caption's words, per region: max and sum over
+    // both token tiles (partner wave = wid ^ 1)""", """    RSTAMP(k, 1);
+    // ---- softmax over the caption's words, per region: max and sum over
+    // both token tiles (partner wave = wid ^ 1)"""),
+    ("""#pragma unroll
+    for (int j = 0; j < NRT; ++j)
+      sj[j] += lds_ldf(FR2_OFF_XS + ((wid ^ 1) * NRT + j) * 128 + lr * 4);""",
+     """#pragma unroll
+    for (int j = 0; j < NRT; ++j)
+      sj[j] += lds_ldf(FR2_OFF_XS + ((wid ^ 1) * NRT + j) * 128 + lr * 4);
+    RSTAMP(k, 2);"""),
+    ("""    const float zr = rs16(zp, lr), nr = rs16(np, lr);
+    if ((lr & 1) == 0) {
+      const int t = acc_row(rs16_index(lr), h);
+      lds_stf(tok + t * 4, zr);
+      lds_stf(tok + 128 + t * 4, nr);
+    }
+    if (ATT && active && b + img_offset == i) {""",
+     """    RSTAMP(k, 3);
+    const float zr = rs16(zp, lr), nr = rs16(np, lr);
+    if ((lr & 1) == 0) {
+      const int t = acc_row(rs16_index(lr), h);
+      lds_stf(tok + t * 4, zr);
+      lds_stf(tok + 128 + t * 4, nr);
+    }
+    if (ATT && active && b + img_offset == i) {"""),
+    ("""    ex += lds_ldf(FR2_OFF_XL + (wid ^ 1) * 4);
+    // The stores are unconditional""", """    ex += lds_ldf(FR2_OFF_XL + (wid ^ 1) * 4);
+    RSTAMP(k, 4);
+    // The stores are unconditional"""),
+    ("""int tgfr_version(void) { return 510; }""",
+     """int tgfr_version(void) { return 510; }
+int tgfr_lab_stamps(void* dst) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_rst), sizeof(g_rst), 0, hipMemcpyDeviceToHost);
+}"""),
+]
 VARIANTS = {
     "base": [],
+    "rstamp": _RSTAMPS,
     "wstamp": _WSTAMPS,
     "head": "HEAD",
     # T=64 backward: phase A of the softmax after G1 instead of under its Q-hat block

@@ -305,14 +305,14 @@ int tgfr_bn_fold(const float* W, const float* b, int O, int C, const float* gamm
                  const float* beta, float* Wf, float* bf, void* stream) {
   if (O <= 0 || C <= 0) return 1001;
   hipLaunchKernelGGL(bn_fold_kernel, dim3((O + 3) / 4), dim3(256), 0, (hipStream_t)stream,
-                     Parts{{W, W, W}, {b, b, b}, O}, O, C, gamma, beta, Wf, bf);
+                     Parts{W, W, W, b, b, b, O}, O, C, gamma, beta, Wf, bf);
   return (int)hipGetLastError();
 }
 
 int tgfr_bn_fold3(const float* const* W, const float* const* b, int rows, int C,
                   const float* gamma, const float* beta, float* Wf, float* bf, void* stream) {
   if (!W || rows <= 0 || C <= 0 || !W[0] || !W[1] || !W[2]) return 1001;
-  const Parts P{{W[0], W[1], W[2]}, {b ? b[0] : nullptr, b ? b[1] : nullptr, b ? b[2] : nullptr},
+  const Parts P{W[0], W[1], W[2], b ? b[0] : nullptr, b ? b[1] : nullptr, b ? b[2] : nullptr,
                 rows};
   hipLaunchKernelGGL(bn_fold_kernel, dim3((3 * rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
                      P, 3 * rows, C, gamma, beta, Wf, bf);
@@ -333,7 +333,7 @@ static int bn_unfold_launch(const float* G, const float* s, const Parts& W, int 
 int tgfr_bn_unfold(const float* G, const float* s, const float* W, int O, int C,
                    const float* gamma, const float* beta, float* dW, float* dgamma, float* dbeta,
                    float* ws, unsigned* counters, void* stream) {
-  return bn_unfold_launch(G, s, Parts{{W, W, W}, {nullptr, nullptr, nullptr}, O}, O, C, gamma,
+  return bn_unfold_launch(G, s, Parts{W, W, W, nullptr, nullptr, nullptr, O}, O, C, gamma,
                           beta, dW, dgamma, dbeta, ws, counters, stream);
 }
 
@@ -341,7 +341,7 @@ int tgfr_bn_unfold3(const float* G, const float* s, const float* const* W, int r
                     const float* gamma, const float* beta, float* dW, float* dgamma,
                     float* dbeta, float* ws, unsigned* counters, void* stream) {
   if (!W || !W[0] || !W[1] || !W[2]) return 1001;
-  return bn_unfold_launch(G, s, Parts{{W[0], W[1], W[2]}, {nullptr, nullptr, nullptr}, rows},
+  return bn_unfold_launch(G, s, Parts{W[0], W[1], W[2], nullptr, nullptr, nullptr, rows},
                           3 * rows, C, gamma, beta, dW, dgamma, dbeta, ws, counters, stream);
 }
 

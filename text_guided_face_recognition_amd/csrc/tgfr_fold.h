@@ -11,17 +11,27 @@ using namespace tgfr;
 // A weight [O][C] given as up to 3 row blocks of `rows` rows each (the
 // three 1x1 projections of a self-attention, read in place: no concatenated
 // copy), and their biases (each nullable).
+// (three named pointers picked behind an empty asm: a select between them
+// had been folded into a dynamic index into the kernel argument, which put a
+// copy of the struct in scratch)
 struct Parts {
-  const float* w[3];
-  const float* b[3];
+  const float *w0, *w1, *w2;
+  const float *b0, *b1, *b2;
   int rows;
+  // (the pointers pass through an empty asm, so the compiler cannot turn the
+  // select back into an index into the argument block)
+  static __device__ __forceinline__ const float* pick(const float* a, const float* b,
+                                                      const float* c, int p) {
+    asm("" : "+v"(a), "+v"(b), "+v"(c));
+    return p == 0 ? a : p == 1 ? b : c;
+  }
   __device__ __forceinline__ const float* row(int o, int C) const {
     const int p = o / rows;
-    return (p == 0 ? w[0] : p == 1 ? w[1] : w[2]) + (long long)(o - p * rows) * C;
+    return pick(w0, w1, w2, p) + (long long)(o - p * rows) * C;
   }
   __device__ __forceinline__ float bias(int o) const {
     const int p = o / rows;
-    const float* bp = p == 0 ? b[0] : p == 1 ? b[1] : b[2];
+    const float* bp = pick(b0, b1, b2, p);
     return bp ? bp[o - p * rows] : 0.f;
   }
 };
@@ -31,7 +41,7 @@ struct Parts {
 // columns, not one per 64.  Indices are clamped, not branched on (a branch per
 // access serialises them): past the end a lane loads and stores column C - 1
 // again -- the same value to the same word.
-__device__ __forceinline__ void bn_fold_row(const Parts& P, int o, int C,
+__device__ __forceinline__ void bn_fold_row(const Parts P, int o, int C,
                                             const float* __restrict__ gamma,
                                             const float* __restrict__ beta,
                                             float* __restrict__ Wf, float* __restrict__ bf,

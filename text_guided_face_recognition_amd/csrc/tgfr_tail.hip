@@ -1076,8 +1076,8 @@ int tgfr_imim_pack(const float* const* Wqkv, const float* const* bqkv, int rows_
   if (!Wqkv || !Wqkv[0] || !Wqkv[1] || !Wqkv[2] || rows_qkv <= 0 || C <= 0 || !gamma || !beta ||
       !Wf || !bf || !W1 || !W2 || !Wp || !pk || !lnw || !lnb || !ws || !ln_tail_ok(rows, hw))
     return 1001;
-  const Parts P{{Wqkv[0], Wqkv[1], Wqkv[2]},
-                {bqkv ? bqkv[0] : nullptr, bqkv ? bqkv[1] : nullptr, bqkv ? bqkv[2] : nullptr},
+  const Parts P{Wqkv[0], Wqkv[1], Wqkv[2],
+                bqkv ? bqkv[0] : nullptr, bqkv ? bqkv[1] : nullptr, bqkv ? bqkv[2] : nullptr,
                 rows_qkv};
   const int O = 3 * rows_qkv, nf = (O + 3) / 4;
   const LnTailWs o = ln_tail_ws(rows, hw);

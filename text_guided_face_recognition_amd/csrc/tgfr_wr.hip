@@ -1412,6 +1412,10 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
       if (n == 190) initn = caption_init(inext, wn_next, big_next);
       __builtin_amdgcn_sched_barrier(0);
     }
+    // |W_t| for the epilogue, issued ahead of the reductions below (pinned
+    // there): its latency hides under them instead of stalling the epilogue
+    const float u = Wnorm[(long long)i * TPAD + lr];
+    __builtin_amdgcn_sched_barrier(0);
     // ---- N per token: reduce-scatter over the region lanes -> LDS
     {
       const float nr = rs16(np, lr);
@@ -1432,7 +1436,6 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     const float zinv = __builtin_amdgcn_rcpf(Z);
     const float cn = sqrtf(csq) * zinv;
     const float n_ = nhat * zinv;
-    const float u = Wnorm[(long long)i * TPAD + t];
     const float cosv = n_ / fmaxf(u * cn, eps);
     const float ex = half_sum(tvalid ? __expf(g2 * cosv) : 0.f);
     logits[(long long)b * ld_logits + i] = g3 * __logf(ex);
@@ -2333,7 +2336,13 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    // ---- softmax over the 64 words (p = exp2(S'), bounded) and both backwards
+    // ---- softmax over the 64 words (p = exp2(S'), bounded) and both backwards.
+    // M_c = f5 ax needs only the softmax-2 term ax; M_w also the softmax-1
+    // backward's row sum rho.  So: ax and the M_c fragments first, then G3's
+    // 32 C-hat MFMAs with the rest of the softmax-1 backward (du, v, rho) one
+    // element per MFMA gap, then the 32 W' MFMAs (tile 1's M_w in the gaps of
+    // tile 0's).  (Computing all of it between G1 and G3 left the matrix core
+    // idle for a quarter of the caption.)
 #pragma unroll
     for (int e = 30; e < 32; ++e) {
       a1[e >> 4][e & 15] = __builtin_amdgcn_exp2f(A0[e >> 4][e & 15]);
@@ -2341,94 +2350,98 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
     }
     const float inv = __builtin_amdgcn_rcpf(sum_floor(xhalf_sum(sum)));
     const float kq = gL * inv;
-    float rho = 0.f;
+    auto pk2 = [](float x, float y) {
+      if constexpr (MODE == MODE_F16) return pack2(f16_bits(x), f16_bits(y));
+      else return pk_bf16(x, y);
+    };
+    auto frag = [](const uint32_t* w, int j) {
+      return __builtin_bit_cast(bf16x8, make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]));
+    };
+    bf16x8 Mc[2][2], Mw[2][2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 2; ++u) {
+      uint32_t c2[8];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const u32x4 f0 = scal(tk, 0, u, g), f1 = scal(tk, 1, u, g);
-        const u32x4 f2 = scal(tk, 2, u, g), f3 = scal(tk, 3, u, g);
+        const u32x4 f0 = scal(tk, 0, u, g), f5 = scal(tk, 5, u, g);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int q = 4 * g + k;
-          const float p = a1[u][q];
-          a1[u][q] = p * inv;                                               // A1
-          ax[u][q] = __builtin_amdgcn_exp2f(fmaf(p, kq, fl(f0, k)));         // g1 A2 / log2e
-          const float du = fmaf(fl(f1, k), A0[u][q], fmaf(fl(f2, k), A1[u][q], -fl(f3, k)));
-          v[u][q] = a1[u][q] * (ax[u][q] * du);                              // A1 dA1 / log2e
-          rho += v[u][q];
-        }
+        for (int k = 0; k < 4; ++k)         // (a1 still holds p here)
+          ax[u][4 * g + k] = __builtin_amdgcn_exp2f(fmaf(a1[u][4 * g + k], kq, fl(f0, k)));
+#pragma unroll
+        for (int k = 0; k < 4; k += 2)
+          c2[(4 * g + k) >> 1] = pk2(fl(f5, k) * ax[u][4 * g + k],
+                                     fl(f5, k + 1) * ax[u][4 * g + k + 1]);
       }
-    rho = xhalf_sum(rho);
-    // ---- dR GEMM over both token tiles: 64 MFMAs n = (tile u, k block, d
-    // tile dt), k outer so consecutive MFMAs update different accumulators; k
-    // block = W' rows (k < 2) or C-hat rows of the tile, 16 tokens each.
-    // Operands read WPF slots ahead; tile 0's M fragments are formed before
-    // the loop, tile 1's in the gaps of tile 0's first 16 MFMAs.
+      Mc[u][0] = frag(c2, 0);
+      Mc[u][1] = frag(c2, 1);
+    }
+    // ---- dR GEMM over both token tiles: 64 MFMAs n = (half: C-hat / W'
+    // blocks, tile u, k block j, d tile dt); operands read WPF slots ahead.
     {
       auto rd3 = [&](int n) {
-        const int u = n >> 5, kk = (n >> 3) & 3, dt = n & 7;
-        const int ks = (kk < 2 ? 0 : 4) + 2 * u + (kk & 1);
+        const int hf = n >> 5, u = (n >> 4) & 1, j = (n >> 3) & 1, dt = n & 7;
+        const int ks = (hf ? 0 : 4) + 2 * u + j;
         const uint32_t kb = base + (dt >> 2) * (128 * 256) + ks * 16 * 256;
         return join_tr(lds_tr4(kb + g2o[0][dt & 3]), lds_tr4(kb + g2o[1][dt & 3]));
-      };
-      auto pk2 = [](float x, float y) {
-        if constexpr (MODE == MODE_F16) return pack2(f16_bits(x), f16_bits(y));
-        else return pk_bf16(x, y);
       };
       bf16x8 ring[8];
 #pragma unroll
       for (int n = 0; n < WPF; ++n) ring[n] = rd3(n);
-      bf16x8 M0[4], M1[4];
-      {
-        uint32_t w2[8], c2[8];
+      // token scalars f1..f3 of element group (u, g), read one group ahead
+      u32x4 fb[2][3], f4v[2][4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const u32x4 f4 = scal(tk, 4, 0, g), f5 = scal(tk, 5, 0, g);
-#pragma unroll
-          for (int kq = 0; kq < 4; kq += 2) {
-            const int q = 4 * g + kq;
-            const float w0 = fmaf(fl(f4, kq), ax[0][q], fmaf(-a1[0][q], rho, v[0][q]));
-            const float w1 = fmaf(fl(f4, kq + 1), ax[0][q + 1], fmaf(-a1[0][q + 1], rho, v[0][q + 1]));
-            w2[q >> 1] = pk2(w0, w1);
-            c2[q >> 1] = pk2(fl(f5, kq) * ax[0][q], fl(f5, kq + 1) * ax[0][q + 1]);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          M0[j] = __builtin_bit_cast(bf16x8, make_uint4(w2[4 * j], w2[4 * j + 1], w2[4 * j + 2], w2[4 * j + 3]));
-          M0[2 + j] = __builtin_bit_cast(bf16x8, make_uint4(c2[4 * j], c2[4 * j + 1], c2[4 * j + 2], c2[4 * j + 3]));
-        }
-      }
-      uint32_t w2[8], c2[8];
-      u32x4 f4 = scal(tk, 4, 1, 0), f5 = scal(tk, 5, 1, 0);
+      for (int c = 0; c < 3; ++c) fb[0][c] = scal(tk, 1 + c, 0, 0);
+      float rho = 0.f;
+      uint32_t w2[8];
 #pragma unroll
       for (int n = 0; n < 64; ++n) {
+        const int hf = n >> 5, u = (n >> 4) & 1, j = (n >> 3) & 1, dt = n & 7;
         const bf16x8 x = ring[n & 7];
-        const int kk = (n >> 3) & 3;
-        const bf16x8 m = n < 32 ? M0[kk] : M1[kk];
-        mma<MODE>(dR[n & 7], m, m, x, x);
+        const bf16x8 m = hf ? Mw[u][j] : Mc[u][j];
+        mma<MODE>(dR[dt], m, m, x, x);
         if (n + WPF < 64) ring[(n + WPF) & 7] = rd3(n + WPF);
-        if (n < 16) {                     // tile 1, token pair q = 2 (n >> 1)
-          const int q = n & ~1;
-          if (n & 1) {
-            c2[q >> 1] = pk2(fl(f5, q) * ax[1][q], fl(f5, q + 1) * ax[1][q + 1]);
-            if ((n & 3) == 3 && n < 15) {
-              f4 = scal(tk, 4, 1, (n + 1) >> 2);
-              f5 = scal(tk, 5, 1, (n + 1) >> 2);
-            }
-          } else {
-            const float w0 = fmaf(fl(f4, q), ax[1][q], fmaf(-a1[1][q], rho, v[1][q]));
-            const float w1 =
-                fmaf(fl(f4, q + 1), ax[1][q + 1], fmaf(-a1[1][q + 1], rho, v[1][q + 1]));
-            w2[q >> 1] = pk2(w0, w1);
-          }
-          if (n == 15) {
+        if (n < 32) {
+          // softmax-1 backward of element e = n (tile ue, token q)
+          const int e = n, ue = e >> 4, q = e & 15, g = (e >> 2) & 3, k = e & 3;
+          const int gi = e >> 2;                        // group index 0..7
+          if (k == 0 && gi + 1 < 8)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              M1[j] = __builtin_bit_cast(bf16x8, make_uint4(w2[4 * j], w2[4 * j + 1], w2[4 * j + 2], w2[4 * j + 3]));
-              M1[2 + j] = __builtin_bit_cast(bf16x8, make_uint4(c2[4 * j], c2[4 * j + 1], c2[4 * j + 2], c2[4 * j + 3]));
+            for (int c = 0; c < 3; ++c)
+              fb[(gi + 1) & 1][c] = scal(tk, 1 + c, (gi + 1) >> 2, (gi + 1) & 3);
+          if (k == 1) f4v[ue][g] = scal(tk, 4, ue, g);
+          const u32x4* f = fb[gi & 1];
+          const float p = a1[ue][q];
+          a1[ue][q] = p * inv;                                             // A1
+          const float du = fmaf(fl(f[0], k), A0[ue][q], fmaf(fl(f[1], k), A1[ue][q], -fl(f[2], k)));
+          v[ue][q] = a1[ue][q] * (ax[ue][q] * du);                          // A1 dA1 / log2e
+          rho += v[ue][q];
+          if (n == 31) {
+            rho = xhalf_sum(rho);
+            // tile 0's M_w before its first W' MFMA (n = 32)
+#pragma unroll
+            for (int qq = 0; qq < 16; qq += 2) {
+              const u32x4 f4 = f4v[0][qq >> 2];
+              const float w0 = fmaf(fl(f4, qq), ax[0][qq], fmaf(-a1[0][qq], rho, v[0][qq]));
+              const float w1 = fmaf(fl(f4, qq + 1), ax[0][qq + 1],
+                                    fmaf(-a1[0][qq + 1], rho, v[0][qq + 1]));
+              w2[qq >> 1] = pk2(w0, w1);
             }
+            Mw[0][0] = frag(w2, 0);
+            Mw[0][1] = frag(w2, 1);
+          }
+        } else if (n < 48) {
+          // tile 1's M_w, one token pair per two gaps
+          const int qq = (n - 32) & ~1;
+          if (!(n & 1)) {
+            const u32x4 f4 = f4v[1][qq >> 2];
+            const float w0 = fmaf(fl(f4, qq), ax[1][qq], fmaf(-a1[1][qq], rho, v[1][qq]));
+            const float w1 = fmaf(fl(f4, qq + 1), ax[1][qq + 1],
+                                  fmaf(-a1[1][qq + 1], rho, v[1][qq + 1]));
+            w2[qq >> 1] = pk2(w0, w1);
+          }
+          if (n == 47) {
+            Mw[1][0] = frag(w2, 0);
+            Mw[1][1] = frag(w2, 1);
           }
         }
         __builtin_amdgcn_sched_barrier(0);

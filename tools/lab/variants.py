@@ -80,17 +80,14 @@ _WSTAMPS = [
      """    const bool has_next = i + 1 < c1;
     WSTAMP(it, 0);
     const uint32_t nb = ((it + 1) & 1) * BUF;   // the next caption's slot"""),
-    ("""    // ---- softmax over the 64 words (p = exp2(S'), bounded) and both backwards
-#pragma unroll
-    for (int e = 30; e < 32; ++e) {""", """    // ---- softmax over the 64 words (p = exp2(S'), bounded) and both backwards
-    WSTAMP(it, 1);
-#pragma unroll
-    for (int e = 30; e < 32; ++e) {"""),
-    ("""      uint32_t w2[8], c2[8];
-      u32x4 f4 = scal(tk, 4, 1, 0), f5 = scal(tk, 5, 1, 0);""",
-     """      uint32_t w2[8], c2[8];
-      WSTAMP(it, 2);
-      u32x4 f4 = scal(tk, 4, 1, 0), f5 = scal(tk, 5, 1, 0);"""),
+    ("""    // ---- softmax over the 64 words (p = exp2(S'), bounded) and both backwards.""",
+     """    WSTAMP(it, 1);
+    // ---- softmax over the 64 words (p = exp2(S'), bounded) and both backwards."""),
+    ("""      float rho = 0.f;
+      uint32_t w2[8];""",
+     """      float rho = 0.f;
+      uint32_t w2[8];
+      WSTAMP(it, 2);"""),
     ("""        __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -156,101 +153,46 @@ int tgfr_lab_stamps(void* dst) {
   return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_rst), sizeof(g_rst), 0, hipMemcpyDeviceToHost);
 }"""),
 ]
+# per-caption s_memtime stamps of the T<=32 pipelined forward
+# (wr_fwd_pipe_kernel): caption top / after the slot loop / before the stores / after
+_PSTAMPS = [
+    ("""constexpr float BIG_C = 10.f;""",
+     """constexpr float BIG_C = 10.f;
+__device__ unsigned long long g_pst[256 * 4 * 16 * 4];
+#define PSTAMP(t, k) do { if (blockIdx.x < 256 && (t) < 16) \
+  g_pst[((blockIdx.x * 4 + wid) * 16 + (t)) * 4 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)"""),
+    ("""  auto caption = [&](auto bigc) {
+    const int len = lens[i];""", """  auto caption = [&](auto bigc) {
+    const int ci = (i - c0) / 4;
+    PSTAMP(ci, 0);
+    const int len = lens[i];"""),
+    ("""    // ---- N per token: reduce-scatter over the region lanes -> LDS
+    {
+      const float nr = rs16(np, lr);""", """    PSTAMP(ci, 1);
+    // ---- N per token: reduce-scatter over the region lanes -> LDS
+    {
+      const float nr = rs16(np, lr);"""),
+    ("""    const float ex = half_sum(tvalid ? __expf(g2 * cosv) : 0.f);
+    logits[(long long)b * ld_logits + i] = g3 * __logf(ex);""",
+     """    const float ex = half_sum(tvalid ? __expf(g2 * cosv) : 0.f);
+    PSTAMP(ci, 2);
+    logits[(long long)b * ld_logits + i] = g3 * __logf(ex);"""),
+    ("""    store_cq<MODE_BF16>(Chi, nullptr, pair, t, h, C);
+    init = initn;""", """    store_cq<MODE_BF16>(Chi, nullptr, pair, t, h, C);
+    PSTAMP(ci, 3);
+    init = initn;"""),
+    ("""int tgfr_version(void) { return 510; }""",
+     """int tgfr_version(void) { return 510; }
+int tgfr_lab_stamps(void* dst) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_pst), sizeof(g_pst), 0, hipMemcpyDeviceToHost);
+}"""),
+]
 VARIANTS = {
     "base": [],
+    "pstamp": _PSTAMPS,
     "rstamp": _RSTAMPS,
     "wstamp": _WSTAMPS,
     "head": "HEAD",
-    # T=64 backward: phase A of the softmax after G1 instead of under its Q-hat block
-    # (and "burst": also the next caption's DMA as one burst at the stage head)
-    "burst": [("""        if (n >= 34) {                   // elements 0..29 of phase A""",
-               """        if (false) {"""),
-              ("""    for (int e = 30; e < 32; ++e) {""", """    for (int e = 0; e < 32; ++e) {"""),
-              ("""        if (has_next && (n & 3) == 1) dma_piece(i + 1, nb, n >> 2);
-        if (has_next && (n == 3 || n == 7)) dma_piece(i + 1, nb, 16 + (n >> 2));
-""", ""),
-              ("""    const uint32_t tk = base + W_XIMG;
-    // ---- [S'^T ; Q-hat^T] of both token tiles""", """    const uint32_t tk = base + W_XIMG;
-    if (has_next)
-#pragma unroll
-      for (int j = 0; j < 18; ++j) dma_piece(i + 1, nb, j);
-    // ---- [S'^T ; Q-hat^T] of both token tiles""")],
-    "nopha": [("""        if (n >= 34) {                   // elements 0..29 of phase A""",
-               """        if (false) {"""),
-              ("""    for (int e = 30; e < 32; ++e) {""", """    for (int e = 0; e < 32; ++e) {""")],
-    "stamp": _STAMPS,
-    # ablations of the two-role backward (timing only: results are wrong)
-    "nosm": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));""")],
-    "nog3": [(_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));""")],
-    "nog1": [(_G1, """      asm volatile("" ::"v"(rd[n & 3]));""")],
-    "nodma": [(_DMA, "")],
-    # timing probes: the stored scores / the X images always from the chunk's
-    # first caption (L2-resident: no HBM latency behind the loads)
-    "spl2": [("""    const uint16_t* rec = spb + (long long)min(k, K - 1) * (NRT * SP_REC);""",
-              """    const uint16_t* rec = spb;""")],
-    "dmal2": [("""      const int kc = min(k, K - 1);
-      const uint32_t base = (k % BD_NB) * BD_BUF;""", """      const int kc = 0;
-      const uint32_t base = (k % BD_NB) * BD_BUF;""")],
-    "skel": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
-             (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
-             (_G1, """      asm volatile("" ::"v"(rd[n & 3]));""")],
-    "skel_nodma": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
-                   (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
-                   (_G1, """      asm volatile("" ::"v"(rd[n & 3]));"""), (_DMA, "")],
-    "mfma_only": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
-                  (_DMA, "")],
-    "pf3_7": [("constexpr int BD_PF3 = 4;", "constexpr int BD_PF3 = 7;")],
-    "skel_l2": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
-                (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
-                (_G1, """      asm volatile("" ::"v"(rd[n & 3]));"""),
-                ("""      const int kc = min(k, K - 1);
-      const uint32_t base = (k % BD_NB) * BD_BUF;""", """      const int kc = 0;
-      const uint32_t base = (k % BD_NB) * BD_BUF;""")],
-    "skel_chat": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
-                  (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
-                  (_G1, """      asm volatile("" ::"v"(rd[n & 3]));"""),
-                  ("""          if (bd_dma_slot(n) >= 0) dma_piece(t + 2, bd_dma_slot(n));""",
-                   """          if (bd_dma_slot(n) >= 0 && (bd_dma_slot(n) % 4 >= 2 || bd_dma_slot(n) == 8)) dma_piece(t + 2, bd_dma_slot(n));""")],
-    "skel_notr": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
-                  (_G3, """          asm volatile("" ::"v"(Mi[n & 3]));"""),
-                  ("""          if (n + BD_PF3 < 32) rd[(n + BD_PF3) & 7] = g3_read(n + BD_PF3, x3);""", ""),
-                  (_G1, """      asm volatile("" ::"v"(rd[n & 3]));""")],
-    "fblead": [("      if (c == PB - 4 + 8 * g)", "      if (c == PB - 8 + 8 * g)")],
-    "fblead2": [("      if (c == PB - 4 + 8 * g)", "      if (c == PB - 8 + 8 * g)"),
-                ("      if (c == PC - 3 + 4 * g) {", "      if (c == PC - 4 + 4 * g) {")],
-    "pf1_4": [("constexpr int BD_PF1 = 3; ", "constexpr int BD_PF1 = 4; "),
-              ("    u32x4 rd[4];\n#pragma unroll\n    for (int n = 0; n < BD_PF1; ++n) rd[n] = g1_read(n, x1);",
-               "    u32x4 rd[8];\n#pragma unroll\n    for (int n = 0; n < BD_PF1; ++n) rd[n] = g1_read(n, x1);"),
-              ("      g1_mfma(n, rd[n & 3], Qn);\n      if (n + BD_PF1 < 16) rd[(n + BD_PF1) & 3] = g1_read(n + BD_PF1, x1);",
-               "      g1_mfma(n, rd[n & 7], Qn);\n      if (n + BD_PF1 < 16) rd[(n + BD_PF1) & 7] = g1_read(n + BD_PF1, x1);")],
-    # forward probes: one caption body only (big captions wrong: timing), no S' stores
-    "fnobig": [("""    if (big_cur)
-      caption(std::true_type{});
-    else
-      caption(std::false_type{});""", """    caption(std::false_type{});""")],
-    "fnostore": [("""        *(uint4*)(spt + lane * 16 + (q & 8)) = make_uint4(spk[0], spk[1], spk[2], spk[3]);""",
-                  """        asm volatile("" ::"v"(spk[0]), "v"(spk[1]), "v"(spk[2]), "v"(spk[3]));""")],
-    "fnoboth": [("""    if (big_cur)
-      caption(std::true_type{});
-    else
-      caption(std::false_type{});""", """    caption(std::false_type{});"""),
-                ("""        *(uint4*)(spt + lane * 16 + (q & 8)) = make_uint4(spk[0], spk[1], spk[2], spk[3]);""",
-                  """        asm volatile("" ::"v"(spk[0]), "v"(spk[1]), "v"(spk[2]), "v"(spk[3]));""")],
-    "prio_s": [(_SWAVE, _SWAVE + "\n  __builtin_amdgcn_s_setprio(1);")],
-    "prio_m": [(_MWAVE, _MWAVE.replace("    // DMA", "    __builtin_amdgcn_s_setprio(1);\n    // DMA"))],
-}
-
-
-# variants of other sources: name -> (file, substitutions); the timing
-# harness for these is the whole bench step (TGFR_LIB=<lib> bench.py)
-FILE_VARIANTS = {
-    # q/k/v projection (bf16 in / out): 512-workgroup budget instead of 256
-    "gemm512": ("tgfr_gemm.hip", [("""  const int per_slice = std::max(1, std::min(m_tiles, 256 / n_slices));
-  const int lds = WR_TN * K * 2 + WR_NS * WR_STG;
-  auto fn = K == 256 ? &bgemm_wres_kernel<256, true, true> : &bgemm_wres_kernel<128, true, true>;""",
-                                   """  const int per_slice = std::max(1, std::min(m_tiles, 512 / n_slices));
-  const int lds = WR_TN * K * 2 + WR_NS * WR_STG;
-  auto fn = K == 256 ? &bgemm_wres_kernel<256, true, true> : &bgemm_wres_kernel<128, true, true>;""")]),
     # optimiser: 2 float4 per thread (twice the workgroups) instead of 4
     "opt2": ("tgfr_optim.hip", [("VEC_PER_BLOCK = 4 * THREADS;", "VEC_PER_BLOCK = 2 * THREADS;")]),
     # BatchNorm normalise: 32 channels per workgroup (512 workgroups) instead of 64

@@ -193,6 +193,79 @@ VARIANTS = {
     "rstamp": _RSTAMPS,
     "wstamp": _WSTAMPS,
     "head": "HEAD",
+    "stamp": _STAMPS,
+    # ablations of the two-role backward (timing only: results are wrong)
+    "nosm": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));""")],
+    "nog3": [(_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));""")],
+    "nog1": [(_G1, """      asm volatile("" ::"v"(rd[n & 3]));""")],
+    "nodma": [(_DMA, "")],
+    # timing probes: the stored scores / the X images always from the chunk's
+    # first caption (L2-resident: no HBM latency behind the loads)
+    "spl2": [("""    const uint16_t* rec = spb + (long long)min(k, K - 1) * (NRT * SP_REC);""",
+              """    const uint16_t* rec = spb;""")],
+    "dmal2": [("""      const int kc = min(k, K - 1);
+      const uint32_t base = (k % BD_NB) * BD_BUF;""", """      const int kc = 0;
+      const uint32_t base = (k % BD_NB) * BD_BUF;""")],
+    "skel": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
+             (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
+             (_G1, """      asm volatile("" ::"v"(rd[n & 3]));""")],
+    "skel_nodma": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
+                   (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
+                   (_G1, """      asm volatile("" ::"v"(rd[n & 3]));"""), (_DMA, "")],
+    "mfma_only": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
+                  (_DMA, "")],
+    "pf3_7": [("constexpr int BD_PF3 = 4;", "constexpr int BD_PF3 = 7;")],
+    "skel_l2": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
+                (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
+                (_G1, """      asm volatile("" ::"v"(rd[n & 3]));"""),
+                ("""      const int kc = min(k, K - 1);
+      const uint32_t base = (k % BD_NB) * BD_BUF;""", """      const int kc = 0;
+      const uint32_t base = (k % BD_NB) * BD_BUF;""")],
+    "skel_chat": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
+                  (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
+                  (_G1, """      asm volatile("" ::"v"(rd[n & 3]));"""),
+                  ("""          if (bd_dma_slot(n) >= 0) dma_piece(t + 2, bd_dma_slot(n));""",
+                   """          if (bd_dma_slot(n) >= 0 && (bd_dma_slot(n) % 4 >= 2 || bd_dma_slot(n) == 8)) dma_piece(t + 2, bd_dma_slot(n));""")],
+    "skel_notr": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
+                  (_G3, """          asm volatile("" ::"v"(Mi[n & 3]));"""),
+                  ("""          if (n + BD_PF3 < 32) rd[(n + BD_PF3) & 7] = g3_read(n + BD_PF3, x3);""", ""),
+                  (_G1, """      asm volatile("" ::"v"(rd[n & 3]));""")],
+    "fblead": [("      if (c == PB - 4 + 8 * g)", "      if (c == PB - 8 + 8 * g)")],
+    "fblead2": [("      if (c == PB - 4 + 8 * g)", "      if (c == PB - 8 + 8 * g)"),
+                ("      if (c == PC - 3 + 4 * g) {", "      if (c == PC - 4 + 4 * g) {")],
+    "pf1_4": [("constexpr int BD_PF1 = 3; ", "constexpr int BD_PF1 = 4; "),
+              ("    u32x4 rd[4];\n#pragma unroll\n    for (int n = 0; n < BD_PF1; ++n) rd[n] = g1_read(n, x1);",
+               "    u32x4 rd[8];\n#pragma unroll\n    for (int n = 0; n < BD_PF1; ++n) rd[n] = g1_read(n, x1);"),
+              ("      g1_mfma(n, rd[n & 3], Qn);\n      if (n + BD_PF1 < 16) rd[(n + BD_PF1) & 3] = g1_read(n + BD_PF1, x1);",
+               "      g1_mfma(n, rd[n & 7], Qn);\n      if (n + BD_PF1 < 16) rd[(n + BD_PF1) & 7] = g1_read(n + BD_PF1, x1);")],
+    # forward probes: one caption body only (big captions wrong: timing), no S' stores
+    "fnobig": [("""    if (big_cur)
+      caption(std::true_type{});
+    else
+      caption(std::false_type{});""", """    caption(std::false_type{});""")],
+    "fnostore": [("""        *(uint4*)(spt + lane * 16 + (q & 8)) = make_uint4(spk[0], spk[1], spk[2], spk[3]);""",
+                  """        asm volatile("" ::"v"(spk[0]), "v"(spk[1]), "v"(spk[2]), "v"(spk[3]));""")],
+    "fnoboth": [("""    if (big_cur)
+      caption(std::true_type{});
+    else
+      caption(std::false_type{});""", """    caption(std::false_type{});"""),
+                ("""        *(uint4*)(spt + lane * 16 + (q & 8)) = make_uint4(spk[0], spk[1], spk[2], spk[3]);""",
+                  """        asm volatile("" ::"v"(spk[0]), "v"(spk[1]), "v"(spk[2]), "v"(spk[3]));""")],
+    "prio_s": [(_SWAVE, _SWAVE + "\n  __builtin_amdgcn_s_setprio(1);")],
+    "prio_m": [(_MWAVE, _MWAVE.replace("    // DMA", "    __builtin_amdgcn_s_setprio(1);\n    // DMA"))],
+}
+
+
+# variants of other sources: name -> (file, substitutions); the timing
+# harness for these is the whole bench step (TGFR_LIB=<lib> bench.py)
+FILE_VARIANTS = {
+    # q/k/v projection (bf16 in / out): 512-workgroup budget instead of 256
+    "gemm512": ("tgfr_gemm.hip", [("""  const int per_slice = std::max(1, std::min(m_tiles, 256 / n_slices));
+  const int lds = WR_TN * K * 2 + WR_NS * WR_STG;
+  auto fn = K == 256 ? &bgemm_wres_kernel<256, true, true> : &bgemm_wres_kernel<128, true, true>;""",
+                                   """  const int per_slice = std::max(1, std::min(m_tiles, 512 / n_slices));
+  const int lds = WR_TN * K * 2 + WR_NS * WR_STG;
+  auto fn = K == 256 ? &bgemm_wres_kernel<256, true, true> : &bgemm_wres_kernel<128, true, true>;""")]),
     # optimiser: 2 float4 per thread (twice the workgroups) instead of 4
     "opt2": ("tgfr_optim.hip", [("VEC_PER_BLOCK = 4 * THREADS;", "VEC_PER_BLOCK = 2 * THREADS;")]),
     # BatchNorm normalise: 32 channels per workgroup (512 workgroups) instead of 64

@@ -802,29 +802,46 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
     for (int j = 0; j < NRT; ++j)
 #pragma unroll
       for (int q = 0; q < 16; ++q) S[j][q] = acc_row(q, h) < tl ? 0.f : -1e30f;
+    // ---- GEMM1 in three groups of region tiles -- {0, 1}, {2, 3}, {4, 5, 6}
+    // -- whose MFMAs alternate tiles over the 16 k-steps, so tiles 0-3 are
+    // complete early.  BOUNDED: the softmax sums of tiles 0-3 (one exp per
+    // gap) then run in the gaps of the later groups' MFMAs; the score shift
+    // is formed in the first group's gaps.
+    float cb = 0.f, psum[4] = {0.f, 0.f, 0.f, 0.f};
     {
-      // 112 MFMAs n = (k-step s, region tile j), R operands read RPF ahead
-      auto rd1 = [&](int n) { return lds_ld16(f1o[(n / NRT) >> 3][(n / NRT) & 7] + (n % NRT) * 32 * 256); };
+      auto sj_of = [](int n, int& s, int& j) {
+        if (n < 32) { s = n >> 1; j = n & 1; }
+        else if (n < 64) { s = (n - 32) >> 1; j = 2 + (n & 1); }
+        else { s = (n - 64) / 3; j = 4 + (n - 64) % 3; }
+      };
+      auto rd1 = [&](int n) {
+        int s, j;
+        sj_of(n, s, j);
+        return lds_ld16(f1o[s >> 3][s & 7] + j * 32 * 256);
+      };
       uint4 ring[4];
 #pragma unroll
       for (int n = 0; n < RPF; ++n) ring[n] = rd1(n);
 #pragma unroll
       for (int n = 0; n < 16 * NRT; ++n) {
-        const int s = n / NRT, j = n % NRT;
+        int s, j;
+        sj_of(n, s, j);
         const bf16x8 bb = as_bf8(ring[n & 3]);
         mma<MODE>(S[j], Wc[s], Wc[s], bb, bb);
         if (n + RPF < 16 * NRT) ring[(n + RPF) & 3] = rd1(n + RPF);
+        if constexpr (BOUNDED) {
+          if (n == 8) cb = bound_shift(wave_max(wn) * rmax);
+          if (n >= 34 && n < 98) {         // tiles 0-1 from slot 34, 2-3 from 66
+            const int e = n - 34, jj = e >> 4, q = e & 15;
+            psum[jj] += __builtin_amdgcn_exp2f(S[jj][q] - L2E * cb);
+          }
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
     // ---- softmax over the caption's words, per region: max and sum over
     // both token tiles (partner wave = wid ^ 1)
     // (BOUNDED: p = exp2(S' - log2(e) bound_shift(c)) needs no max)
-    float cb = 0.f;
-    if (BOUNDED) {
-      cb = wave_max(wn) * rmax;
-      cb = bound_shift(cb);
-    }
     float mj[NRT];
 #pragma unroll
     for (int j = 0; j < NRT; ++j) mj[j] = L2E * cb;
@@ -849,9 +866,10 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
     float sj[NRT];
 #pragma unroll
     for (int j = 0; j < NRT; ++j) {
-      float sum = 0.f;
+      float sum = BOUNDED && j < 4 ? psum[j & 3] : 0.f;
+      if (!BOUNDED || j >= 4)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) sum += __builtin_amdgcn_exp2f(S[j][q] - mj[j]);
+        for (int q = 0; q < 16; ++q) sum += __builtin_amdgcn_exp2f(S[j][q] - mj[j]);
       sj[j] = sum + __shfl_xor(sum, 32);
     }
     if (h == 0)

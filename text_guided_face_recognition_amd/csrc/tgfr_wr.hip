@@ -968,13 +968,36 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
       len_n = lens[min(i + 2, c1 - 1)];
       load_w(min(i + 2, c1 - 1));
     }
-    // ---- per-token epilogue (lane t = lr), log-sum-exp over both tiles
+    // ---- per-token epilogue (lane t = lr), log-sum-exp over both tiles.
+    // C-hat goes out first, |C_t|^2 summed from the same accumulator reads.
+    // (Stores are unconditional buffer ops -- a descriptor with no records or
+    // a lane offset past its end drops the ones that do not apply -- so the
+    // compiler counts them, and the next step's waits on the loads prefetched
+    // above do not wait for these stores to retire: vmcnt counts stores and
+    // retires in order.)
     const int t = lr, tg = 32 * tt + lr;
+    const long long pair = (long long)b * B_cap + ic;
+    constexpr uint32_t OOB = 0x80000000u;
     float csq = 0.f;
+    {
+      const auto rc = uniform_rsrc(Chi + pair * 32 * TP * 8, Chi && active ? 32 * TP * 16 : 0);
+      const uint32_t vo = (tg * 8 + 4 * h) * 2;
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
+      for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) csq = fmaf(C[dt][q], C[dt][q], csq);
+        for (int g = 0; g < 4; ++g) {
+          uint16_t hh[4];
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const float c = C[dt][4 * g + kk];
+            csq = fmaf(c, c, csq);
+            hh[kk] = lowp_bits<MODE>(c);
+          }
+          __builtin_amdgcn_raw_buffer_store_b64(
+              __builtin_bit_cast(u32x2, make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3]))),
+              rc, vo + (4 * dt + g) * TP * 16, 0, 0);
+        }
+    }
     csq += __shfl_xor(csq, 32);
     const float Z = lds_ldf(tok + t * 4);
     // (np sums E S' = log2(e) N over the regions)
@@ -989,13 +1012,6 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
     if (lane == 0) lds_stf(FR2_OFF_XL + wid * 4, ex);
     __syncthreads();
     ex += lds_ldf(FR2_OFF_XL + (wid ^ 1) * 4);
-    // The stores are unconditional buffer ops (a descriptor with no records
-    // or a lane offset past its end drops the ones that do not apply): the
-    // compiler then counts them, and the next step's waits on the loads
-    // prefetched above (issued before these stores) do not wait for the
-    // stores to retire -- vmcnt counts stores and retires in order.
-    const long long pair = (long long)b * B_cap + ic;
-    constexpr uint32_t OOB = 0x80000000u;
     __builtin_amdgcn_raw_buffer_store_b32(
         __float_as_uint(g3 * __logf(ex)),
         uniform_rsrc(logits + (long long)b * ld_logits + ic, active ? 4 : 0),
@@ -1006,21 +1022,6 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
           __builtin_bit_cast(u32x4, sv),
           uniform_rsrc(stats + pair * TP, stats && active ? TP * 16 : 0), h == 0 ? tg * 16 : OOB,
           0, 0);
-    }
-    {
-      const auto rc = uniform_rsrc(Chi + pair * 32 * TP * 8, Chi && active ? 32 * TP * 16 : 0);
-      const uint32_t vo = (tg * 8 + 4 * h) * 2;
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          uint16_t hh[4];
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk) hh[kk] = lowp_bits<MODE>(C[dt][4 * g + kk]);
-          __builtin_amdgcn_raw_buffer_store_b64(
-              __builtin_bit_cast(u32x2, make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3]))),
-              rc, vo + (4 * dt + g) * TP * 16, 0, 0);
-        }
     }
   }
 }

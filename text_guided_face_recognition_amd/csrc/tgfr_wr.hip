@@ -1431,22 +1431,37 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
       if (n == 190) initn = caption_init(inext, wn_next, big_next);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // |W_t| for the epilogue, issued ahead of the reductions below (pinned
-    // there): its latency hides under them instead of stalling the epilogue
-    const float u = Wnorm[(long long)i * TPAD + lr];
-    __builtin_amdgcn_sched_barrier(0);
+    // |W_t| for the epilogue, issued ahead of the reductions and the C-hat
+    // stores below (pinned there by the memory clobber: a load issued after
+    // the stores would wait for them to retire, vmcnt retiring in order)
+    // (a buffer load: a plain load of the restrict-qualified norms is free to
+    // sink below the stores)
+    const float u = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+        uniform_rsrc(Wnorm + (long long)i * TPAD, TPAD * 4), lr * 4, 0, 0));
+    asm volatile("" ::: "memory");
     // ---- N per token: reduce-scatter over the region lanes -> LDS
     {
       const float nr = rs16(np, lr);
       lds_stf(tok + acc_row(rs16_index(lr), h) * 4, nr);
     }
-    // ---- per-token epilogue (lane t = lr; both halves hold the same token)
+    // ---- per-token epilogue (lane t = lr; both halves hold the same token):
+    // C-hat goes out first, |C_t|^2 summed from the same accumulator reads
     const int t = lr;
     float csq = 0.f;
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) csq = fmaf(C[dt][q], C[dt][q], csq);
+      for (int g = 0; g < 4; ++g) {
+        uint16_t hh[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float c = C[dt][4 * g + k];
+          csq = fmaf(c, c, csq);
+          hh[k] = lowp_bits<MODE_BF16>(c);
+        }
+        const long long o = ((pair * 32 + (4 * dt + g)) * TPAD + t) * 8 + 4 * h;
+        *(uint2*)(Chi + o) = make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3]));
+      }
     csq = xhalf_sum(csq);
     const float Z = C[8][0];
     // np sums E * S' = log2(e) N over the regions (valid tokens: bias 0)
@@ -1460,7 +1475,6 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     logits[(long long)b * ld_logits + i] = g3 * __logf(ex);
     stats[pair * TPAD + t] =
         tvalid ? make_float4(Z, n_, cn, cosv) : make_float4(0.f, 0.f, 0.f, 0.f);
-    store_cq<MODE_BF16>(Chi, nullptr, pair, t, h, C);
     init = initn;
     big_cur = big_next;
   };

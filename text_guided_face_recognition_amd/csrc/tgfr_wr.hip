@@ -2333,38 +2333,59 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
           A1[u][4 * g + k] = 0.f;
         }
       }
-    // 64 MFMAs n = (W' / C-hat block c, k-step s, tile u): the 32 S' MFMAs
-    // of both token tiles first, then the 32 Q-hat ones, whose issue gaps
-    // carry phase A of the softmax (p = exp2(S') and its per-region sum: S'
-    // is complete by then) and the next caption's X-image DMA (one piece
-    // every 4 slots: the burst at the stage head cost ~100 cycles of issue a
-    // piece with the matrix core idle).  Operands read WPF slots ahead
-    // through a ring (one wave per SIMD: an LDS read waited on right before
-    // its MFMA stalls the wave for the whole LDS latency).
+    // 64 MFMAs: the 32 S' MFMAs first, tile 0's 16 k-steps then tile 1's,
+    // then the 32 Q-hat ones (k-step outer, tiles alternating).  Phase A of
+    // the softmax (p = exp2(S'), Σp) runs one element per gap as soon as a
+    // tile's S' is complete (tile 0 under tile 1's S' MFMAs, tile 1 under the
+    // first Q-hat ones), then the softmax-2 term ax (needs the sum) in the
+    // last Q-hat gaps; the next caption's X-image DMA goes one piece every 4
+    // slots.  Operands read WPF slots ahead through a ring (one wave per
+    // SIMD: an LDS read waited on right before its MFMA stalls the wave for
+    // the whole LDS latency).
     float a1[2][16], ax[2][16], v[2][16];
-    float sum = 0.f;
+    float sum = 0.f, inv = 0.f, kq = 0.f;
+    constexpr int AX0 = 51, AXN = 64 - AX0;     // ax elements 0..AXN-1 in the gaps
     {
+      auto su = [](int n, int& c, int& s, int& u) {
+        c = n >> 5;
+        if (c) { s = (n >> 1) & 15; u = n & 1; }
+        else { u = (n >> 4) & 1; s = n & 15; }
+      };
       auto rd1 = [&](int n) {
-        const int c = n >> 5, s = (n >> 1) & 15, u = n & 1;
+        int c, s, u;
+        su(n, c, s, u);
         return lds_ld16(base + g1o[s & 7] + (s >> 3) * (128 * 256) + u * 32 * 256 +
                         c * 64 * 256);
       };
       uint4 ring[8];
 #pragma unroll
       for (int n = 0; n < WPF; ++n) ring[n] = rd1(n);
+      u32x4 f0b[2];                                // f0 of the ax group, read a group ahead
 #pragma unroll
       for (int n = 0; n < 64; ++n) {
-        const int c = n >> 5, s = (n >> 1) & 15, u = n & 1;
+        int c, s, u;
+        su(n, c, s, u);
         const bf16x8 x = as_bf8(ring[n & 7]);
         if (c) mma<MODE>(A1[u], x, x, Rf[s], Rf[s]);
         else mma<MODE>(A0[u], x, x, Rf[s], Rf[s]);
         if (n + WPF < 64) ring[(n + WPF) & 7] = rd1(n + WPF);
         if (has_next && (n & 3) == 1) dma_piece(i + 1, nb, n >> 2);
         if (has_next && (n == 3 || n == 7)) dma_piece(i + 1, nb, 16 + (n >> 2));
-        if (n >= 34) {                   // elements 0..29 of phase A
-          const int e = n - 34, uu = e >> 4, q = e & 15;
+        if (n >= 18 && n < 50) {                   // phase A, element e = n - 18
+          const int e = n - 18, uu = e >> 4, q = e & 15;
           a1[uu][q] = __builtin_amdgcn_exp2f(A0[uu][q]);
           sum += a1[uu][q];
+        }
+        if (n == 46) f0b[0] = scal(tk, 0, 0, 0);
+        if (n == 50) {
+          inv = __builtin_amdgcn_rcpf(sum_floor(xhalf_sum(sum)));
+          kq = gL * inv;
+        }
+        if (n >= AX0) {                            // ax element e (a1 holds p)
+          const int e = n - AX0, uu = e >> 4, q = e & 15, g = q >> 2, k = q & 3;
+          if (k == 0 && e + 4 < 32) f0b[((e >> 2) + 1) & 1] = scal(tk, 0, (e + 4) >> 4, ((e + 4) >> 2) & 3);
+          ax[uu][q] = __builtin_amdgcn_exp2f(fmaf(a1[uu][q], kq, fl(f0b[(e >> 2) & 1], k)));
+          (void)g;
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -2376,13 +2397,6 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
     // element per MFMA gap, then the 32 W' MFMAs (tile 1's M_w in the gaps of
     // tile 0's).  (Computing all of it between G1 and G3 left the matrix core
     // idle for a quarter of the caption.)
-#pragma unroll
-    for (int e = 30; e < 32; ++e) {
-      a1[e >> 4][e & 15] = __builtin_amdgcn_exp2f(A0[e >> 4][e & 15]);
-      sum += a1[e >> 4][e & 15];
-    }
-    const float inv = __builtin_amdgcn_rcpf(sum_floor(xhalf_sum(sum)));
-    const float kq = gL * inv;
     auto pk2 = [](float x, float y) {
       if constexpr (MODE == MODE_F16) return pack2(f16_bits(x), f16_bits(y));
       else return pk_bf16(x, y);
@@ -2396,10 +2410,14 @@ __global__ __launch_bounds__(256, 1) void wr_bwd_wide2_kernel(
       uint32_t c2[8];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const u32x4 f0 = scal(tk, 0, u, g), f5 = scal(tk, 5, u, g);
+        const u32x4 f5 = scal(tk, 5, u, g);
+        if (16 * u + 4 * g + 3 >= AXN) {           // the ax the G1 gaps did not reach
+          const u32x4 f0 = scal(tk, 0, u, g);
 #pragma unroll
-        for (int k = 0; k < 4; ++k)         // (a1 still holds p here)
-          ax[u][4 * g + k] = __builtin_amdgcn_exp2f(fmaf(a1[u][4 * g + k], kq, fl(f0, k)));
+          for (int k = 0; k < 4; ++k)
+            if (16 * u + 4 * g + k >= AXN)
+              ax[u][4 * g + k] = __builtin_amdgcn_exp2f(fmaf(a1[u][4 * g + k], kq, fl(f0, k)));
+        }
 #pragma unroll
         for (int k = 0; k < 4; k += 2)
           c2[(4 * g + k) >> 1] = pk2(fl(f5, k) * ax[u][4 * g + k],

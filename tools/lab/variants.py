@@ -215,6 +215,9 @@ VARIANTS = {
     "mfma_only": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
                   (_DMA, "")],
     "pf3_7": [("constexpr int BD_PF3 = 4;", "constexpr int BD_PF3 = 7;")],
+    # the 64-token backward's LDS operand prefetch distance
+    "wpf3": [("constexpr int WPF = 4;", "constexpr int WPF = 3;")],
+    "wpf6": [("constexpr int WPF = 4;", "constexpr int WPF = 6;")],
     "skel_l2": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
                 (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
                 (_G1, """      asm volatile("" ::"v"(rd[n & 3]));"""),

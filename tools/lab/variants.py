@@ -218,6 +218,17 @@ VARIANTS = {
     # the 64-token backward's LDS operand prefetch distance
     "wpf3": [("constexpr int WPF = 4;", "constexpr int WPF = 3;")],
     "wpf6": [("constexpr int WPF = 4;", "constexpr int WPF = 6;")],
+    # the 64-token backward's phase-A window (slots a..a+31, 1/sum at a+32)
+    "ph17": [("n >= 18 && n < 50", "n >= 17 && n < 49"),
+             ("const int e = n - 18, uu", "const int e = n - 17, uu"),
+             ("if (n == 50) {", "if (n == 49) {"),
+             ("AX0 = 51", "AX0 = 50"),
+             ("if (n == 46) f0b", "if (n == 45) f0b")],
+    "ph16": [("n >= 18 && n < 50", "n >= 16 && n < 48"),
+             ("const int e = n - 18, uu", "const int e = n - 16, uu"),
+             ("if (n == 50) {", "if (n == 48) {"),
+             ("AX0 = 51", "AX0 = 49"),
+             ("if (n == 46) f0b", "if (n == 44) f0b")],
     "skel_l2": [(_SM, """        asm volatile("" ::"v"(Q), "v"(spc[0].x), "v"(spc[1].x), "v"(mc));"""),
                 (_G3, """          asm volatile("" ::"v"(Mi[n & 3]), "v"(rd[n & 7]));"""),
                 (_G1, """      asm volatile("" ::"v"(rd[n & 3]));"""),

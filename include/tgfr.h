@@ -29,6 +29,9 @@
  *     token stride of every words / stats / C / token-table buffer.  t_pad =
  *     64 (modes 0 / 2): two waves per caption; bounded = 1 drops the running
  *     max both ways (scores bounded as below; Rnorm unused).
+ *   - ABI 600: the max-free t_pad-32 kernels (pipelined forward, two-role
+ *     backward) run in mode 2 as well as mode 0; in mode 2 the forward
+ *     stores C-hat scaled by 2^-8 and the token-table calls take bounded = 2.
  */
 #ifndef TGFR_H
 #define TGFR_H
@@ -68,7 +71,8 @@ int tgfr_prep_rows_f16(const float* x, long long s_item, long long s_row, long l
  * [B_cap][32].  Mode 0 keeps the image's R resident in LDS (Rlo/Wlo unused, may
  * be NULL) and takes the words scaled by log2(e) (Whi = bf16(log2(e) W),
  * tgfr_prep_rows scale).  bounded = 1 (with Rnorm = |R_r| [B_img][224]) lets
- * the mode-0 forward run without a running max.  t_pad 32 (with Sp): the
+ * the mode-0 / mode-2 forward run without a running max (mode 2: fp16
+ * operands, words scaled as in mode 0, C-hat stored x 2^-8).  t_pad 32 (with Sp): the
  * max-free pipelined kernel, exact for ANY input -- each caption whose
  * score bound max|W| max|R| exceeds 84.5 takes its running-max variant on
  * the device (the unit-norm BERT-path features have ~1) -- which also
@@ -113,9 +117,10 @@ int tgfr_wr_guard(const float* Wnorm, int n_w, const float* Rnorm, int n_r, int*
  * bound c = max|W| max|R| is formed again here, giving the same per-caption
  * variant (t_pad 32) / score shift (t_pad 64) as the forward's.
  * The text side is detached in the reference (utils/dataset_utils.py:42).
- * bounded = 1 (mode 0 with t_pad 32 after a bounded forward, or modes 0 / 2
- * with t_pad 64; scores bounded as for tgfr_wr_fwd): both calls must pass
- * it, Whi is the forward's log2(e)-scaled words, and the max-free kernels
+ * bounded = 1 (modes 0 / 2 with t_pad 32 after a bounded forward, or modes
+ * 0 / 2 with t_pad 64; scores bounded as for tgfr_wr_fwd): both calls must
+ * pass it -- tgfr_wr_bwd_tok(_ce) as 2 in mode 2 with t_pad 32 (its table
+ * then folds the forward's 2^-8 C-hat scale back in) -- Whi is the forward's log2(e)-scaled words, and the max-free kernels
  * run (t_pad 32: the two-role one, wr_bwd_duo_kernel, which reads the
  * forward's stored scores Sp instead of recomputing them -- required then;
  * NULL otherwise).  guard: the forward's (tgfr_wr_guard; NULL: none); with

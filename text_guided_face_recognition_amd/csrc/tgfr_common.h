@@ -63,6 +63,26 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
 }
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+// Two fp32 -> the packed single-operand encoding of a mode (bf16x2, or fp16x2
+// rounded to nearest)
+template <int MODE>
+__device__ __forceinline__ uint32_t pk_lowp(float a, float b) {
+  if constexpr (MODE == MODE_F16)
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, f16x2));
+  else
+    return pk_bf16(a, b);
+}
+// One single-operand 32x32x16 MFMA of a mode; the operands are bf16x8
+// carriers holding bf16 or fp16 bits
+template <int MODE>
+__device__ __forceinline__ f32x16 mfma_lp(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  if constexpr (MODE == MODE_F16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
 
 template <int MODE>
 __device__ __forceinline__ void mma(f32x16& acc, const bf16x8& ahi, const bf16x8& alo,

@@ -1075,6 +1075,12 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_res2_kernel(
 constexpr float BIG_C = 10.f;
 constexpr float PAD_BIAS = -60000.f;
 constexpr int SP_REC = 64 * 16 + 64;   // uint16 per (pair, tile): 64 lanes x 16 fp16 + 32 fp32 m_r
+// fp16 mode: the forward forms E (the softmax-2 numerators) scaled by 2^-8,
+// so C-hat and Z come out scaled by 2^-8 (|C-hat| <= Z max|R_d| and Z <=
+// 196 e^g1 would leave fp16 past max|R_d| ~ 2); |C|, n and cos are ratios
+// and do not change, and the token table's layout 3 takes the true 1 / Z
+constexpr float CHAT_F16 = 1.f / 256.f;
+constexpr float CHAT_F16_LOG2 = -8.f;
 // the score bound's image factor max_r |R_r| (norm rows 0..223; one wave):
 // formed identically by the forward and the backward's token-table kernel,
 // so both take the same BIG_C decision for a pair
@@ -1098,7 +1104,6 @@ __device__ __forceinline__ uint4 sp_pack(const f32x16& v, int o, float m) {
   }
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 // fp32 results of fp16 operands on v_fma_mix_f32 (the conversion is free):
 // h * f, and h + g
 __device__ __forceinline__ float mix_mul(_Float16 h, float f) {
@@ -1189,6 +1194,7 @@ static_assert([] {
 }(), "operand reads per caption must be a multiple of the ring size");
 __device__ __forceinline__ int fwd_ring(int n) { return kFwdRing.r[n]; }
 
+template <int MODE>
 __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi,
     const float* __restrict__ Wnorm, const float* __restrict__ Rnorm,
@@ -1270,7 +1276,8 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
   const int ewx = (lr >> 2) & 3;
   const float kg = g1 * L2E;
   const float rb6 = lr < NREG - 6 * 32 ? 0.f : -1e30f;   // padding regions of tile 6
-  const bf16x8 ones = as_bf8(make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
+  constexpr uint32_t ONE2 = MODE == MODE_F16 ? 0x3C003C00u : 0x3F803F80u;
+  const bf16x8 ones = as_bf8(make_uint4(ONE2, ONE2, ONE2, ONE2));
 
   bf16x8 Wc[16];
   auto load_w = [&](int ii) {
@@ -1345,10 +1352,14 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
       kk = kg * __builtin_amdgcn_rcpf(sum_floor(xhalf_sum((ma[0] + ma[1]) + (ma[2] + ma[3]))));
     } else {
       const int q = c - 16;
-      const float e = __builtin_amdgcn_exp2f(j == 6 ? fmaf(p[q], kk, rb6) : p[q] * kk);
+      // (fp16: E scaled by CHAT_F16 inside the exponent)
+      const float e = MODE == MODE_F16
+                          ? __builtin_amdgcn_exp2f(
+                                fmaf(p[q], kk, j == 6 ? rb6 + CHAT_F16_LOG2 : CHAT_F16_LOG2))
+                          : __builtin_amdgcn_exp2f(j == 6 ? fmaf(p[q], kk, rb6) : p[q] * kk);
       np[q] = fmaf(e, S[q], np[q]);
       p[q] = e;
-      if (q & 1) pk[q >> 1] = pk_bf16(p[q - 1], p[q]);
+      if (q & 1) pk[q >> 1] = pk_lowp<MODE>(p[q - 1], p[q]);
       if ((q & 3) == 3) {
         const int g = q >> 2;
         lds_st8(etb + ew + ((g ^ ewx) << 4), make_uint2(pk[2 * g], pk[2 * g + 1]));
@@ -1365,8 +1376,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     f32x16 acc = init;
 #pragma unroll
     for (int s = 0; s < 16; ++s)
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Wc[s], as_bf8(lds_ld16(f1o[s >> 3][s & 7])),
-                                                    acc, 0, 0, 0);
+      acc = mfma_lp<MODE>(Wc[s], as_bf8(lds_ld16(f1o[s >> 3][s & 7])), acc);
     S[0] = acc;
   }
 #pragma unroll
@@ -1398,16 +1408,15 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
         // builtins (not inline asm): the compiler's hazard recognizer then
         // places the VALU-write -> MFMA-read and MFMA -> VALU-read waits
         const int s = sl.idx, j = sl.tile;
-        S[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            Wc[s], __builtin_bit_cast(bf16x8, opnd), s == 0 ? (j == 0 ? initn : init) : S[j],
-            0, 0, 0);
+        S[j] = mfma_lp<MODE>(Wc[s], __builtin_bit_cast(bf16x8, opnd),
+                             s == 0 ? (j == 0 ? initn : init) : S[j]);
       } else {
         const int s = g2_s(sl.idx), dt = g2_dt(sl.idx);
         const bf16x8 a = dt < 8 ? __builtin_bit_cast(bf16x8, opnd) : ones;
         if (sl.tile == 0 && s == 0)
-          C[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, eb[0], (f32x16){}, 0, 0, 0);
+          C[dt] = mfma_lp<MODE>(a, eb[0], (f32x16){});
         else
-          C[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, eb[s], C[dt], 0, 0, 0);
+          C[dt] = mfma_lp<MODE>(a, eb[s], C[dt]);
       }
       // ---- reads of the slot three ahead (wrapping into the next caption)
       issue_read(fwd_slot((n + PF_FWD) % FWD_SLOTS), rd[fwd_ring((n + PF_FWD) % FWD_SLOTS)]);
@@ -1457,7 +1466,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
         for (int k = 0; k < 4; ++k) {
           const float c = C[dt][4 * g + k];
           csq = fmaf(c, c, csq);
-          hh[k] = lowp_bits<MODE_BF16>(c);
+          hh[k] = lowp_bits<MODE>(c);
         }
         const long long o = ((pair * 32 + (4 * dt + g)) * TPAD + t) * 8 + 4 * h;
         *(uint2*)(Chi + o) = make_uint2(pack2(hh[0], hh[1]), pack2(hh[2], hh[3]));
@@ -1537,7 +1546,7 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
   const int len = lens[i];
   const bool valid = t < len;
   const float4 st = valid ? stats[pair * TP + t] : make_float4(1.f, 0.f, 0.f, 0.f);
-  // layouts 1 / 2: the pair's score bound c = max_t |W_t| max_r |R_r| (as the
+  // layouts 1 / 2 / 3: the pair's score bound c = max_t |W_t| max_r |R_r| (as the
   // bounded forwards form it).  Layout 1 (wr_bwd_wide2_kernel): the max-free
   // backward shifts S' by -log2(e) bound_shift(c) through the G1 initial row,
   // and sigma absorbs alpha times it.  Layout 2 (wr_bwd_duo_kernel): no shift;
@@ -1577,8 +1586,12 @@ __global__ __launch_bounds__(256) void wr_tok_kernel(const float4* __restrict__ 
     } else {
       // wr_bwd_pipe_kernel: scores S' = log2(e) S, rows W' = log2(e) W, C-hat
       constexpr float L2E = 1.4426950408889634f;
-      o[0] = __log2f(g1 * iz / L2E);    // E -> g1 A2 / log2e, as an exp2 offset
+      // E -> g1 A2 / log2e, as an exp2 offset
       o[1] = alpha / L2E;               // coefficient of S' in dA2
+      // (layout 3, the fp16 forward: Z and C-hat are stored x CHAT_F16, so
+      // the exp2 offset takes the true 1 / Z; beta / Z applied to C-hat is
+      // unchanged)
+      o[0] = __log2f(g1 * iz * (layout == 3 ? CHAT_F16 : 1.f) / L2E);
       o[2] = beta * iz;                 // coefficient of Q-hat in dA2
       o[3] = sigma - alpha * cb;        // (S' enters as S' - log2(e) c)
       o[4] = alpha / g1;                // M_w = dS / log2e + o4 * (g1 A2 / log2e)
@@ -2575,6 +2588,7 @@ __device__ __forceinline__ void lds_wait_ge(uint32_t off, int v) {
   while (lds_ld_acquire(off) < v) __builtin_amdgcn_s_sleep(1);
 }
 
+template <int MODE>
 __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
     const uint16_t* __restrict__ Rhi, const uint16_t* __restrict__ Whi, int B_img, int B_cap,
     int n_chunks, float g1, const float* __restrict__ tok, const uint16_t* __restrict__ Chi,
@@ -2683,8 +2697,7 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
         for (int n = 0; n < BD_PF3; ++n) rd[n] = g3_read(n, x3);
 #pragma clang loop unroll(full)
         for (int n = 0; n < 32; ++n) {
-          dR[n >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Mi[n & 3], rd[n & 7], dR[n >> 2],
-                                                              0, 0, 0);
+          dR[n >> 2] = mfma_lp<MODE>(Mi[n & 3], rd[n & 7], dR[n >> 2]);
           if (n + BD_PF3 < 32) rd[(n + BD_PF3) & 7] = g3_read(n + BD_PF3, x3);
           if (bd_dma_slot(n) >= 0) dma_piece(t + 2, bd_dma_slot(n));
           __builtin_amdgcn_sched_barrier(0);
@@ -2694,7 +2707,9 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
         for (int j = 0; j < 9; ++j) dma_piece(t + 2, j);
       }
     }
-    if (rt < NRT) store_dr_tile(dR, n_chunks, chunk, b, rt, B_img, lane, out, s_b, s_r, s_d, slab);
+    if (rt < NRT)
+      store_dr_tile<MODE == MODE_F16>(dR, n_chunks, chunk, b, rt, B_img, lane, out, s_b, s_r, s_d,
+                                      slab);
     return;
   }
 
@@ -2719,8 +2734,7 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
                               lds_ld16(xb + g1o[s & 7] + (s >> 3) * (64 * 256) + 32 * 256));
   };
   auto g1_mfma = [&](int s, const u32x4& op, f32x16& A) {
-    A = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, op), Rf[s],
-                                                s == 0 ? (f32x16){} : A, 0, 0, 0);
+    A = mfma_lp<MODE>(__builtin_bit_cast(bf16x8, op), Rf[s], s == 0 ? (f32x16){} : A);
   };
   // stored S' of caption k (clamped to the chunk) for this tile: 2 x 16 B per
   // lane, and the region max m_r of a BIG_C caption (unused otherwise)
@@ -2821,8 +2835,8 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
       v[q] = fmaf(fl(fc_[0], q), ax[q], dsx);                  // M_w (scaled for W')
       ax[q] = fl(fc_[1], q) * ax[q];                           // M_c (for C-hat)
       if (q & 1) {
-        mw2[q >> 1] = pk_bf16(v[q - 1], v[q]);
-        mc2[q >> 1] = pk_bf16(ax[q - 1], ax[q]);
+        mw2[q >> 1] = pk_lowp<MODE>(v[q - 1], v[q]);
+        mc2[q >> 1] = pk_lowp<MODE>(ax[q - 1], ax[q]);
       }
       if (q == 15) {
 #pragma unroll
@@ -3076,7 +3090,8 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   if (const int e = allow_lds(wr_fwd_kernel<MODE_SPLIT, 2>, F_LDS2)) return e;
   if (const int e = allow_lds(wr_fwd_kernel<MODE_F16, 1>, F_LDS)) return e;
   if (const int e = allow_lds(wr_fwd_res_kernel, FR_LDS)) return e;
-  if (const int e = allow_lds(wr_fwd_pipe_kernel, FR_LDS)) return e;
+  if (const int e = allow_lds(wr_fwd_pipe_kernel<MODE_BF16>, FR_LDS)) return e;
+  if (const int e = allow_lds(wr_fwd_pipe_kernel<MODE_F16>, FR_LDS)) return e;
   if (t_pad == 64) {
     // 64-token captions: two waves per caption, two captions at a time
     const int grid2 = ((B_cap + 1) / 2) * B_img;
@@ -3118,7 +3133,13 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
     hipLaunchKernelGGL((wr_fwd_kernel<MODE_SPLIT, 1>), dim3(grid), dim3(256), F_LDS, s, Rhi, Rlo,
                        Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1, gamma2, gamma3,
                        eps, logits, ld_logits, (float4*)stats, Chi, Clo, att, att_T);
-  else if (mode == MODE_F16)
+  else if (mode == MODE_F16 && bounded && Rnorm && !att && stats && Chi && Sp) {
+    // the pipelined max-free forward on fp16 operands (C-hat stored x CHAT_F16)
+    const int n_chunks = max(1, min((B_cap + 3) / 4, (256 + B_img - 1) / B_img));
+    hipLaunchKernelGGL(wr_fwd_pipe_kernel<MODE_F16>, dim3(n_chunks * B_img), dim3(256), FR_LDS, s,
+                       Rhi, Whi, Wnorm, Rnorm, lens, B_img, B_cap, n_chunks, gamma1, gamma2,
+                       gamma3, eps, logits, ld_logits, (float4*)stats, Chi, Sp);
+  } else if (mode == MODE_F16)
     hipLaunchKernelGGL((wr_fwd_kernel<MODE_F16, 1>), dim3(grid), dim3(256), F_LDS, s, Rhi, Rlo,
                        Whi, Wlo, Wnorm, lens, B_img, B_cap, img_offset, gamma1, gamma2, gamma3,
                        eps, logits, ld_logits, (float4*)stats, Chi, Clo, att, att_T);
@@ -3126,8 +3147,8 @@ int tgfr_wr_fwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
     // R resident in LDS; caption chunks sized for >= ~256 workgroups
     const int n_chunks = max(1, min((B_cap + 3) / 4, (256 + B_img - 1) / B_img));
     if (bounded && Rnorm && !att && stats && Chi && Sp)
-      hipLaunchKernelGGL(wr_fwd_pipe_kernel, dim3(n_chunks * B_img), dim3(256), FR_LDS, s,
-                         Rhi, Whi, Wnorm, Rnorm, lens, B_img, B_cap, n_chunks, gamma1, gamma2,
+      hipLaunchKernelGGL(wr_fwd_pipe_kernel<MODE_BF16>, dim3(n_chunks * B_img), dim3(256), FR_LDS,
+                         s, Rhi, Whi, Wnorm, Rnorm, lens, B_img, B_cap, n_chunks, gamma1, gamma2,
                          gamma3, eps, logits, ld_logits, (float4*)stats, Chi, Sp);
     else
       hipLaunchKernelGGL(wr_fwd_res_kernel, dim3(n_chunks * B_img), dim3(256), FR_LDS, s,
@@ -3158,8 +3179,8 @@ static int wr_tok_launch(const float* stats, const float* Wnorm, const float* Rn
   else if (t_pad == 32)
     hipLaunchKernelGGL(wr_tok_kernel<32>, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, (const float4*)stats, Wnorm, Rnorm, lens, dlogits, ld,
-                       B_img, B_cap, gamma1, gamma2, gamma3, eps, bounded ? 2 : 0, tok_ws, ce,
-                       nullptr);
+                       B_img, B_cap, gamma1, gamma2, gamma3, eps,
+                       bounded == 2 ? 3 : bounded ? 2 : 0, tok_ws, ce, nullptr);
   else
     return 1001;
   return (int)hipGetLastError();
@@ -3230,12 +3251,19 @@ int tgfr_wr_bwd(const uint16_t* Rhi, const uint16_t* Rlo, const uint16_t* Whi,
   }
   if (bounded && t_pad != 64) {
     if (t_pad != 32 || !Sp) return 1001;
-    if (mode != MODE_BF16) return 1002;
-    if (const int e = allow_lds(wr_bwd_duo_kernel, BD_LDS)) return e;
-    hipLaunchKernelGGL(wr_bwd_duo_kernel, dim3(grid), dim3(512), BD_LDS, s, Rhi, Whi, B_img,
-                       B_cap, n_chunks, gamma1, tok_ws, Chi, Sp, dR, s_b, s_r, s_d,
-                       (uint16_t*)ws);
-    return frag_reduce(n_chunks, B_img, (const uint16_t*)ws, dR, s_b, s_r, s_d, s);
+    if (mode != MODE_BF16 && mode != MODE_F16) return 1002;
+    if (const int e = allow_lds(wr_bwd_duo_kernel<MODE_BF16>, BD_LDS)) return e;
+    if (const int e = allow_lds(wr_bwd_duo_kernel<MODE_F16>, BD_LDS)) return e;
+    if (mode == MODE_F16)
+      hipLaunchKernelGGL(wr_bwd_duo_kernel<MODE_F16>, dim3(grid), dim3(512), BD_LDS, s, Rhi, Whi,
+                         B_img, B_cap, n_chunks, gamma1, tok_ws, Chi, Sp, dR, s_b, s_r, s_d,
+                         (uint16_t*)ws);
+    else
+      hipLaunchKernelGGL(wr_bwd_duo_kernel<MODE_BF16>, dim3(grid), dim3(512), BD_LDS, s, Rhi, Whi,
+                         B_img, B_cap, n_chunks, gamma1, tok_ws, Chi, Sp, dR, s_b, s_r, s_d,
+                         (uint16_t*)ws);
+    return frag_reduce(n_chunks, B_img, (const uint16_t*)ws, dR, s_b, s_r, s_d, s,
+                       mode == MODE_F16);
   } else if (mode == MODE_SPLIT && (!Rlo || !Wlo || !Clo)) {
     return 1001;
   } else if (t_pad == 64) {
@@ -3284,6 +3312,6 @@ int tgfr_wr_lds_bytes(int which) {
   return which == 0 ? F_LDS : which == 1 ? BwdCfg<MODE_SPLIT>::LDS : FR_LDS;
 }
 
-int tgfr_version(void) { return 510; }
+int tgfr_version(void) { return 600; }
 
 }  // extern "C"

@@ -51,13 +51,13 @@ WR_BOUND_MAX = 85.9
 
 def wr_fast(mode, t_words, bounded, att_T=0):
     """True when the word<->region forward / backward take the bounded
-    (max-free) kernels, which read only the words' operand rows: bf16 with
-    t_pad = 32, or bf16 / fp16 with t_pad = 64 (_wr_fwd)."""
+    (max-free) kernels, which read only the words' operand rows: bf16 / fp16
+    with t_pad = 32 (the pipelined forward and the two-role backward, no
+    attention maps) or t_pad = 64 (_wr_fwd)."""
     m = _wr_mode(mode)
     t_pad = TPAD if t_words <= TPAD else 2 * TPAD
-    return bool(bounded) and (
-        (m == MODES["bf16"] and not att_T and t_pad == TPAD) or
-        (m != MODES["fp32"] and t_pad == 2 * TPAD))
+    return bool(bounded) and m != MODES["fp32"] and (
+        (not att_T and t_pad == TPAD) or t_pad == 2 * TPAD)
 
 
 def wr_rows_path(mode, t_words, bounded):
@@ -219,7 +219,10 @@ def _wr_bwd(saved, cfg, tok_call):
                      device=dev)
     tok = torch.empty(b_img, b_cap, t_pad, 8, dtype=torch.float32, device=dev)
     split = m == MODES["fp32"]
-    tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, fast, t_pad, tok, guard)
+    # the token table's `bounded` code: 2 = the fp16 two-role backward, whose
+    # forward stored C-hat scaled by 2^-8 (tgfr.h, tgfr_wr_bwd_tok)
+    tok_bounded = 2 if fast and m == MODES["fp16"] and t_pad == TPAD else int(fast)
+    tok_call(stats, w_norm, r_norm, lens, b_img, b_cap, tok_bounded, t_pad, tok, guard)
     d_reg = torch.empty(b_img, NREG, D, dtype=torch.float32, device=dev)
     call("tgfr_wr_bwd", ptr(r_hi), ptr(r_lo) if split else None, ptr(w_hi),
          ptr(w_lo) if split else None, b_img, b_cap, gamma1, ptr(tok),

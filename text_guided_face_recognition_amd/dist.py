@@ -30,6 +30,7 @@ import torch
 import torch.distributed as dist
 
 _CAPTURE = None
+_SIDE = {}          # per-device side stream of the eager overlapped collectives
 
 
 def active_capture():
@@ -190,6 +191,31 @@ class DistContext:
             c += w
         return tuple(outs)
 
+    def gather_text_async(self, *tensors):
+        """gather_text started on a side stream after the current stream's
+        work (StepCapture.cut_async under capture), so that the work launched
+        next -- IMIM's forward in the DP step -- overlaps the all-gather;
+        returns finish(), which orders the current stream after the
+        collective (a join) and unpacks the gathered tensors.  gloo (CPU
+        tests) gathers synchronously."""
+        if not self.active:
+            return lambda: tensors
+        flat = [t.contiguous().view(torch.uint8).reshape(t.shape[0], -1) for t in tensors]
+        widths = [f.shape[1] for f in flat]
+        packed = torch.cat(flat, 1)
+        allp, ev = all_gather_cat_async(packed, self.group)
+
+        def finish():
+            _join(ev)
+            _ = packed      # alive until the collective is joined (its block must
+            outs, c = [], 0  # not be handed to the overlapped work's tensors)
+            for t, w in zip(tensors, widths):
+                part = allp[:, c:c + w].contiguous().view(t.dtype)
+                outs.append(part.reshape((allp.shape[0],) + tuple(t.shape[1:])))
+                c += w
+            return tuple(outs)
+        return finish
+
     def reduce_grads_async(self, params):
         """reduce_grads of `params` started now and overlapped with the work
         that follows (a side stream; a cut of its own under StepCapture);
@@ -214,17 +240,21 @@ class DistContext:
         if handle is not None:
             _join(handle)
 
-    def reduce_grads(self, params):
+    def reduce_grads(self, params, after=None):
         """Sum the gradients of `params` over ranks in one all-reduce of a flat
         buffer (the DDP replacement: losses are pre-weighted so that the SUM is
-        the global-batch gradient); p.grad become views of the reduced buffer."""
+        the global-batch gradient); p.grad become views of the reduced buffer.
+        after: a reduce_grads_async handle the current stream also waits for
+        here (one step boundary for both buckets under StepCapture)."""
         if not self.active:
+            _join(after)
             return
         ps = [p for p in params if p.grad is not None]
         if not ps:
+            _join(after)
             return
         flat = torch.cat([p.grad.reshape(-1) for p in ps])
-        all_reduce_sum_(flat, self.group)
+        all_reduce_sum_(flat, self.group, after=after)
         off = 0
         for p in ps:
             n = p.numel()
@@ -281,13 +311,49 @@ def all_gather_cat(t, group=None):
     return out
 
 
-def all_reduce_sum_(t, group=None):
+def all_gather_cat_async(t, group=None):
+    """all_gather_cat started on a side stream after the current stream's work
+    (StepCapture.cut_async under capture): returns (out, event to join before
+    reading out).  gloo (CPU tests): synchronous, event None."""
+    t = t.contiguous()
+    replica = isinstance(group, ReplicaGroup)
+    if not replica and dist.get_backend(group) == "gloo":
+        return all_gather_cat(t, group), None
+    world = group.world if replica else dist.get_world_size(group)
+    out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
+                      device=t.device)
+
+    def run():
+        if replica:
+            out.view((world,) + tuple(t.shape)).copy_(t.unsqueeze(0).expand(
+                (world,) + tuple(t.shape)))
+        else:
+            dist.all_gather_into_tensor(out, t, group=group)
+    if _CAPTURE is not None:
+        return out, _CAPTURE.cut_async(run)
+    dev = torch.cuda.current_device()
+    side = _SIDE.setdefault(dev, torch.cuda.Stream())
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        run()
+    ev = torch.cuda.Event()
+    ev.record(side)
+    t.record_stream(side)
+    out.record_stream(side)
+    return out, ev
+
+
+def all_reduce_sum_(t, group=None, after=None):
     """In-place SUM all-reduce (gloo stages device tensors through host
-    memory).  Capture-aware (StepCapture)."""
+    memory).  Capture-aware (StepCapture).  after: an event (of an overlapped
+    collective) the current stream waits for first -- inside the same step
+    boundary under capture."""
     replica = isinstance(group, ReplicaGroup)
     gloo = not replica and dist.get_backend(group) == "gloo"
 
     def run():
+        if after is not None:
+            torch.cuda.current_stream().wait_event(after)
         if replica:
             t.mul_(group.world)
         elif gloo and t.is_cuda:
@@ -298,9 +364,6 @@ def all_reduce_sum_(t, group=None):
             dist.all_reduce(t, group=group)
     _run_or_cut(run)
     return t
-
-
-_SIDE = {}
 
 
 def all_reduce_sum_async_(t, group=None):

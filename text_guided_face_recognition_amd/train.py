@@ -221,19 +221,41 @@ class Train:
         labels = self._labels(ctx.n_global, g.device)
         self.optimizer.zero_grad(set_to_none=True)
         wi, lc = float(args.lambda_id), float(args.lambda_clip)
-        with torch.cuda.stream(side):
-            img_features = self.image_head.global_features(g)
-            s0, s1, cl = sent_global_loss(img_features, sent_g, labels, cls_g, b, args)
-            tid, iid = self._identity(sent, img_features, class_ids, ctx)
-            torch.autograd.backward((s0, s1, cl, tid, iid),
-                                    self._weights((1.0, 1.0, lc, wi, wi), g.device))
-            # the classifiers' gradients are final: their SGD update (group 1,
-            # most of the optimiser's bytes) runs here, beside the
-            # word<->region branch (0.434-0.437 -> 0.429-0.430 ms per step)
-            self.optimizer.step(groups=[1])
-        if text_ev is not None:
-            main.wait_event(text_ev)
-        w0, w1, _ = words_loss(words_features, words_g, labels, None, cls_g, b, args)
+        order = os.environ.get("TGFR_ORDER", "a")
+
+        def side_fwd():
+            with torch.cuda.stream(side):
+                img_features = self.image_head.global_features(g)
+                s0, s1, cl = sent_global_loss(img_features, sent_g, labels, cls_g, b, args)
+                tid, iid = self._identity(sent, img_features, class_ids, ctx)
+            return s0, s1, cl, tid, iid
+
+        def side_bwd(terms):
+            with torch.cuda.stream(side):
+                torch.autograd.backward(terms, self._weights((1.0, 1.0, lc, wi, wi), g.device))
+                # the classifiers' gradients are final: their SGD update (group 1,
+                # most of the optimiser's bytes) runs here, beside the
+                # word<->region branch (0.434-0.437 -> 0.429-0.430 ms per step)
+                self.optimizer.step(groups=[1])
+
+        def wr_fwd():
+            if text_ev is not None:
+                main.wait_event(text_ev)
+            return words_loss(words_features, words_g, labels, None, cls_g, b, args)[:2]
+
+        if order == "a":
+            terms = side_fwd()
+            side_bwd(terms)
+            w0, w1 = wr_fwd()
+        elif order == "b":
+            terms = side_fwd()
+            w0, w1 = wr_fwd()
+            side_bwd(terms)
+        else:
+            w0, w1 = wr_fwd()
+            terms = side_fwd()
+            side_bwd(terms)
+        s0, s1, cl, tid, iid = terms
         torch.autograd.backward((w0, w1), self._weights((1.0, 1.0), g.device))
         main.wait_stream(side)
         return self._finish(w0, w1, s0, s1, cl, tid, iid, lc, wi, None, groups=[0])
@@ -252,55 +274,82 @@ class Train:
     def _step_forked_dp(self, batch):
         """One process per GPU: the forked step of _step_forked with the
         reference's DataParallel global-batch semantics
-        (src/train_encoders_bert.py:146-169), cut at only three collectives:
+        (src/train_encoders_bert.py:146-169), cut at three collectives:
 
-          1. the text side's all-gather (after the frozen TextHeading);
+          1. the text side's all-gather (after the frozen TextHeading, with
+             the g' projection beside it);
           2. ONE all-gather of every rank's mid-step partials -- the word<->
              region CE's column (max, sum exp) partials, the sentence / global
              losses' column partials and both identity heads' NLL sums -- packed
              in one buffer by the three losses' first stages (kernels.ce_partials,
              sent_global_dist_parts, identity_heads_parts); their second stages
              read the gathered rows in place (any row stride);
-          3. one flat all-reduce of every trained gradient, then the optimiser.
+          3. one flat all-reduce of every trained gradient, then ONE optimiser
+             launch.  (Splitting it -- the classifiers' bucket on a side stream
+             beside IMIM's backward -- cuts the backward into two graphs, and
+             the g' branch's backward chain, ~150 us beside the word<->region
+             backward alone, then bounds the first: +0.12 ms per rank step in
+             the simulate-world-8 configs[2] step, more than the bucket's
+             all-reduce it would hide.)
 
-        Between 1 and 2 the main stream runs IMIM and the word<->region
-        forward while the side stream runs the g' projection and the
-        sentence / global and identity-head forwards; between 2 and 3 the main
-        stream runs the word<->region and IMIM backward while the side runs
-        the g' branch's losses and backward.  (The linear DP step cuts at six
-        collectives and a join and runs the g' branch in series.)"""
+        The g' projection runs beside TextHeading; after 1, IMIM's forward
+        beside both identity heads' forwards on the side stream (they need
+        only this rank's rows), then the word<->region forward beside the
+        sentence / global partials; between 2 and 3 the main stream runs the word<->region
+        and IMIM backward while the side runs the g' branch's losses and
+        backward.  (Round 5 ran TextHeading, the text gather and IMIM in
+        series; the linear DP step cuts at six collectives and a join and runs
+        the g' branch in series.)"""
         args, ctx = self.args, self.ctx
         main, side = torch.cuda.current_stream(), self._side
+        g = batch[0]
+        b = g.shape[0]
+        ctx.set_batch(b)
+        args.dist = ctx
+        dev = g.device
+        self.optimizer.zero_grad(set_to_none=True)
+        # the g' projection needs only this rank's rows: beside TextHeading
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            img_features = self.image_head.global_features(g)
         if len(batch) == 4:
             g, local, hidden, class_ids = batch
             with torch.no_grad():
                 words, sent = self.text_head(hidden, None)
         else:
             g, local, words, sent, class_ids = batch
-        b = g.shape[0]
-        ctx.set_batch(b)
-        args.dist = ctx
-        words_g, sent_g, cls_g = self._gather_text(words, sent, class_ids)      # 1
-        n_c = words_g.shape[0]
-        dev = g.device
-        self.optimizer.zero_grad(set_to_none=True)
+        main.wait_stream(side)
+        # (TGFR_TEXT_ASYNC=1: the gather on a side stream beside IMIM's
+        # forward -- its join is one more graph boundary, which cost more than
+        # a 7 MB gather takes: simulate-world-8 configs[2] 1.290-1.312 against
+        # 1.257-1.267 ms per rank step, three interleaved rounds)
+        if os.environ.get("TGFR_TEXT_ASYNC", "0") == "1":
+            finish_text = self._gather_text_async(words, sent, class_ids)        # 1
+        else:
+            text_g = self._gather_text(words, sent, class_ids)
+
+            def finish_text():
+                return text_g
         wi, lc = float(args.lambda_id), float(args.lambda_clip)
         gamma3, eps, temp3 = args.TRAIN.SMOOTH.GAMMA3, 1e-8, 10.0
         row_offset, n_global = ctx.row_offset, ctx.n_global
+        n_c = b * ctx.world
         # this rank's mid-step partials: [words CE 2 n_c | sent/global | NLL sums 2]
         n_sg = K.sent_global_dist_cols(b, n_c)
         buf = torch.empty(2 * n_c + n_sg + 2, dtype=torch.float32, device=dev)
-        cls_t = _class_tensor(cls_g, dev)
-        start = torch.cuda.Event()
-        start.record(main)
+        side.wait_stream(main)
         words_features = self.image_head.imim(local)
-        side.wait_event(start)
         with torch.cuda.stream(side):
-            img_features = self.image_head.global_features(g)
-            sg = K.sent_global_dist_parts(img_features, sent_g, cls_t, gamma3, temp3, eps,
-                                          row_offset, buf[2 * n_c:2 * n_c + n_sg])
             ih = K.identity_heads_parts(sent, self.text_cls, img_features, self.image_cls,
                                         class_ids, self.ident_loss.gamma, buf[2 * n_c + n_sg:])
+        main.wait_stream(side)
+        words_g, sent_g, cls_g = finish_text()
+        assert words_g.shape[0] == n_c
+        cls_t = _class_tensor(cls_g, dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            sg = K.sent_global_dist_parts(img_features, sent_g, cls_t, gamma3, temp3, eps,
+                                          row_offset, buf[2 * n_c:2 * n_c + n_sg])
         logits = words_logits_bert(words_features, words_g, args)
         row_lse = K.ce_partials(logits, buf[:2 * n_c].view(2, n_c))
         main.wait_stream(side)
@@ -326,6 +375,31 @@ class Train:
         ctx.reduce_grads(self.params)                                             # 3
         self.optimizer.step()
         return out
+
+    def _gather_text_async(self, words, sent, class_ids):
+        """_gather_text as gather_text_async: returns finish() -> (words,
+        sent, class ids) of the global batch."""
+        ctx = self.ctx
+        words_bt = words.transpose(1, 2)
+        f16 = self.args.precision == "fp16"
+        pre = K.attached_rows(words_bt, f16, scale=K.LOG2E) \
+            if K.wr_rows_path(self.args.precision, words.shape[2],
+                              self.args.en_type == "BERT") else None
+        n_words = words.shape[2]
+        if pre is not None:
+            rows, norms = pre
+            fin = ctx.gather_text_async(rows, norms, sent, class_ids)
+
+            def finish():
+                rows_g, norms_g, sent_g, cls_g = fin()
+                return K.rows_only_words(rows_g, norms_g, n_words, f16), sent_g, cls_g
+            return finish
+        fin = ctx.gather_text_async(words_bt, sent, class_ids)
+
+        def finish():
+            words_g, sent_g, cls_g = fin()
+            return words_g.transpose(1, 2), sent_g, cls_g
+        return finish
 
     def _report(self, w0, w1, s0, s1, cl, tid, iid, lc, wi):
         """The logged terms (and the objective) in one launch."""

@@ -1,6 +1,47 @@
-O=gpurun_out/r6a
+# round-6 GPU steps (run from the repo root on a GPU box): STEP selects
+O=gpurun_out/${R:-r6}
 mkdir -p $O
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_words.py tests/test_gpu_step_parity.py -m gpu -v -s --timeout 200 --timeout-method thread -k "fp16 or captured or seeded or reduced" > $O/words.log 2>&1
-rc=$?; echo "tests rc=$rc: $(tail -1 $O/words.log)"; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-timeout -k 10 300 python3 -u bench.py --no-cpu > $O/bench.log 2>&1 || exit 12
-echo "bench: $(tail -1 $O/bench.log | cut -c1-400)"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+case "${STEP:-trace}" in
+trace)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench \
+    -- python3 bench.py --steps 20 --warmup 5 --no-cpu --alt-precision "" > $O/trace.log 2>&1 || exit 12
+  tail -1 $O/trace.log | cut -c1-200
+  ;;
+envab)
+  # interleaved A/B of environment settings: VARS="A=1 A=2 ..."
+  for i in $(seq 1 ${ROUNDS:-3}); do
+    for e in ${VARS}; do
+      env $e timeout -k 10 180 python3 -u bench.py --no-cpu --alt-precision "" ${BENCH_ARGS} > $O/bench_${e}_$i.log 2>&1 || exit 12
+      echo "$e round $i: $(grep -o '"ms_per_step": [0-9.]*' $O/bench_${e}_$i.log | head -1)"
+    done
+  done
+  ;;
+esac
+case "${STEP}" in
+tracevars)
+  for e in ${VARS}; do
+    env $e timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace_$e -o bench \
+      -- python3 bench.py --steps 10 --warmup 3 --no-cpu --alt-precision "" > $O/trace_$e.log 2>&1 || exit 12
+    echo "$e: $(grep -o '"ms_per_step": [0-9.]*' $O/trace_$e.log | head -1)"
+  done
+  ;;
+esac
+case "${STEP}" in
+dp)
+  timeout -k 10 900 python3 -u -m pytest tests/test_gpu_dp.py tests/test_gpu_train.py -m gpu -v -s --timeout 600 --timeout-method thread > $O/dp.log 2>&1
+  rc=$?; echo "dp tests rc=$rc: $(tail -1 $O/dp.log)"; [ $rc -le 1 ] || exit $rc
+  timeout -k 10 240 python3 -u bench.py --simulate-world 8 --no-cpu --alt-precision "" > $O/sim8_cfg3.log 2>&1 || exit 22
+  echo "sim8 cfg3: $(grep -o '"ms_per_step": [0-9.]*' $O/sim8_cfg3.log)"
+  ;;
+esac
+case "${STEP}" in
+dp2)
+  timeout -k 10 300 python3 -u -m pytest tests/test_gpu_dp.py -m gpu -v -s --timeout 600 --timeout-method thread -k "fp32-0-2" > $O/dp.log 2>&1
+  echo "dp rc=$?: $(tail -1 $O/dp.log)"
+  for i in 1 2 3; do for e in TGFR_TEXT_ASYNC=1 TGFR_TEXT_ASYNC=0; do
+    env $e timeout -k 10 240 python3 -u bench.py --simulate-world 8 --no-cpu --alt-precision "" > $O/sim8_${e}_$i.log 2>&1 || exit 22
+    echo "$e $i: $(grep -o '"ms_per_step": [0-9.]*' $O/sim8_${e}_$i.log)"
+  done; done
+  ;;
+esac

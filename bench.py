@@ -106,6 +106,19 @@ def config_key(args, world):
     return f"b{args.batch}_w{args.words}_{args.precision}_n{world}"
 
 
+def committed_entry(kernel, key):
+    """The newest round's committed profile entry (profiles/rNN/pmc.json,
+    tools/summarize_profile.py) of `kernel` for THIS configuration, or {}."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                          "profiles", "r*", "pmc.json")))
+    for f in reversed(files):
+        entry = json.load(open(f)).get("configs", {}).get(key, {}).get("kernels", {}).get(kernel)
+        if entry is not None:
+            return entry
+    return {}
+
+
 def pmc_traffic(kernel, key):
     """HBM bytes per launch of `kernel` measured for THIS configuration `key`
     (config_key) by the newest round's committed PMC passes
@@ -122,6 +135,17 @@ def pmc_traffic(kernel, key):
         if entry is not None:
             return entry.get("hbm_bytes_per_launch")
     return None
+
+
+def rocprof_fracs(flop, entry):
+    """Peak fractions of a word<->region entry from its committed rocprof
+    durations (isolated re-launch burst, in-step graph replay)."""
+    out = {}
+    for k in ("isolated", "in_step"):
+        us = entry.get(f"avg_us_{k}")
+        out[f"frac_rocprof_{k}"] = None if not us else round(
+            flop / (us * 1e-6) / 1e12 / PEAK_BF16_TFLOPS, 4)
+    return out
 
 
 def host_cores():
@@ -331,12 +355,15 @@ def main():
                 "avg_launch_ms": round(dom_ms, 4),
                 "flop_per_launch": flops[dominant],
                 "timing": "HIP events around 20 back-to-back re-launches of the call "
-                          "(the isolated-launch figure; the in-step average under the "
-                          "side stream is the rocprof summary in profiles/)",
+                          "(the isolated-launch figure); frac_rocprof_* from the committed "
+                          "rocprof trace of this configuration (profiles/rNN/pmc.json): the "
+                          "same burst, and the graph-replayed step beside the side stream",
+                **rocprof_fracs(flops[dominant], committed_entry(dominant, config_key(args, n))),
                 # the other word<->region entry point, timed the same way
                 "others": {k: {"avg_launch_ms": round(v, 4),
                                "achieved": round(flops[k] / (v * 1e-3) / 1e12, 2),
                                "frac": round(flops[k] / (v * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+                               **rocprof_fracs(flops[k], committed_entry(k, config_key(args, n))),
                                "traffic": pmc_traffic(k, config_key(args, n))}
                            for k, v in ktimer.replayed.items() if k in flops and k != dominant}}
 

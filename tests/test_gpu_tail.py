@@ -282,3 +282,42 @@ def test_imim_fused_node(gpu, n, precision):
         assert err <= 1e-2, (na, err)
     torch.testing.assert_close(a.bn_img.running_mean, b.bn_img.running_mean)
     torch.testing.assert_close(a.bn_img.running_var, b.bn_img.running_var)
+
+
+@pytest.mark.parametrize("n,hw", [(64, 196), (5, 196), (3, 144)])
+def test_bn_qkv_fused(gpu, n, hw):
+    """tgfr_bn_qkv_bf16 (BN apply + the packed q/k/v projection in one launch,
+    reading the NCHW map) against the two-pass path it replaces
+    (tgfr_bn_fwd_cl_bf16's normalised map -> tgfr_linear_bf16io): the same
+    bf16 xhat bit for bit, px within one bf16 rounding of it (the fp32 sums
+    run in another order), and both against an fp32 torch reference of
+    bn -> 1x1 projection on the same folded weights."""
+    from text_guided_face_recognition_amd._hip import call, ptr, stream
+    torch.manual_seed(hw + n)
+    c, o = 256, 768
+    x = (torch.randn(n, c, hw, device=gpu) * 1.7 + 0.4).contiguous()
+    wf = torch.randn(o, c, device=gpu) / 16
+    bf = torch.randn(o, device=gpu)
+    mean = torch.empty(c, device=gpu)
+    rstd = torch.empty(c, device=gpu)
+    xh2 = torch.empty(n, hw, c, dtype=torch.int16, device=gpu)
+    call("tgfr_bn_fwd_cl_bf16", ptr(x), n, c, hw, 1e-5, 0.1, 1, None, None, None, ptr(mean),
+         ptr(rstd), ptr(xh2), stream())
+    y2 = torch.empty(n * hw, o, dtype=torch.int16, device=gpu)
+    call("tgfr_linear_bf16io", ptr(xh2), c, n * hw, c, ptr(wf), c, ptr(bf), o, ptr(y2), o,
+         stream())
+    xh1 = torch.empty_like(xh2)
+    y1 = torch.empty_like(y2)
+    call("tgfr_bn_qkv_bf16", ptr(x), n, c, hw, ptr(mean), ptr(rstd), ptr(wf), ptr(bf), o, ptr(y1),
+         ptr(xh1), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(xh1, xh2)
+    bf16 = lambda t: t.view(torch.bfloat16).float()   # noqa: E731
+    p1, p2 = bf16(y1), bf16(y2)
+    ref = bf16(xh2).reshape(n * hw, c) @ wf.to(torch.bfloat16).float().t() + bf
+    scale = ref.abs().max().item()
+    e12 = (p1 - p2).abs().max().item() / scale
+    e1 = (p1 - ref).abs().max().item() / scale
+    print(f"bn_qkv n={n} hw={hw}: fused vs two-pass {e12:.2e}, vs fp32 {e1:.2e} of max")
+    assert e12 < 1e-2 and e1 < 1e-2
+    assert torch.isfinite(p1).all()

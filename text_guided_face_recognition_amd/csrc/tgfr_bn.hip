@@ -24,82 +24,14 @@ using namespace tgfr;
 
 namespace {
 
-// grid C; 256 threads.  Up to 256 * BN_REG values per channel (B = 64 at
-// 14 x 14: 49 per thread) are loaded once into registers; larger maps take the
-// two-pass loop (thread t owns positions hw = t, t+256, ... of every sample).
-constexpr int BN_REG = 64;
+// grid C; 256 threads (bn_stats_block, tgfr_fold.h)
 __global__ __launch_bounds__(256) void bn_stats_kernel(
     const float* __restrict__ x, int N, int C, int HW, float eps, float momentum, int training,
     float* __restrict__ running_mean, float* __restrict__ running_var,
     long long* __restrict__ nbt, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
   __shared__ float red[4];
-  const int c = blockIdx.x, tid = threadIdx.x, wid = tid / WAVE, lane = tid % WAVE;
-  if (!training) {
-    if (tid == 0) {
-      mean_out[c] = running_mean[c];
-      rstd_out[c] = rsqrtf(running_var[c] + eps);
-    }
-    return;
-  }
-  const long long cnt = (long long)N * HW;
-  const float* xc = x + (long long)c * HW;
-  const long long sn = (long long)C * HW;
-  float s = 0.f, m2 = 0.f, mean;
-  if (cnt <= 256 * BN_REG) {
-    // the channel's N x HW values, flattened over all 256 threads, loaded once
-    // with every load in flight (one HBM round trip; clamped indices, so no
-    // branch -- and no wait -- per load), both moments from registers
-    const int last = (int)cnt - 1;
-    float v[BN_REG];
-#pragma unroll
-    for (int u = 0; u < BN_REG; ++u) {
-      const int e = min(tid + 256 * u, last), n = e / HW, hw = e - n * HW;
-      v[u] = xc[n * sn + hw];
-    }
-#pragma unroll
-    for (int u = 0; u < BN_REG; ++u) s += tid + 256 * u <= last ? v[u] : 0.f;
-    s = wave_sum(s);
-    if (lane == 0) red[wid] = s;
-    __syncthreads();
-    mean = (red[0] + red[1] + red[2] + red[3]) / (float)cnt;
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < BN_REG; ++u) {
-      const float d = tid + 256 * u < cnt ? v[u] - mean : 0.f;
-      m2 += d * d;
-    }
-  } else {
-    for (int hw = tid; hw < HW; hw += 256) {
-#pragma unroll 8
-      for (int n = 0; n < N; ++n) s += xc[n * sn + hw];
-    }
-    s = wave_sum(s);
-    if (lane == 0) red[wid] = s;
-    __syncthreads();
-    mean = (red[0] + red[1] + red[2] + red[3]) / (float)cnt;
-    __syncthreads();
-    for (int hw = tid; hw < HW; hw += 256) {
-#pragma unroll 8
-      for (int n = 0; n < N; ++n) {
-        const float d = xc[n * sn + hw] - mean;
-        m2 += d * d;
-      }
-    }
-  }
-  m2 = wave_sum(m2);
-  if (lane == 0) red[wid] = m2;
-  __syncthreads();
-  if (tid == 0) {
-    const float var = (red[0] + red[1] + red[2] + red[3]) / (float)cnt;
-    mean_out[c] = mean;
-    rstd_out[c] = rsqrtf(var + eps);
-    if (running_mean) {
-      const float unbiased = cnt > 1 ? var * (float)cnt / (float)(cnt - 1) : var;
-      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
-    }
-    if (nbt && c == 0) nbt[0] += 1;
-  }
+  bn_stats_block(x, N, C, HW, eps, momentum, training, running_mean, running_var, nbt, mean_out,
+                 rstd_out, blockIdx.x, red);
 }
 
 // grid (ceil(C / BN_CT), N); 256 threads; LDS [BN_CT][HW + 1] floats.  OBF: y is
@@ -254,9 +186,199 @@ __global__ __launch_bounds__(256) void bn_unfold_kernel(
   }
 }
 
+// ------------------------------------------ BN apply + q/k/v projection ---
+// IMIM's bf16-mode front end in ONE launch (models/models.py:394 then
+// models/fusion_nets.py:97-109): xhat = (x - mean) rstd read straight from
+// the NCHW input map x [N][C = 256][HW] and
+//   px[n][hw][o] = bf16(sum_c xhat[n][c][hw] W'[o][c] + b'[o])
+// with the BN-folded weights W' / b' (tgfr_imim_pack / bn_fold), plus the
+// channels-last bf16 xhat [N][HW][256] the projection's weight gradient
+// reads -- no normalised-map pass (bn_norm_cl) and no staging GEMM ring.
+// Workgroup = (sample n, 128-column slice of O), 8 waves: wave = (32-column
+// tile, m-group of the sample's 32-row tiles {0-3} | {4-6}); the product is
+// formed transposed, px^T = W' xhat^T, so the weights are the MFMA's A
+// operand (their k-contiguous rows, loaded per chunk with the map and
+// converted to bf16 fragments) and xhat^T the B operand, read from an LDS image
+// [32 channels][224 positions] (the input's own layout) by
+// ds_read_b64_tr_b16.  K runs in 8 chunks of 32 channels: chunk k + 2's
+// global loads are in flight while chunk k is normalised into one of two LDS
+// images and multiplied (one barrier per chunk).  Each lane's accumulator
+// quad is 4 consecutive output columns of one position: 8-byte stores.  The
+// slices of one sample run on one XCD (xcd_remap), so the map is read from
+// HBM once and from L2 five more times; slice s writes xhat for the chunks
+// k = s (mod O / 128).
+constexpr int QKV_MP = 224;              // LDS image pitch (positions), 7 x 32
+constexpr int QKV_CK = 32;               // channels per chunk
+constexpr int QKV_IMG = QKV_CK * QKV_MP * 2;
+constexpr int QKV_MS = 2 * QKV_IMG;     // mean / rstd of the 256 channels (LDS)
+constexpr int QKV_LDS = QKV_MS + 2 * 256 * 4;
+constexpr int QKV_LOADS = 4;             // float4 loads per thread per chunk (<= 2048 / 512)
+
+__global__ __launch_bounds__(512) void bn_qkv_kernel(
+    const float* __restrict__ x, int HW, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ Wf, const float* __restrict__ bf,
+    int O, uint16_t* __restrict__ px, uint16_t* __restrict__ xhat) {
+  constexpr int C = 256, NCH = C / QKV_CK;
+  const int n_sl = O / 128;
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int nb = work / n_sl, sl = work % n_sl;
+  const int tid = threadIdx.x, lane = tid % WAVE;
+  const int wv = __builtin_amdgcn_readfirstlane(tid / WAVE);
+  const int wn = wv & 3, mg = wv >> 2;          // 32-column tile, m-group
+  const int mt0 = mg * 4, n_mt = mg ? (HW + 31) / 32 - 4 : min(4, (HW + 31) / 32);
+  const int n0 = sl * 128 + wn * 32;
+  const int lr = lane & 31, h = lane >> 5;
+  const int q4 = HW / 4;                        // float4 per channel row
+  const int items = QKV_CK * q4;                // float4 per chunk
+  const float* xs = x + (long long)nb * C * HW;
+
+  // chunk loads: item i -> channel i / q4, positions 4 (i % q4) .. + 3
+  // (clamped: a thread past the end repeats the last item)
+  // per chunk: the map's float4s and this wave's W' rows for the chunk's two
+  // k steps (fp32, 32 rows x 32 channels: L2-resident, shared by the
+  // sample workgroups of the slice), both issued two chunks ahead
+  const float* wr = Wf + (long long)(n0 + lr) * C + 8 * h;
+  float4 ld[2][QKV_LOADS], wl[2][4];
+  auto issue = [&](int ck, float4 (&dst)[QKV_LOADS], float4 (&wd)[4]) {
+#pragma unroll
+    for (int j = 0; j < QKV_LOADS; ++j) {
+      const int i = min(tid + 512 * j, items - 1);
+      const int c = ck * QKV_CK + i / q4, p = i % q4;
+      dst[j] = *(const float4*)(xs + (long long)c * HW + 4 * p);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wd[k] = *(const float4*)(wr + 32 * ck + 16 * (k >> 1) + 4 * (k & 1));
+  };
+  // the channels' statistics into LDS once (a global load per chunk would
+  // be the youngest memory op there, and its wait would drain the prefetch)
+  // (loaded first, stored after the first chunks' loads are issued, so the
+  // wait for them does not hold those back)
+  const float mu0 = mean[min(tid, C - 1)], rs0 = rstd[min(tid, C - 1)];
+  issue(0, ld[0], wl[0]);
+  if (NCH > 1) issue(1, ld[1], wl[1]);
+  if (tid < C) {
+    lds_stf(QKV_MS + tid * 4, mu0);
+    lds_stf(QKV_MS + (C + tid) * 4, rs0);
+  }
+  auto wfrag = [](const float4& a, const float4& b) {
+    return as_bf8(make_uint4(pk_bf16(a.x, a.y), pk_bf16(a.z, a.w), pk_bf16(b.x, b.y),
+                             pk_bf16(b.z, b.w)));
+  };
+  float bias[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) bias[q] = bf[n0 + acc_row(q, h)];
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+  __syncthreads();                     // the statistics in LDS
+
+  // B fragment (xhat^T: column = position, 8 consecutive channels) of k step
+  // ksl (0, 1) of the chunk image at img, m tile mt: two transposing reads
+  const int g16 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  const uint32_t boff = ((8 * (g16 >> 1) + qq) * QKV_MP + 16 * (g16 & 1) + 4 * pp) * 2;
+  auto bfrag = [&](uint32_t img, int ksl, int mt) {
+    const uint32_t o = img + boff + (16 * ksl * QKV_MP + 32 * mt) * 2;
+    return join_tr(lds_tr4(o), lds_tr4(o + 4 * QKV_MP * 2));
+  };
+
+#pragma unroll
+  for (int ck = 0; ck < NCH; ++ck) {
+    const uint32_t img = (ck & 1) * QKV_IMG;
+    // normalise chunk ck into its image (rows = channels, 8-byte writes)
+    {
+      float4 (&src)[QKV_LOADS] = ld[ck & 1];
+#pragma unroll
+      for (int j = 0; j < QKV_LOADS; ++j) {
+        const int i = min(tid + 512 * j, items - 1);
+        const int cl = i / q4, p = i % q4, c = ck * QKV_CK + cl;
+        const float mu = lds_ldf(QKV_MS + c * 4), rs = lds_ldf(QKV_MS + (C + c) * 4);
+        const float4 v = src[j];
+        lds_st8(img + (cl * QKV_MP + 4 * p) * 2,
+                make_uint2(pk_bf16((v.x - mu) * rs, (v.y - mu) * rs),
+                           pk_bf16((v.z - mu) * rs, (v.w - mu) * rs)));
+      }
+    }
+    const bf16x8 wa0 = wfrag(wl[ck & 1][0], wl[ck & 1][1]);
+    const bf16x8 wa1 = wfrag(wl[ck & 1][2], wl[ck & 1][3]);
+    __syncthreads();
+    if (ck + 2 < NCH) issue(ck + 2, ld[ck & 1], wl[ck & 1]);
+#pragma unroll
+    for (int ksl = 0; ksl < 2; ++ksl)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (t < n_mt)
+          acc[t] = mfma_lp<MODE_BF16>(ksl ? wa1 : wa0, bfrag(img, ksl, mt0 + t), acc[t]);
+    // this slice's share of the channels-last xhat: positions x 8-channel groups
+    if (ck % n_sl == sl) {
+      for (int it = tid; it < HW * (QKV_CK / 8); it += 512) {
+        const int m = it % HW, cg = it / HW;
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint16_t a = *(LDS_AS uint16_t*)(lds_base() + img + ((8 * cg + 2 * k) * QKV_MP + m) * 2);
+          const uint16_t b = *(LDS_AS uint16_t*)(lds_base() + img + ((8 * cg + 2 * k + 1) * QKV_MP + m) * 2);
+          w[k] = pack2(a, b);
+        }
+        *(uint4*)(xhat + ((long long)nb * HW + m) * C + ck * QKV_CK + 8 * cg) =
+            make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
+  }
+  // epilogue: px[n][m][n0 + 8 g + 4 h .. + 3] = bf16(acc + b')
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t >= n_mt) continue;
+    const int m = (mt0 + t) * 32 + lr;
+    if (m >= HW) continue;
+    uint16_t* dst = px + ((long long)nb * HW + m) * O + n0 + 4 * h;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *(uint2*)(dst + 8 * g) =
+          make_uint2(pk_bf16(acc[t][4 * g] + bias[4 * g], acc[t][4 * g + 1] + bias[4 * g + 1]),
+                     pk_bf16(acc[t][4 * g + 2] + bias[4 * g + 2],
+                             acc[t][4 * g + 3] + bias[4 * g + 3]));
+  }
+}
+
+// BN batch statistics alone (bn_fwd_cl's first launch)
+static int bn_stats_launch(const float* x, int N, int C, int HW, float eps, float momentum,
+                           int training, float* running_mean, float* running_var,
+                           long long* nbt, float* mean, float* rstd, hipStream_t st) {
+  if (N <= 0 || C <= 0 || HW <= 0) return 1001;
+  if (!training && (!running_mean || !running_var)) return 1001;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(C), dim3(256), 0, st, x, N, C, HW, eps, momentum,
+                     training, running_mean, running_var, nbt, mean, rstd);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
+
+int tgfr_bn_stats(const float* x, int N, int C, int HW, float eps, float momentum, int training,
+                  float* running_mean, float* running_var, long long* nbt, float* mean,
+                  float* rstd, void* stream) {
+  return bn_stats_launch(x, N, C, HW, eps, momentum, training, running_mean, running_var, nbt,
+                         mean, rstd, (hipStream_t)stream);
+}
+
+int tgfr_bn_qkv_bf16(const float* x, int N, int C, int HW, const float* mean, const float* rstd,
+                     const float* Wf, const float* bf, int O, uint16_t* px, uint16_t* xhat,
+                     void* stream) {
+  if (!x || !mean || !rstd || !Wf || !bf || !px || !xhat || N <= 0) return 1001;
+  if (C != 256 || HW <= 128 || HW > QKV_MP || HW % 4 || O % 128 || O / 128 > 12 ||
+      QKV_CK * (HW / 4) > 512 * QKV_LOADS)
+    return 1001;
+  if (((uintptr_t)x & 15) || ((uintptr_t)Wf & 15) || ((uintptr_t)px & 7) || ((uintptr_t)xhat & 15))
+    return 1001;
+  const dim3 grid(N * (O / 128));
+  hipLaunchKernelGGL(bn_qkv_kernel, grid, dim3(512), QKV_LDS, (hipStream_t)stream, x, HW, mean,
+                     rstd, Wf, bf, O, px, xhat);
+  return (int)hipGetLastError();
+}
+
 
 int tgfr_bn_bwd_cl(const float* dxh, const float* xhat, const float* rstd, int N, int C, int HW,
                    int training, float* dx, void* stream) {

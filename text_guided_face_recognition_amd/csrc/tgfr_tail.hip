@@ -166,32 +166,58 @@ __global__ __launch_bounds__(256) void tail_pack_kernel(const float* __restrict_
 // fold bn_img into the packed q/k/v projection (one wave per row, as
 // bn_fold_kernel), the rest run tail_pack_kernel's elements (weights and the
 // LayerNorm affine maps).
-__global__ __launch_bounds__(256) void imim_pack_kernel(Parts P, int O, int C,
-                                                        const float* __restrict__ gamma,
-                                                        const float* __restrict__ beta,
-                                                        float* __restrict__ Wf,
-                                                        float* __restrict__ bf, int nf,
-                                                        const float* __restrict__ W1,
-                                                        const float* __restrict__ W2,
-                                                        const float* __restrict__ Wp,
-                                                        uint16_t* __restrict__ pk,
-                                                        const float* __restrict__ lnw,
-                                                        const float* __restrict__ lnb, int hw,
-                                                        float* __restrict__ aff) {
-  if ((int)blockIdx.x < nf) {
-    const int o = blockIdx.x * 4 + threadIdx.x / WAVE;
-    if (o < O) bn_fold_row(P, o, C, gamma, beta, Wf, bf, threadIdx.x % WAVE);
+struct ImimPackArgs {
+  Parts P;
+  int O, C;
+  const float *gamma, *beta;
+  float *Wf, *bf;
+  int nf;
+  const float *W1, *W2, *Wp;
+  uint16_t* pk;
+  const float *lnw, *lnb;
+  int hw;
+  float* aff;
+};
+__device__ __forceinline__ void imim_pack_block(const ImimPackArgs& A, int bid) {
+  if (bid < A.nf) {
+    const int o = bid * 4 + threadIdx.x / WAVE;
+    if (o < A.O) bn_fold_row(A.P, o, A.C, A.gamma, A.beta, A.Wf, A.bf, threadIdx.x % WAVE);
     return;
   }
-  const int e = (blockIdx.x - nf) * 256 + threadIdx.x;
+  const int e = (bid - A.nf) * 256 + threadIdx.x;
   if (e >= PACK_UNITS) {
-    const int f = e - PACK_UNITS, n = hw * TC;
+    const int f = e - PACK_UNITS, n = A.hw * TC;
     if (f >= 2 * n) return;
     const int j = f / n, r = f % n, p = r / TC, c = r % TC;
-    aff[f] = (j ? lnb : lnw)[(long long)c * hw + p];
+    A.aff[f] = (j ? A.lnb : A.lnw)[(long long)c * A.hw + p];
     return;
   }
-  pack_frag(W1, W2, Wp, pk, e);
+  pack_frag(A.W1, A.W2, A.Wp, A.pk, e);
+}
+__global__ __launch_bounds__(256) void imim_pack_kernel(ImimPackArgs A) {
+  imim_pack_block(A, blockIdx.x);
+}
+
+// The same with IMIM's BatchNorm batch statistics as its first C workgroups
+// (bn_stats_block): the whole per-step preparation of the head in ONE launch
+// (the fold does not depend on the statistics; tgfr_bn_qkv_bf16 reads both).
+struct BnStatsArgs {
+  const float* x;
+  int N, C, HW;
+  float eps, momentum;
+  int training;
+  float *running_mean, *running_var;
+  long long* nbt;
+  float *mean, *rstd;
+};
+__global__ __launch_bounds__(256) void imim_prep_kernel(BnStatsArgs S, ImimPackArgs A) {
+  __shared__ float red[4];
+  if ((int)blockIdx.x < S.C) {
+    bn_stats_block(S.x, S.N, S.C, S.HW, S.eps, S.momentum, S.training, S.running_mean,
+                   S.running_var, S.nbt, S.mean, S.rstd, blockIdx.x, red);
+    return;
+  }
+  imim_pack_block(A, blockIdx.x - S.C);
 }
 
 // ------------------------------------------------------------ forward ---
@@ -1082,9 +1108,34 @@ int tgfr_imim_pack(const float* const* Wqkv, const float* const* bqkv, int rows_
   const int O = 3 * rows_qkv, nf = (O + 3) / 4;
   const LnTailWs o = ln_tail_ws(rows, hw);
   const long long n = PACK_UNITS + 2 * o.E;
+  const ImimPackArgs A{P, O, C, gamma, beta, Wf, bf, nf, W1, W2, Wp, pk, lnw, lnb, hw, ws + o.aff};
   hipLaunchKernelGGL(imim_pack_kernel, dim3((unsigned)(nf + (n + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, P, O, C, gamma, beta, Wf, bf, nf, W1, W2, Wp, pk, lnw,
-                     lnb, hw, ws + o.aff);
+                     (hipStream_t)stream, A);
+  return (int)hipGetLastError();
+}
+
+int tgfr_imim_prep(const float* x, int N, int HW, float bn_eps, float momentum, int training,
+                   float* running_mean, float* running_var, long long* nbt, float* mean,
+                   float* rstd, const float* const* Wqkv, const float* const* bqkv, int rows_qkv,
+                   int C, const float* gamma, const float* beta, float* Wf, float* bf,
+                   const float* W1, const float* W2, const float* Wp, const float* lnw,
+                   const float* lnb, int rows, int hw, uint16_t* pk, float* ws, void* stream) {
+  if (!x || N <= 0 || HW <= 0 || !mean || !rstd || (!training && (!running_mean || !running_var)))
+    return 1001;
+  if (!Wqkv || !Wqkv[0] || !Wqkv[1] || !Wqkv[2] || rows_qkv <= 0 || C <= 0 || !gamma || !beta ||
+      !Wf || !bf || !W1 || !W2 || !Wp || !pk || !lnw || !lnb || !ws || !ln_tail_ok(rows, hw))
+    return 1001;
+  const Parts P{Wqkv[0], Wqkv[1], Wqkv[2],
+                bqkv ? bqkv[0] : nullptr, bqkv ? bqkv[1] : nullptr, bqkv ? bqkv[2] : nullptr,
+                rows_qkv};
+  const int O = 3 * rows_qkv, nf = (O + 3) / 4;
+  const LnTailWs o = ln_tail_ws(rows, hw);
+  const long long n = PACK_UNITS + 2 * o.E;
+  const ImimPackArgs A{P, O, C, gamma, beta, Wf, bf, nf, W1, W2, Wp, pk, lnw, lnb, hw, ws + o.aff};
+  const BnStatsArgs S{x, N, C, HW, bn_eps, momentum, training, running_mean, running_var, nbt,
+                      mean, rstd};
+  hipLaunchKernelGGL(imim_prep_kernel, dim3((unsigned)(C + nf + (n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, S, A);
   return (int)hipGetLastError();
 }
 

@@ -1311,6 +1311,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
   // softmax chunk c (0..31) of the tile in S (region tile j), E^T -> etb;
   // chunks 0-3 store the tile's scores for the backward (and, big, form each
   // region's max over the words first)
+  __amdgpu_buffer_rsrc_t sprs;     // the caption's stored-score records (set per caption)
   auto sm_chunk = [&](auto bigc, int c, int j, const f32x16& S, uint32_t etb, uint16_t* spt) {
     constexpr bool BIG = decltype(bigc)::value;
     if (c < 4) {
@@ -1318,7 +1319,8 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
         if (c == 0) rm = max3f(max3f(S[0], S[1], S[2]), max3f(S[3], S[4], S[5]), max3f(S[6], S[7], S[8]));
         if (c == 1) {
           rm = xhalf_max(max3f(max3f(rm, S[9], S[10]), max3f(S[11], S[12], S[13]), fmaxf(S[14], S[15])));
-          ((float*)(spt + 1024))[lr] = rm;     // (both halves: the same value)
+          // (both halves: the same value)
+          ((float*)(spt + 1024))[lr] = rm;
         }
       }
     } else if (c < 12) {
@@ -1338,7 +1340,13 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
       }
       spk[(q >> 1) & 3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(s0, s1));
       if ((q & 6) == 6)
-        *(uint4*)(spt + lane * 16 + (q & 8)) = make_uint4(spk[0], spk[1], spk[2], spk[3]);
+        // (a buffer store through the pair's records; tile 6 writes only the
+        // lanes of its 4 real regions -- 256 B of the 2-KB record, the rest is
+        // never read: the others' offset is out of range, so the store drops)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            (u32x4){spk[0], spk[1], spk[2], spk[3]}, sprs,
+            j == 6 && lr >= NREG - 6 * 32 ? 0x7ffffff0u : (uint32_t)((j * SP_REC + lane * 16 + (q & 8)) * 2),
+            0, 0);
     } else if (c == 12) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) ma[q] = p[q] + p[q + 8];
@@ -1390,6 +1398,7 @@ __global__ __launch_bounds__(256, 1) void wr_fwd_pipe_kernel(
     const float wn_next = Wnorm[(long long)inext * TPAD + lr];
     const long long pair = (long long)b * B_cap + i;
     uint16_t* sp = Sp + pair * (NRT * SP_REC);     // wave-uniform
+    sprs = uniform_rsrc(sp, NRT * SP_REC * 2);
     f32x16 initn;
 #pragma unroll
     for (int q = 0; q < 16; ++q) np[q] = 0.f;
@@ -2740,11 +2749,19 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
   // lane, and the region max m_r of a BIG_C caption (unused otherwise)
   const uint16_t* spb = Sp + ((long long)b * B_cap + c0) * (NRT * SP_REC) +
                         min(rt, NRT - 1) * SP_REC;
-  auto sp_load = [&](int k, uint4 (&dst)[2], float& m) {
+  // (tile 6: the forward stored only its 4 real regions' lanes; a padding
+  // region's lane reads a real one's scores -- finite, and its M rows only
+  // reach dR rows >= 196, which are never stored)
+  const int sl = rt == NRT - 1 ? (lane & 32) | (lr & 3) : lane;
+  auto sp_load = [&](int k, uint4 (&dst)[2]) {
     const uint16_t* rec = spb + (long long)min(k, K - 1) * (NRT * SP_REC);
-    dst[0] = ((const uint4*)(rec + lane * 16))[0];
-    dst[1] = ((const uint4*)(rec + lane * 16))[1];
-    m = ((const float*)(rec + 1024))[lr];
+    dst[0] = ((const uint4*)(rec + sl * 16))[0];
+    dst[1] = ((const uint4*)(rec + sl * 16))[1];
+  };
+  // the region maxima of a BIG_C caption (loaded only for one)
+  auto m_load = [&](int k) {
+    const uint16_t* rec = spb + (long long)min(k, K - 1) * (NRT * SP_REC);
+    return ((const float*)(rec + 1024))[sl & 31];
   };
   // token scalar k for the lane's tokens 8g + 4h + 0..3 (q = 4g .. 4g+3)
   auto scal = [&](uint32_t tb, int k, int g) {
@@ -2859,7 +2876,7 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
                    float mc, uint4 (&spn)[2], float& mn, int& bign) {
     constexpr int NCH = 64;            // SM chunks over the 16 MFMA slots
     ring_barrier<0>();                 // B1: X(t+1) landed everywhere
-    sp_load(t + 1, spn, mn);
+    sp_load(t + 1, spn);
     // caption t+1's variant flag: read now, made uniform at the stage's end
     // (its LDS latency off the stage head)
     const float bigv = lds_ldf(((t + 1) % BD_NB) * BD_BUF + B_XIMG + 6 * 128);
@@ -2884,6 +2901,7 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
       __builtin_amdgcn_sched_barrier(0);
     }
     bign = __builtin_amdgcn_readfirstlane((int)(bigv != 0.f));
+    mn = bign ? m_load(t + 1) : 0.f;
     // M(t-1) consumed by the partner M wave (it reads the slot right after
     // B1 of stage t, so this rarely waits), then M(t) into the slot
     if (cnt < t + 1) lds_wait_ge(BD_CNT + 4 * wid, t + 1);
@@ -2898,8 +2916,9 @@ __global__ __launch_bounds__(512) void wr_bwd_duo_kernel(
   float ma = 0.f, mq = 0.f;
   int big0 = 0, big1 = 0;
   if (live) {
-    sp_load(0, spa, ma);
+    sp_load(0, spa);
     big0 = big_of(0);
+    ma = big0 ? m_load(0) : 0.f;
     u32x4 rd[16];
 #pragma unroll
     for (int s = 0; s < 16; ++s) rd[s] = g1_read(s, 0);

@@ -7,6 +7,7 @@ in a HIP graph.  There is no CPU fallback: CPU tensors raise.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -1014,7 +1015,7 @@ def attention_core(px, py, cq, ck, cv, scale, mode="fp32"):
 
 # ------------------------------------------------- batch norm -> linear ---
 def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf16=False,
-                   xhat_bf16=False, fold3=None):
+                   xhat_bf16=False, fold3=None, prep=None):
     """BatchNorm2d (batch or running statistics) folded into the following
     1x1 projection; returns y [N, HW, O] (fp32, or bf16 with out_bf16) and
     stores what _bn_linear_bwd needs on ctx.  xhat_bf16 (with out_bf16: the
@@ -1037,12 +1038,20 @@ def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf
     if training and track and bn.momentum is None:
         raise NotImplementedError("cumulative-average BatchNorm (momentum=None)")
     use_batch = training or bn.running_mean is None
-    call("tgfr_bn_fwd_cl_bf16" if xhat_bf16 else "tgfr_bn_fwd_cl", ptr(x), n, c, hw, float(bn.eps),
-         float(bn.momentum or 0.0), int(use_batch),
-         ptr(bn.running_mean) if (track or not use_batch) else None,
-         ptr(bn.running_var) if (track or not use_batch) else None,
-         ptr(bn.num_batches_tracked) if track else None, ptr(mean), ptr(rstd), ptr(xhat),
-         _hip.stream())
+    # the bf16 q/k/v path normalises inside the projection launch
+    # (tgfr_bn_qkv_bf16): only the statistics here
+    fused = (xhat_bf16 and isinstance(weight, tuple) and c == 256 and 128 < hw <= 224 and
+             hw % 4 == 0 and o % 128 == 0 and os.environ.get("TGFR_BN_QKV", "1") == "1")
+    stats = (ptr(x), n, c, hw, float(bn.eps), float(bn.momentum or 0.0), int(use_batch),
+             ptr(bn.running_mean) if (track or not use_batch) else None,
+             ptr(bn.running_var) if (track or not use_batch) else None,
+             ptr(bn.num_batches_tracked) if track else None, ptr(mean), ptr(rstd))
+    # prep (ImimFused): the statistics launched together with the weight
+    # preparation (tgfr_imim_prep), one launch for both
+    prep = prep if fused and isinstance(weight, tuple) else None
+    if prep is None:
+        call("tgfr_bn_stats" if fused else "tgfr_bn_fwd_cl_bf16" if xhat_bf16 else
+             "tgfr_bn_fwd_cl", *stats, *(() if fused else (ptr(xhat),)), _hip.stream())
     g = gamma.float().contiguous()
     bf = torch.empty(o, dtype=torch.float32, device=dev)
     if isinstance(weight, tuple):
@@ -1053,7 +1062,9 @@ def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf
         wf = torch.empty(o, c, dtype=torch.float32, device=dev)
         wp = (ctypes.c_void_p * 3)(*[ptr(t) for t in w2])
         bp = (ctypes.c_void_p * 3)(*[ptr(t) for t in b2])
-        if fold3 is not None:
+        if prep is not None:
+            prep(stats, wp, bp, rows, c, g, beta.float().contiguous(), wf, bf)
+        elif fold3 is not None:
             fold3(wp, bp, rows, c, g, beta.float().contiguous(), wf, bf)
         else:
             call("tgfr_bn_fold3", ctypes.addressof(wp), ctypes.addressof(bp), rows, c, ptr(g),
@@ -1064,7 +1075,11 @@ def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf
         call("tgfr_bn_fold", ptr(w2), ptr(None if bias is None else bias.float().contiguous()),
              o, c, ptr(g), ptr(beta.float().contiguous()), ptr(wf), ptr(bf), _hip.stream())
     rows = n * hw
-    if out_bf16:
+    if fused:
+        y = torch.empty(rows, o, dtype=torch.int16, device=dev)
+        call("tgfr_bn_qkv_bf16", ptr(x), n, c, hw, ptr(mean), ptr(rstd), ptr(wf), ptr(bf), o,
+             ptr(y), ptr(xhat), _hip.stream())
+    elif out_bf16:
         y = torch.empty(rows, o, dtype=torch.int16, device=dev)
         call("tgfr_linear_bf16io" if xhat_bf16 else "tgfr_linear_bf16out", ptr(xhat), c, rows, c,
              ptr(wf), c, ptr(bf), o, ptr(y), o, _hip.stream())
@@ -1488,8 +1503,15 @@ class ImimFused(torch.autograd.Function):
                  ptr(g), ptr(bt), ptr(wf), ptr(bf), *[ptr(t) for t in tw], rows, hw, ptr(pk),
                  ptr(ws), _hip.stream())
 
+        def prep(stats, wptr, bptr, qrows, cc, g, bt, wf, bf):
+            x_, n_, c_, hw_, *rest = stats
+            call("tgfr_imim_prep", x_, n_, hw_, *rest, ctypes.addressof(wptr),
+                 ctypes.addressof(bptr), qrows, cc, ptr(g), ptr(bt), ptr(wf), ptr(bf),
+                 *[ptr(t) for t in tw], rows, hw, ptr(pk), ptr(ws), _hip.stream())
+
         px = _bn_linear_fwd(ctx, x, gamma, beta, (wk, wq, wv), (bk, bq, bv), bn, training,
-                            "bf16", out_bf16=True, xhat_bf16=True, fold3=fold3)
+                            "bf16", out_bf16=True, xhat_bf16=True, fold3=fold3,
+                            prep=prep if os.environ.get("TGFR_IMIM_PREP", "1") == "1" else None)
         o = torch.empty(nb, hw, _TAIL_C, dtype=torch.float32, device=dev)
         lse = torch.empty(rows, dtype=torch.float32, device=dev)
         # (the attention forward also leaves the LayerNorm's tile moments in ws)

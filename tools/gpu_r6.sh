@@ -45,3 +45,27 @@ dp2)
   done; done
   ;;
 esac
+case "${STEP}" in
+qkv)
+  timeout -k 10 400 python3 -u -m pytest tests/test_gpu_tail.py tests/test_gpu_step_parity.py tests/test_gpu_modules.py tests/test_gpu_words.py -m gpu -v -s --timeout 200 --timeout-method thread -k "bn_qkv or imim or reduced or heading or image or bounded or seeded" > $O/qkv.log 2>&1
+  rc=$?; echo "tests rc=$rc: $(tail -1 $O/qkv.log)"; [ $rc -le 1 ] || exit $rc
+  for i in 1 2 3; do for e in TGFR_BN_QKV=1 TGFR_BN_QKV=0; do
+    env $e timeout -k 10 180 python3 -u bench.py --no-cpu --alt-precision "" > $O/bench_${e}_$i.log 2>&1 || exit 22
+    echo "$e $i: $(grep -o '"ms_per_step": [0-9.]*' $O/bench_${e}_$i.log)"
+  done; done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench \
+    -- python3 bench.py --steps 20 --warmup 5 --no-cpu --alt-precision "" > $O/trace.log 2>&1 || exit 12
+  ;;
+esac
+case "${STEP}" in
+qkv2)
+  timeout -k 10 400 python3 -u -m pytest tests/test_gpu_tail.py tests/test_gpu_step_parity.py tests/test_gpu_modules.py -m gpu -v -s --timeout 200 --timeout-method thread -k "bn_qkv or imim or reduced or heading or image" > $O/qkv.log 2>&1
+  rc=$?; echo "tests rc=$rc: $(tail -1 $O/qkv.log)"; [ $rc -le 1 ] || exit $rc
+  for i in 1 2 3; do for e in "TGFR_BN_QKV=1 TGFR_IMIM_PREP=1" "TGFR_BN_QKV=1 TGFR_IMIM_PREP=0" "TGFR_BN_QKV=0 TGFR_IMIM_PREP=0"; do
+    t=$(echo $e | tr -d ' =_'); env $e timeout -k 10 180 python3 -u bench.py --no-cpu --alt-precision "" > $O/bench_${t}_$i.log 2>&1 || exit 22
+    echo "$e $i: $(grep -o '"ms_per_step": [0-9.]*' $O/bench_${t}_$i.log)"
+  done; done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench \
+    -- python3 bench.py --steps 20 --warmup 5 --no-cpu --alt-precision "" > $O/trace.log 2>&1 || exit 12
+  ;;
+esac

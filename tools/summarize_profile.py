@@ -50,7 +50,41 @@ def read_pmc(path):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
-def main(src, dst, key):
+def entry_timings(trace_csv, names, steps):
+    """Per-call durations of a C-ABI entry whose launches are the kernels
+    `names` (base names, one launch each per call) from the kernel trace:
+    (isolated, in_step) averages in us.  isolated = the longest run of
+    back-to-back calls with nothing else dispatched between them (bench.py's
+    HIP-event re-launch burst, _hip.KernelTimer); in_step = the last `steps`
+    calls (the timed graph replays, beside the other stream's kernels).  A
+    call's duration = first kernel's start .. last kernel's end."""
+    rows = list(csv.DictReader(open(trace_csv)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    calls, i, seq = [], 0, list(names)
+    while i < len(rows):
+        if base(rows[i]["Kernel_Name"]) == seq[0] and i + len(seq) <= len(rows) and all(
+                base(rows[i + j]["Kernel_Name"]) == seq[j] for j in range(len(seq))):
+            calls.append((i, int(rows[i]["Start_Timestamp"]),
+                          int(rows[i + len(seq) - 1]["End_Timestamp"])))
+            i += len(seq)
+        else:
+            i += 1
+    if not calls:
+        return None, None
+    runs, cur = [], [calls[0]]
+    for c in calls[1:]:
+        if c[0] == cur[-1][0] + len(seq):
+            cur.append(c)
+        else:
+            runs.append(cur)
+            cur = [c]
+    runs.append(cur)
+    burst = max(runs, key=len)
+    avg = lambda cs: sum(e - s for _, s, e in cs) / len(cs) / 1e3  # noqa: E731
+    return round(avg(burst), 2), round(avg(calls[-steps:]), 2)
+
+
+def main(src, dst, key, steps=20):
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "bench_kernel_stats.csv"))))
     fetch = read_pmc(os.path.join(src, "fetch", "bench_counter_collection.csv"))
     write = read_pmc(os.path.join(src, "write", "bench_counter_collection.csv"))
@@ -79,8 +113,11 @@ def main(src, dst, key):
     by_base = collections.defaultdict(list)
     for k in kernels:
         by_base[base(k)].append(k)
-    abi_lines = ["", "C-ABI entry points (sum of their kernels per call):", "",
-                 "| entry | kernels | avg us | HBM MB per call |", "|---|---|---|---|"]
+    abi_lines = ["", "C-ABI entry points (sum of their kernels' averages per call; and per "
+                 "call from the trace: the isolated back-to-back re-launch burst bench.py times "
+                 "with HIP events, and the last 20 graph-replayed steps):", "",
+                 "| entry | kernels | avg us | isolated us | in-step us | HBM MB per call |",
+                 "|---|---|---|---|---|---|"]
     for abi, sets in ABI_KERNELS.items():
         for names in sets:
             if all(n in by_base for n in names):
@@ -88,9 +125,13 @@ def main(src, dst, key):
                 us = sum(kernels[k]["avg_us"] for k in ks)
                 hbm = [kernels[k]["hbm_bytes_per_launch"] for k in ks]
                 tot = None if None in hbm else sum(hbm)
+                iso, step = entry_timings(os.path.join(src, "trace", "bench_kernel_trace.csv"),
+                                          names, steps)
                 kernels[abi] = {"kernels": ks, "avg_us": round(us, 2),
+                                "avg_us_isolated": iso, "avg_us_in_step": step,
                                 "hbm_bytes_per_launch": tot}
                 abi_lines.append(f"| `{abi}` | {' + '.join(base(k) for k in ks)} | {us:.1f} | "
+                                 f"{iso} | {step} | "
                                  f"{'-' if tot is None else f'{tot / 1e6:.1f}'} |")
                 break
     lines += abi_lines

@@ -488,13 +488,15 @@ int tgfr_imim_pack(const float* const* Wqkv, const float* const* bqkv, int rows_
 /* tgfr_imim_pack with IMIM's BatchNorm batch statistics (tgfr_bn_stats of
  * x [N][C][HW]; eps, momentum, training and the running buffers as there) as
  * the same launch's first C workgroups (ABI 600): the head's whole per-step
- * preparation before tgfr_bn_qkv_bf16 in one launch. */
+ * preparation before tgfr_bn_qkv_bf16 in one launch; Wfb (nullable) also
+ * receives the folded q/k/v weights in bf16 [O][C]. */
 int tgfr_imim_prep(const float* x, int N, int HW, float bn_eps, float momentum, int training,
                    float* running_mean, float* running_var, long long* nbt, float* mean,
                    float* rstd, const float* const* Wqkv, const float* const* bqkv, int rows_qkv,
-                   int C, const float* gamma, const float* beta, float* Wf, float* bf,
-                   const float* W1, const float* W2, const float* Wp, const float* lnw,
-                   const float* lnb, int rows, int hw, uint16_t* pk, float* ws, void* stream);
+                   int C, const float* gamma, const float* beta, float* Wf, uint16_t* Wfb,
+                   float* bf, const float* W1, const float* W2, const float* Wp,
+                   const float* lnw, const float* lnb, int rows, int hw, uint16_t* pk, float* ws,
+                   void* stream);
 int tgfr_ln_tail_bwd_att(const float* dR, const float* R, const float* inv, int rows, float eps,
                          const uint16_t* pk, const uint16_t* H1b, const uint16_t* H2b,
                          const float* X, int hw, float* ws, float* dZ, uint16_t* dPb,
@@ -577,13 +579,13 @@ int tgfr_bn_stats(const float* x, int N, int C, int HW, float eps, float momentu
 /* IMIM's bf16 front end in one launch (ABI 600; models/models.py:394,
  * models/fusion_nets.py:97-109): px [N][HW][O] bf16 = bf16((x - mean) rstd)
  * W'^T + b' straight from the NCHW map x [N][C][HW] with the BN-folded
- * weights Wf [O][C] / bf [O] (tgfr_bn_fold3 / tgfr_imim_pack), and the
+ * weights in bf16, Wfb [O][C] (tgfr_imim_prep), and bf [O], and the
  * channels-last bf16 xhat [N][HW][C] for the weight gradient.  Replaces
  * tgfr_bn_fwd_cl_bf16's normalisation pass + tgfr_linear_bf16io.  C = 256,
- * 128 < HW <= 224, HW % 4 == 0, O % 128 == 0, O <= 1536; x, Wf, xhat 16-B
+ * 128 < HW <= 224, HW % 4 == 0, O % 256 == 0, O <= 2048; x, Wfb, xhat 16-B
  * aligned, px 8-B aligned. */
 int tgfr_bn_qkv_bf16(const float* x, int N, int C, int HW, const float* mean, const float* rstd,
-                     const float* Wf, const float* bf, int O, uint16_t* px, uint16_t* xhat,
+                     const uint16_t* Wfb, const float* bf, int O, uint16_t* px, uint16_t* xhat,
                      void* stream);
 /* BatchNorm2d input gradient: dx [N][C][HW] from the channels-last gradient
  * of xhat, dxh [N][HW][C], xhat and rstd of tgfr_bn_fwd_cl; training = batch

@@ -124,7 +124,7 @@ SIGNATURES = {
     "tgfr_bn_fwd_cl_bf16": [P, I, I, I, F, F, I, P, P, P, P, P, P, P],
     "tgfr_bn_stats": [P, I, I, I, F, F, I, P, P, P, P, P, P],
     "tgfr_imim_prep": [P, I, I, F, F, I, P, P, P, P, P, P, P, I, I, P, P, P, P, P, P, P, P, P,
-                       I, I, P, P, P],
+                       P, I, I, P, P, P],
     "tgfr_bn_qkv_bf16": [P, I, I, I, P, P, P, P, I, P, P, P],
     "tgfr_linear_bf16io": [P, L, I, I, P, L, P, I, P, L, P],
     "tgfr_tail_pack_ln": [P, P, P, P, P, I, I, P, P, P],

@@ -41,11 +41,12 @@ struct Parts {
 // columns, not one per 64.  Indices are clamped, not branched on (a branch per
 // access serialises them): past the end a lane loads and stores column C - 1
 // again -- the same value to the same word.
+// (Wfb, nullable: the folded row also as bf16, the operand tgfr_bn_qkv_bf16 reads)
 __device__ __forceinline__ void bn_fold_row(const Parts P, int o, int C,
                                             const float* __restrict__ gamma,
                                             const float* __restrict__ beta,
                                             float* __restrict__ Wf, float* __restrict__ bf,
-                                            int lane) {
+                                            int lane, uint16_t* __restrict__ Wfb = nullptr) {
   constexpr int U = 8;
   const float* wr = P.row(o, C);
   float acc = 0.f;
@@ -62,6 +63,7 @@ __device__ __forceinline__ void bn_fold_row(const Parts P, int o, int C,
     for (int u = 0; u < U; ++u) {
       const int c = c0 + u * WAVE + lane;
       Wf[(long long)o * C + min(c, C - 1)] = w[u] * g[u];
+      if (Wfb) Wfb[(long long)o * C + min(c, C - 1)] = bf_bits(w[u] * g[u]);
       acc += c < C ? w[u] * b[u] : 0.f;
     }
   }

@@ -171,6 +171,7 @@ struct ImimPackArgs {
   int O, C;
   const float *gamma, *beta;
   float *Wf, *bf;
+  uint16_t* Wfb;       // nullable: the folded q/k/v weights also in bf16
   int nf;
   const float *W1, *W2, *Wp;
   uint16_t* pk;
@@ -181,7 +182,8 @@ struct ImimPackArgs {
 __device__ __forceinline__ void imim_pack_block(const ImimPackArgs& A, int bid) {
   if (bid < A.nf) {
     const int o = bid * 4 + threadIdx.x / WAVE;
-    if (o < A.O) bn_fold_row(A.P, o, A.C, A.gamma, A.beta, A.Wf, A.bf, threadIdx.x % WAVE);
+    if (o < A.O)
+      bn_fold_row(A.P, o, A.C, A.gamma, A.beta, A.Wf, A.bf, threadIdx.x % WAVE, A.Wfb);
     return;
   }
   const int e = (bid - A.nf) * 256 + threadIdx.x;
@@ -1108,7 +1110,8 @@ int tgfr_imim_pack(const float* const* Wqkv, const float* const* bqkv, int rows_
   const int O = 3 * rows_qkv, nf = (O + 3) / 4;
   const LnTailWs o = ln_tail_ws(rows, hw);
   const long long n = PACK_UNITS + 2 * o.E;
-  const ImimPackArgs A{P, O, C, gamma, beta, Wf, bf, nf, W1, W2, Wp, pk, lnw, lnb, hw, ws + o.aff};
+  const ImimPackArgs A{P, O, C, gamma, beta, Wf, bf, nullptr, nf, W1, W2, Wp, pk, lnw, lnb, hw,
+                       ws + o.aff};
   hipLaunchKernelGGL(imim_pack_kernel, dim3((unsigned)(nf + (n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, A);
   return (int)hipGetLastError();
@@ -1117,9 +1120,10 @@ int tgfr_imim_pack(const float* const* Wqkv, const float* const* bqkv, int rows_
 int tgfr_imim_prep(const float* x, int N, int HW, float bn_eps, float momentum, int training,
                    float* running_mean, float* running_var, long long* nbt, float* mean,
                    float* rstd, const float* const* Wqkv, const float* const* bqkv, int rows_qkv,
-                   int C, const float* gamma, const float* beta, float* Wf, float* bf,
-                   const float* W1, const float* W2, const float* Wp, const float* lnw,
-                   const float* lnb, int rows, int hw, uint16_t* pk, float* ws, void* stream) {
+                   int C, const float* gamma, const float* beta, float* Wf, uint16_t* Wfb,
+                   float* bf, const float* W1, const float* W2, const float* Wp,
+                   const float* lnw, const float* lnb, int rows, int hw, uint16_t* pk, float* ws,
+                   void* stream) {
   if (!x || N <= 0 || HW <= 0 || !mean || !rstd || (!training && (!running_mean || !running_var)))
     return 1001;
   if (!Wqkv || !Wqkv[0] || !Wqkv[1] || !Wqkv[2] || rows_qkv <= 0 || C <= 0 || !gamma || !beta ||
@@ -1131,7 +1135,8 @@ int tgfr_imim_prep(const float* x, int N, int HW, float bn_eps, float momentum, 
   const int O = 3 * rows_qkv, nf = (O + 3) / 4;
   const LnTailWs o = ln_tail_ws(rows, hw);
   const long long n = PACK_UNITS + 2 * o.E;
-  const ImimPackArgs A{P, O, C, gamma, beta, Wf, bf, nf, W1, W2, Wp, pk, lnw, lnb, hw, ws + o.aff};
+  const ImimPackArgs A{P, O, C, gamma, beta, Wf, bf, Wfb, nf, W1, W2, Wp, pk, lnw, lnb, hw,
+                       ws + o.aff};
   const BnStatsArgs S{x, N, C, HW, bn_eps, momentum, training, running_mean, running_var, nbt,
                       mean, rstd};
   hipLaunchKernelGGL(imim_prep_kernel, dim3((unsigned)(C + nf + (n + 255) / 256)), dim3(256), 0,

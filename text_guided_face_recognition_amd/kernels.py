@@ -1040,15 +1040,16 @@ def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf
     use_batch = training or bn.running_mean is None
     # the bf16 q/k/v path normalises inside the projection launch
     # (tgfr_bn_qkv_bf16): only the statistics here
-    fused = (xhat_bf16 and isinstance(weight, tuple) and c == 256 and 128 < hw <= 224 and
-             hw % 4 == 0 and o % 128 == 0 and os.environ.get("TGFR_BN_QKV", "1") == "1")
+    fused = (xhat_bf16 and isinstance(weight, tuple) and prep is not None and c == 256 and
+             128 < hw <= 224 and hw % 4 == 0 and o % 256 == 0 and
+             os.environ.get("TGFR_BN_QKV", "1") == "1")
     stats = (ptr(x), n, c, hw, float(bn.eps), float(bn.momentum or 0.0), int(use_batch),
              ptr(bn.running_mean) if (track or not use_batch) else None,
              ptr(bn.running_var) if (track or not use_batch) else None,
              ptr(bn.num_batches_tracked) if track else None, ptr(mean), ptr(rstd))
     # prep (ImimFused): the statistics launched together with the weight
     # preparation (tgfr_imim_prep), one launch for both
-    prep = prep if fused and isinstance(weight, tuple) else None
+    prep = prep if fused else None
     if prep is None:
         call("tgfr_bn_stats" if fused else "tgfr_bn_fwd_cl_bf16" if xhat_bf16 else
              "tgfr_bn_fwd_cl", *stats, *(() if fused else (ptr(xhat),)), _hip.stream())
@@ -1060,10 +1061,11 @@ def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf
         w2 = tuple(w_.reshape(rows, c).float().contiguous() for w_ in weight)
         b2 = tuple(None if b_ is None else b_.float().contiguous() for b_ in bias)
         wf = torch.empty(o, c, dtype=torch.float32, device=dev)
+        wfb = torch.empty(o, c, dtype=torch.int16, device=dev) if fused else None
         wp = (ctypes.c_void_p * 3)(*[ptr(t) for t in w2])
         bp = (ctypes.c_void_p * 3)(*[ptr(t) for t in b2])
         if prep is not None:
-            prep(stats, wp, bp, rows, c, g, beta.float().contiguous(), wf, bf)
+            prep(stats, wp, bp, rows, c, g, beta.float().contiguous(), wf, wfb, bf)
         elif fold3 is not None:
             fold3(wp, bp, rows, c, g, beta.float().contiguous(), wf, bf)
         else:
@@ -1077,7 +1079,7 @@ def _bn_linear_fwd(ctx, x, gamma, beta, weight, bias, bn, training, mode, out_bf
     rows = n * hw
     if fused:
         y = torch.empty(rows, o, dtype=torch.int16, device=dev)
-        call("tgfr_bn_qkv_bf16", ptr(x), n, c, hw, ptr(mean), ptr(rstd), ptr(wf), ptr(bf), o,
+        call("tgfr_bn_qkv_bf16", ptr(x), n, c, hw, ptr(mean), ptr(rstd), ptr(wfb), ptr(bf), o,
              ptr(y), ptr(xhat), _hip.stream())
     elif out_bf16:
         y = torch.empty(rows, o, dtype=torch.int16, device=dev)
@@ -1503,10 +1505,10 @@ class ImimFused(torch.autograd.Function):
                  ptr(g), ptr(bt), ptr(wf), ptr(bf), *[ptr(t) for t in tw], rows, hw, ptr(pk),
                  ptr(ws), _hip.stream())
 
-        def prep(stats, wptr, bptr, qrows, cc, g, bt, wf, bf):
+        def prep(stats, wptr, bptr, qrows, cc, g, bt, wf, wfb, bf):
             x_, n_, c_, hw_, *rest = stats
             call("tgfr_imim_prep", x_, n_, hw_, *rest, ctypes.addressof(wptr),
-                 ctypes.addressof(bptr), qrows, cc, ptr(g), ptr(bt), ptr(wf), ptr(bf),
+                 ctypes.addressof(bptr), qrows, cc, ptr(g), ptr(bt), ptr(wf), ptr(wfb), ptr(bf),
                  *[ptr(t) for t in tw], rows, hw, ptr(pk), ptr(ws), _hip.stream())
 
         px = _bn_linear_fwd(ctx, x, gamma, beta, (wk, wq, wv), (bk, bq, bv), bn, training,

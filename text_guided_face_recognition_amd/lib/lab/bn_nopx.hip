@@ -202,11 +202,10 @@ __global__ __launch_bounds__(256) void bn_unfold_kernel(
 // operand (their k-contiguous rows, loaded per chunk with the map and
 // converted to bf16 fragments) and xhat^T the B operand, read from an LDS image
 // [32 channels][224 positions] (the input's own layout) by
-// ds_read_b64_tr_b16.  K runs in 8 chunks of 32 channels: chunk k + 1's
-// global loads are in flight while chunk k is normalised into one of two LDS
-// images and multiplied (one barrier per chunk; a third chunk in flight
-// measured slower).  The output tile goes out through LDS as 512-byte row
-// segments (8-byte column quads straight from the accumulators: 10 us more).  The
+// ds_read_b64_tr_b16.  K runs in 8 chunks of 32 channels: chunks k + 1 and
+// k + 2's global loads are in flight while chunk k is normalised into one of
+// two LDS images and multiplied (one barrier per chunk).  Each lane's accumulator
+// quad is 4 consecutive output columns of one position: 8-byte stores.  The
 // slices of one sample run on one XCD (xcd_remap), so the map is read from
 // HBM once and from L2 twice more; slice s writes xhat for the chunks
 // k = s (mod O / 256).
@@ -214,9 +213,7 @@ constexpr int QKV_MP = 224;              // LDS image pitch (positions), 7 x 32
 constexpr int QKV_CK = 32;               // channels per chunk
 constexpr int QKV_IMG = QKV_CK * QKV_MP * 2;
 constexpr int QKV_MS = 2 * QKV_IMG;     // mean / rstd of the 256 channels (LDS)
-constexpr int QKV_OUT = QKV_MS + 2 * 256 * 4;   // the output tile, staged for row stores
-constexpr int QKV_OP = 256 * 2 + 16;    // its row pitch (bytes): 16-B aligned, 4 banks apart
-constexpr int QKV_LDS = QKV_OUT + QKV_MP * QKV_OP;
+constexpr int QKV_LDS = QKV_MS + 2 * 256 * 4;
 constexpr int QKV_LOADS = 4;             // float4 loads per thread per chunk (<= 2048 / 512)
 constexpr int QKV_COLS = 256;            // output columns per workgroup (8 waves x 32)
 constexpr int QKV_MT = QKV_MP / 32;      // 32-row tiles per sample (7)
@@ -246,8 +243,8 @@ __global__ __launch_bounds__(512) void bn_qkv_kernel(
   // chunk's two k steps (bf16, 32 rows x 32 channels: L2-resident, shared by
   // the sample workgroups of the slice), both issued two chunks ahead
   const uint16_t* wr = Wb + (long long)(n0 + lr) * C + 8 * h;
-  float4 ld[2][QKV_LOADS];
-  uint4 wl[2][2];
+  float4 ld[3][QKV_LOADS];
+  uint4 wl[3][2];
   auto issue = [&](int ck, float4 (&dst)[QKV_LOADS], uint4 (&wd)[2]) {
 #pragma unroll
     for (int j = 0; j < QKV_LOADS; ++j) {
@@ -265,6 +262,7 @@ __global__ __launch_bounds__(512) void bn_qkv_kernel(
   const float mu0 = mean[min(tid, C - 1)], rs0 = rstd[min(tid, C - 1)];
   issue(0, ld[0], wl[0]);
   issue(1, ld[1], wl[1]);
+  issue(2, ld[2], wl[2]);
   if (tid < C) {
     lds_stf(QKV_MS + tid * 4, mu0);
     lds_stf(QKV_MS + (C + tid) * 4, rs0);
@@ -294,7 +292,7 @@ __global__ __launch_bounds__(512) void bn_qkv_kernel(
     const uint32_t img = (ck & 1) * QKV_IMG;
     // normalise chunk ck into its image (rows = channels, 8-byte writes)
     {
-      float4 (&src)[QKV_LOADS] = ld[ck & 1];
+      float4 (&src)[QKV_LOADS] = ld[ck % 3];
 #pragma unroll
       for (int j = 0; j < QKV_LOADS; ++j) {
         const int i = min(tid + 512 * j, items - 1);
@@ -306,20 +304,15 @@ __global__ __launch_bounds__(512) void bn_qkv_kernel(
                            pk_bf16((v.z - mu) * rs, (v.w - mu) * rs)));
       }
     }
-    const bf16x8 wa0 = as_bf8(wl[ck & 1][0]), wa1 = as_bf8(wl[ck & 1][1]);
+    const bf16x8 wa0 = as_bf8(wl[ck % 3][0]), wa1 = as_bf8(wl[ck % 3][1]);
     __syncthreads();
-    if (ck + 2 < NCH) issue(ck + 2, ld[ck & 1], wl[ck & 1]);
-    // per k step: every m tile's B fragment read first, then the MFMAs (the
-    // reads' latency overlaps instead of one wait per MFMA)
+    if (ck + 3 < NCH) issue(ck + 3, ld[ck % 3], wl[ck % 3]);
 #pragma unroll
-    for (int ksl = 0; ksl < 2; ++ksl) {
-      bf16x8 bb[QKV_MT];
-#pragma unroll
-      for (int t = 0; t < QKV_MT; ++t) bb[t] = bfrag(img, ksl, mt0 + min(t, n_mt - 1));
+    for (int ksl = 0; ksl < 2; ++ksl)
 #pragma unroll
       for (int t = 0; t < QKV_MT; ++t)
-        if (t < n_mt) acc[t] = mfma_lp<MODE_BF16>(ksl ? wa1 : wa0, bb[t], acc[t]);
-    }
+        if (t < n_mt)
+          acc[t] = mfma_lp<MODE_BF16>(ksl ? wa1 : wa0, bfrag(img, ksl, mt0 + t), acc[t]);
     // this slice's share of the channels-last xhat: positions x 8-channel groups
     if (ck % n_sl == sl) {
       for (int it = tid; it < HW * (QKV_CK / 8); it += 512) {
@@ -336,25 +329,19 @@ __global__ __launch_bounds__(512) void bn_qkv_kernel(
       }
     }
   }
-  // epilogue: bf16(acc + b') into the LDS tile [m][256 columns] (a lane's
-  // quad = 4 consecutive columns of one position: 8-byte writes), then the
-  // tile's rows out as 512-byte row segments (16 B per lane, coalesced)
+  // epilogue: px[n][m][n0 + 8 g + 4 h .. + 3] = bf16(acc + b')
 #pragma unroll
   for (int t = 0; t < QKV_MT; ++t) {
     if (t >= n_mt) continue;
-    const uint32_t row = QKV_OUT + ((mt0 + t) * 32 + lr) * QKV_OP + (wv * 32 + 4 * h) * 2;
+    const int m = (mt0 + t) * 32 + lr;
+    if (m < 1000000) continue;
+    uint16_t* dst = px + ((long long)nb * HW + m) * O + n0 + 4 * h;
 #pragma unroll
     for (int g = 0; g < 4; ++g)
-      lds_st8(row + 16 * g,
-              make_uint2(pk_bf16(acc[t][4 * g] + bias[4 * g], acc[t][4 * g + 1] + bias[4 * g + 1]),
-                         pk_bf16(acc[t][4 * g + 2] + bias[4 * g + 2],
-                                 acc[t][4 * g + 3] + bias[4 * g + 3])));
-  }
-  __syncthreads();
-  uint16_t* dst = px + (long long)nb * HW * O + sl * QKV_COLS;
-  for (int it = tid; it < HW * 32; it += 512) {
-    const int m = it >> 5, j = it & 31;
-    *(uint4*)(dst + (long long)m * O + 8 * j) = lds_ld16(QKV_OUT + m * QKV_OP + 16 * j);
+      *(uint2*)(dst + 8 * g) =
+          make_uint2(pk_bf16(acc[t][4 * g] + bias[4 * g], acc[t][4 * g + 1] + bias[4 * g + 1]),
+                     pk_bf16(acc[t][4 * g + 2] + bias[4 * g + 2],
+                             acc[t][4 * g + 3] + bias[4 * g + 3]));
   }
 }
 
@@ -391,7 +378,6 @@ int tgfr_bn_qkv_bf16(const float* x, int N, int C, int HW, const float* mean, co
   if (((uintptr_t)x & 15) || ((uintptr_t)Wf & 15) || ((uintptr_t)px & 7) || ((uintptr_t)xhat & 15))
     return 1001;
   const dim3 grid(N * (O / QKV_COLS));
-  if (const int e = set_max_lds((const void*)bn_qkv_kernel, QKV_LDS)) return e;
   hipLaunchKernelGGL(bn_qkv_kernel, grid, dim3(512), QKV_LDS, (hipStream_t)stream, x, HW, mean,
                      rstd, Wf, bf, O, px, xhat);
   return (int)hipGetLastError();

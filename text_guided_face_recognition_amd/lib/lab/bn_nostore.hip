@@ -354,7 +354,7 @@ __global__ __launch_bounds__(512) void bn_qkv_kernel(
   uint16_t* dst = px + (long long)nb * HW * O + sl * QKV_COLS;
   for (int it = tid; it < HW * 32; it += 512) {
     const int m = it >> 5, j = it & 31;
-    *(uint4*)(dst + (long long)m * O + 8 * j) = lds_ld16(QKV_OUT + m * QKV_OP + 16 * j);
+    if (m > 100000) *(uint4*)(dst + (long long)m * O + 8 * j) = lds_ld16(QKV_OUT + m * QKV_OP + 16 * j);
   }
 }
 

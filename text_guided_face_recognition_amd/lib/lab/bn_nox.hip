@@ -321,7 +321,7 @@ __global__ __launch_bounds__(512) void bn_qkv_kernel(
         if (t < n_mt) acc[t] = mfma_lp<MODE_BF16>(ksl ? wa1 : wa0, bb[t], acc[t]);
     }
     // this slice's share of the channels-last xhat: positions x 8-channel groups
-    if (ck % n_sl == sl) {
+    if (false) {
       for (int it = tid; it < HW * (QKV_CK / 8); it += 512) {
         const int m = it % HW, cg = it / HW;
         uint32_t w[4];

@@ -69,3 +69,8 @@ qkv2)
     -- python3 bench.py --steps 20 --warmup 5 --no-cpu --alt-precision "" > $O/trace.log 2>&1 || exit 12
   ;;
 esac
+case "${STEP}" in
+qkvlab)
+  timeout -k 10 120 python3 -u tools/qkv_lab.py time > $O/qkvlab.log 2>&1; cat $O/qkvlab.log
+  ;;
+esac

@@ -25,10 +25,10 @@ def main(path, which=-3):
     # launch; approximate: the window between two wr_fwd launches, shifted back
     # to the step's first kernel (the IMIM BN statistics)
     lo = idx[which]
-    while lo > 0 and "bn_stats" not in rows[lo]["Kernel_Name"]:
+    while lo > 0 and not any(k in rows[lo]["Kernel_Name"] for k in ("bn_stats", "imim_prep")):
         lo -= 1
     hi = idx[which + 1]
-    while hi > 0 and "bn_stats" not in rows[hi]["Kernel_Name"]:
+    while hi > 0 and not any(k in rows[hi]["Kernel_Name"] for k in ("bn_stats", "imim_prep")):
         hi -= 1
     step = rows[lo:hi]
     t0 = int(step[0]["Start_Timestamp"])

@@ -24,7 +24,12 @@ def _worker(rank, world, port, q):
         from text_guided_face_recognition_amd.kernels import gather_col_partials
 
         def combine_col_partials(parts):
-            # the math of tgfr_col_lse_combine (a kernel: device tensors only)
+            # the math of tgfr_col_lse_combine.  The shipped combine is that
+            # kernel alone (no CPU fallback by design, tests/test_abi.py
+            # ::test_device_only_contract), so this CPU test covers the
+            # exchange layout and the collective; the kernel itself is checked
+            # on the GPU against this same math (tests/test_gpu_dp.py
+            # ::test_dp_glue_kernels)
             gmax = parts[:, 0].max(0).values
             return gmax + torch.log((parts[:, 1] * torch.exp(parts[:, 0] - gmax)).sum(0))
 

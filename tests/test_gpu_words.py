@@ -410,11 +410,13 @@ def test_words_bounded_past_unit_norm(gpu, mode, nw, wn, rn, ltol, gtol):
     """The max-free (bounded) kernels fed features far from the unit-norm
     contract through the drop-in path (kernels.word_region_logits with
     bounded=True, as words_loss does for en_type BERT): |W| = 6, |R| = 8 (score
-    bound c = 48) and |W| = 8, |R| = 10 (c = 80): exact, no shift (the window
-    of csrc/tgfr_wr.hip bound_shift, c <= 84.5); |W| = |R| = 12 (c = 144):
-    bf16 with 30 words takes the running-max variant of the max-free kernels
-    on the device (per caption, BIG_C); 62 words / fp16 past WR_BOUND_MAX the
-    device guard (tgfr_wr_guard) runs the exact running-max twins.
+    bound c = 48) and |W| = 8, |R| = 10 (c = 80), |W| = |R| = 12 (c = 144).
+    30 words (bf16 and, since round 6, fp16): every caption past BIG_C = 10
+    (each of these) takes the running-max variant of the pipelined max-free
+    kernels, chosen per caption on the device (csrc/tgfr_wr.hip caption_init,
+    wr_tok_kernel); 62 words: unshifted up to c = 84.5 (bound_shift), and past
+    WR_BOUND_MAX the device guard (tgfr_wr_guard) runs the exact running-max
+    twins.
     Logits and gradients finite and matching the oracle (models/losses.py:83-109
     on unnormalised BERT-path features); the tolerance grows with c because
     the operands' relative rounding scales every score by |W| |R|."""

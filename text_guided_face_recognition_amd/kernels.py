@@ -154,14 +154,16 @@ def _wr_fwd(img_features, words, lens, gamma1, gamma2, gamma3, mode, img_offset=
             w_fwd, _, w_norm = prep_rows(words.float(), t_words, t_pad, lens=lens,
                                          want_norms=True, scale=LOG2E, f16=f16)
         # 32-token captions: the max-free kernels decide per caption on the
-        # device (a caption whose score bound max|W| max|R| exceeds 84.5
-        # takes their running-max variant), exact for any input, also under
-        # graph capture.  64-token captions: exact while the bound is <=
+        # device (a caption whose score bound max|W| max|R| exceeds BIG_C = 10,
+        # formed in the forward and again in the token-table kernel, takes
+        # their running-max variant): overflow-free for any input, also under
+        # graph capture (the bf16 / fp16 operands' rounding still moves each
+        # score by ~c 2^-9 / c 2^-11).  64-token captions: exact while the bound is <=
         # WR_BOUND_MAX (csrc/tgfr_wr.hip, bound_shift).  Rows made by this
         # package's heads are L2-normalised (bound ~1); other inputs get a
         # device guard (tgfr_wr_guard): every launch of the path has its exact
         # running-max twin beside it and the guard picks one on the device --
-        # exact for any input, also under graph capture, with no host read --
+        # overflow-free for any input, also under graph capture, with no host read --
         # as the reference's softmax never overflows (models/attention.py:28-36)
         if bounded and t_pad != TPAD and not own_rows:
             if not _rows_only(words):
@@ -2029,10 +2031,14 @@ class FocalCE(torch.autograd.Function):
     The reference applies the focal factor to the mean cross-entropy of the
     WHOLE batch it sees (DataParallel gathers every replica's logits on GPU 0).
     With a process group each rank holds its own rows: the per-rank NLL sums
-    of all pairs are summed over ranks by ONE all-reduce, the focal loss is
-    formed from the global mean on every rank, and each rank's logit gradient
-    carries f'(CE_global) / N_global -- so the gradients summed over ranks are
-    the reference's global-batch gradients."""
+    are summed over ranks by all-reduces -- one per group of at most two pairs
+    with the same row count (tgfr_focal_global packs two heads), so the
+    trainers' two identity heads of one batch cost ONE; more pairs or other
+    row counts cost one more collective (and one more graph segment under
+    dist.StepCapture) per group -- the focal loss is formed from the global
+    mean on every rank, and each rank's logit gradient carries
+    f'(CE_global) / N_global -- so the gradients summed over ranks are the
+    reference's global-batch gradients."""
 
     @staticmethod
     def forward(ctx, gamma, group, n_global, *pairs):

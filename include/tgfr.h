@@ -32,6 +32,8 @@
  *   - ABI 600: the max-free t_pad-32 kernels (pipelined forward, two-role
  *     backward) run in mode 2 as well as mode 0; in mode 2 the forward
  *     stores C-hat scaled by 2^-8 and the token-table calls take bounded = 2.
+ *   - ABI 610: tgfr_imim_dw_ln; tgfr_ln_tail_bwd / _att accept dlnw = dlnb =
+ *     NULL (the LayerNorm's dw / db partials stay in ws for it).
  */
 #ifndef TGFR_H
 #define TGFR_H
@@ -523,6 +525,17 @@ int tgfr_imim_dw(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
                  float* dWp, float* dbp, float* dW2, float* db2, float* dW1, float* db1,
                  const uint16_t* Xq, const uint16_t* Yq, int Nq, int Kq, float* dWq, float* dbq,
                  float* ws, void* stream);
+/* tgfr_imim_dw + the IMIM LayerNorm's dw / db [256][hw] (ABI 610): with
+ * dlnw = dlnb = NULL, tgfr_ln_tail_bwd_att leaves the LayerNorm's per-group
+ * partials in its tail workspace lnws, and this launch's reduce sums them
+ * (same order, same values as the separate reduce) -- one kernel less on the
+ * step's critical path.  Same ws as tgfr_imim_dw. */
+int tgfr_imim_dw_ln(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
+                    const uint16_t* H1b, const uint16_t* dH1b, const uint16_t* Zb, int rows,
+                    float* dWp, float* dbp, float* dW2, float* db2, float* dW1, float* db1,
+                    const uint16_t* Xq, const uint16_t* Yq, int Nq, int Kq, float* dWq,
+                    float* dbq, const float* lnws, int hw, float* dlnw, float* dlnb, float* ws,
+                    void* stream);
 int tgfr_attn_bwd_prepped(const uint16_t* Q, const uint16_t* K, const uint16_t* V, long long ld,
                           long long sb, int B, int hw, float scale, const float* lse,
                           uint16_t* dQ, uint16_t* dK, uint16_t* dV, long long ldg, long long sbg,

@@ -284,6 +284,34 @@ def test_imim_fused_node(gpu, n, precision):
     torch.testing.assert_close(a.bn_img.running_var, b.bn_img.running_var)
 
 
+@pytest.mark.parametrize("n,precision", [(64, "bf16"), (13, "bf16"), (3, "fp16")])
+def test_imim_ln_dw_deferred(gpu, n, precision, monkeypatch):
+    """The IMIM LayerNorm's dw / db summed by the weight gradients' reduce
+    launch (tgfr_imim_dw_ln, TGFR_LN_DW_DEFER=1, the default) against its own
+    reduce launch (ln_bwd_dw, TGFR_LN_DW_DEFER=0): the same group partials
+    summed in the same order, so every gradient is bit-identical (n = 13: a
+    ragged last group of 5 samples; n = 64: 8 groups)."""
+    import copy
+    from text_guided_face_recognition_amd.config import make_args
+    from text_guided_face_recognition_amd.models.models import IMIM
+    torch.manual_seed(n)
+    a = IMIM(make_args(precision=precision), 256).to(gpu)
+    for p_ in a.parameters():
+        p_.data.add_(torch.randn_like(p_) * 0.05)
+    b = copy.deepcopy(a)
+    x = torch.randn(n, 256, 14, 14, device=gpu) * 1.5 + 0.3
+    probe = torch.randn(n, 256, 14, 14, device=gpu)
+    for m, flag in ((a, "1"), (b, "0")):
+        monkeypatch.setenv("TGFR_LN_DW_DEFER", flag)
+        (m(x) * probe).sum().backward()
+    torch.cuda.synchronize()
+    assert b.ln.weight.grad.abs().max() > 0
+    for (na, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert (pa.grad is None) == (pb.grad is None), na
+        if pa.grad is not None:
+            assert torch.equal(pa.grad, pb.grad), na
+
+
 @pytest.mark.parametrize("n,hw", [(64, 196), (5, 196), (3, 144)])
 def test_bn_qkv_fused(gpu, n, hw):
     """tgfr_bn_qkv_bf16 (BN apply + the packed q/k/v projection in one launch,

@@ -116,6 +116,8 @@ SIGNATURES = {
     "tgfr_ln_tail_ws": [I, I, P],
     "tgfr_imim_dw_ws": [I, I, I, P],
     "tgfr_imim_dw": [P, P, P, P, P, P, I, P, P, P, P, P, P, P, P, I, I, P, P, P, P],
+    "tgfr_imim_dw_ln": [P, P, P, P, P, P, I, P, P, P, P, P, P, P, P, I, I, P, P, P, I, P, P,
+                        P, P],
     "tgfr_attn_fwd_ln": [P, P, P, L, L, I, I, F, P, P, P, P],
     "tgfr_ln_tail_fwd_att": [P, I, I, F, P, P, P, P, P, F, P, L, P, P, P, P, P, P, I, I, I, P],
     "tgfr_ln_tail_bwd_att": [P, P, P, I, F, P, P, P, P, I, P, P, P, P, P, P, P, P, P],

@@ -271,8 +271,9 @@ int ln_bwd_tail_launch(const float* dy, const float* x, int rows, long long E, c
   else
     hipLaunchKernelGGL(ln_bwd_dx_kernel<false>, grid, dim3(NT), 0, s, dy, x, E, src, w_cl, 0,
                        stats, rows, LN_GROUP, dx, dwp, dbp, nullptr, nullptr);
-  hipLaunchKernelGGL(ln_bwd_dw_kernel, dim3((unsigned)((E + NT - 1) / NT)), dim3(NT), 0, s,
-                     dwp, dbp, E, groups, ch, dw, db);
+  if (dw)   // (NULL: the caller reduces the group partials later)
+    hipLaunchKernelGGL(ln_bwd_dw_kernel, dim3((unsigned)((E + NT - 1) / NT)), dim3(NT), 0, s,
+                       dwp, dbp, E, groups, ch, dw, db);
   return (int)hipGetLastError();
 }
 

@@ -913,15 +913,44 @@ __global__ __launch_bounds__(256) void tail_dw_kernel(DwArgs A, float* __restric
 struct DwOut {
   float* dW[DW_MAXP];
   float* db[DW_MAXP];
+  // optional (lnE > 0): the IMIM LayerNorm's weight / bias gradients from the
+  // group partials its backward left (ln_bwd_dx: dw [lng][lnE] then db
+  // [lng][lnE], channels-last e = p * 256 + c), summed in group order like
+  // ln_bwd_dw and scattered to the reference's [256][hw] maps
+  const float* lnp;
+  long long lnE;
+  int lng, lnhw;
+  float* dlnw;
+  float* dlnb;
 };
 
 // out = sum over slices, in slice order; thread = 2 consecutive outputs (a
-// grid of ~2 workgroups per CU) with 8 slice loads in flight
+// grid of ~2 workgroups per CU) with 8 slice loads in flight.  Threads past
+// the products' e_total outputs reduce the LayerNorm partials (O.lnE > 0).
 __global__ __launch_bounds__(256) void tail_dw_reduce_kernel(DwArgs A, DwOut O,
                                                              const float* __restrict__ ws,
                                                              long long e_total) {
   const long long e4 = (blockIdx.x * 256LL + threadIdx.x) * 2;
-  if (e4 >= e_total) return;
+  if (e4 >= e_total) {
+    long long off = e4 - e_total;      // (e_total and lnE are even: pairs never straddle)
+    if (off >= 2 * O.lnE) return;
+    const bool bias = off >= O.lnE;
+    if (bias) off -= O.lnE;
+    const float* src = O.lnp + (bias ? (long long)O.lng * O.lnE : 0) + off;
+    float2 s = make_float2(0.f, 0.f);
+    for (int k = 0; k < O.lng; ++k) {
+      const float2 v = *(const float2*)(src + k * O.lnE);
+      s.x += v.x;
+      s.y += v.y;
+    }
+    float* dst = bias ? O.dlnb : O.dlnw;
+    // channels-last e -> channel-major [TC][hw] (e and e + 1: channels c, c + 1)
+    const long long p = off / TC;
+    const int c = (int)(off % TC);
+    dst[(long long)c * O.lnhw + p] = s.x;
+    dst[(long long)(c + 1) * O.lnhw + p] = s.y;
+    return;
+  }
   // which product / region: products laid out as [dW N*K][db N] each
   long long off = e4;
   int pi = 0;
@@ -1003,7 +1032,8 @@ int dw_launch(const DwArgs& A, int n_wg, const DwOut& O, float* ws, hipStream_t 
   hipLaunchKernelGGL(fn, dim3(n_wg), dim3(256), DW_LDS, s, A, ws);
   long long e_total = 0;
   for (int i = 0; i < DW_MAXP; ++i) e_total += (long long)A.p[i].N * A.p[i].K + A.p[i].N;
-  hipLaunchKernelGGL(tail_dw_reduce_kernel, dim3((unsigned)((e_total / 2 + 255) / 256)),
+  const long long e_all = e_total + 2 * O.lnE;
+  hipLaunchKernelGGL(tail_dw_reduce_kernel, dim3((unsigned)((e_all / 2 + 255) / 256)),
                      dim3(256), 0, s, A, O, ws, e_total);
   return (int)hipGetLastError();
 }
@@ -1180,8 +1210,10 @@ static int ln_tail_bwd(const float* dR, const float* R, const float* inv, int ro
       ((uintptr_t)X & 15) || ((uintptr_t)dZ & 15) || ((uintptr_t)dX & 15) ||
       ((uintptr_t)dOb & 7))
     return 1001;
+  // (dlnw and dlnb both NULL: the LayerNorm's dw / db group partials stay in
+  // ws for tgfr_imim_dw_ln's reduce)
   if (!inv || !pk || !H1b || !H2b || !dZ || !dPb || !dH2b || !dH1b || !(dX || (D && dOb)) ||
-      !dlnw || !dlnb)
+      !dlnw != !dlnb)
     return 1001;
   const LnTailWs o = ln_tail_ws(rows, hw);
   const LnWs l = ln_ws(o.n, o.E, TC);
@@ -1309,6 +1341,45 @@ int tgfr_imim_dw(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
   O.dW[1] = dW2; O.db[1] = db2;
   O.dW[2] = dW1; O.db[2] = db1;
   O.dW[3] = dWq; O.db[3] = dbq;
+  return dw_launch(A, n_wg, O, ws, (hipStream_t)stream);
+}
+
+// tgfr_imim_dw with the IMIM LayerNorm's dw / db reduce as extra workgroups of
+// its slab reduce: lnws is the tail workspace that tgfr_ln_tail_bwd_att,
+// called with dlnw = dlnb = NULL, left the LayerNorm's group partials in
+// (one launch less on the step's critical path; same sums, same order as
+// ln_bwd_dw).  dlnw / dlnb: the reference's [256][hw] maps.
+int tgfr_imim_dw_ln(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
+                    const uint16_t* H1b, const uint16_t* dH1b, const uint16_t* Zb, int rows,
+                    float* dWp, float* dbp, float* dW2, float* db2, float* dW1, float* db1,
+                    const uint16_t* Xq, const uint16_t* Yq, int Nq, int Kq, float* dWq,
+                    float* dbq, const float* lnws, int hw, float* dlnw, float* dlnb, float* ws,
+                    void* stream) {
+  if (rows <= 0 || !dPb || !H2b || !dH2b || !H1b || !dH1b || !Zb || !dWp || !dbp || !dW2 ||
+      !db2 || !dW1 || !db1 || !Xq || !Yq || !dWq || !dbq || !ws || Nq <= 0 || Kq <= 0 ||
+      Nq % DW_NB || Kq % DW_NB || !lnws || !dlnw || !dlnb || !ln_tail_ok(rows, hw))
+    return 1001;
+  DwArgs A;
+  long long wsf;
+  int n_wg;
+  imim_dw_plan(rows, Nq, Kq, A, wsf, n_wg);
+  A.p[0].X = dPb;  A.p[0].Y = H2b;
+  A.p[1].X = dH2b; A.p[1].Y = H1b;
+  A.p[2].X = dH1b; A.p[2].Y = Zb;
+  A.p[3].X = Xq;   A.p[3].Y = Yq;
+  DwOut O = {};
+  O.dW[0] = dWp; O.db[0] = dbp;
+  O.dW[1] = dW2; O.db[1] = db2;
+  O.dW[2] = dW1; O.db[2] = db1;
+  O.dW[3] = dWq; O.db[3] = dbq;
+  const LnTailWs o = ln_tail_ws(rows, hw);
+  const LnWs l = ln_ws(o.n, o.E, TC);
+  O.lnp = lnws + o.ln + l.bwd;
+  O.lnE = o.E;
+  O.lng = (o.n + LN_GROUP - 1) / LN_GROUP;
+  O.lnhw = hw;
+  O.dlnw = dlnw;
+  O.dlnb = dlnb;
   return dw_launch(A, n_wg, O, ws, (hipStream_t)stream);
 }
 

@@ -1482,9 +1482,10 @@ class ImimFused(torch.autograd.Function):
     (tgfr_attn_fwd_ln), so no statistics pass runs either.
     Forward: BN statistics + bf16 xhat, the pack, the q/k/v GEMM, attention
     (+ LN moments), the fused tail (6 launches).  Backward: tail + LN sums,
-    LN input gradient (as attention operands), LN dw/db, attention dK/dV, dQ,
-    the tail's and the q/k/v projection's weight gradients in one launch
-    (+ reduce), BN unfold (8 launches)."""
+    LN input gradient (as attention operands), attention dK/dV, dQ, the
+    tail's and the q/k/v projection's weight gradients in one launch (+ a
+    reduce that also sums the LN dw/db partials, tgfr_imim_dw_ln), BN unfold
+    (7 launches; TGFR_LN_DW_DEFER=0: the LN dw/db reduce as its own launch)."""
 
     @staticmethod
     def forward(ctx, x, gamma, beta, wk, wq, wv, bk, bq, bv, lnw, lnb, w1, b1, w2, b2, wp, bp,
@@ -1564,9 +1565,12 @@ class ImimFused(torch.autograd.Function):
         dh1 = torch.empty(rows, _TAIL_H, dtype=torch.int16, device=dev)
         dlnw = torch.empty(hw * _TAIL_C, dtype=torch.float32, device=dev)
         dlnb = torch.empty_like(dlnw)
+        # (deferred: the LayerNorm's dw / db partials are reduced by the weight
+        # gradients' reduce launch below, tgfr_imim_dw_ln)
+        defer = os.environ.get("TGFR_LN_DW_DEFER", "1") == "1"
         call("tgfr_ln_tail_bwd_att", ptr(dr2), ptr(r), ptr(inv), rows, eps, ptr(pk), ptr(h1),
              ptr(h2), ptr(o), hw, ptr(ws), ptr(dz), ptr(dp), ptr(dh2), ptr(dh1), ptr(aws),
-             ptr(dlnw), ptr(dlnb), _hip.stream())
+             None if defer else ptr(dlnw), None if defer else ptr(dlnb), _hip.stream())
         dpx = torch.empty(nb, hw, 768, dtype=torch.int16, device=dev)
         call("tgfr_attn_bwd_prepped", ptr(px), ptr(px[..., 256:]), ptr(px[..., 512:]),
              px.stride(1), px.stride(0), nb, hw, scale, ptr(lse), ptr(dpx), ptr(dpx[..., 256:]),
@@ -1587,9 +1591,14 @@ class ImimFused(torch.autograd.Function):
         db1 = torch.empty(_TAIL_H, dtype=torch.float32, device=dev)
         gm = torch.empty(n, c, dtype=torch.float32, device=dev)
         s = torch.empty(n, dtype=torch.float32, device=dev)
-        call("tgfr_imim_dw", ptr(dp), ptr(h2), ptr(dh2), ptr(h1), ptr(dh1), ptr(zb), rows,
-             ptr(dwp), ptr(dbp), ptr(dw2), ptr(db2), ptr(dw1), ptr(db1), ptr(dpx), ptr(xhat), n,
-             c, ptr(gm), ptr(s), ptr(wsd), _hip.stream())
+        dw_args = (ptr(dp), ptr(h2), ptr(dh2), ptr(h1), ptr(dh1), ptr(zb), rows, ptr(dwp),
+                   ptr(dbp), ptr(dw2), ptr(db2), ptr(dw1), ptr(db1), ptr(dpx), ptr(xhat), n, c,
+                   ptr(gm), ptr(s))
+        if defer:
+            call("tgfr_imim_dw_ln", *dw_args, ptr(ws), hw, ptr(dlnw), ptr(dlnb), ptr(wsd),
+                 _hip.stream())
+        else:
+            call("tgfr_imim_dw", *dw_args, ptr(wsd), _hip.stream())
         att = _imim_grads(_bn_unfold(ctx, gm, s))[:9]
         return att + (dlnw.reshape(lnshape), dlnb.reshape(lnshape), dw1.reshape(w1shape), db1,
                       dw2.reshape(w2shape), db2, dwp, dbp) + (None,) * 6

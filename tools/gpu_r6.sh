@@ -74,3 +74,15 @@ qkvlab)
   timeout -k 10 120 python3 -u tools/qkv_lab.py time > $O/qkvlab.log 2>&1; cat $O/qkvlab.log
   ;;
 esac
+case "${STEP}" in
+lndw)
+  timeout -k 10 400 python3 -u -m pytest tests/test_gpu_tail.py tests/test_abi.py -m gpu -v -s --timeout 200 --timeout-method thread > $O/lndw.log 2>&1
+  rc=$?; echo "tests rc=$rc: $(tail -1 $O/lndw.log)"; [ $rc -le 1 ] || exit $rc
+  for i in 1 2 3; do for e in TGFR_LN_DW_DEFER=1 TGFR_LN_DW_DEFER=0; do
+    env $e timeout -k 10 180 python3 -u bench.py --no-cpu --alt-precision "" > $O/bench_${e}_$i.log 2>&1 || exit 22
+    echo "$e $i: $(grep -o '"ms_per_step": [0-9.]*' $O/bench_${e}_$i.log)"
+  done; done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench \
+    -- python3 bench.py --steps 20 --warmup 5 --no-cpu --alt-precision "" > $O/trace.log 2>&1 || exit 12
+  ;;
+esac

@@ -70,11 +70,6 @@ qkv2)
   ;;
 esac
 case "${STEP}" in
-qkvlab)
-  timeout -k 10 120 python3 -u tools/qkv_lab.py time > $O/qkvlab.log 2>&1; cat $O/qkvlab.log
-  ;;
-esac
-case "${STEP}" in
 lndw)
   timeout -k 10 400 python3 -u -m pytest tests/test_gpu_tail.py tests/test_abi.py -m gpu -v -s --timeout 200 --timeout-method thread > $O/lndw.log 2>&1
   rc=$?; echo "tests rc=$rc: $(tail -1 $O/lndw.log)"; [ $rc -le 1 ] || exit $rc

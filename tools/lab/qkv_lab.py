@@ -2,17 +2,17 @@
 csrc/tgfr_bn.hip, each built as its own small library (that file alone), and
 (on a GPU box) the kernel timed alone per variant with HIP events.
 
-    python tools/qkv_lab.py build        # here
-    python tools/qkv_lab.py time         # GPU box
+    python tools/lab/qkv_lab.py build        # here
+    python tools/lab/qkv_lab.py time         # GPU box
 """
 import ctypes
 import os
 import subprocess
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CSRC = os.path.join(ROOT, "text_guided_face_recognition_amd", "csrc")
-OUT = os.path.join(ROOT, "text_guided_face_recognition_amd", "lib", "lab")
+OUT = os.path.join(ROOT, "tools", "lab", "build", "qkv")
 
 VARIANTS = {
     "base": [],

@@ -174,15 +174,24 @@ __global__ __launch_bounds__(256) void bn_unfold_kernel(
     pp[1] = red[256 + tx] + red[320 + tx] + red[384 + tx] + red[448 + tx];
   }
   if (!last_arrival(counters + blockIdx.x, gridDim.y, (int*)&red[512])) return;
-  if (ry == 0 && c < C) {
-    float a = 0.f, b = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < (int)gridDim.y; ++k) {
-      a += part[((long long)k * C + c) * 2];
-      b += part[((long long)k * C + c) * 2 + 1];
+  // the chunks' partials: row lane ry sums chunks ry, ry + 4, ... (all its
+  // loads in flight), then the four lanes' sums combine in lane order
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    const int nch = (int)gridDim.y;
+#pragma unroll 12
+    for (int k = ry; k < nch; k += 4) {
+      const float2 v = *(const float2*)(part + ((long long)k * C + c) * 2);
+      a += v.x;
+      b += v.y;
     }
-    dgamma[c] = a;
-    dbeta[c] = b;
+  }
+  red[ry * 64 + tx] = a;
+  red[256 + ry * 64 + tx] = b;
+  __syncthreads();
+  if (ry == 0 && c < C) {
+    dgamma[c] = (red[tx] + red[64 + tx]) + (red[128 + tx] + red[192 + tx]);
+    dbeta[c] = (red[256 + tx] + red[320 + tx]) + (red[384 + tx] + red[448 + tx]);
   }
 }
 

@@ -81,3 +81,16 @@ lndw)
     -- python3 bench.py --steps 20 --warmup 5 --no-cpu --alt-precision "" > $O/trace.log 2>&1 || exit 12
   ;;
 esac
+case "${STEP}" in
+quick)
+  # TESTS="file::k ..." (pytest -k expression in KEXPR), then 3 benches and a trace
+  timeout -k 10 600 python3 -u -m pytest ${TESTS} -m gpu -v -s --timeout 200 --timeout-method thread -k "${KEXPR}" > $O/tests.log 2>&1
+  rc=$?; echo "tests rc=$rc: $(tail -1 $O/tests.log)"; [ $rc -le 1 ] || exit $rc
+  for i in 1 2 3; do
+    timeout -k 10 180 python3 -u bench.py --no-cpu --alt-precision "" > $O/bench_$i.log 2>&1 || exit 22
+    echo "bench $i: $(grep -o '"ms_per_step": [0-9.]*' $O/bench_$i.log)"
+  done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench \
+    -- python3 bench.py --steps 20 --warmup 5 --no-cpu --alt-precision "" > $O/trace.log 2>&1 || exit 12
+  ;;
+esac

@@ -121,6 +121,21 @@ __global__ __launch_bounds__(NT) void ln_bwd_dx_kernel(
     float* __restrict__ Dout, uint16_t* __restrict__ dOb) {
   __shared__ float coef[3][64];
   const int g0 = blockIdx.y * per_group, g1 = min(rows, g0 + per_group);
+  const long long i = blockIdx.x * (long long)NT + threadIdx.x;
+  const bool live = i < E / 4;
+  // the group's loads all in flight before the arithmetic (per_group <=
+  // LN_GROUP), issued ahead of the per-sample coefficients' dependent loads
+  // below so that both memory rounds overlap
+  float4 vv[LN_GROUP], dd[LN_GROUP];
+#pragma unroll
+  for (int k = 0; k < LN_GROUP; ++k) {
+    const int b = g0 + k;
+    if (live && b < g1) {
+      vv[k] = ((const float4*)(x + (long long)b * E))[i];
+      dd[k] = ((const float4*)(dy + (long long)b * E))[i];
+    }
+  }
+  const float4 ww = live ? aff4(w, i, ch, ch ? (int)(E / ch) : 0) : make_float4(0.f, 0.f, 0.f, 0.f);
   // per-sample coefficients: rstd, mean(g), mean(g xhat)
   for (int b = g0 + threadIdx.x; b < g1; b += NT) {
     float sg, sgx;
@@ -130,20 +145,8 @@ __global__ __launch_bounds__(NT) void ln_bwd_dx_kernel(
     coef[2][b - g0] = sgx / (float)E;
   }
   __syncthreads();
-  const long long i = blockIdx.x * (long long)NT + threadIdx.x;
-  if (i >= E / 4) return;
-  const float4 ww = aff4(w, i, ch, ch ? (int)(E / ch) : 0);
+  if (!live) return;
   float4 dw = make_float4(0.f, 0.f, 0.f, 0.f), db = dw;
-  // the group's loads all in flight before the arithmetic (per_group <= LN_GROUP)
-  float4 vv[LN_GROUP], dd[LN_GROUP];
-#pragma unroll
-  for (int k = 0; k < LN_GROUP; ++k) {
-    const int b = g0 + k;
-    if (b < g1) {
-      vv[k] = ((const float4*)(x + (long long)b * E))[i];
-      dd[k] = ((const float4*)(dy + (long long)b * E))[i];
-    }
-  }
 #pragma unroll
   for (int k = 0; k < LN_GROUP; ++k) {
     const int b = g0 + k;

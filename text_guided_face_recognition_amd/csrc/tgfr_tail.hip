@@ -566,6 +566,32 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
     lds_st8(B_DP + img_at<TD>(m, 4 * lane), v);
     if (row < rows) *(uint2*)(dPb + (long long)row * TD + 4 * lane) = v;
   }
+  // LN: the X / affine values (and the two samples' statistics) the epilogue's
+  // LayerNorm sums read, issued here so that their latency hides behind the
+  // three GEMMs instead of trailing the kernel (64 registers; the LDS already
+  // limits the CU to two workgroups, whose register budget this fits)
+  float lx[MT][16][2], lw[MT][16][2], lm0 = 0.f, lr0 = 0.f, lm1 = 0.f, lr1 = 0.f;
+  if constexpr (LN) {
+    const int s0 = row0 / L.hw;
+    lm0 = L.stats[s0];
+    lr0 = L.stats[L.n + s0];
+    if (s0 + 1 < L.n) {
+      lm1 = L.stats[s0 + 1];
+      lr1 = L.stats[L.n + s0 + 1];
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = min(row0 + 32 * mt + acc_row(q, h), rows - 1), p = row % L.hw;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const int c = 64 * w + 32 * ct + lr;
+          lx[mt][q][ct] = L.X[(long long)row * TC + c];
+          lw[mt][q][ct] = L.w[(long long)p * TC + c];
+        }
+      }
+  }
   __syncthreads();
 
   // dH2^T[j][m] = sum_n Wp[n][j] dP[m][n] (A = Wp^T rows); wave w: j in [64w, 64w+64)
@@ -697,9 +723,6 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
     }
   if constexpr (LN) {
     const int s0 = row0 / L.hw;
-    const bool two = s0 + 1 < L.n;
-    const float m0 = L.stats[s0], r0 = L.stats[L.n + s0];
-    const float m1 = two ? L.stats[s0 + 1] : 0.f, r1 = two ? L.stats[L.n + s0 + 1] : 0.f;
     float sg[2] = {0.f, 0.f}, sgx[2] = {0.f, 0.f};
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -707,13 +730,12 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
       for (int q = 0; q < 16; ++q) {
         const int row = row0 + 32 * mt + acc_row(q, h);
         if (row >= rows) continue;
-        const int p = row % L.hw, sl = row / L.hw - s0;
-        const float mean = sl ? m1 : m0, rstd = sl ? r1 : r0;
+        const int sl = row / L.hw - s0;
+        const float mean = sl ? lm1 : lm0, rstd = sl ? lr1 : lr0;
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
-          const int c = 64 * w + 32 * ct + lr;
-          const float g = acc[mt][ct][q] * L.w[(long long)p * TC + c];
-          const float xh = (L.X[(long long)row * TC + c] - mean) * rstd;
+          const float g = acc[mt][ct][q] * lw[mt][q][ct];
+          const float xh = (lx[mt][q][ct] - mean) * rstd;
           if (sl) { sg[1] += g; sgx[1] += g * xh; }
           else { sg[0] += g; sgx[0] += g * xh; }
         }

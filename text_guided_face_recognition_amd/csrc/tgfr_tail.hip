@@ -595,6 +595,7 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
   __syncthreads();
 
   // dH2^T[j][m] = sum_n Wp[n][j] dP[m][n] (A = Wp^T rows); wave w: j in [64w, 64w+64)
+  bf16x8 g2[TC / 16];
   {
     // relu masks first: H2[m][j0..j0+3] for this lane's accumulator quads
     uint2 msk[2][MT][4];
@@ -628,6 +629,9 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
           acc[jt][mt] =
               __builtin_amdgcn_mfma_f32_32x32x16_bf16(gld16(frag_ptr(pk, OFF_WPT, TD, 2 * w + jt, s, lane)), b[mt], acc[jt][mt], 0, 0, 0);
     }
+    // the next GEMM's W2^T fragments, loaded across this phase's barrier
+#pragma unroll
+    for (int s = 0; s < TC / 16; ++s) g2[s] = gld16(frag_ptr(pk, OFF_W2T, TC, w, s, lane));
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
@@ -649,6 +653,7 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
   copy_out<TC>(B_DH2, dH2b, TC, row0, rows, tid);
 
   // dH1^T[i][m] = sum_j W2[j][i] dH2[m][j] (A = W2^T rows); wave w: i in [32w, 32w+32)
+  bf16x8 g1[TH / 16][2];
   {
     uint2 msk[MT][4];
 #pragma unroll
@@ -669,9 +674,13 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const bf16x8 b = as_bf8(lds_ld16(B_DH2 + img<TC>(32 * mt + lr, 2 * s + h)));
-        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gld16(frag_ptr(pk, OFF_W2T, TC, w, s, lane)), b, acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(g2[s], b, acc[mt], 0, 0, 0);
       }
     }
+#pragma unroll
+    for (int s = 0; s < TH / 16; ++s)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) g1[s][ct] = gld16(frag_ptr(pk, OFF_W1T, TH, 2 * w + ct, s, lane));
     // the dP image is dead (every wave passed the barrier before this GEMM)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -708,7 +717,7 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
-        acc[mt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mt], gld16(frag_ptr(pk, OFF_W1T, TH, 2 * w + ct, s, lane)), acc[mt][ct], 0, 0, 0);
+        acc[mt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mt], g1[s][ct], acc[mt][ct], 0, 0, 0);
   }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)

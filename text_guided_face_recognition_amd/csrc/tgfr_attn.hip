@@ -501,25 +501,14 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(
 // dQr = dS Kr: one 4-wave workgroup per (sample, pair of query tiles); wave w
 // computes query tile 2 j + (w & 1), output columns [128 (w >> 1), +128) -- all
 // four SIMDs busy (the 2-wave version, one query tile per wave, left two idle)
-// and half the MFMA chain per wave.  The Kr tiles stream through a DMA ring
-// (rolled loop); each query tile's dS rows are staged in LDS first by its two
-// waves (464-B rows: conflict-free ds_read_b128).
+// and half the MFMA chain per wave.  All the sample's Kr tiles are DMA-staged
+// at once (7 x 16 KiB), together with each query tile's dS rows (staged by
+// its two waves, 464-B rows: conflict-free ds_read_b128).
 constexpr int Q_NS = 7;
 constexpr int DS_PITCH = 464;
 constexpr int Q_LDS = Q_NS * IMG + 2 * 32 * DS_PITCH;
 
-// ring_wait8 for rings of 4 pieces per wave per stage
-__device__ __forceinline__ void ring_wait4(int younger) {
-  switch (younger) {
-    case 0: ring_barrier<0>(); break;
-    case 1: ring_barrier<4>(); break;
-    case 2: ring_barrier<8>(); break;
-    case 3: ring_barrier<12>(); break;
-    case 4: ring_barrier<16>(); break;
-    case 5: ring_barrier<20>(); break;
-    default: ring_barrier<24>(); break;
-  }
-}
+static_assert(Q_NS >= AT, "attn_bwd_q stages every key tile of a sample at once");
 
 __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const uint16_t* __restrict__ Kp,
                                                          long long ld, long long sb, int hw,
@@ -533,29 +522,27 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(const uint16_t* __restr
   const int b = wid / np, qt = 2 * (wid % np) + qsel;
   const uint16_t* Kb = Kp + b * sb;
   const uint32_t dsimg = Q_NS * IMG + qsel * 32 * DS_PITCH;
-  // the query tile's 32 dS rows (kp bf16 each) -> LDS, half by each of its
-  // two waves; plain loads, drained before the ring starts so its counted
-  // waits see only DMA (the first ring wait publishes the rows)
+  // every Kr tile (nt <= AT = Q_NS: the whole sample fits) goes out by DMA
+  // first, then the query tile's 32 dS rows (kp bf16 each) -> LDS, half by
+  // each of its two waves, with plain loads: both in ONE memory round (the
+  // dS stores wait for their loads, the youngest, so every DMA piece has
+  // landed too); one barrier then publishes all of it
+  for (int st = 0; st < nt; ++st) dma_tile(Kb, ld, 32 * st, hw, st * IMG, w, 4, lane);
   for (int i = lane + 64 * dh; i < 32 * (kp / 8); i += 128) {
     const int r = i / (kp / 8), c8 = i % (kp / 8), q = 32 * qt + r;
     const uint4 v = q < hw ? *(const uint4*)(dS + ((long long)b * hw + q) * kp + 8 * c8)
                            : make_uint4(0, 0, 0, 0);
     lds_st16(dsimg + r * DS_PITCH + 16 * c8, v);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ring_barrier<0>();
   constexpr int NTD = AD / 32 / 2;                   // d tiles per wave
   f32x16 acc[NTD];
 #pragma unroll
   for (int t = 0; t < NTD; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  for (int st = 0; st < Q_NS - 1 && st < nt; ++st)
-    dma_tile(Kb, ld, 32 * st, hw, st * IMG, w, 4, lane);
   for (int kt = 0; kt < nt; ++kt) {
-    ring_wait4(min(Q_NS - 2, nt - 1 - kt));
-    if (kt + Q_NS - 1 < nt)
-      dma_tile(Kb, ld, 32 * (kt + Q_NS - 1), hw, ((kt + Q_NS - 1) % Q_NS) * IMG, w, 4, lane);
-    const uint32_t buf = (kt % Q_NS) * IMG;
+    const uint32_t buf = kt * IMG;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 a = as_bf8(lds_ld16(dsimg + lr * DS_PITCH + 2 * (32 * kt + 16 * s2 + 8 * h)));

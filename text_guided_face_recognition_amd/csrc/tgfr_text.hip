@@ -206,10 +206,15 @@ __global__ __launch_bounds__(TC_NT) void text_conv_kernel(
   constexpr int NS = G::NS, STG = G::STG, PER = G::PER, XP = G::X_PIECES;
   const int mt_n = gridDim.y;
   const int wid_ = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * mt_n);
-  // an XCD takes consecutive row tiles x all 8 channel tiles: its X rows are
-  // read from HBM once, the 3.5 MB of bf16 taps stay in its L2
-  const int tn = wid_ % (TH_D / TC_TN);
-  const int tm = wid_ / (TH_D / TC_TN);
+  // channel-tile major: the 8 channel tiles <-> the 8 XCDs (consecutive work
+  // indices share an XCD), so an XCD's taps are one channel tile's 442 KB,
+  // resident in its 4 MB L2 for all the row tiles, and only X (6.5 MB, one
+  // read per XCD, MALL-resident) streams.  Alone the two mappings time the
+  // same (30.2 / 30.6 us); beside the main stream's kernels, whose data
+  // shares the L2, row-tile major (every XCD cycling all 3.5 MB of taps)
+  // made the step 0.414-0.419 ms against 0.408-0.413 (gpurun_out/r6aa).
+  const int tn = wid_ / mt_n;
+  const int tm = wid_ % mt_n;
   const int m0 = tm * TC_TM, n0 = tn * TC_TN;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
   const int wm = wid & 1, ks = (wid >> 1) & 1, tg = wid >> 2;

@@ -109,11 +109,11 @@ def test_overlapped_grad_reduce_graphed(gpu, precision, monkeypatch):
 
     def build():
         torch.manual_seed(5)
-        args = make_args(batch_size=16, num_classes=300, precision=precision,
-                         bert_words_num=32)
+        args = make_args(batch_size=b, num_classes=300, precision=precision,
+                         bert_words_num=words)
         return Train(args, gpu, DistContext(ReplicaGroup(4)))
 
-    batch = synthetic_batch(16, 30, gpu, seed=9, n_ids=300, bert_hidden=True)
+    batch = synthetic_batch(b, words - 2, gpu, seed=9, n_ids=300, bert_hidden=True)
     eager, graphed = build(), build()
     outs_e = [eager.step(batch) for _ in range(5)]
     gs = GraphedStep(graphed, tuple(t.clone() for t in batch), warmup=3)
@@ -186,13 +186,15 @@ def test_dp_glue_kernels(gpu):
     assert torch.equal(got2, got)
 
 
-@pytest.mark.parametrize("precision", ["bf16", "fp16"])
-def test_dp_forked_step_matches_linear(gpu, precision, monkeypatch):
+@pytest.mark.parametrize("precision,b,words", [("bf16", 16, 32), ("fp16", 16, 32),
+                                               ("fp16", 128, 64)])
+def test_dp_forked_step_matches_linear(gpu, precision, b, words, monkeypatch):
     """Train._step_forked_dp (two streams, three collectives: the text gather,
     ONE merged all-gather of the three losses' partials, one gradient
     all-reduce) against the linear DP step (six collectives and a join), one
     process as rank 0 of 4 replicas (dist.ReplicaGroup): the same losses and
-    parameters after three steps, eagerly and replayed as graphs."""
+    parameters after three steps, eagerly and replayed as graphs.  b = 128 at
+    64-token captions is configs[4]'s per-rank shape (forked since round 6)."""
     from text_guided_face_recognition_amd.config import make_args
     from text_guided_face_recognition_amd.dist import DistContext, ReplicaGroup
     from text_guided_face_recognition_amd.train import GraphedStep, Train, synthetic_batch
@@ -200,11 +202,11 @@ def test_dp_forked_step_matches_linear(gpu, precision, monkeypatch):
     def build(fork):
         monkeypatch.setenv("TGFR_FORK", fork)
         torch.manual_seed(5)
-        args = make_args(batch_size=16, num_classes=300, precision=precision,
-                         bert_words_num=32)
+        args = make_args(batch_size=b, num_classes=300, precision=precision,
+                         bert_words_num=words)
         return Train(args, gpu, DistContext(ReplicaGroup(4)))
 
-    batch = synthetic_batch(16, 30, gpu, seed=9, n_ids=300, bert_hidden=True)
+    batch = synthetic_batch(b, words - 2, gpu, seed=9, n_ids=300, bert_hidden=True)
     lin, frk, gfr = build("0"), build("2"), build("2")
     assert lin._side is None and frk._side is not None
     outs_l = [lin.step(batch) for _ in range(3)]

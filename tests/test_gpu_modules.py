@@ -107,11 +107,14 @@ def test_sent_global_fused(gpu, n):
         assert _relerr(xg.grad, g["d_cnn"]) < 1e-4
 
 
-@pytest.mark.parametrize("n_r,world", [(64, 8), (16, 3), (37, 2), (64, 1)])
+@pytest.mark.parametrize("n_r,world", [(64, 8), (16, 3), (37, 2), (64, 1), (128, 2), (100, 3),
+                                       (128, 1)])
 def test_sent_global_dist_ranks(gpu, n_r, world):
     """The per-rank sent_loss + global_loss kernels (tgfr_sent_global_dist_*,
-    the one-process-per-GPU stage-1 path) with `world` ranks emulated in one
-    process through the C ABI: every rank's forward, the column partials
+    the one-process-per-GPU stage-1 path; n_r > 64 -- configs[4]'s 128 per
+    rank -- in two 64-row tiles, each with its own column partials) with
+    `world` ranks emulated in one process through the C ABI: every rank's
+    forward, the column partials
     concatenated rank-major (what the all-gather delivers), every rank's loss
     and backward.  The summed contributions equal the oracle's global-batch
     losses (1e-4) and the stacked row gradients of s0 + 2 s1 + 3 gl its
@@ -521,7 +524,8 @@ def test_arc_head_fused(gpu, b, d, c, easy, precision):
 
 
 @pytest.mark.parametrize("b,c,precision", [(64, 4500, "fp32"), (64, 4500, "bf16"),
-                                             (17, 300, "fp32")])
+                                             (17, 300, "fp32"), (128, 4500, "fp32"),
+                                             (100, 300, "fp32")])
 def test_identity_heads(gpu, b, c, precision):
     """Both identity heads of the stage-1 step in one launch per direction
     (kernels.IdentityHeads: two ArcMargin heads, two focal losses, the focal

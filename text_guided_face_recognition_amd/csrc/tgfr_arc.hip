@@ -757,7 +757,9 @@ int tgfr_arc_fwd_heads(const tgfr_arc_head* heads, int n_heads, int B, int D, in
 
 int tgfr_arc_focal_bwd_heads(const tgfr_arc_head* heads, int n_heads, int B, int D, int C,
                              float m, int easy, float eps, float gamma, void* stream) {
-  if (!heads || n_heads < 1 || n_heads > 2 || B <= 0 || B > 64 || C <= 0 || D <= 0 || D % 4 ||
+  // (B <= 128: one row slice of every batch row per class block -- the
+  // focal source needs the whole row -- staged in 16-row x chunks past 64)
+  if (!heads || n_heads < 1 || n_heads > 2 || B <= 0 || B > 128 || C <= 0 || D <= 0 || D % 4 ||
       D > 1024)
     return 1001;
   for (int k = 0; k < n_heads; ++k)

@@ -257,6 +257,7 @@ __global__ void focal_global_kernel(int phase, float* __restrict__ sums, int wor
 // backward is one launch of n row workgroups (softmax gradients of both
 // losses folded into one dcos, then the cosine backward to img).
 constexpr int SG_N = 64;
+constexpr int SGD_MAXR = 2 * SG_N;     // rows per rank of the dist kernels (row tiles of 64)
 
 // 8 fp32 -> bf16x8 hi and lo = bf16(x - hi) by packed conversions
 __device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8& hi, bf16x8& lo) {
@@ -467,21 +468,22 @@ __global__ __launch_bounds__(256) void sg_bwd_kernel(
 }
 
 // --------------------------- sent_loss + global_loss, rows x global columns ---
-// The same two losses when this rank holds n_r <= 64 images (global rows
+// The same two losses when this rank holds n_r <= 128 images (global rows
 // row_offset ..) against n_c all-gathered captions (DataParallel over
 // processes, or one process with n > 64): three launches and, with a process
 // group, ONE all-gather between the first two.
-//   sgd_fwd   grid = 64-column tiles: the tile's cosines (sg_cos_tile), per
-//             (set, row) the tile's online (max, sum exp) partial and per (set,
-//             column) the column's (max, sum exp) over this rank's rows -- the
-//             column partials are what the ranks exchange
+//   sgd_fwd   grid = 64-column tiles x 64-row tiles: the tile's cosines
+//             (sg_cos_tile), per (set, row) the tile's online (max, sum exp)
+//             partial and per (set, column) the column's (max, sum exp) over
+//             the row tile's rows -- the column partials (one set per row
+//             tile) are what the ranks exchange
 //   sgd_loss  one workgroup: column LSEs from every rank's partials, row LSEs
 //             from the tiles', this rank's four CE contributions (/ N_global)
 //   sgd_bwd   one workgroup per row: both losses' softmax gradients folded into
 //             one dcos per column, then the cosine backward (as sg_bwd)
 // Sets: 0 = sent (gamma3, same-class off-diagonal entries masked), 1 = global
-// (temp3).  Layouts: rowpart [2][tiles][n_r][2], colpart [2][2][n_c] (max,
-// sum), stats = row LSE [2][n_r] then column LSE [2][n_c].
+// (temp3).  Layouts: rowpart [2][tiles][n_r][2], colpart [row tiles][2][2][n_c]
+// (max, sum), stats = row LSE [2][n_r] then column LSE [2][n_c].
 __device__ __forceinline__ void lse_push(float& m, float& sum, float L) {
   if (L > m) {
     sum = sum * __expf(m - L) + 1.f;
@@ -506,23 +508,25 @@ __global__ __launch_bounds__(SG_T) void sgd_fwd_kernel(
   __shared__ long long clr[SG_N], clc[SG_N];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tile = blockIdx.x, tiles = gridDim.x, c0 = tile * SG_N;
-  const int n_y = min(SG_N, n_c - c0);
-  if (tid < n_r) clr[tid] = cls[row_offset + tid];
+  const int rt = blockIdx.y, r0 = rt * SG_N;            // this block's row tile
+  const int n_y = min(SG_N, n_c - c0), n_x = min(SG_N, n_r - r0);
+  if (tid < n_x) clr[tid] = cls[row_offset + r0 + tid];
   if (tid < n_y) clc[tid] = cls[c0 + tid];
-  sg_cos_tile(x, ldx, n_r, y + (long long)c0 * ldy, ldy, n_y, eps, cs, nxp, nyp);
-  for (int e = tid; e < n_r * n_y; e += SG_T)
-    cosv[(long long)(e / n_y) * n_c + c0 + e % n_y] = cs[(e / n_y) * (SG_N + 1) + e % n_y];
+  sg_cos_tile(x + (long long)r0 * ldx, ldx, n_x, y + (long long)c0 * ldy, ldy, n_y, eps, cs, nxp,
+              nyp);
+  for (int e = tid; e < n_x * n_y; e += SG_T)
+    cosv[(long long)(r0 + e / n_y) * n_c + c0 + e % n_y] = cs[(e / n_y) * (SG_N + 1) + e % n_y];
   // ls = w >> 2: 0 sent rows, 1 sent columns, 2 global rows, 3 global columns;
   // row / column j = 16 (w & 3) + lane / 4, four lanes each
   const int ls = w >> 2, j = 16 * (w & 3) + (lane >> 2), sub = lane & 3;
   const bool glob = ls >= 2, col = ls & 1;
   const float sc = glob ? s_glob : s_sent;
-  const int nj = col ? n_y : n_r, nk = col ? n_r : n_y;
+  const int nj = col ? n_y : n_x, nk = col ? n_x : n_y;
   float m = -INFINITY, sum = 0.f;
   if (j < nj) {
     for (int k = sub; k < nk; k += 4) {
       const int b = col ? k : j, i = col ? j : k;
-      if (!glob && clr[b] == clc[i] && row_offset + b != c0 + i) continue;
+      if (!glob && clr[b] == clc[i] && row_offset + r0 + b != c0 + i) continue;
       lse_push(m, sum, sc * cs[b * (SG_N + 1) + i]);
     }
   }
@@ -531,36 +535,41 @@ __global__ __launch_bounds__(SG_T) void sgd_fwd_kernel(
   if (j < nj && sub == 0) {
     const int set = glob ? 1 : 0;
     if (col) {
-      colpart[(set * 2 + 0) * n_c + c0 + j] = m;
-      colpart[(set * 2 + 1) * n_c + c0 + j] = sum;
+      float* cp = colpart + (long long)rt * 4 * n_c;
+      cp[(set * 2 + 0) * n_c + c0 + j] = m;
+      cp[(set * 2 + 1) * n_c + c0 + j] = sum;
     } else {
-      float* rp = rowpart + (((long long)set * tiles + tile) * n_r + j) * 2;
+      float* rp = rowpart + (((long long)set * tiles + tile) * n_r + r0 + j) * 2;
       rp[0] = m;
       rp[1] = sum;
     }
   }
-  if (tile == 0 && tid < n_r) nrm[tid] = sqrtf(nxp[0][tid] + nxp[1][tid] + nxp[2][tid] + nxp[3][tid]);
-  if (tid < n_y) nrm[n_r + c0 + tid] = sqrtf(nyp[0][tid] + nyp[1][tid] + nyp[2][tid] + nyp[3][tid]);
+  if (tile == 0 && tid < n_x)
+    nrm[r0 + tid] = sqrtf(nxp[0][tid] + nxp[1][tid] + nxp[2][tid] + nxp[3][tid]);
+  if (rt == 0 && tid < n_y)
+    nrm[n_r + c0 + tid] = sqrtf(nyp[0][tid] + nyp[1][tid] + nyp[2][tid] + nyp[3][tid]);
 }
 
 __global__ __launch_bounds__(SG_T) void sgd_loss_kernel(
     const float* __restrict__ cosv, int n_r, int n_c, int row_offset, float s_sent, float s_glob,
     int tiles, const float* __restrict__ rowpart, const float* __restrict__ colparts, int world,
     long long ld_parts, float inv_n, float* __restrict__ stats, float* __restrict__ loss) {
-  __shared__ float rl[2][SG_N], cl[2][SG_N];
+  __shared__ float rl[2][SGD_MAXR], cl[2][SGD_MAXR];
   __shared__ float red[SG_T / WAVE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   float* row_lse = stats;
   float* col_lse = stats + 2 * n_r;
-  // column LSEs over every rank's partials (rank r's [2 sets][2][n_c] at
-  // colparts + r * ld_parts)
+  // column LSEs over every rank's partials (rank r's [row tiles][2 sets][2][n_c]
+  // at colparts + r * ld_parts; every rank holds n_r rows, so as many tiles)
+  const int rtiles = (n_r + SG_N - 1) / SG_N;
   for (int e = tid; e < 2 * n_c; e += SG_T) {
     const int set = e / n_c, c = e % n_c;
     float m = -INFINITY, sum = 0.f;
-    for (int r = 0; r < world; ++r) {
-      const float* cp = colparts + (long long)r * ld_parts + set * 2 * n_c;
-      lse_merge(m, sum, cp[c], cp[n_c + c]);
-    }
+    for (int r = 0; r < world; ++r)
+      for (int t = 0; t < rtiles; ++t) {
+        const float* cp = colparts + (long long)r * ld_parts + ((long long)t * 2 + set) * 2 * n_c;
+        lse_merge(m, sum, cp[c], cp[n_c + c]);
+      }
     const float lse = m + __logf(sum);
     col_lse[set * n_c + c] = lse;
     const int b = c - row_offset;
@@ -580,20 +589,21 @@ __global__ __launch_bounds__(SG_T) void sgd_loss_kernel(
   }
   __syncthreads();
   // this rank's diagonal terms: waves 0-3 sent rows / sent columns / global
-  // rows / global columns
+  // rows / global columns of rows 0-63, waves 4-7 the same of rows 64-127
   float term = 0.f;
-  if (w < 4 && lane < n_r) {
-    const int set = w >> 1;
-    const float d = (set ? s_glob : s_sent) * cosv[(long long)lane * n_c + row_offset + lane];
-    term = ((w & 1) ? cl[set][lane] : rl[set][lane]) - d;
+  const int db = lane + SG_N * (w >> 2);
+  if (w < 8 && db < n_r) {
+    const int set = (w >> 1) & 1;
+    const float d = (set ? s_glob : s_sent) * cosv[(long long)db * n_c + row_offset + db];
+    term = ((w & 1) ? cl[set][db] : rl[set][db]) - d;
   }
   term = wave_sum(term);
   if (lane == 0) red[w] = term;
   __syncthreads();
   if (tid == 0) {
-    loss[0] = red[0] * inv_n;                // sent loss0 (rows)
-    loss[1] = red[1] * inv_n;                // sent loss1 (columns)
-    loss[2] = (red[2] + red[3]) * inv_n;     // global loss0 + loss1
+    loss[0] = (red[0] + red[4]) * inv_n;                        // sent loss0 (rows)
+    loss[1] = (red[1] + red[5]) * inv_n;                        // sent loss1 (columns)
+    loss[2] = ((red[2] + red[6]) + (red[3] + red[7])) * inv_n;  // global loss0 + loss1
   }
 }
 
@@ -705,10 +715,10 @@ int tgfr_sent_global_bwd(const float* gs0, const float* gs1, const float* ggl, c
 
 int tgfr_sent_global_dist_ws(int n_r, int n_c, long long* rowpart, long long* colpart,
                              long long* stats) {
-  if (n_r <= 0 || n_r > SG_N || n_c <= 0 || n_c > 8192 || !rowpart || !colpart || !stats)
+  if (n_r <= 0 || n_r > SGD_MAXR || n_c <= 0 || n_c > 8192 || !rowpart || !colpart || !stats)
     return 1001;
   *rowpart = 2ll * ((n_c + SG_N - 1) / SG_N) * n_r * 2;
-  *colpart = 4ll * n_c;
+  *colpart = 4ll * n_c * ((n_r + SG_N - 1) / SG_N);
   *stats = 2ll * (n_r + n_c);
   return 0;
 }
@@ -717,12 +727,13 @@ int tgfr_sent_global_dist_fwd(const float* x, long long ldx, int n_r, const floa
                               long long ldy, int n_c, const long long* cls, int row_offset,
                               float s_sent, float s_glob, float eps, float* cosv, float* rowpart,
                               float* colpart, float* nrm, void* stream) {
-  if (n_r <= 0 || n_r > SG_N || n_c <= 0 || n_c > 8192 || row_offset < 0 ||
+  if (n_r <= 0 || n_r > SGD_MAXR || n_c <= 0 || n_c > 8192 || row_offset < 0 ||
       row_offset + n_r > n_c || !x || !y || !cls || !cosv || !rowpart || !colpart || !nrm ||
       ldx % 4 || ldy % 4 || ((uintptr_t)x & 15) || ((uintptr_t)y & 15))
     return 1001;
   if (const int e = set_max_lds((const void*)sgd_fwd_kernel, SG_LDS)) return e;
-  hipLaunchKernelGGL(sgd_fwd_kernel, dim3((n_c + SG_N - 1) / SG_N), dim3(SG_T), SG_LDS,
+  hipLaunchKernelGGL(sgd_fwd_kernel, dim3((n_c + SG_N - 1) / SG_N, (n_r + SG_N - 1) / SG_N),
+                     dim3(SG_T), SG_LDS,
                      (hipStream_t)stream, x, ldx, n_r, y, ldy, n_c, cls, row_offset, s_sent,
                      s_glob, eps, cosv, rowpart, colpart, nrm);
   return (int)hipGetLastError();
@@ -732,11 +743,12 @@ int tgfr_sent_global_dist_loss(const float* cosv, int n_r, int n_c, int row_offs
                                float s_glob, const float* rowpart, const float* colparts,
                                int world, long long ld_parts, float inv_n, float* stats,
                                float* loss, void* stream) {
-  if (n_r <= 0 || n_r > SG_N || n_c <= 0 || world <= 0 || !cosv || !rowpart || !colparts ||
+  if (n_r <= 0 || n_r > SGD_MAXR || n_c <= 0 || world <= 0 || !cosv || !rowpart || !colparts ||
       !stats || !loss)
     return 1001;
-  if (ld_parts == 0) ld_parts = 4LL * n_c;
-  if (ld_parts < 4LL * n_c) return 1001;
+  const long long cp = 4LL * n_c * ((n_r + SG_N - 1) / SG_N);    // one rank's column partials
+  if (ld_parts == 0) ld_parts = cp;
+  if (ld_parts < cp) return 1001;
   hipLaunchKernelGGL(sgd_loss_kernel, dim3(1), dim3(SG_T), 0, (hipStream_t)stream, cosv, n_r, n_c,
                      row_offset, s_sent, s_glob, (n_c + SG_N - 1) / SG_N, rowpart, colparts,
                      world, ld_parts, inv_n, stats, loss);
@@ -749,8 +761,8 @@ int tgfr_sent_global_dist_bwd(const float* gs0, const float* gs1, const float* g
                               float s_sent, float s_glob, float eps, float inv_n,
                               const float* cosv, const float* stats, const float* nrm, float* dx,
                               long long lddx, void* stream) {
-  if (n_r <= 0 || n_r > SG_N || n_c <= 0 || n_c > 8192 || !x || !y || !cls || !cosv || !stats ||
-      !nrm || !dx)
+  if (n_r <= 0 || n_r > SGD_MAXR || n_c <= 0 || n_c > 8192 || !x || !y || !cls || !cosv ||
+      !stats || !nrm || !dx)
     return 1001;
   hipLaunchKernelGGL(sgd_bwd_kernel, dim3(n_r), dim3(256), n_c * sizeof(float),
                      (hipStream_t)stream, gs0, gs1, ggl, x, ldx, n_r, y, ldy, n_c, cls,

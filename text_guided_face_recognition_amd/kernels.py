@@ -600,7 +600,7 @@ def _sgd_ws(n_r, n_c):
 
 
 class SentGlobalDist(torch.autograd.Function):
-    """SentGlobal for this rank's n_r <= 64 images (global rows row_offset ..)
+    """SentGlobal for this rank's n_r <= 128 images (global rows row_offset ..)
     against n_c gathered captions: cosines and both losses' row / column
     partials in one launch over column tiles, ONE all-gather of the column
     partials of both losses (with a process group), one loss launch; backward
@@ -1927,7 +1927,7 @@ def _heads_fwd(x_t, w_t, x_i, w_i, label, s_t, s_i, m, easy, eps, gamma):
 class IdentityHeads(torch.autograd.Function):
     """The stage-1 step's two identity losses, focal(ArcMargin_text(sent)) and
     focal(ArcMargin_image(img)) (src/train_encoders_bert.py:293-306, one
-    process, B <= 64, heads of one (D, C)): both heads' cosine + margin in one
+    process, B <= 128, heads of one (D, C)): both heads' cosine + margin in one
     launch, both focal losses in one launch; backward: the focal logit
     gradient formed inside the ArcMargin backward of both heads (one launch),
     then dx of the heads whose input is trained (dcs W GEMM + l2-norm

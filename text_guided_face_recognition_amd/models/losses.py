@@ -171,7 +171,7 @@ def sent_global_loss(cnn_code, rnn_code, labels, class_ids, batch_size, args, ep
     """(sent loss0, sent loss1, global loss) = sent_loss(...) and
     global_loss(..., temp3) of the trainer (src/train_encoders_bert.py:276-277,
     :310) on the same features.  One process with the whole batch (n <= 64):
-    one fused kernel each way (kernels.SentGlobal); this rank's <= 64 images
+    one fused kernel each way (kernels.SentGlobal); this rank's <= 128 images
     against the gathered captions (one process per GPU, or n > 64 on one):
     kernels.SentGlobalDist, the same arithmetic over column tiles with ONE
     column-partial exchange for both losses; otherwise the two losses as
@@ -181,9 +181,9 @@ def sent_global_loss(cnn_code, rnn_code, labels, class_ids, batch_size, args, ep
     # the fused kernels return no gradient for the sentence codes (the
     # reference's text side is detached, utils/dataset_utils.py:42); a caller
     # whose codes require grad takes the per-loss path, which computes it
-    if labels is not None and n <= 64 and not rnn_code.requires_grad:
+    if labels is not None and n <= 128 and not rnn_code.requires_grad:
         cls = _class_tensor(class_ids, cnn_code.device)
-        if group is None and n == rnn_code.shape[0]:
+        if n <= 64 and group is None and n == rnn_code.shape[0]:
             return K.sent_global(cnn_code, rnn_code, cls, args.TRAIN.SMOOTH.GAMMA3, temp3, eps)
         if rnn_code.shape[0] <= 8192:
             return K.sent_global_dist(cnn_code, rnn_code, cls, args.TRAIN.SMOOTH.GAMMA3, temp3,

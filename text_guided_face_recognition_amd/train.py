@@ -262,12 +262,13 @@ class Train:
 
     def _dp_forkable(self, batch):
         """The data-parallel forked step needs the fused loss paths: the BERT
-        word<->region path without attention maps, this rank's <= 64 images
-        (sentence / global and identity-head kernels) against <= 8192 gathered
-        captions, and two identity heads of one (D, C) and margin."""
+        word<->region path without attention maps, this rank's <= 128 images
+        (sentence / global and identity-head kernels; configs[4]'s 128 per rank
+        included) against <= 8192 gathered captions, and two identity heads of
+        one (D, C) and margin."""
         tc, ic = self.text_cls, self.image_cls
         b = batch[0].shape[0]
-        return (self.args.en_type == "BERT" and b <= 64 and b * self.ctx.world <= 8192
+        return (self.args.en_type == "BERT" and b <= 128 and b * self.ctx.world <= 8192
                 and tc.weight.shape == ic.weight.shape and tc.m == ic.m
                 and tc.easy_margin == ic.easy_margin)
 
@@ -446,7 +447,7 @@ class Train:
         one all-reduce of the two NLL sums gives the global-batch focal
         factor), else the per-head path."""
         tc, ic = self.text_cls, self.image_cls
-        if (sent.shape[0] <= 64 and tc.weight.shape == ic.weight.shape
+        if (sent.shape[0] <= 128 and tc.weight.shape == ic.weight.shape
                 and tc.m == ic.m and tc.easy_margin == ic.easy_margin):
             return K.identity_heads(sent, tc, img_features, ic, class_ids, self.ident_loss.gamma,
                                     group=ctx.group if ctx.active else None,

@@ -94,3 +94,15 @@ quick)
     -- python3 bench.py --steps 20 --warmup 5 --no-cpu --alt-precision "" > $O/trace.log 2>&1 || exit 12
   ;;
 esac
+case "${STEP}" in
+cfg4fork)
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_modules.py tests/test_gpu_dp.py tests/test_gpu_train.py -m gpu -v -s --timeout 300 --timeout-method thread -k "sent_global or identity or forked or dp_" > $O/tests.log 2>&1
+  rc=$?; echo "tests rc=$rc: $(tail -1 $O/tests.log)"; [ $rc -le 1 ] || exit $rc
+  for e in TGFR_FORK=2 TGFR_FORK=0; do
+    env $e timeout -k 10 300 python3 -u bench.py --batch 128 --words 64 --precision fp16 --simulate-world 8 --alt-precision "" > $O/sim8_cfg5_${e}.log 2>&1 || exit 22
+    echo "$e sim8 cfg5: $(grep -o '"ms_per_step": [0-9.]*' $O/sim8_cfg5_${e}.log)"
+  done
+  timeout -k 10 240 python3 -u bench.py --simulate-world 8 --no-cpu --alt-precision "" > $O/sim8_cfg3.log 2>&1 || exit 23
+  echo "sim8 cfg3: $(grep -o '"ms_per_step": [0-9.]*' $O/sim8_cfg3.log)"
+  ;;
+esac

@@ -106,3 +106,13 @@ cfg4fork)
   echo "sim8 cfg3: $(grep -o '"ms_per_step": [0-9.]*' $O/sim8_cfg3.log)"
   ;;
 esac
+case "${STEP}" in
+order)
+  for i in 1 2 3; do for e in ${VARS:-TGFR_ORDER=a TGFR_ORDER=g}; do
+    env $e timeout -k 10 180 python3 -u bench.py --no-cpu --alt-precision "" > $O/bench_${e}_$i.log 2>&1 || exit 22
+    echo "$e $i: $(grep -o '"ms_per_step": [0-9.]*' $O/bench_${e}_$i.log)"
+  done; done
+  TGFR_ORDER=${TRACE_ORDER:-g} timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o bench \
+    -- python3 bench.py --steps 20 --warmup 5 --no-cpu --alt-precision "" > $O/trace.log 2>&1 || exit 12
+  ;;
+esac

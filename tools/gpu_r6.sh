@@ -116,3 +116,24 @@ order)
     -- python3 bench.py --steps 20 --warmup 5 --no-cpu --alt-precision "" > $O/trace.log 2>&1 || exit 12
   ;;
 esac
+case "${STEP}" in
+textpmc)
+  P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"
+  P2="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
+  timeout -s KILL 120 rocprofv3 --pmc $P1 --kernel-trace --output-format csv -d $O/pmct1 -o t -- python3 tools/text_bench.py --reps 5 > $O/pmct1.log 2>&1 || exit 16
+  timeout -s KILL 120 rocprofv3 --pmc $P2 --kernel-trace --output-format csv -d $O/pmct2 -o t -- python3 tools/text_bench.py --reps 5 > $O/pmct2.log 2>&1 || exit 17
+  echo textpmc ok
+  ;;
+esac
+case "${STEP}" in
+text)
+  timeout -k 10 300 python3 -u -m pytest tests/test_gpu_text.py tests/test_gpu_step_parity.py -m gpu -v -s --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+  rc=$?; echo "tests rc=$rc: $(tail -1 $O/tests.log)"; [ $rc -le 1 ] || exit $rc
+  timeout -k 10 120 python3 -u tools/text_bench.py > $O/text.log 2>&1 || exit 21
+  grep "B=64" $O/text.log
+  for i in 1 2 3; do
+    timeout -k 10 180 python3 -u bench.py --no-cpu --alt-precision "" > $O/bench_$i.log 2>&1 || exit 22
+    echo "bench $i: $(grep -o '"ms_per_step": [0-9.]*' $O/bench_$i.log)"
+  done
+  ;;
+esac

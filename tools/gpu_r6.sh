@@ -137,3 +137,11 @@ text)
   done
   ;;
 esac
+case "${STEP}" in
+sim8prof)
+  mkdir -p $O/prof_sim8
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_sim8/trace -o bench -- python3 bench.py --steps 10 --warmup 3 --no-cpu --alt-precision "" --batch 128 --words 64 --precision fp16 --simulate-world 8 > $O/prof_sim8.trace.log 2>&1 || exit 13
+  timeout -k 10 300 python3 -u bench.py --batch 128 --words 64 --precision fp16 --simulate-world 8 --alt-precision "" > $O/sim8_cfg5.log 2>&1 || exit 14
+  echo "sim8 cfg5: $(grep -o '"ms_per_step": [0-9.]*' $O/sim8_cfg5.log)"
+  ;;
+esac

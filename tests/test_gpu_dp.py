@@ -109,11 +109,11 @@ def test_overlapped_grad_reduce_graphed(gpu, precision, monkeypatch):
 
     def build():
         torch.manual_seed(5)
-        args = make_args(batch_size=b, num_classes=300, precision=precision,
-                         bert_words_num=words)
+        args = make_args(batch_size=16, num_classes=300, precision=precision,
+                         bert_words_num=32)
         return Train(args, gpu, DistContext(ReplicaGroup(4)))
 
-    batch = synthetic_batch(b, words - 2, gpu, seed=9, n_ids=300, bert_hidden=True)
+    batch = synthetic_batch(16, 30, gpu, seed=9, n_ids=300, bert_hidden=True)
     eager, graphed = build(), build()
     outs_e = [eager.step(batch) for _ in range(5)]
     gs = GraphedStep(graphed, tuple(t.clone() for t in batch), warmup=3)

@@ -53,15 +53,8 @@ class StepCapture:
 
     def _begin(self):
         g = torch.cuda.CUDAGraph()
-        if os.environ.get("TGFR_GRAPH_DOT"):      # (tools: dump each graph's DOT)
-            g.enable_debug_mode()
         g.capture_begin(pool=self.pool)
         self.graphs.append(g)
-
-    def dump(self, prefix):
-        """Write each captured graph as DOT (TGFR_GRAPH_DOT set at capture)."""
-        for i, g in enumerate(self.graphs):
-            g.debug_dump(f"{prefix}_{i}.dot")
 
     def cut(self, fn):
         """Close the current graph, run collective `fn` now and at every

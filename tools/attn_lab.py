@@ -39,6 +39,12 @@ VARIANTS = {
     # forward: without the S MFMAs
     "f_nos": [("      sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(kbuf, s, lane), qf[s], sc, 0, 0, 0);",
                "      sc[s] += (float)frag(kbuf, s, lane)[0] + (float)qf[s][1];")],
+    # forward: every key tile read from stage 0 (wrong values): no DMA waits in the loop
+    "f_nodmawait": [("      if (i + 1 < iters) {\n        ring_barrier<0>();\n        issue(i + 1);\n      } else {\n        ring_barrier<0>();\n      }",
+                     "      __syncthreads();"),
+                    ("  if (iters > 1) issue(1);\n", ""),
+                    ("    const uint32_t kbuf = ring + (i & 1) * FWD_STAGE + (2 * half) * IMG, vbuf = kbuf + IMG;",
+                     "    const uint32_t kbuf = ring + (2 * half) * IMG, vbuf = kbuf + IMG;")],
     # forward: without the O stores
     "f_nostore": [("      if (qv)\n        *(float4*)(orow + 32 * t + 8 * g + 4 * h) =",
                    "      if (q < 0)\n        *(float4*)(orow + 32 * t + 8 * g + 4 * h) =")],

@@ -50,3 +50,26 @@ def test_device_only_contract():
     from text_guided_face_recognition_amd import kernels as K
     with pytest.raises(RuntimeError):
         K.cos_logits(torch.randn(4, 256), torch.randn(4, 256), 10.0)
+
+
+def test_round6_argument_contracts():
+    """The round-6 entry points' host-side contracts, checked without a GPU
+    (each call returns before any launch): the sentence / global dist
+    kernels take up to 128 rows per rank in 64-row tiles, one column-partial
+    set per tile (tgfr_sent_global_dist_ws), and reject more; the deferred
+    LayerNorm reduce (tgfr_imim_dw_ln) and the fused identity-head backward
+    reject missing operands with 1001."""
+    import ctypes
+    from text_guided_face_recognition_amd import _hip
+    lib = _hip.lib()
+    out = (ctypes.c_longlong * 3)()
+    a = [ctypes.addressof(out) + 8 * k for k in range(3)]
+    for n_r, n_c, tiles in ((64, 512, 1), (65, 512, 2), (128, 1024, 2)):
+        assert lib.tgfr_sent_global_dist_ws(n_r, n_c, *a) == 0
+        assert out[1] == 4 * n_c * tiles, (n_r, out[1])
+        assert out[0] == 2 * -(-n_c // 64) * n_r * 2
+    assert lib.tgfr_sent_global_dist_ws(129, 1024, *a) == 1001
+    nul = [None] * 25
+    nul[6], nul[15], nul[16], nul[20] = 12544, 768, 256, 196       # rows, Nq, Kq, hw
+    assert lib.tgfr_imim_dw_ln(*nul) == 1001
+    assert lib.tgfr_arc_focal_bwd_heads(None, 2, 128, 256, 4500, 0.5, 0, 1e-12, 2.0, None) == 1001

@@ -35,6 +35,7 @@
 #include "tgfr_ln.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 using namespace tgfr;
@@ -791,6 +792,7 @@ constexpr int DW_MAXP = 4;   // products per launch
 struct DwArgs {
   DwProb p[DW_MAXP];
   int rows, slices, rows_per;
+  int bf16slab;      // 1: the dW slabs in bf16 (half the slab bytes), column sums fp32
 };
 
 // operand fragment from a staged chunk: lane (col c = col0 + lane%32, rows
@@ -920,19 +922,40 @@ __global__ __launch_bounds__(256) void tail_dw_kernel(DwArgs A, float* __restric
   }
 
   // slab [slice][N][K] (+ [slice][N] column sums after all products' dW slabs)
-  float* slab = ws + P.slab + (long long)slice * P.N * P.K;
+  if (A.bf16slab) {
+    // bf16 slab: lanes lr, lr ^ 1 hold adjacent k: they swap one value so each
+    // stores a 4-byte pair -- the even lane row acc_row(q), the odd lane row
+    // acc_row(q + 1)
+    uint16_t* slab = (uint16_t*)(ws + P.slab) + (long long)slice * P.N * P.K;
+    const bool odd = lane & 1;
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int n = bn * DW_NB + 64 * wn + 32 * t + acc_row(q, lane >> 5);
-        const int k = bk * DW_NB + 64 * wk + 32 * u + (lane & 31);
-        slab[(long long)n * P.K + k] = acc[t][u][q];
-      }
+        for (int q = 0; q < 16; q += 2) {
+          const float a = acc[t][u][q], b = acc[t][u][q + 1];
+          const float y = __shfl_xor(odd ? a : b, 1);
+          const int n = bn * DW_NB + 64 * wn + 32 * t + acc_row(odd ? q + 1 : q, lane >> 5);
+          const int k = bk * DW_NB + 64 * wk + 32 * u + ((lane & 31) & ~1);
+          *(uint32_t*)(slab + (long long)n * P.K + k) = odd ? pk_bf16(y, b) : pk_bf16(a, y);
+        }
+  } else {
+    float* slab = ws + P.slab + (long long)slice * P.N * P.K;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int n = bn * DW_NB + 64 * wn + 32 * t + acc_row(q, lane >> 5);
+          const int k = bk * DW_NB + 64 * wk + 32 * u + (lane & 31);
+          slab[(long long)n * P.K + k] = acc[t][u][q];
+        }
+  }
   if (wk == 0 && bk == 0) {
-    float* cslab = ws + P.slab + (long long)A.slices * P.N * P.K + (long long)slice * P.N;
+    float* cslab = ws + P.slab + (long long)A.slices * P.N * P.K / (A.bf16slab ? 2 : 1) +
+                   (long long)slice * P.N;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const float v = xhalf_sum(cs[t]);
@@ -992,6 +1015,19 @@ __global__ __launch_bounds__(256) void tail_dw_reduce_kernel(DwArgs A, DwOut O,
   }
   const DwProb P = A.p[pi];
   const long long nk = (long long)P.N * P.K;
+  if (A.bf16slab && off < nk) {
+    // bf16 dW slabs: one 4-byte pair per slice
+    const uint32_t* bsrc = (const uint32_t*)((const uint16_t*)(ws + P.slab) + off);
+    float2 s = make_float2(0.f, 0.f);
+#pragma unroll 8
+    for (int z = 0; z < A.slices; ++z) {
+      const uint32_t v = bsrc[(long long)z * (nk / 2)];
+      s.x += __uint_as_float(v << 16);
+      s.y += __uint_as_float(v & 0xffff0000u);
+    }
+    *(float2*)(O.dW[pi] + off) = s;
+    return;
+  }
   const float* src;
   long long stride;
   float* dst;
@@ -1000,7 +1036,7 @@ __global__ __launch_bounds__(256) void tail_dw_reduce_kernel(DwArgs A, DwOut O,
     stride = nk;
     dst = O.dW[pi] + off;
   } else {
-    src = ws + P.slab + A.slices * nk + (off - nk);
+    src = ws + P.slab + A.slices * nk / (A.bf16slab ? 2 : 1) + (off - nk);
     stride = P.N;
     dst = O.db[pi] + (off - nk);
   }
@@ -1019,7 +1055,7 @@ __global__ __launch_bounds__(256) void tail_dw_reduce_kernel(DwArgs A, DwOut O,
 // read back once more by the reduce, so fewer slices trade chip fill for
 // traffic)
 void dw_plan_n(int rows, int n, const int* NS, const int* KS, int wg_budget, DwArgs& A,
-               long long& ws_floats, int& n_wg) {
+               long long& ws_floats, int& n_wg, bool bf16slab = false) {
   int blocks = 0;
   for (int i = 0; i < n; ++i) blocks += (NS[i] / DW_NB) * (KS[i] / DW_NB);
   const int want = std::max(1, wg_budget / blocks);
@@ -1027,6 +1063,7 @@ void dw_plan_n(int rows, int n, const int* NS, const int* KS, int wg_budget, DwA
   A.slices = std::min(want, max_slices);
   A.rows_per = ((rows + A.slices - 1) / A.slices + DW_CH - 1) / DW_CH * DW_CH;
   A.rows = rows;
+  A.bf16slab = bf16slab ? 1 : 0;
   long long slab = 0;
   int first = 0;
   for (int i = 0; i < n; ++i) {
@@ -1039,7 +1076,7 @@ void dw_plan_n(int rows, int n, const int* NS, const int* KS, int wg_budget, DwA
     p.slab = slab;
     p.yf32 = 0;
     first += p.nb_n * p.nb_k * A.slices;
-    slab += (long long)A.slices * (p.N * (long long)p.K + p.N);
+    slab += (long long)A.slices * (p.N * (long long)p.K / (bf16slab ? 2 : 1) + p.N);
   }
   for (int i = n; i < DW_MAXP; ++i) {  // unused: no workgroup, nothing to reduce
     A.p[i] = DwProb{nullptr, nullptr, 0, 0, 0, 0, 0, first, slab};
@@ -1339,7 +1376,9 @@ int tgfr_tail_dw(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
 // tools/lab/lib_ab.sh, profiles/r04/fork_ab.txt).
 static void imim_dw_plan(int rows, int Nq, int Kq, DwArgs& A, long long& wsf, int& n_wg) {
   const int NS[4] = {TD, TC, TH, Nq}, KS[4] = {TC, TH, TC, Kq};
-  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg);
+  // bf16 dW slabs (TGFR_DW_F32SLAB=1: fp32, the lab A/B)
+  const char* e = getenv("TGFR_DW_F32SLAB");
+  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg, !(e && atoi(e) == 1));
 }
 
 int tgfr_imim_dw_ws(int rows, int Nq, int Kq, long long* floats) {

@@ -145,3 +145,17 @@ sim8prof)
   echo "sim8 cfg5: $(grep -o '"ms_per_step": [0-9.]*' $O/sim8_cfg5.log)"
   ;;
 esac
+case "${STEP}" in
+abtrace)
+  # tests, interleaved bench A/B of VARS, then one kernel trace per variant
+  timeout -k 10 600 python3 -u -m pytest ${TESTS} -m gpu -q --timeout 200 --timeout-method thread -k "${KEXPR}" > $O/tests.log 2>&1
+  rc=$?; echo "tests rc=$rc: $(tail -1 $O/tests.log)"; [ $rc -le 1 ] || exit $rc
+  for i in 1 2 3; do for e in ${VARS}; do
+    env $e timeout -k 10 180 python3 -u bench.py --no-cpu --alt-precision "" > $O/bench_${e}_$i.log 2>&1 || exit 22
+    echo "$e $i: $(grep -o '"ms_per_step": [0-9.]*' $O/bench_${e}_$i.log)"
+  done; done
+  for e in ${VARS}; do
+    env $e timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$e -o bench -- python3 bench.py --steps 20 --warmup 5 --no-cpu --alt-precision "" > $O/trace_$e.log 2>&1 || exit 12
+  done
+  ;;
+esac

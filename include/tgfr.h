@@ -34,6 +34,7 @@
  *     stores C-hat scaled by 2^-8 and the token-table calls take bounded = 2.
  *   - ABI 610: tgfr_imim_dw_ln; tgfr_ln_tail_bwd / _att accept dlnw = dlnb =
  *     NULL (the LayerNorm's dw / db partials stay in ws for it).
+ *   - ABI 620: tgfr_ln_tail_bwd_att keeps dZ in bf16 (half the scratch).
  */
 #ifndef TGFR_H
 #define TGFR_H
@@ -481,7 +482,9 @@ int tgfr_ln_tail_bwd(const float* dR, const float* R, const float* inv, int rows
  * folded with gamma / beta into Wf, bf) + tgfr_tail_pack_ln, one launch;
  * tgfr_ln_tail_bwd_att = tgfr_ln_tail_bwd writing, instead of dX, the
  * attention backward's operands into att_ws (tgfr_attn_bwd's workspace: D
- * [rows] = rowsum(dX * X), then dX [rows][256] in bf16); tgfr_attn_bwd_prepped
+ * [rows] = rowsum(dX * X), then dX [rows][256] in bf16), with dZ a scratch of
+ * rows x 256 bf16 values (ABI 620: the LayerNorm backward reads dZ in bf16;
+ * a float* of rows x 128 suffices); tgfr_attn_bwd_prepped
  * = tgfr_attn_bwd without its prep pass, reading them from ws. */
 int tgfr_imim_pack(const float* const* Wqkv, const float* const* bqkv, int rows_qkv, int C,
                    const float* gamma, const float* beta, float* Wf, float* bf, const float* W1,

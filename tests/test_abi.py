@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol():
     for name, n in decl.items():
         assert len(_hip.SIGNATURES[name]) == n, (name, n, len(_hip.SIGNATURES[name]))
     lib = _hip.lib()
-    assert lib.tgfr_version() == 610
+    assert lib.tgfr_version() == 620
     assert lib.tgfr_wr_lds_bytes(0) < 160 * 1024 and lib.tgfr_wr_lds_bytes(1) < 160 * 1024
 
 

@@ -132,7 +132,13 @@ __global__ __launch_bounds__(NT) void ln_bwd_dx_kernel(
     const int b = g0 + k;
     if (live && b < g1) {
       vv[k] = ((const float4*)(x + (long long)b * E))[i];
-      dd[k] = ((const float4*)(dy + (long long)b * E))[i];
+      if constexpr (ATT) {   // dy: the tail backward's bf16 dZ rows
+        const uint2 u = ((const uint2*)((const uint16_t*)dy + (long long)b * E))[i];
+        dd[k] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                            __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+      } else {
+        dd[k] = ((const float4*)(dy + (long long)b * E))[i];
+      }
     }
   }
   const float4 ww = live ? aff4(w, i, ch, ch ? (int)(E / ch) : 0) : make_float4(0.f, 0.f, 0.f, 0.f);

@@ -535,6 +535,7 @@ struct LnBwd {
   const float* w;         // affine w as channels-last rows [hw][TC]
   float* part;            // [gridDim.x][2][2]
   int hw, n;
+  int dzb;                // dZ rows in bf16 (the attention path's LayerNorm dx reads them)
 };
 constexpr int B_RED = B_LDS, B_LDS_LN = B_LDS + 4 * 4 * 4;
 
@@ -720,17 +721,38 @@ __global__ __launch_bounds__(256) void tail_bwd_kernel(
       for (int ct = 0; ct < 2; ++ct)
         acc[mt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mt], g1[s][ct], acc[mt][ct], 0, 0, 0);
   }
+  if (LN && L.dzb) {
+    // bf16 rows (stride lddz elements): lanes lr, lr ^ 1 trade one value so
+    // that the even lane stores row q's column pair and the odd lane row q + 1's
+    uint16_t* dzb = (uint16_t*)dZ;
+    const bool odd = lr & 1;
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int row = row0 + 32 * mt + acc_row(q, h);
-      if (row < rows) {
-        float* o = dZ + (long long)row * lddz + 64 * w + lr;
-        o[0] = acc[mt][0][q];
-        o[32] = acc[mt][1][q];
+      for (int q = 0; q < 16; q += 2) {
+        const int row = row0 + 32 * mt + acc_row(odd ? q + 1 : q, h);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const float a = acc[mt][ct][q], b = acc[mt][ct][q + 1];
+          const float y = __shfl_xor(odd ? a : b, 1);
+          if (row < rows)
+            *(uint32_t*)(dzb + (long long)row * lddz + 64 * w + 32 * ct + (lr & ~1)) =
+                odd ? pk_bf16(y, b) : pk_bf16(a, y);
+        }
       }
-    }
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = row0 + 32 * mt + acc_row(q, h);
+        if (row < rows) {
+          float* o = dZ + (long long)row * lddz + 64 * w + lr;
+          o[0] = acc[mt][0][q];
+          o[32] = acc[mt][1][q];
+        }
+      }
+  }
   if constexpr (LN) {
     const int s0 = row0 / L.hw;
     float sg[2] = {0.f, 0.f}, sgx[2] = {0.f, 0.f};
@@ -1286,7 +1308,7 @@ static int ln_tail_bwd(const float* dR, const float* R, const float* inv, int ro
   const LnTailWs o = ln_tail_ws(rows, hw);
   const LnWs l = ln_ws(o.n, o.E, TC);
   auto* s = (hipStream_t)stream;
-  const LnBwd L{X, ws + o.ln + l.stats, ws + o.aff, ws + o.tp, hw, o.n};
+  const LnBwd L{X, ws + o.ln + l.stats, ws + o.aff, ws + o.tp, hw, o.n, dOb ? 1 : 0};
   hipLaunchKernelGGL(tail_bwd_kernel<true>, dim3((rows + TM - 1) / TM), dim3(256), B_LDS_LN, s,
                      dR, (long long)TD, R, (long long)TD, inv, rows, eps, pk, H1b, H2b, dZ,
                      (long long)TC, dPb, dH2b, dH1b, L);

@@ -3331,6 +3331,6 @@ int tgfr_wr_lds_bytes(int which) {
   return which == 0 ? F_LDS : which == 1 ? BwdCfg<MODE_SPLIT>::LDS : FR_LDS;
 }
 
-int tgfr_version(void) { return 610; }
+int tgfr_version(void) { return 620; }
 
 }  // extern "C"

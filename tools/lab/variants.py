@@ -290,34 +290,41 @@ FILE_VARIANTS = {
                                  "  dw_plan_n(rows, 4, NS, KS, 768, A, wsf, n_wg);")]),
     "dw256": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg);",
                                  "  dw_plan_n(rows, 4, NS, KS, 256, A, wsf, n_wg);")]),
+    # the committed tail + LayerNorm sources (A/B of a work-tree change to both)
+    "headtn": (("tgfr_tail.hip", "tgfr_norm.hip"), "HEAD"),
 }
 
 
 def build_variant(name, subs, fname="tgfr_wr.hip"):
-    if subs == "HEAD":          # the committed source, for A/B against the work tree
-        src = subprocess.run(["git", "show", f"HEAD:text_guided_face_recognition_amd/csrc/{fname}"],
-                             cwd=ROOT, check=True, capture_output=True, text=True).stdout
-        subs = []
-    else:
-        src = open(os.path.join(B.CSRC, fname)).read()
-    for old, new in subs:
-        if old not in src:
-            raise SystemExit(f"{name}: substitution not found: {old[:60]!r}")
-        src = src.replace(old, new)
+    """fname: one source, or a tuple of sources when subs == "HEAD" (each
+    taken at the committed revision)."""
+    fnames = fname if isinstance(fname, tuple) else (fname,)
     os.makedirs(OUT, exist_ok=True)
-    stem = fname[:-4]
-    vsrc = os.path.join(OUT, f"{stem}_{name}.hip")
-    open(vsrc, "w").write(src)
-    obj = os.path.join(OUT, f"{stem}_{name}.o")
-    cmd = [B.HIPCC, f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-fPIC", "-fno-gpu-rdc",
-           "-Wno-unused-result", "-Wno-unused-value", "-I", B.CSRC,
-           *B.FILE_FLAGS.get(fname, []), "-c", vsrc, "-o", obj]
-    subprocess.run(cmd, check=True, capture_output=True)
+    objs = []
+    for fn in fnames:
+        if subs == "HEAD":      # the committed source, for A/B against the work tree
+            src = subprocess.run(["git", "show", f"HEAD:text_guided_face_recognition_amd/csrc/{fn}"],
+                                 cwd=ROOT, check=True, capture_output=True, text=True).stdout
+        else:
+            src = open(os.path.join(B.CSRC, fn)).read()
+            for old, new in subs:
+                if old not in src:
+                    raise SystemExit(f"{name}: substitution not found: {old[:60]!r}")
+                src = src.replace(old, new)
+        stem = fn[:-4]
+        vsrc = os.path.join(OUT, f"{stem}_{name}.hip")
+        open(vsrc, "w").write(src)
+        obj = os.path.join(OUT, f"{stem}_{name}.o")
+        cmd = [B.HIPCC, f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-fPIC", "-fno-gpu-rdc",
+               "-Wno-unused-result", "-Wno-unused-value", "-I", B.CSRC,
+               *B.FILE_FLAGS.get(fn, []), "-c", vsrc, "-o", obj]
+        subprocess.run(cmd, check=True, capture_output=True)
+        objs.append(obj)
     others = [os.path.join(B.OBJ_DIR, os.path.basename(s).replace(".hip", ".o"))
-              for s in B.sources() if not s.endswith(fname)]
+              for s in B.sources() if os.path.basename(s) not in fnames]
     lib = os.path.join(OUT, f"lib_{name}.so")
     subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-fno-gpu-rdc",
-                    "-o", lib, obj, *others], check=True, capture_output=True)
+                    "-o", lib, *objs, *others], check=True, capture_output=True)
     return lib
 
 

@@ -1366,7 +1366,7 @@ class ImimTail(torch.autograd.Function):
         eps, shape, w1shape, w2shape = ctx.cfg
         rows, dev = r.shape[0], r.device
         dr2 = _aligned(dr.reshape(rows, _TAIL_D))
-        dz = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)   # bf16 dZ scratch
+        dz = torch.empty(rows, _TAIL_C, dtype=torch.float32, device=dev)
         dp = torch.empty(rows, _TAIL_D, dtype=torch.int16, device=dev)
         dh2 = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)
         dh1 = torch.empty(rows, _TAIL_H, dtype=torch.int16, device=dev)
@@ -1445,7 +1445,7 @@ class ImimLnTail(torch.autograd.Function):
         eps, xshape, hw, lnshape, w1shape, w2shape = ctx.cfg
         rows, dev = r.shape[0], r.device
         dr2 = _aligned(dr.reshape(rows, _TAIL_D))
-        dz = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)   # bf16 dZ scratch
+        dz = torch.empty(rows, _TAIL_C, dtype=torch.float32, device=dev)
         dp = torch.empty(rows, _TAIL_D, dtype=torch.int16, device=dev)
         dh2 = torch.empty(rows, _TAIL_C, dtype=torch.int16, device=dev)
         dh1 = torch.empty(rows, _TAIL_H, dtype=torch.int16, device=dev)

@@ -282,6 +282,7 @@ FILE_VARIANTS = {
   auto fn = K == 256 ? &bgemm_wres_kernel<256, true, true> : &bgemm_wres_kernel<128, true, true>;""")]),
     # optimiser: 2 float4 per thread (twice the workgroups) instead of 4
     "opt2": ("tgfr_optim.hip", [("VEC_PER_BLOCK = 4 * THREADS;", "VEC_PER_BLOCK = 2 * THREADS;")]),
+    "opt1": ("tgfr_optim.hip", [("VEC_PER_BLOCK = 4 * THREADS;", "VEC_PER_BLOCK = 1 * THREADS;")]),
     # BatchNorm normalise: 32 channels per workgroup (512 workgroups) instead of 64
     "bnct32": ("tgfr_bn.hip", [("constexpr int BN_CT = 64;", "constexpr int BN_CT = 32;")]),
     # IMIM weight gradients: the workgroup budget of the row-slice split

@@ -35,7 +35,6 @@
 #include "tgfr_ln.h"
 
 #include <algorithm>
-#include <cstdlib>
 #include <type_traits>
 
 using namespace tgfr;
@@ -1398,9 +1397,8 @@ int tgfr_tail_dw(const uint16_t* dPb, const uint16_t* H2b, const uint16_t* dH2b,
 // tools/lab/lib_ab.sh, profiles/r04/fork_ab.txt).
 static void imim_dw_plan(int rows, int Nq, int Kq, DwArgs& A, long long& wsf, int& n_wg) {
   const int NS[4] = {TD, TC, TH, Nq}, KS[4] = {TC, TH, TC, Kq};
-  // bf16 dW slabs (TGFR_DW_F32SLAB=1: fp32, the lab A/B)
-  const char* e = getenv("TGFR_DW_F32SLAB");
-  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg, !(e && atoi(e) == 1));
+  // bf16 dW slabs (fp32 slabs: the lab variant dwf32slab, tools/lab/variants.py)
+  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg, true);
 }
 
 int tgfr_imim_dw_ws(int rows, int Nq, int Kq, long long* floats) {

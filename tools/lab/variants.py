@@ -287,14 +287,17 @@ FILE_VARIANTS = {
     "bnct32": ("tgfr_bn.hip", [("constexpr int BN_CT = 64;", "constexpr int BN_CT = 32;")]),
     # IMIM weight gradients: the workgroup budget of the row-slice split
     # (512 kept in round 4; 256 and 128 measured slower)
-    "dw768": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg,",
-                                 "  dw_plan_n(rows, 4, NS, KS, 768, A, wsf, n_wg,")]),
-    "dw1024": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg,",
-                                  "  dw_plan_n(rows, 4, NS, KS, 1024, A, wsf, n_wg,")]),
-    "dw384": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg,",
-                                 "  dw_plan_n(rows, 4, NS, KS, 384, A, wsf, n_wg,")]),
-    "dw256": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg,",
-                                 "  dw_plan_n(rows, 4, NS, KS, 256, A, wsf, n_wg,")]),
+    "dw768": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg, true);",
+                                 "  dw_plan_n(rows, 4, NS, KS, 768, A, wsf, n_wg, true);")]),
+    "dw1024": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg, true);",
+                                  "  dw_plan_n(rows, 4, NS, KS, 1024, A, wsf, n_wg, true);")]),
+    "dw384": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg, true);",
+                                 "  dw_plan_n(rows, 4, NS, KS, 384, A, wsf, n_wg, true);")]),
+    "dw256": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg, true);",
+                                 "  dw_plan_n(rows, 4, NS, KS, 256, A, wsf, n_wg, true);")]),
+    # IMIM weight gradients with fp32 row-slice slabs (the pre-bf16-slab path)
+    "dwf32slab": ("tgfr_tail.hip", [("  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg, true);",
+                                     "  dw_plan_n(rows, 4, NS, KS, 512, A, wsf, n_wg, false);")]),
     # the committed tail + LayerNorm sources (A/B of a work-tree change to both)
     "headtn": (("tgfr_tail.hip", "tgfr_norm.hip"), "HEAD"),
 }
